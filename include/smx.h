@@ -1,0 +1,154 @@
+/*
+ * smx.h — C ABI of the MI355X op-log composition library (libsmx.so).
+ *
+ * Replaces, as a drop-in behind the unchanged Python entry points:
+ *   smx_compose   <- semmerge/compose.py:11-114  compose_oplogs(delta_a, delta_b)
+ *                    (sort_key/_precedence :16-21,130-149; merge loop :51-112;
+ *                     DivergentRename check :60-70,88-98 with conflict.py:34-49;
+ *                     rename/move chains :27-28,71-82,99-110; materialize :30-49)
+ *   smx_rga_replay <- semmerge/crdt.py:23-57  RGA.insert/move/delete/materialize,
+ *                    batched over many independent lists
+ *
+ * Plain C types only.  All device pointers are HIP device (or managed) memory
+ * owned by the caller; the library never allocates: temporary space comes from a
+ * caller-provided workspace sized by the *_workspace_bytes queries.  Calls are
+ * stream-ordered on `stream` (a hipStream_t passed as void*; NULL = the null
+ * stream).  smx_compose performs one internal stream synchronisation to choose its
+ * sort strategy; read device-side counts only after synchronising the stream.
+ *
+ * Return value: 0 on success, a negative SMX_E* code otherwise; the message is
+ * available from smx_last_error() (thread-local).  Nothing aborts the process.
+ */
+#ifndef SMX_H
+#define SMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMX_OK 0
+#define SMX_E_ARG (-1)      /* bad argument / shape */
+#define SMX_E_CAPACITY (-2) /* an output buffer is too small; required size reported */
+#define SMX_E_HIP (-3)      /* a HIP runtime call failed */
+#define SMX_E_WORKSPACE (-4) /* workspace too small */
+
+/* Dense precedence ranks (compose.py:130-149; unknown type -> 99 -> rank 17). */
+#define SMX_KIND_MOVE 0     /* moveDecl, precedence 10 */
+#define SMX_KIND_RENAME 1   /* renameSymbol, precedence 11 */
+#define SMX_N_KINDS 18
+#define SMX_NONE (-1)
+
+/*
+ * One merge's input: ops of branch A (indices [0, n_a)) followed by ops of
+ * branch B (indices [n_a, n_a + n_b)), struct-of-arrays, device memory.
+ *   kind[i]   precedence rank 0..17 of ops[i].type
+ *   ts[i]     order-preserving key of str(provenance["timestamp"])
+ *   oid_hi/lo order-preserving 128-bit key of ops[i].id
+ *   sym[i]    interned target.symbolId, < n_sym
+ *   v0[i]     rename: equality class of params["newName"] (conflict test)
+ *             move:   string id of str(params["newAddress"]) or SMX_NONE
+ *   v1[i]     rename: string id of str(params["newName"]) (rename chain value)
+ *             move:   string id of str(params["newFile"] or params["file"]) or SMX_NONE
+ *             other kinds: ignored
+ */
+typedef struct smx_ops {
+  int64_t n_a;
+  int64_t n_b;
+  int64_t n_sym;
+  const uint8_t* kind;
+  const uint64_t* ts;
+  const uint64_t* oid_hi;
+  const uint64_t* oid_lo;
+  const uint32_t* sym;
+  const int32_t* v0;
+  const int32_t* v1;
+} smx_ops;
+
+/*
+ * Composed output, device memory, capacity n_a + n_b for the per-op arrays.
+ *   order[k]      source index (into A||B) of the k-th composed op
+ *   addr[k]       string id of the move-chain newAddress it sees, or SMX_NONE
+ *   file[k]       string id of the move-chain newFile it sees, or SMX_NONE
+ *   ctx[k]        string id of its renameContext (non-renames), or SMX_NONE
+ *   conflicts     (a_idx, b_idx) pairs in the reference's discovery order;
+ *                 capacity conflict_cap pairs (min(n_a, n_b) always suffices)
+ *   counts[0]     number of composed ops, counts[1] number of conflicts
+ */
+typedef struct smx_compose_out {
+  int32_t* order;
+  int32_t* addr;
+  int32_t* file;
+  int32_t* ctx;
+  int32_t* conflicts;
+  int64_t conflict_cap;
+  int64_t* counts;
+} smx_compose_out;
+
+/* Workspace needed by smx_compose for these sizes. */
+int smx_compose_workspace_bytes(int64_t n_a, int64_t n_b, int64_t n_sym, size_t* bytes);
+
+/* Compose one merge on the GPU (see the header comment for semantics). */
+int smx_compose(const smx_ops* ops, const smx_compose_out* out, void* workspace,
+                size_t workspace_bytes, void* stream);
+
+/*
+ * Per-stage device timing of the last smx_compose calls on this thread, for the
+ * benchmark: when enabled, each stage is bracketed by hipEvents on the call's
+ * stream and the elapsed milliseconds are accumulated per stage.
+ * smx_stage_times copies up to `cap` entries and returns the number of stages;
+ * smx_stage_name(i) names stage i.
+ */
+int smx_set_profiling(int enabled);
+int smx_stage_times(double* ms, int64_t* calls, int cap);
+const char* smx_stage_name(int i);
+int smx_reset_stage_times(void);
+
+/*
+ * Batched RGA replay (crdt.py:23-57): n_ops events over n_lists independent
+ * lists, events of one list in stream order (list[i] non-decreasing is NOT
+ * required; stream order is the index order).
+ *   list[i]   list id < n_lists
+ *   op[i]     0 = insert(key, value), 1 = move(value, key), 2 = delete(value)
+ *   value[i]  interned value (equality class of the value string)
+ *   key_*[i]  order-preserving image of Key(anchor, t, author, opid):
+ *             anchor rank (u32), t (i64, compared signed), author rank (u32),
+ *             opid 128-bit key; ignored for delete
+ * Output: out_value[k] for the surviving elements of every list in list order
+ * then list-position order, out_offsets[l] = first output index of list l
+ * (n_lists + 1 entries), out_src[k] = index of the event that created element k.
+ */
+typedef struct smx_rga_ops {
+  int64_t n_ops;
+  int64_t n_lists;
+  const uint32_t* list;
+  const uint8_t* op;
+  const uint32_t* value;
+  const uint32_t* anchor;
+  const int64_t* t;
+  const uint32_t* author;
+  const uint64_t* opid_hi;
+  const uint64_t* opid_lo;
+} smx_rga_ops;
+
+typedef struct smx_rga_out {
+  uint32_t* out_value;
+  int32_t* out_src;
+  int64_t* out_offsets;
+  int64_t* counts; /* counts[0] = surviving elements */
+} smx_rga_out;
+
+int smx_rga_workspace_bytes(int64_t n_ops, int64_t n_lists, size_t* bytes);
+int smx_rga_replay(const smx_rga_ops* ops, const smx_rga_out* out, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
+const char* smx_last_error(void);
+const char* smx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SMX_H */

@@ -1,0 +1,104 @@
+"""ctypes mirror of include/smx.h (structs and prototypes).
+
+Shared by the product loader (``_lib.py``) and, in tests, by the CPU oracle
+loader (``oracle/oracle.py``): both libraries use the same structs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+c_i64p = C.POINTER(C.c_int64)
+
+
+class SmxOps(C.Structure):
+    _fields_ = [
+        ("n_a", C.c_int64),
+        ("n_b", C.c_int64),
+        ("n_sym", C.c_int64),
+        ("kind", C.c_void_p),
+        ("ts", C.c_void_p),
+        ("oid_hi", C.c_void_p),
+        ("oid_lo", C.c_void_p),
+        ("sym", C.c_void_p),
+        ("v0", C.c_void_p),
+        ("v1", C.c_void_p),
+    ]
+
+
+class SmxComposeOut(C.Structure):
+    _fields_ = [
+        ("order", C.c_void_p),
+        ("addr", C.c_void_p),
+        ("file", C.c_void_p),
+        ("ctx", C.c_void_p),
+        ("conflicts", C.c_void_p),
+        ("conflict_cap", C.c_int64),
+        ("counts", C.c_void_p),
+    ]
+
+
+class SmxRgaOps(C.Structure):
+    _fields_ = [
+        ("n_ops", C.c_int64),
+        ("n_lists", C.c_int64),
+        ("list", C.c_void_p),
+        ("op", C.c_void_p),
+        ("value", C.c_void_p),
+        ("anchor", C.c_void_p),
+        ("t", C.c_void_p),
+        ("author", C.c_void_p),
+        ("opid_hi", C.c_void_p),
+        ("opid_lo", C.c_void_p),
+    ]
+
+
+class SmxRgaOut(C.Structure):
+    _fields_ = [
+        ("out_value", C.c_void_p),
+        ("out_src", C.c_void_p),
+        ("out_offsets", C.c_void_p),
+        ("counts", C.c_void_p),
+    ]
+
+
+# Every symbol include/smx.h declares (tests check the built library exports them).
+EXPORTS = (
+    "smx_compose_workspace_bytes",
+    "smx_compose",
+    "smx_set_profiling",
+    "smx_stage_times",
+    "smx_stage_name",
+    "smx_reset_stage_times",
+    "smx_rga_workspace_bytes",
+    "smx_rga_replay",
+    "smx_last_error",
+    "smx_version",
+)
+
+
+def declare(lib: C.CDLL) -> C.CDLL:
+    """Attach argtypes/restype for the product library."""
+    lib.smx_compose_workspace_bytes.argtypes = [C.c_int64, C.c_int64, C.c_int64,
+                                                C.POINTER(C.c_size_t)]
+    lib.smx_compose_workspace_bytes.restype = C.c_int
+    lib.smx_compose.argtypes = [C.POINTER(SmxOps), C.POINTER(SmxComposeOut), C.c_void_p,
+                                C.c_size_t, C.c_void_p]
+    lib.smx_compose.restype = C.c_int
+    lib.smx_set_profiling.argtypes = [C.c_int]
+    lib.smx_set_profiling.restype = C.c_int
+    lib.smx_stage_times.argtypes = [C.POINTER(C.c_double), c_i64p, C.c_int]
+    lib.smx_stage_times.restype = C.c_int
+    lib.smx_stage_name.argtypes = [C.c_int]
+    lib.smx_stage_name.restype = C.c_char_p
+    lib.smx_reset_stage_times.argtypes = []
+    lib.smx_reset_stage_times.restype = C.c_int
+    lib.smx_rga_workspace_bytes.argtypes = [C.c_int64, C.c_int64, C.POINTER(C.c_size_t)]
+    lib.smx_rga_workspace_bytes.restype = C.c_int
+    lib.smx_rga_replay.argtypes = [C.POINTER(SmxRgaOps), C.POINTER(SmxRgaOut), C.c_void_p,
+                                   C.c_size_t, C.c_void_p]
+    lib.smx_rga_replay.restype = C.c_int
+    lib.smx_last_error.argtypes = []
+    lib.smx_last_error.restype = C.c_char_p
+    lib.smx_version.argtypes = []
+    lib.smx_version.restype = C.c_char_p
+    return lib

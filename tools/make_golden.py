@@ -1,0 +1,291 @@
+"""Generate tests/golden/ by running the REFERENCE implementation in this container.
+
+The reference (``/root/reference/semmerge``) is imported read-only with
+``PYTHONDONTWRITEBYTECODE`` semantics and a json-backed stand-in for ``orjson``
+(only ``OpLog.to_json/from_json`` use it, ops.py:112-118; compose, conflict and
+crdt never do).  Nothing from the reference is copied: the committed fixtures are
+inputs and the reference's outputs (JSON), plus sha256 digests for the large
+synthetic configs.  The GPU box never reads /root/reference.
+
+    python tools/make_golden.py [--big]
+
+``--big`` also composes the 1M-op config 2 (~25 s of reference CPU time).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import random
+import sys
+import time
+import types
+import uuid
+
+sys.dont_write_bytecode = True
+REF = os.environ.get("SMX_REFERENCE", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+GOLD = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, REPO)
+
+
+def _import_reference():
+    stub = types.ModuleType("orjson")
+    stub.dumps = lambda obj, *a, **k: json.dumps(obj).encode()
+    stub.loads = lambda s, *a, **k: json.loads(s)
+    sys.modules.setdefault("orjson", stub)
+    sys.path.insert(0, REF)
+    from semmerge import compose, crdt, ops  # noqa: E402
+    return compose, crdt, ops
+
+
+def dumps_line(obj) -> str:
+    return json.dumps(obj, ensure_ascii=False, separators=(",", ":"))
+
+
+def digest(dicts) -> str:
+    h = hashlib.sha256()
+    for d in dicts:
+        h.update(dumps_line(d).encode("utf-8"))
+        h.update(b"\n")
+    return h.hexdigest()
+
+
+# ---------------------------------------------------------------------------
+# random edge-case compose cases
+TYPES = ["moveDecl", "renameSymbol", "editStmtBlock", "addDecl", "deleteDecl",
+         "modifyImport", "reorderImports", "changeSignature", "updateCall", "extractMethod",
+         "inlineMethod", "reorderParams", "addParam", "removeParam", "moveFile",
+         "renameFile", "modifyNamespace", "customOp"]
+NAMES = ["x", "y", "z", "3", 3, 3.0, True, 1, None, ["l"], {"d": 1}, ""]
+ADDRS = ["a1", "a2", "a3", "", 5, None, "MISSING"]
+FILES = ["f1.ts", "f2.ts", "", None, "MISSING"]
+
+
+def rand_ts(rng, mode):
+    if mode == "iso":
+        return rng.choice(["2025-11-14T00:00:00.000Z", "2025-11-14T00:00:00.001Z",
+                           "2025-11-14T00:00:00.002Z", "2025-11-14T00:00:00Z",
+                           "1970-01-01T00:00:00Z", "1970-01-01T00:00:00.999Z", "MISSING"])
+    return rng.choice(["2025-11-14T00:00:00.000Z", "2025-11-14T00:00:00Z", "abc", "b",
+                       "2025-11-14 00:00:00", 5, None, "", "MISSING", "ä", "\U0001f600"])
+
+
+def rand_id(rng, mode, pool):
+    if mode == "uuid":
+        if pool and rng.random() < 0.1:
+            return rng.choice(pool)
+        return str(uuid.UUID(int=rng.getrandbits(128), version=4))
+    if mode == "short":
+        return rng.choice(["op1", "op2", "op3", "a", "b", "", "op10", "é", "z" * 15])
+    return rng.choice(["op-" + "x" * 20, "op-" + "y" * 20, "short", "a", "op-" + "x" * 19])
+
+
+def rand_op(rng, ts_mode, id_mode, syms, pool):
+    typ = rng.choice(TYPES[:6] * 4 + TYPES)
+    params = {}
+    if typ == "renameSymbol":
+        params["oldName"] = "old"
+        nn = rng.choice(NAMES + ["MISSING"])
+        if nn != "MISSING":
+            params["newName"] = nn
+        f = rng.choice(FILES)
+        if f != "MISSING":
+            params["file"] = f
+        if rng.random() < 0.2:
+            params["newFile"] = rng.choice(["nf.ts", ""])
+    elif typ == "moveDecl":
+        params["oldAddress"] = "a0"
+        a = rng.choice(ADDRS)
+        if a != "MISSING":
+            params["newAddress"] = a
+        f = rng.choice(FILES)
+        if f != "MISSING":
+            params["newFile"] = f
+        f2 = rng.choice(FILES)
+        if f2 != "MISSING":
+            params["file"] = f2
+    else:
+        if rng.random() < 0.5:
+            params["file"] = "f.ts"
+    if rng.random() < 0.15:
+        params["renameContext"] = "pre"
+    prov = {"rev": "base"}
+    ts = rand_ts(rng, ts_mode)
+    if ts != "MISSING":
+        prov["timestamp"] = ts
+    oid = rand_id(rng, id_mode, pool)
+    pool.append(oid)
+    return {
+        "id": oid,
+        "schemaVersion": 1,
+        "type": typ,
+        "target": {"symbolId": rng.choice(syms), "addressId": rng.choice(["ad0", None, "ad1"])},
+        "params": params,
+        "guards": {"exists": True, "nested": {"k": [1, {"z": None}]}} if rng.random() < 0.3 else {},
+        "effects": {"summary": "s", "list": [1, 2]} if rng.random() < 0.3 else {},
+        "provenance": prov,
+    }
+
+
+def make_cases(compose, ops_mod, n_cases: int, seed: int):
+    rng = random.Random(seed)
+    cases = []
+    for c in range(n_cases):
+        ts_mode = "iso" if c % 3 else "any"
+        id_mode = ["uuid", "uuid", "short", "long"][c % 4]
+        nsym = rng.choice([1, 2, 3, 5])
+        syms = [f"s{i}" for i in range(nsym)]
+        pool = []
+        na = rng.choice([0, 1, 2, 3, 5, 8, 13, 25])
+        nb = rng.choice([0, 1, 2, 3, 5, 8, 13, 25])
+        if c % 5 == 0:  # rename-heavy to provoke walk regions
+            A = [rand_op(rng, ts_mode, id_mode, syms, pool) for _ in range(na)]
+            B = [rand_op(rng, ts_mode, id_mode, syms, pool) for _ in range(nb)]
+            for d in A + B:
+                if rng.random() < 0.8:
+                    d["type"] = "renameSymbol"
+                    d["params"]["newName"] = rng.choice(["p", "q", "r", None])
+        else:
+            A = [rand_op(rng, ts_mode, id_mode, syms, pool) for _ in range(na)]
+            B = [rand_op(rng, ts_mode, id_mode, syms, pool) for _ in range(nb)]
+        cases.append(run_case(compose, ops_mod, A, B))
+    return cases
+
+
+def run_case(compose, ops_mod, A, B):
+    oa = [ops_mod.Op.from_dict(d) for d in A]
+    ob = [ops_mod.Op.from_dict(d) for d in B]
+    before = json.dumps([o.to_dict() for o in oa + ob])
+    out, conf = compose.compose_oplogs(oa, ob)
+    assert json.dumps([o.to_dict() for o in oa + ob]) == before, "reference mutated inputs"
+    return {"A": A, "B": B, "out": [o.to_dict() for o in out],
+            "conflicts": [c.to_dict() for c in conf]}
+
+
+def scenarios(compose, ops_mod):
+    """The reference's own test scenarios with fixed ids (tests/test_compose.py:10-25,
+    tests/e2e_rename_move_decl.sh:22-65)."""
+    mv = {"id": "7d2c9a4e-1b3f-4c8a-9e6d-2f1a0b9c8d7e", "schemaVersion": 1, "type": "moveDecl",
+          "target": {"symbolId": "symbol-123", "addressId": "old-address"},
+          "params": {"newAddress": "new-address"}, "guards": {}, "effects": {}, "provenance": {}}
+    rn = {"id": "11111111-2222-4333-8444-555555555555", "schemaVersion": 1,
+          "type": "renameSymbol", "target": {"symbolId": "symbol-foo", "addressId": "addr-old"},
+          "params": {"oldName": "foo", "newName": "bar", "file": "src/util.ts"},
+          "guards": {}, "effects": {}, "provenance": {}}
+    mv2 = {"id": "66666666-7777-4888-9999-aaaaaaaaaaaa", "schemaVersion": 1, "type": "moveDecl",
+           "target": {"symbolId": "symbol-foo", "addressId": "addr-old"},
+           "params": {"oldAddress": "addr-old", "newAddress": "addr-new",
+                      "oldFile": "src/util.ts", "newFile": "lib/util.ts"},
+           "guards": {}, "effects": {}, "provenance": {}}
+    return {
+        "test_compose_move_only": run_case(compose, ops_mod, [mv], []),
+        "e2e_rename_move_decl": run_case(compose, ops_mod, [rn], [mv2]),
+    }
+
+
+# ---------------------------------------------------------------------------
+# synthetic configs: digests of the reference output
+def synth_digest(compose, ops_mod, name, spec):
+    from semantic_merge_amd import synth
+    logs = synth.lift_logs(spec)
+    A, B = synth.lift_op_dicts(logs)
+    oa = [ops_mod.Op.from_dict(d) for d in A]
+    ob = [ops_mod.Op.from_dict(d) for d in B]
+    t0 = time.perf_counter()
+    out, conf = compose.compose_oplogs(oa, ob)
+    dt = time.perf_counter() - t0
+    rec = {
+        "name": name,
+        "spec": {k: v for k, v in spec.__dict__.items() if k != "mix"},
+        "mix": [list(x) for x in spec.mix],
+        "n_out": len(out),
+        "n_conflicts": len(conf),
+        "out_sha256": digest(o.to_dict() for o in out),
+        "conflicts_sha256": digest(c.to_dict() for c in conf),
+        # first/last records verbatim, for a readable failure
+        "out_head": [o.to_dict() for o in out[:3]],
+        "conflicts_head": [c.to_dict() for c in conf[:2]],
+        "reference_seconds": round(dt, 3),
+    }
+    print(f"{name}: n={spec.n_total} out={len(out)} conflicts={len(conf)} ref {dt:.2f}s",
+          flush=True)
+    return rec
+
+
+# ---------------------------------------------------------------------------
+# RGA cases
+def make_rga_cases(crdt, n_cases: int, seed: int):
+    rng = random.Random(seed)
+    cases = []
+    for c in range(n_cases):
+        nvals = rng.choice([1, 2, 3, 6])
+        vals = [f"v{i}" for i in range(nvals)]
+        anchors = rng.choice([["root"], ["a", "b"], ["", "a", "ab", "b"]])
+        authors = rng.choice([["u1"], ["u1", "u2"], ["A", "a", "b"]])
+        events = []
+        for _ in range(rng.choice([0, 1, 3, 8, 20, 40])):
+            kind = rng.choices(["insert", "move", "delete"], [0.6, 0.25, 0.15])[0]
+            key = [rng.choice(anchors), rng.choice([0, 1, 2, 5, -1, 2 ** 40]),
+                   rng.choice(authors), rng.choice(["o1", "o2", "o3", "p"])]
+            if c % 4 == 0:
+                key[3] = str(uuid.UUID(int=rng.getrandbits(128), version=4))
+            if kind == "delete":
+                events.append(["delete", rng.choice(vals)])
+            else:
+                events.append([kind, rng.choice(vals), key])
+        rga = crdt.RGA()
+        for ev in events:
+            if ev[0] == "insert":
+                rga.insert(crdt.Key(*ev[2]), ev[1])
+            elif ev[0] == "move":
+                rga.move(ev[1], crdt.Key(*ev[2]))
+            else:
+                rga.delete(ev[1])
+        cases.append({"events": events, "out": rga.materialize()})
+    return cases
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--big", action="store_true")
+    args = ap.parse_args()
+    compose, crdt, ops_mod = _import_reference()
+    os.makedirs(GOLD, exist_ok=True)
+
+    cases = make_cases(compose, ops_mod, 600, seed=20251114)
+    with open(os.path.join(GOLD, "compose_cases.json"), "w") as fh:
+        json.dump(cases, fh, separators=(",", ":"))
+    with open(os.path.join(GOLD, "compose_scenarios.json"), "w") as fh:
+        json.dump(scenarios(compose, ops_mod), fh, indent=1)
+    print(f"compose cases: {len(cases)}, "
+          f"with conflicts: {sum(1 for c in cases if c['conflicts'])}")
+
+    with open(os.path.join(GOLD, "rga_cases.json"), "w") as fh:
+        json.dump(make_rga_cases(crdt, 600, seed=13), fh, separators=(",", ":"))
+
+    from semantic_merge_amd import synth
+    specs = [
+        ("lift_20k", synth.LiftSpec(20_000, 200, 3)),
+        ("lift_200k", synth.LiftSpec(200_000, 2_000, 5)),
+        ("lift_100k_shuffled", synth.LiftSpec(100_000, 1_000, 9, shuffle=True)),
+        ("adversarial_100k", synth.LiftSpec(100_000, 500, 17, ops_per_ms=4096,
+                                            mix=synth.ADVERSARIAL_MIX, rename_overlap=0.30)),
+    ]
+    if args.big:
+        specs.append(("c2_1M", synth.CONFIGS["c2"]))
+    recs = [synth_digest(compose, ops_mod, name, spec) for name, spec in specs]
+    path = os.path.join(GOLD, "compose_digests.json")
+    old = {}
+    if os.path.exists(path):
+        old = {r["name"]: r for r in json.load(open(path))}
+    for r in recs:
+        old[r["name"]] = r
+    with open(path, "w") as fh:
+        json.dump(list(old.values()), fh, indent=1, ensure_ascii=False)
+
+
+if __name__ == "__main__":
+    main()
