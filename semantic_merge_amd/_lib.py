@@ -1,0 +1,159 @@
+"""Loader for libsmx.so (the HIP library) and device-buffer plumbing.
+
+PyTorch-ROCm is used only to own device memory and to name the current HIP
+stream; every computation happens in libsmx's kernels through the C ABI of
+include/smx.h.  There is no CPU fallback: without the library or a GPU these
+functions raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _abi
+from .marshal import SoA
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SMX_LIB", os.path.join(HERE, "libsmx.so"))
+_lib: Optional[C.CDLL] = None
+
+
+class SmxError(RuntimeError):
+    def __init__(self, code: int, msg: str) -> None:
+        super().__init__(f"smx error {code}: {msg}")
+        self.code = code
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libsmx.so not built at {LIB_PATH}; run __graft_entry__.build()")
+        _lib = _abi.declare(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise SmxError(rc, lib().smx_last_error().decode(errors="replace"))
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("semantic_merge_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+    return torch
+
+
+def _ptr(t) -> int:
+    return t.data_ptr() if t is not None and t.numel() > 0 else 0
+
+
+class DeviceCompose:
+    """Device-resident inputs, outputs and workspace for repeated smx_compose calls."""
+
+    def __init__(self, soa: SoA, device: str = "cuda") -> None:
+        torch = _torch()
+        self.torch = torch
+        self.soa = soa
+        self.n = soa.n
+        dev = torch.device(device)
+        self.device = dev
+
+        def up(a, dt):
+            return torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev, non_blocking=False)
+
+        self.kind = up(soa.kind, np.uint8)
+        self.ts = up(soa.ts, np.int64)      # bit-identical u64 payload
+        self.hi = up(soa.oid_hi, np.int64)
+        self.lo = up(soa.oid_lo, np.int64)
+        self.sym = up(soa.sym, np.int32)
+        self.v0 = up(soa.v0, np.int32)
+        self.v1 = up(soa.v1, np.int32)
+        n = max(self.n, 1)
+        self.order = torch.empty(n, dtype=torch.int32, device=dev)
+        self.addr = torch.empty(n, dtype=torch.int32, device=dev)
+        self.file = torch.empty(n, dtype=torch.int32, device=dev)
+        self.ctx = torch.empty(n, dtype=torch.int32, device=dev)
+        self.cap = max(min(soa.n_a, soa.n_b), 1)
+        self.conf = torch.empty(2 * self.cap, dtype=torch.int32, device=dev)
+        self.counts = torch.zeros(2, dtype=torch.int64, device=dev)
+        ws = C.c_size_t(0)
+        check(lib().smx_compose_workspace_bytes(soa.n_a, soa.n_b, soa.n_sym, C.byref(ws)))
+        self.ws_bytes = ws.value
+        self.ws = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=dev)
+        self._ops = _abi.SmxOps(soa.n_a, soa.n_b, soa.n_sym, _ptr(self.kind), _ptr(self.ts),
+                                _ptr(self.hi), _ptr(self.lo), _ptr(self.sym), _ptr(self.v0),
+                                _ptr(self.v1))
+        self._out = _abi.SmxComposeOut(_ptr(self.order), _ptr(self.addr), _ptr(self.file),
+                                       _ptr(self.ctx), _ptr(self.conf), self.cap,
+                                       _ptr(self.counts))
+
+    def run(self, stream=None) -> None:
+        """Enqueue one composition on `stream` (default: torch's current stream)."""
+        s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
+        check(lib().smx_compose(C.byref(self._ops), C.byref(self._out), _ptr(self.ws),
+                                self.ws_bytes, s.cuda_stream))
+
+    def results(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+        self.torch.cuda.synchronize(self.device)
+        k, nc = (int(x) for x in self.counts.cpu().tolist())
+        if nc > self.cap:
+            raise SmxError(-2, f"{nc} conflicts exceed capacity {self.cap}")
+        return (self.order[:k].cpu().numpy(), self.addr[:k].cpu().numpy(),
+                self.file[:k].cpu().numpy(), self.ctx[:k].cpu().numpy(),
+                self.conf[: 2 * nc].cpu().numpy().reshape(nc, 2))
+
+
+def compose_soa(soa: SoA, device: str = "cuda"):
+    """(order, addr, file, ctx, conflict_pairs) of one merge, computed on the GPU."""
+    if soa.n == 0:
+        e = np.zeros(0, np.int32)
+        return e, e, e, e, np.zeros((0, 2), np.int32)
+    dc = DeviceCompose(soa, device)
+    dc.run()
+    return dc.results()
+
+
+def stage_times():
+    """{stage: (total_ms, calls)} accumulated while smx_set_profiling(1)."""
+    L = lib()
+    ms = (C.c_double * 16)()
+    calls = (C.c_int64 * 16)()
+    n = L.smx_stage_times(ms, calls, 16)
+    return {L.smx_stage_name(i).decode(): (ms[i], calls[i]) for i in range(n)}
+
+
+def rga_replay_device(batch, device: str = "cuda"):
+    """(values, src, offsets) of a batched RGA replay computed on the GPU."""
+    torch = _torch()
+    dev = torch.device(device)
+    n = batch.n
+    if n == 0:
+        return (np.zeros(0, np.uint32), np.zeros(0, np.int32),
+                np.zeros(batch.n_lists + 1, np.int64))
+
+    def up(a, dt):
+        return torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
+
+    ins = [up(batch.list_id, np.int32), up(batch.op, np.uint8), up(batch.value, np.int32),
+           up(batch.anchor, np.int32), up(batch.t, np.int64), up(batch.author, np.int32),
+           up(batch.opid_hi, np.int64), up(batch.opid_lo, np.int64)]
+    vals = torch.empty(n, dtype=torch.int32, device=dev)
+    src = torch.empty(n, dtype=torch.int32, device=dev)
+    offs = torch.empty(batch.n_lists + 1, dtype=torch.int64, device=dev)
+    counts = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = C.c_size_t(0)
+    check(lib().smx_rga_workspace_bytes(n, batch.n_lists, C.byref(ws)))
+    wst = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=dev)
+    ops = _abi.SmxRgaOps(n, batch.n_lists, *[_ptr(t) for t in ins])
+    out = _abi.SmxRgaOut(_ptr(vals), _ptr(src), _ptr(offs), _ptr(counts))
+    check(lib().smx_rga_replay(C.byref(ops), C.byref(out), _ptr(wst), ws.value,
+                               torch.cuda.current_stream(dev).cuda_stream))
+    torch.cuda.synchronize(dev)
+    k = int(counts.item())
+    return (vals[:k].cpu().numpy().view(np.uint32), src[:k].cpu().numpy(),
+            offs.cpu().numpy())

@@ -1,0 +1,91 @@
+// smx_scan.h — device-wide exclusive scans (sum / max) with a host- or device-held
+// length.  Three launches: per-block reduce, scan of block partials, block scans.
+// Each block owns one contiguous chunk; each thread scans 8 consecutive items.
+#pragma once
+
+#include "smx_common.h"
+
+#define SCAN_NB 512
+#define SCAN_ITEMS 8
+#define SCAN_TILE (BLOCK * SCAN_ITEMS)
+
+__device__ __forceinline__ i64 scan_len(const u64* n_dev, i64 n_host) {
+  return n_dev ? (i64)(*n_dev) : n_host;
+}
+
+template <typename Op, typename TI, typename TO>
+__global__ void __launch_bounds__(BLOCK) k_scan_reduce(const TI* __restrict__ in, i64 n_host,
+                                                       const u64* n_dev, TO* partials) {
+  __shared__ TO s[NWAVES + 1];
+  const i64 n = scan_len(n_dev, n_host);
+  const i64 chunk = SMX_CEIL_DIV(SMX_CEIL_DIV(n, (i64)SCAN_NB), (i64)SCAN_TILE) * SCAN_TILE;
+  const i64 lo = (i64)blockIdx.x * chunk;
+  const i64 hi = lo + chunk < n ? lo + chunk : n;
+  TO acc = Op::template identity<TO>();
+  for (i64 i = lo + threadIdx.x; i < hi; i += BLOCK) acc = Op::apply(acc, (TO)in[i]);
+  TO total;
+  block_excl_scan<Op, TO>(acc, s, &total);
+  if (threadIdx.x == 0) partials[blockIdx.x] = total;
+}
+
+// Exclusive scan of the SCAN_NB partials in place; optionally stores the grand total.
+template <typename Op, typename TO>
+__global__ void __launch_bounds__(BLOCK) k_scan_partials(TO* partials, TO* total_out) {
+  __shared__ TO s[SCAN_NB];
+  for (int i = threadIdx.x; i < SCAN_NB; i += BLOCK) s[i] = partials[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    TO acc = Op::template identity<TO>();
+    for (int i = 0; i < SCAN_NB; ++i) {
+      TO x = s[i];
+      s[i] = acc;
+      acc = Op::apply(acc, x);
+    }
+    if (total_out) *total_out = acc;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < SCAN_NB; i += BLOCK) partials[i] = s[i];
+}
+
+template <typename Op, typename TI, typename TO>
+__global__ void __launch_bounds__(BLOCK) k_scan_down(const TI* __restrict__ in, TO* __restrict__ out,
+                                                     i64 n_host, const u64* n_dev,
+                                                     const TO* partials) {
+  __shared__ TO s[NWAVES + 1];
+  const i64 n = scan_len(n_dev, n_host);
+  const i64 chunk = SMX_CEIL_DIV(SMX_CEIL_DIV(n, (i64)SCAN_NB), (i64)SCAN_TILE) * SCAN_TILE;
+  const i64 lo = (i64)blockIdx.x * chunk;
+  const i64 hi = lo + chunk < n ? lo + chunk : n;
+  TO carry = partials[blockIdx.x];
+  for (i64 t0 = lo; t0 < hi; t0 += SCAN_TILE) {
+    const i64 b = t0 + (i64)threadIdx.x * SCAN_ITEMS;
+    TO v[SCAN_ITEMS];
+    TO acc = Op::template identity<TO>();
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+      v[j] = (b + j < hi) ? (TO)in[b + j] : Op::template identity<TO>();
+      acc = Op::apply(acc, v[j]);
+    }
+    TO total;
+    TO pre = block_excl_scan<Op, TO>(acc, s, &total);
+    TO run = Op::apply(carry, pre);
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+      if (b + j < hi) out[b + j] = run;
+      run = Op::apply(run, v[j]);
+    }
+    carry = Op::apply(carry, total);
+  }
+}
+
+// out[i] = op-exclusive-prefix of in[0..i); *total_out (optional) = op over all.
+template <typename Op, typename TI, typename TO>
+static hipError_t scan_excl(const TI* in, TO* out, i64 n_host, const u64* n_dev, TO* partials,
+                            TO* total_out, hipStream_t st) {
+  hipLaunchKernelGGL((k_scan_reduce<Op, TI, TO>), dim3(SCAN_NB), dim3(BLOCK), 0, st, in, n_host,
+                     n_dev, partials);
+  hipLaunchKernelGGL((k_scan_partials<Op, TO>), dim3(1), dim3(BLOCK), 0, st, partials, total_out);
+  hipLaunchKernelGGL((k_scan_down<Op, TI, TO>), dim3(SCAN_NB), dim3(BLOCK), 0, st, in, out, n_host,
+                     n_dev, partials);
+  return hipGetLastError();
+}

@@ -1,0 +1,106 @@
+"""GPU parity: libsmx (through the C ABI) == reference golden vectors == CPU oracle."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from semantic_merge_amd import synth
+from semantic_merge_amd._lib import DeviceCompose, compose_soa
+from semantic_merge_amd.compose import compose_oplogs
+from semantic_merge_amd.marshal import marshal
+
+from _util import assert_case, jline, load, to_ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _eq_soa(gpu, ref, label):
+    names = ("order", "addr", "file", "ctx", "conflicts")
+    for name, g, r in zip(names, gpu, ref):
+        assert g.shape == r.shape, f"{label}: {name} shape {g.shape} vs {r.shape}"
+        if not np.array_equal(g, r):
+            bad = np.flatnonzero(g.reshape(-1) != r.reshape(-1))[:5]
+            raise AssertionError(f"{label}: {name} differs at {bad.tolist()}")
+
+
+def test_library_runs_on_gpu():
+    import torch
+    assert torch.cuda.is_available()
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(5000, 50, 1)))
+    _eq_soa(compose_soa(soa), oracle.compose(soa), "lift_5k")
+
+
+def test_scenarios_gpu():
+    for name, case in load("compose_scenarios.json").items():
+        assert_case(compose_soa, case, name)
+
+
+def test_edge_cases_gpu():
+    for i, case in enumerate(load("compose_cases.json")):
+        assert_case(compose_soa, case, f"case {i}")
+
+
+def test_dropin_compose_oplogs_matches_reference():
+    case = load("compose_scenarios.json")["e2e_rename_move_decl"]
+    A, B = to_ops(case["A"]), to_ops(case["B"])
+    before = jline([o.to_dict() for o in A + B])
+    out, conf = compose_oplogs(A, B)
+    assert jline([o.to_dict() for o in out]) == jline(case["out"])
+    assert conf == []
+    assert jline([o.to_dict() for o in A + B]) == before  # inputs untouched
+    ren = [o for o in out if o.type == "renameSymbol"][0]
+    assert ren.params["file"] == "lib/util.ts" and ren.params["newFile"] == "lib/util.ts"
+    assert all(o is not a for o in out for a in A + B)
+
+
+def _digest(dicts):
+    h = hashlib.sha256()
+    for d in dicts:
+        h.update(jline(d).encode("utf-8"))
+        h.update(b"\n")
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("name", ["lift_20k", "lift_100k_shuffled", "adversarial_100k",
+                                  "lift_200k"])
+def test_synthetic_digests_gpu(name):
+    rec = {r["name"]: r for r in load("compose_digests.json")}[name]
+    kw = dict(rec["spec"])
+    kw["mix"] = tuple(tuple(x) for x in rec["mix"])
+    logs = synth.lift_logs(synth.LiftSpec(**kw))
+    A, B = synth.lift_op_dicts(logs)
+    out, conf = compose_oplogs(to_ops(A), to_ops(B))
+    assert len(out) == rec["n_out"] and len(conf) == rec["n_conflicts"]
+    assert _digest(o.to_dict() for o in out) == rec["out_sha256"]
+    assert _digest(c.to_dict() for c in conf) == rec["conflicts_sha256"]
+
+
+@pytest.mark.parametrize("spec", [
+    synth.LiftSpec(1_000_000, 10_000, 7),                       # config 2
+    synth.LiftSpec(1_000_000, 10_000, 7, shuffle=True),         # robustness variant
+    synth.LiftSpec(2_000_000, 2_000, 17, ops_per_ms=4096, mix=synth.ADVERSARIAL_MIX,
+                   rename_overlap=0.30),                         # config 5 shape
+    synth.LiftSpec(1_000_000, 64, 23, ops_per_ms=16, mix=synth.ADVERSARIAL_MIX),  # hot symbols
+    synth.LiftSpec(333_333, 1, 29, ops_per_ms=1),               # one symbol, every head collides
+], ids=["c2_1M", "c2_1M_shuffled", "c5_2M", "hot64_1M", "onesym"])
+def test_gpu_equals_oracle_soa(spec):
+    soa = synth.lift_soa(synth.lift_logs(spec))
+    _eq_soa(compose_soa(soa), oracle.compose(soa), str(spec))
+
+
+def test_gpu_repeatable_and_none_moves():
+    spec = synth.LiftSpec(300_000, 3_000, 31)
+    soa = synth.lift_soa(synth.lift_logs(spec))
+    rng = np.random.default_rng(5)
+    mv = np.flatnonzero(soa.kind == 0)
+    soa.v0[rng.choice(mv, len(mv) // 3, replace=False)] = -1   # None newAddress
+    soa.v1[rng.choice(mv, len(mv) // 4, replace=False)] = -1   # falsy newFile and file
+    dc = DeviceCompose(soa)
+    dc.run()
+    first = dc.results()
+    dc.run()
+    second = dc.results()
+    ref = oracle.compose(soa)
+    _eq_soa(first, ref, "none-moves")
+    _eq_soa(second, ref, "none-moves rerun")
