@@ -1,0 +1,192 @@
+"""Benchmark: op-log compose+conflict throughput on device-resident synthetic logs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--n-ops N]
+
+One step = one smx_compose call (semmerge/compose.py:11-114 restated on the GPU)
+over one merge of SURVEY §8(d) config 3: 100M lift-shaped ops (50M per branch),
+1M symbols, seed 11 (+rank).  Inputs are resident in HBM before timing.  With
+N > 1 (torchrun, one process per GPU) every rank composes its own independent
+merge (weak scaling; the merge itself is not sharded yet) and
+the time is the max over ranks.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "op-log compose+conflict throughput (ops/s), 100M-op logs, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+PIPE_BYTES_PER_OP = 53         # 37 B in + 16 B out per op (+8 B per conflict)
+WINDOW_BYTES_PER_OP = 41       # k_window: 37 B of input read once + 4 B T-order index written
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--n-ops", type=int, default=0, help="override the config's op count")
+    ap.add_argument("--cpu-sample", type=int, default=40_000_000,
+                    help="ops in the CPU-baseline sample (rank 0, N=1 only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="check GPU == oracle (slow)")
+    args = ap.parse_args()
+
+    import torch
+    from semantic_merge_amd import _lib, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    spec = synth.CONFIGS[args.config]
+    if args.n_ops:
+        spec = synth.LiftSpec(**{**spec.__dict__, "n_total": args.n_ops})
+    spec = synth.LiftSpec(**{**spec.__dict__, "seed": spec.seed + rank})
+    t0 = time.time()
+    logs = synth.lift_logs(spec)
+    soa = synth.lift_soa(logs)
+    del logs
+    log(f"[rank {rank}] generated {soa.n:,} ops in {time.time() - t0:.1f}s")
+    dc = _lib.DeviceCompose(soa, f"cuda:{local}")
+    log(f"[rank {rank}] resident on {dev}; workspace {dc.ws_bytes / 2**30:.2f} GiB")
+
+    for _ in range(args.warmup):
+        dc.run()
+    torch.cuda.synchronize(dev)
+
+    lib = _lib.lib()
+    lib.smx_reset_stage_times()
+    lib.smx_set_profiling(1)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dc.run()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lib.smx_set_profiling(0)
+    stages = _lib.stage_times()
+    k, nconf = (int(x) for x in dc.counts.cpu().tolist())
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if args.verify:
+        from oracle import oracle
+        ref = oracle.compose(soa)
+        got = dc.results()
+        ok = all(np.array_equal(g, r) for g, r in zip(got, ref))
+        log(f"[rank {rank}] verify vs oracle: {'OK' if ok else 'MISMATCH'}")
+        if not ok:
+            sys.exit(3)
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    n = soa.n
+    ms_step = elapsed / args.steps * 1e3
+    value = world * n * args.steps / elapsed
+    win_ms, win_calls = stages.get("window", (0.0, 0))
+    win_avg = win_ms / max(win_calls, 1)
+    achieved = WINDOW_BYTES_PER_OP * n / (win_avg * 1e-3) / 1e9 if win_avg > 0 else None
+    traffic = None
+    prof = os.path.join(REPO, "profiles", "pmc_window.json")
+    if os.path.exists(prof):
+        rec = json.load(open(prof))
+        if rec.get("n_ops") == n:
+            traffic = rec.get("hbm_bytes_per_launch")
+    pipe_gbs = (PIPE_BYTES_PER_OP * n + 8 * nconf) / (ms_step * 1e-3) / 1e9
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle
+        from semantic_merge_amd.marshal import SoA
+        half = min(args.cpu_sample // 2, soa.n_a, soa.n_b)
+        idx = np.concatenate([np.arange(half), soa.n_a + np.arange(half)])
+        sample = SoA(half, half, soa.kind[idx], soa.ts[idx], soa.oid_hi[idx], soa.oid_lo[idx],
+                     soa.sym[idx], soa.v0[idx], soa.v1[idx], soa.n_sym)
+        t0 = time.perf_counter()
+        oracle.compose(sample)
+        dt = time.perf_counter() - t0
+        cpu = {"value": round(2 * half / dt, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+               "sample": f"first {half:,} ops of each branch of the same workload "
+                         f"({2 * half:,} ops) through oracle/compose_ref.c, 1 thread, "
+                         f"{dt:.1f}s"}
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (lift-shaped op logs generated from a seed, SURVEY §8(d))",
+        "config": {
+            "workload": f"{args.config}: {n:,} ops ({soa.n_a:,} per branch), {soa.n_sym:,} symbols,"
+                        f" {spec.ops_per_ms} ops/ms, seed {spec.seed - rank}+rank",
+            "n_ops_per_gpu": n,
+            "n_sym": soa.n_sym,
+            "composed_ops": k,
+            "conflicts": nconf,
+            "parallelism": f"independent merges x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_window",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": traffic,
+            "bytes_per_op": WINDOW_BYTES_PER_OP,
+            "avg_launch_ms": round(win_avg, 4),
+        },
+        "pipeline_roofline": {
+            "bytes_per_op": PIPE_BYTES_PER_OP,
+            "achieved": round(pipe_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),
+        },
+        "stages_ms_per_step": {k2: round(v[0] / max(v[1], 1), 4) for k2, v in stages.items()
+                               if v[1]},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -101,6 +101,8 @@ class DeviceCompose:
     def results(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
         self.torch.cuda.synchronize(self.device)
         k, nc = (int(x) for x in self.counts.cpu().tolist())
+        if k < 0:
+            raise SmxError(-1, "invalid input: sym >= n_sym or kind >= 18")
         if nc > self.cap:
             raise SmxError(-2, f"{nc} conflicts exceed capacity {self.cap}")
         return (self.order[:k].cpu().numpy(), self.addr[:k].cpu().numpy(),

@@ -14,9 +14,9 @@
 //            regions cluster by cluster.
 //
 // Pipeline (one merge):
-//   k_stats     kind histogram, per-branch timestamp monotonicity, key masks
 //   k_fpart     presorted windows: merge-path on timestamps, cut at ts boundaries
-//   k_wcount    per-window kind counts          k_wscan   window offsets, T bases
+//   k_wcount    per-window kind counts + presorted-layout checks
+//   k_wscan     window offsets and kind totals  k_bases   T segment starts
 //   [generic]   radix-sort each branch by (ts, oid) and cut fixed windows
 //   k_window    per window, in LDS: merge A/B parts, multisplit by kind, sort
 //               equal-timestamp groups by id, write T-ordered arrays
@@ -29,13 +29,8 @@
 #include <vector>
 
 #include "smx_sort.h"
+#include "smx_window.h"
 
-#define WIN_CAP 2048               // max ops per window held in LDS
-#define WIN_TGT 1024               // target window size, presorted path
-#define WIN_ITEMS (WIN_CAP / BLOCK)
-#define NCNT (SMX_N_KINDS + 2)     // kinds + renames per side
-#define KMOVE SMX_KIND_MOVE
-#define KREN SMX_KIND_RENAME
 
 // ---------------------------------------------------------------------------
 // error / profiling state
@@ -59,111 +54,84 @@ static int g_prof = 0;
 static double g_stage_ms[ST_N];
 static int64_t g_stage_calls[ST_N];
 
+// Stage events are recorded on the call's stream and only resolved when the
+// caller asks for the times (smx_stage_times), so profiling adds no host sync.
+struct PendingEv {
+  int stage;
+  hipEvent_t a, b;
+};
+static std::vector<PendingEv> g_pending;
+
 struct StageTimer {
   hipStream_t st;
   bool on;
-  hipEvent_t ev[ST_N][2];
-  bool used[ST_N];
-  StageTimer(hipStream_t s, bool enabled) : st(s), on(enabled) {
-    for (int i = 0; i < ST_N; ++i) used[i] = false;
-    if (!on) return;
-    for (int i = 0; i < ST_N; ++i) {
-      (void)hipEventCreate(&ev[i][0]);
-      (void)hipEventCreate(&ev[i][1]);
-    }
-  }
+  hipEvent_t open[ST_N];
+  std::vector<PendingEv> done;
+  StageTimer(hipStream_t s, bool enabled) : st(s), on(enabled) {}
   void begin(int i) {
-    if (on) (void)hipEventRecord(ev[i][0], st);
+    if (!on) return;
+    (void)hipEventCreate(&open[i]);
+    (void)hipEventRecord(open[i], st);
   }
   void end(int i) {
-    if (on) {
-      (void)hipEventRecord(ev[i][1], st);
-      used[i] = true;
-    }
+    if (!on) return;
+    hipEvent_t b;
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(b, st);
+    done.push_back({i, open[i], b});
   }
   void flush() {
     if (!on) return;
-    (void)hipStreamSynchronize(st);
     std::lock_guard<std::mutex> g(g_prof_mu);
-    for (int i = 0; i < ST_N; ++i) {
-      if (used[i]) {
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, ev[i][0], ev[i][1]);
-        g_stage_ms[i] += ms;
-        g_stage_calls[i] += 1;
-      }
-    }
+    for (auto& p : done) g_pending.push_back(p);
+    done.clear();
   }
   ~StageTimer() {
-    if (!on) return;
-    for (int i = 0; i < ST_N; ++i) {
-      (void)hipEventDestroy(ev[i][0]);
-      (void)hipEventDestroy(ev[i][1]);
+    for (auto& p : done) {  // an error path left events unpublished
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
     }
   }
 };
 
+static void resolve_pending_locked() {
+  for (auto& p : g_pending) {
+    (void)hipEventSynchronize(p.b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    g_stage_ms[p.stage] += ms;
+    g_stage_calls[p.stage] += 1;
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  g_pending.clear();
+}
+
 // ---------------------------------------------------------------------------
 // kernels: planning
 
-__global__ void __launch_bounds__(BLOCK) k_stats(const u8* __restrict__ kind, const u64* __restrict__ ts,
-                                                 const u64* __restrict__ hi, const u64* __restrict__ lo,
-                                                 const u32* __restrict__ sym, const i32* __restrict__ v0,
-                                                 const i32* __restrict__ v1, i64 na, i64 n, i64 n_sym,
-                                                 ComposeMeta* meta) {
-  __shared__ u32 cnt[SMX_N_KINDS + 4];
-  __shared__ u64 kor[2][3], kand[2][3];
-  const int t = threadIdx.x;
-  if (t < SMX_N_KINDS + 4) cnt[t] = 0;
-  if (t < 6) {
-    kor[t / 3][t % 3] = 0;
-    kand[t / 3][t % 3] = ~0ull;
-  }
-  __syncthreads();
+// Per-branch OR / AND of the key words (generic path: skip constant radix digits).
+__global__ void __launch_bounds__(BLOCK) k_keymask(const u64* __restrict__ ts, const u64* __restrict__ hi,
+                                                   const u64* __restrict__ lo, i64 na, i64 n,
+                                                   ComposeMeta* meta) {
   u64 ro[2][3] = {{0, 0, 0}, {0, 0, 0}};
   u64 ra[2][3] = {{~0ull, ~0ull, ~0ull}, {~0ull, ~0ull, ~0ull}};
-  bool nonmono0 = false, nonmono1 = false, badsym = false;
-  u32 none_moves = 0;
-  for (i64 i = (i64)blockIdx.x * BLOCK + t; i < n; i += (i64)gridDim.x * BLOCK) {
-    const u32 k = kind[i];
-    const int side = i >= na;
-    atomicAdd(&cnt[k < SMX_N_KINDS ? k : SMX_N_KINDS - 1], 1u);
-    const u64 tv = ts[i], hv = hi[i], lv = lo[i];
-    if (side) {
-      ro[1][0] |= tv; ro[1][1] |= hv; ro[1][2] |= lv;
-      ra[1][0] &= tv; ra[1][1] &= hv; ra[1][2] &= lv;
-    } else {
-      ro[0][0] |= tv; ro[0][1] |= hv; ro[0][2] |= lv;
-      ra[0][0] &= tv; ra[0][1] &= hv; ra[0][2] &= lv;
+  for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (i64)gridDim.x * BLOCK) {
+    const u64 v[3] = {ts[i], hi[i], lo[i]};
+    const int s = i >= na;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      ro[s][q] |= v[q];
+      ra[s][q] &= v[q];
     }
-    if (i != 0 && i != na && ts[i - 1] > tv) {
-      if (side) nonmono1 = true; else nonmono0 = true;
-    }
-    if (sym[i] >= (u64)n_sym || k >= SMX_N_KINDS) badsym = true;
-    if (k == KMOVE && (v0[i] < 0 || v1[i] < 0)) ++none_moves;
-    if (k == KREN) atomicAdd(&cnt[SMX_N_KINDS + side], 1u);
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      atomicOr((unsigned long long*)&kor[s][q], (unsigned long long)ro[s][q]);
-      atomicAnd((unsigned long long*)&kand[s][q], (unsigned long long)ra[s][q]);
+      atomicOr((unsigned long long*)&meta->key_or[s][q], (unsigned long long)ro[s][q]);
+      atomicAnd((unsigned long long*)&meta->key_and[s][q], (unsigned long long)ra[s][q]);
     }
-  if (none_moves) atomicAdd(&cnt[SMX_N_KINDS + 2], none_moves);
-  if (nonmono0) meta->nonmono[0] = 1;
-  if (nonmono1) meta->nonmono[1] = 1;
-  if (badsym) meta->bad_sym = 1;
-  __syncthreads();
-  if (t < SMX_N_KINDS && cnt[t]) atomicAdd((unsigned long long*)&meta->kcnt[t], (unsigned long long)cnt[t]);
-  if (t < 2 && cnt[SMX_N_KINDS + t])
-    atomicAdd((unsigned long long*)&meta->n_ren_side[t], (unsigned long long)cnt[SMX_N_KINDS + t]);
-  if (t == 2 && cnt[SMX_N_KINDS + 2])
-    atomicAdd((unsigned long long*)&meta->n_move_none, (unsigned long long)cnt[SMX_N_KINDS + 2]);
-  if (t < 6) {
-    atomicOr((unsigned long long*)&meta->key_or[t / 3][t % 3], (unsigned long long)kor[t / 3][t % 3]);
-    atomicAnd((unsigned long long*)&meta->key_and[t / 3][t % 3], (unsigned long long)kand[t / 3][t % 3]);
-  }
 }
 
 __global__ void k_meta_init(ComposeMeta* meta) {
@@ -213,12 +181,6 @@ __global__ void k_fpart(const u64* __restrict__ ts, i64 na, i64 nb, i64 W, i64* 
   bnd[2 * k + 1] = lo;
 }
 
-__device__ __forceinline__ bool key_le(u64 ta, u64 ha, u64 la, u64 tb, u64 hb, u64 lb) {
-  if (ta != tb) return ta < tb;
-  if (ha != hb) return ha < hb;
-  return la <= lb;
-}
-
 // Generic windows over branch logs sorted by (ts, oid): fixed diagonals of WIN_CAP.
 __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi,
                         const u64* __restrict__ slo, i64 na, i64 nb, i64 W, i64* __restrict__ bnd) {
@@ -239,34 +201,46 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
   bnd[2 * k + 1] = d - lo;
 }
 
-// Per-window counts of each kind, plus renames per branch.  perm == nullptr: the
-// presorted layout (branch position j is op base+j).  Column-major [c][W].
-__global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, const u32* __restrict__ perm,
-                                                  const i64* __restrict__ bnd, i64 na, i64 W,
-                                                  u32* __restrict__ wcnt, ComposeMeta* meta, int check_cap) {
+// Per-window counts: each kind, renames per branch, moves with a None value.
+// perm == nullptr: presorted layout (branch position j is op j); then the kernel
+// also checks what the presorted windows rely on: boundaries non-decreasing,
+// window size <= WIN_CAP, timestamps non-decreasing inside each branch (every
+// adjacent pair is checked by exactly one window).  Column-major [c][W].
+__global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, const u64* __restrict__ ts,
+                                                  const i32* __restrict__ v0, const i32* __restrict__ v1,
+                                                  const u32* __restrict__ perm, const i64* __restrict__ bnd,
+                                                  i64 na, i64 W, u32* __restrict__ wcnt, ComposeMeta* meta) {
   __shared__ u32 c[NCNT];
+  __shared__ u32 fail;
   const i64 w = blockIdx.x;
   if (threadIdx.x < NCNT) c[threadIdx.x] = 0;
+  if (threadIdx.x == 0) fail = 0;
   __syncthreads();
   const i64 a0 = bnd[2 * w], b0 = bnd[2 * w + 1], a1 = bnd[2 * w + 2], b1 = bnd[2 * w + 3];
-  if (check_cap && threadIdx.x == 0 && (a1 - a0) + (b1 - b0) > WIN_CAP) meta->f_fail = 1;
-  for (i64 j = a0 + threadIdx.x; j < a1; j += BLOCK) {
-    const u32 src = perm ? perm[j] : (u32)j;
-    const u32 k = min((u32)kind[src], (u32)SMX_N_KINDS - 1);  // validated in k_stats
-    atomicAdd(&c[k], 1u);
-    if (k == KREN) atomicAdd(&c[SMX_N_KINDS], 1u);
+  const bool presorted = perm == nullptr;
+  if (presorted && threadIdx.x == 0 && (a1 < a0 || b1 < b0 || (a1 - a0) + (b1 - b0) > WIN_CAP)) fail = 1;
+  bool bad = false, mono_fail = false;
+  for (int side = 0; side < 2; ++side) {
+    const i64 lo = side ? b0 : a0, hi = side ? b1 : a1, off = side ? na : 0;
+    for (i64 j = lo + threadIdx.x; j < hi; j += BLOCK) {
+      const u32 src = presorted ? (u32)(off + j) : perm[off + j];
+      const u32 k0 = kind[src];
+      bad |= k0 >= SMX_N_KINDS;
+      const u32 k = k0 < SMX_N_KINDS ? k0 : SMX_N_KINDS - 1;
+      atomicAdd(&c[k], 1u);
+      if (k == KREN) atomicAdd(&c[CNT_REN_A + side], 1u);
+      if (k == KMOVE && (v0[src] < 0 || v1[src] < 0)) atomicAdd(&c[CNT_NONE_MV], 1u);
+      if (presorted && j > 0 && ts[src - 1] > ts[src]) mono_fail = true;
+    }
   }
-  for (i64 j = b0 + threadIdx.x; j < b1; j += BLOCK) {
-    const u32 src = perm ? perm[na + j] : (u32)(na + j);
-    const u32 k = min((u32)kind[src], (u32)SMX_N_KINDS - 1);
-    atomicAdd(&c[k], 1u);
-    if (k == KREN) atomicAdd(&c[SMX_N_KINDS + 1], 1u);
-  }
+  if (mono_fail) fail = 1;
+  if (bad) meta->bad_sym = 1;
   __syncthreads();
+  if (threadIdx.x == 0 && fail) meta->f_fail = 1;
   if (threadIdx.x < NCNT) wcnt[(i64)threadIdx.x * W + w] = c[threadIdx.x];
 }
 
-// Exclusive scan of each count column over windows; block 0 also sets the T bases.
+// Exclusive scan of each count column over windows; column totals into meta.
 __global__ void __launch_bounds__(BLOCK) k_wscan(const u32* __restrict__ wcnt, u32* __restrict__ woff,
                                                  i64 W, ComposeMeta* meta) {
   __shared__ u32 s[NWAVES + 1];
@@ -292,242 +266,22 @@ __global__ void __launch_bounds__(BLOCK) k_wscan(const u32* __restrict__ wcnt, u
     }
     carry += tot;
   }
-  if (c == 0 && threadIdx.x == 0) {
-    u64 acc = 0;
-    for (int k = 0; k < SMX_N_KINDS; ++k) {
-      meta->base[k] = acc;
-      acc += meta->kcnt[k];
-    }
-    meta->base[SMX_N_KINDS] = acc;
+  if (threadIdx.x == 0) {
+    if (c < SMX_N_KINDS) meta->kcnt[c] = carry;
+    else if (c == CNT_REN_A) meta->n_ren_side[0] = carry;
+    else if (c == CNT_REN_B) meta->n_ren_side[1] = carry;
+    else meta->n_move_none = carry;
   }
 }
 
-// ---------------------------------------------------------------------------
-// kernel: one window -> T-ordered arrays
-
-struct WinArgs {
-  const u8* kind;
-  const u32* sym;
-  const i32* v0;
-  const i32* v1;
-  // branch views: presorted -> keys at op index base+j; generic -> sorted copies at j
-  const u64* kts;
-  const u64* khi;
-  const u64* klo;
-  const u32* perm;  // generic only: op index of sorted position (A at [0,na), B at [na,n))
-  i64 na;
-  i64 W;
-  const i64* bnd;
-  const u32* woff;  // [NCNT][W]
-  const ComposeMeta* meta;
-  i32* order;
-  u32* symT;
-  i32* mvA;
-  i32* mvF;
-  u32* Msym;
-  i32* Mcls;
-  i32* Mstr;
-  u8* Mside;
-  u32* Mown;
-  u32* RA;
-  u32* RB;
-};
-
-template <bool PRESORTED>
-__global__ void __launch_bounds__(BLOCK) k_window(WinArgs P) {
-  __shared__ u64 sts[WIN_CAP];
-  __shared__ u64 shi[WIN_CAP];
-  __shared__ u64 slo[WIN_CAP];
-  __shared__ u32 ssrc[WIN_CAP];
-  __shared__ u16 sord[WIN_CAP];
-  __shared__ u16 fin[WIN_CAP];
-  __shared__ u16 rown[WIN_CAP];
-  __shared__ u8 skind[WIN_CAP];
-  __shared__ u8 srank[WIN_CAP];
-  __shared__ u16 ccnt[WIN_CAP / WAVE][SMX_N_KINDS];
-  __shared__ u16 rc[WIN_CAP / WAVE][2];
-  __shared__ u32 kbase[SMX_N_KINDS + 1];
-  __shared__ u32 wck[SMX_N_KINDS];
-
-  const int t = threadIdx.x;
-  const int lane = t & (WAVE - 1);
-  const int wv = t / WAVE;
-  const i64 w = blockIdx.x;
-  const i64 a0 = P.bnd[2 * w], b0 = P.bnd[2 * w + 1];
-  const int na = (int)(P.bnd[2 * w + 2] - a0);
-  const int nb = (int)(P.bnd[2 * w + 3] - b0);
-  const int sz = na + nb;
-  if (sz == 0) return;
-
-  // 1. stage keys, kinds and op indices of both branch parts
-  for (int e = t; e < sz; e += BLOCK) {
-    const i64 j = e < na ? a0 + e : P.na + b0 + (e - na);  // position in the branch layout
-    u32 src;
-    u64 tv, hv, lv;
-    if (PRESORTED) {
-      src = (u32)j;
-      tv = P.kts[j]; hv = P.khi[j]; lv = P.klo[j];
-    } else {
-      src = P.perm[j];
-      tv = P.kts[j]; hv = P.khi[j]; lv = P.klo[j];
-    }
-    sts[e] = tv; shi[e] = hv; slo[e] = lv;
-    ssrc[e] = src;
-    skind[e] = P.kind[src];
+// T bases: exclusive prefix of the kind totals.
+__global__ void k_bases(ComposeMeta* meta) {
+  u64 acc = 0;
+  for (int k = 0; k < SMX_N_KINDS; ++k) {
+    meta->base[k] = acc;
+    acc += meta->kcnt[k];
   }
-  for (int i = t; i < (WIN_CAP / WAVE) * SMX_N_KINDS; i += BLOCK) (&ccnt[0][0])[i] = 0;
-  __syncthreads();
-
-  // 2. merge the A part [0,na) and B part [na,sz) -> S order (A first on ties)
-  {
-    const int d0 = t * WIN_ITEMS < sz ? t * WIN_ITEMS : sz;
-    const int d1 = d0 + WIN_ITEMS < sz ? d0 + WIN_ITEMS : sz;
-    int lo = d0 - nb > 0 ? d0 - nb : 0, hi = d0 < na ? d0 : na;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      const int j = na + d0 - 1 - mid;
-      const bool af = PRESORTED ? (sts[mid] <= sts[j])
-                                : key_le(sts[mid], shi[mid], slo[mid], sts[j], shi[j], slo[j]);
-      if (af) lo = mid + 1; else hi = mid;
-    }
-    int ia = lo, ib = d0 - lo;
-    for (int d = d0; d < d1; ++d) {
-      bool take_a;
-      if (ia >= na) take_a = false;
-      else if (ib >= nb) take_a = true;
-      else {
-        const int j = na + ib;
-        take_a = PRESORTED ? (sts[ia] <= sts[j])
-                           : key_le(sts[ia], shi[ia], slo[ia], sts[j], shi[j], slo[j]);
-      }
-      sord[d] = (u16)(take_a ? ia++ : na + ib++);
-    }
-  }
-  __syncthreads();
-
-  // 3. stable multisplit of S by kind (wave ballots), window-local slots
-  const int nch = (sz + WAVE - 1) / WAVE;
-  for (int c = wv; c < nch; c += NWAVES) {
-    const int m = c * WAVE + lane;
-    const bool valid = m < sz;
-    const int e = valid ? sord[m] : 0;
-    const u32 k = valid ? skind[e] : 0u;
-    const u64 peers = wave_peers<5>(k, valid);
-    const u32 r = __popcll(peers & lanemask_lt());
-    if (valid) {
-      srank[m] = (u8)r;
-      if (r == 0) ccnt[c][k] = (u16)__popcll(peers);
-    }
-  }
-  __syncthreads();
-  if (t < SMX_N_KINDS) {
-    u32 acc = 0;
-    for (int c = 0; c < nch; ++c) {
-      const u32 x = ccnt[c][t];
-      ccnt[c][t] = (u16)acc;
-      acc += x;
-    }
-    wck[t] = acc;
-  }
-  __syncthreads();
-  if (t == 0) {
-    u32 acc = 0;
-    for (int k = 0; k < SMX_N_KINDS; ++k) {
-      kbase[k] = acc;
-      acc += wck[k];
-    }
-    kbase[SMX_N_KINDS] = acc;
-  }
-  __syncthreads();
-  for (int m = t; m < sz; m += BLOCK) {
-    const int e = sord[m];
-    const u32 k = skind[e];
-    fin[kbase[k] + ccnt[m / WAVE][k] + srank[m]] = (u16)e;
-  }
-  __syncthreads();
-
-  // 4. presorted path: equal-(kind, ts) groups are contiguous; order them by
-  //    (oid, side, index) = (oid, slot) with a counting rank
-  const u16* fo = fin;
-  if (PRESORTED) {
-    for (int p = t; p < sz; p += BLOCK) {
-      const int e = fin[p];
-      const u32 k = skind[e];
-      const int kb = kbase[k], ke = kb + wck[k];
-      const u64 t0 = sts[e];
-      int gs = p;
-      while (gs > kb && sts[fin[gs - 1]] == t0) --gs;
-      int ge = p + 1;
-      while (ge < ke && sts[fin[ge]] == t0) ++ge;
-      int r = p;
-      if (ge - gs > 1) {
-        const u64 h = shi[e], l = slo[e];
-        r = gs;
-        for (int q = gs; q < ge; ++q) {
-          const int f = fin[q];
-          const u64 hq = shi[f], lq = slo[f];
-          r += (hq < h) || (hq == h && (lq < l || (lq == l && q < p)));
-        }
-      }
-      sord[r] = (u16)e;
-    }
-    __syncthreads();
-    fo = sord;
-  }
-
-  // 5. renames: rank among same-branch renames of this window (final order)
-  const int R0 = kbase[KREN], RN = wck[KREN];
-  const int nrc = (RN + WAVE - 1) / WAVE;
-  for (int c = wv; c < nrc; c += NWAVES) {
-    const int x = c * WAVE + lane;
-    const bool valid = x < RN;
-    const int e = valid ? fo[R0 + x] : 0;
-    const bool sb = valid && e >= na;
-    const u64 bm = __ballot(sb), vm = __ballot(valid);
-    const u64 lt = lanemask_lt();
-    if (valid) rown[x] = (u16)(sb ? __popcll(bm & lt) : __popcll(vm & ~bm & lt));
-    if (lane == 0) {
-      rc[c][0] = (u16)__popcll(vm & ~bm);
-      rc[c][1] = (u16)__popcll(bm);
-    }
-  }
-  __syncthreads();
-  if (t < 2) {
-    u32 acc = 0;
-    for (int c = 0; c < nrc; ++c) {
-      const u32 x = rc[c][t];
-      rc[c][t] = (u16)acc;
-      acc += x;
-    }
-  }
-  __syncthreads();
-
-  // 6. write T-ordered outputs (coalesced along the final order)
-  const u64* base = P.meta->base;
-  for (int x = t; x < sz; x += BLOCK) {
-    const int e = fo[x];
-    const u32 k = skind[e];
-    const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (u32)(x - kbase[k]);
-    const u32 src = ssrc[e];
-    P.order[T] = (i32)src;
-    const u32 s = P.sym[src];
-    P.symT[T] = s;
-    if (k == KMOVE) {
-      P.mvA[T] = P.v0[src];
-      P.mvF[T] = P.v1[src];
-    } else if (k == KREN) {
-      const u64 m = T - base[KREN];
-      const int side = e >= na;
-      const int xr = x - R0;
-      const u32 own = P.woff[(i64)(SMX_N_KINDS + side) * P.W + w] + rc[xr / WAVE][side] + rown[xr];
-      P.Msym[m] = s;
-      P.Mcls[m] = P.v0[src];
-      P.Mstr[m] = P.v1[src];
-      P.Mside[m] = (u8)side;
-      P.Mown[m] = own;
-      (side ? P.RB : P.RA)[own] = (u32)m;
-    }
-  }
+  meta->base[SMX_N_KINDS] = acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -551,133 +305,18 @@ __global__ void k_offset(u32* __restrict__ v, i64 n, u32 off) {
   for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (i64)gridDim.x * BLOCK) v[i] += off;
 }
 
-// ---------------------------------------------------------------------------
-// kernels: DivergentRename walk over the rename block M (T order)
-
-struct WalkArgs {
-  const u32* Msym;
-  const i32* Mcls;
-  const u8* Mside;
-  const u32* Mown;
-  const u32* RA;
-  const u32* RB;
-  u64 nR, nRA, nRB;
-};
-
-// Natural-head test: element m against the other branch's head when no skip
-// has happened yet (d = 0): that head is R_other[m - own(m)].
-__global__ void k_flags(WalkArgs W, u8* __restrict__ flags) {
-  for (u64 m = (u64)blockIdx.x * BLOCK + threadIdx.x; m < W.nR; m += (u64)gridDim.x * BLOCK) {
-    const int s = W.Mside[m];
-    const u64 k = m - W.Mown[m];
-    const u64 no = s ? W.nRA : W.nRB;
-    u8 f = 0;
-    if (k < no) {
-      const u32 u = (s ? W.RA : W.RB)[k];
-      f = (W.Msym[u] == W.Msym[m]) && (W.Mcls[u] != W.Mcls[m]);
-    }
-    flags[m] = f;
-  }
-}
-
-__global__ void k_compact(const u8* __restrict__ flags, const u32* __restrict__ pos, u64 n,
-                          u32* __restrict__ out) {
-  for (u64 m = (u64)blockIdx.x * BLOCK + threadIdx.x; m < n; m += (u64)gridDim.x * BLOCK)
-    if (flags[m]) out[pos[m]] = (u32)m;
-}
-
-// Replays the reference loop restricted to renames from a d = 0 candidate start
-// p: state (ahead branch, d = how many of its next renames were consumed early).
-// Returns the end q (first position after which d is back to 0).
-template <bool WRITE>
-__device__ u32 replay_region(const WalkArgs& W, u32 p, u32* nconf, const i32* order_ren,
-                             i32* pairs, u64 pair_cap, u32 pair_off, u8* skip) {
-  int ahead = -1;
-  u32 d = 0;
-  u32 m = p;
-  u32 nc = 0;
-  do {
-    const int s = W.Mside[m];
-    if (d > 0 && s == ahead) {
-      --d;  // consumed as the other head of an earlier conflict
-    } else {
-      const int o = 1 - s;
-      const u64 k = (u64)(m - W.Mown[m]) + (o == ahead ? d : 0u);
-      const u64 no = s ? W.nRA : W.nRB;
-      if (k < no) {
-        const u32 u = (s ? W.RA : W.RB)[k];
-        if (W.Msym[u] == W.Msym[m] && W.Mcls[u] != W.Mcls[m]) {
-          if (WRITE) {
-            const u64 slot = (u64)pair_off + nc;
-            if (slot < pair_cap) {
-              pairs[2 * slot] = order_ren[s ? u : m];
-              pairs[2 * slot + 1] = order_ren[s ? m : u];
-            }
-            skip[m] = 1;
-            skip[u] = 1;
-          }
-          ++nc;
-          ++d;
-          ahead = o;
-        }
-      }
-    }
-    ++m;
-  } while (d > 0 && m < W.nR);
-  *nconf = nc;
-  return m;
-}
-
-__global__ void k_replay_q(WalkArgs W, const u32* __restrict__ cand, const ComposeMeta* meta,
-                           u32* __restrict__ q, u32* __restrict__ nconf) {
-  const u64 nc = meta->n_cand;
-  for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
-    u32 k;
-    q[c] = replay_region<false>(W, cand[c], &k, nullptr, nullptr, 0, 0, nullptr);
-    nconf[c] = k;
-  }
-}
-
-// Real region starts: the first candidate of each cluster (no earlier candidate's
-// region reaches it) is real; inside a cluster, walk sequentially.
-__global__ void k_cluster(const u32* __restrict__ cand, const u32* __restrict__ q,
-                          const u32* __restrict__ pm, const u32* __restrict__ nconf,
-                          const ComposeMeta* meta, u32* __restrict__ nreal) {
-  const u64 nc = meta->n_cand;
-  for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
-    if (pm[c] > cand[c]) continue;  // not a cluster start
-    u32 last_q = 0;
-    for (u64 j = c; j < nc && (j == c || pm[j] > cand[j]); ++j) {
-      if (cand[j] >= last_q) {
-        nreal[j] = nconf[j];
-        last_q = q[j];
-      } else {
-        nreal[j] = 0;
-      }
-    }
-  }
-}
-
-__global__ void k_replay_write(WalkArgs W, const u32* __restrict__ cand, const u32* __restrict__ nreal,
-                               const u32* __restrict__ coff, const ComposeMeta* meta,
-                               const i32* __restrict__ order_ren, i32* __restrict__ pairs,
-                               u64 pair_cap, u8* __restrict__ skip) {
-  const u64 nc = meta->n_cand;
-  for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
-    if (nreal[c] == 0) continue;
-    u32 k;
-    replay_region<true>(W, cand[c], &k, order_ren, pairs, pair_cap, coff[c], skip);
-  }
-}
+#include "smx_walk.h"
 
 // ---------------------------------------------------------------------------
 // kernels: per-symbol last writers and output
 
+// Invalid syms (flagged by the window kernel, reported through counts) are
+// clamped so that every access stays in bounds.
 __global__ void k_tab_move(const u32* __restrict__ symT, const i32* __restrict__ mvA,
                            const i32* __restrict__ mvF, u64 nMv, u64* __restrict__ tabA,
-                           u64* __restrict__ tabF) {
+                           u64* __restrict__ tabF, u32 smax) {
   for (u64 T = (u64)blockIdx.x * BLOCK + threadIdx.x; T < nMv; T += (u64)gridDim.x * BLOCK) {
-    const u32 s = symT[T];
+    const u32 s = min(symT[T], smax);
     const i32 a = mvA[T], f = mvF[T];
     if (a >= 0) atomicMax((unsigned long long*)&tabA[s], (unsigned long long)(((T + 1) << 32) | (u32)a));
     if (f >= 0) atomicMax((unsigned long long*)&tabF[s], (unsigned long long)(((T + 1) << 32) | (u32)f));
@@ -685,10 +324,10 @@ __global__ void k_tab_move(const u32* __restrict__ symT, const i32* __restrict__
 }
 
 __global__ void k_tab_ren(const u32* __restrict__ Msym, const i32* __restrict__ Mstr,
-                          const u8* __restrict__ skip, u64 nR, u64* __restrict__ tabR) {
+                          const u8* __restrict__ skip, u64 nR, u64* __restrict__ tabR, u32 smax) {
   for (u64 m = (u64)blockIdx.x * BLOCK + threadIdx.x; m < nR; m += (u64)gridDim.x * BLOCK) {
     if (skip[m]) continue;
-    atomicMax((unsigned long long*)&tabR[Msym[m]], (unsigned long long)(((m + 1) << 32) | (u32)Mstr[m]));
+    atomicMax((unsigned long long*)&tabR[min(Msym[m], smax)], (unsigned long long)(((m + 1) << 32) | (u32)Mstr[m]));
   }
 }
 
@@ -735,6 +374,7 @@ struct EmitArgs {
   const int4* fin;
   const ComposeMeta* meta;
   u64 n, nMv, nR;
+  u32 smax;
   i32* out_order;
   i32* out_addr;
   i32* out_file;
@@ -756,13 +396,13 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
       const u64 m = T - E.nMv;
       if (E.skip[m]) continue;
       o = T - E.skipex[m];
-      const int4 F = E.fin[E.symT[T]];
+      const int4 F = E.fin[min(E.symT[T], E.smax)];
       a = F.x;
       f = F.y;
       c = -1;
     } else {
       o = T - nskip;
-      const int4 F = E.fin[E.symT[T]];
+      const int4 F = E.fin[min(E.symT[T], E.smax)];
       a = F.x;
       f = F.y;
       c = F.z;
@@ -775,6 +415,11 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
 }
 
 __global__ void k_counts(const ComposeMeta* meta, u64 n, i64* counts) {
+  if (meta->bad_sym) {  // invalid input (sym >= n_sym or kind >= 18)
+    counts[0] = -1;
+    counts[1] = -1;
+    return;
+  }
   counts[0] = (i64)(n - 2 * meta->n_conf);
   counts[1] = (i64)meta->n_conf;
 }
@@ -879,27 +524,23 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
   }
   StageTimer tm(st, prof != 0);
 
-  // ---- plan: stats + presorted partition + counts (one host sync) ----
+  // ---- plan: presorted windows + per-window counts/checks (one host sync) ----
   tm.begin(ST_PLAN);
   HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
-  hipLaunchKernelGGL(k_meta_init, dim3(1), dim3(1), 0, st, meta);
-  hipLaunchKernelGGL(k_stats, dim3(grid_for(n, BLOCK * 16)), dim3(BLOCK), 0, st, ops->kind, ops->ts,
-                     ops->oid_hi, ops->oid_lo, ops->sym, ops->v0, ops->v1, na, n, n_sym, meta);
   const i64 Wf = SMX_CEIL_DIV(n, (i64)WIN_TGT);
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(Wf + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, ops->ts, na, nb,
                      Wf, bnd);
-  hipLaunchKernelGGL(k_wcount, dim3(Wf), dim3(BLOCK), 0, st, ops->kind, (const u32*)nullptr, bnd, na, Wf,
-                     wcnt, meta, 1);
+  hipLaunchKernelGGL(k_wcount, dim3(Wf), dim3(BLOCK), 0, st, ops->kind, ops->ts, ops->v0, ops->v1,
+                     (const u32*)nullptr, bnd, na, Wf, wcnt, meta);
   hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, Wf, meta);
+  hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
   HIP_TRY(hipGetLastError());
   ComposeMeta hm;
   HIP_TRY(hipMemcpyAsync(&hm, meta, sizeof(ComposeMeta), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   tm.end(ST_PLAN);
-  if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
-  const bool presorted = !hm.nonmono[0] && !hm.nonmono[1] && !hm.f_fail;
-  const u64 nMv = hm.kcnt[KMOVE], nR = hm.kcnt[KREN];
-  const u64 nRA = hm.n_ren_side[0], nRB = hm.n_ren_side[1];
+  if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: kind[i] >= 18");
+  const bool presorted = !hm.f_fail;
 
   WinArgs P;
   P.kind = ops->kind;
@@ -907,6 +548,7 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
   P.v0 = ops->v0;
   P.v1 = ops->v1;
   P.na = na;
+  P.n_sym = n_sym;
   P.bnd = bnd;
   P.woff = woff;
   P.meta = meta;
@@ -919,8 +561,6 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
   P.Mstr = WS(i32, B_MSTR);
   P.Mside = WS(u8, B_MSIDE);
   P.Mown = WS(u32, B_MOWN);
-  P.RA = WS(u32, B_RAB);
-  P.RB = WS(u32, B_RAB) + nRA;
   i64 W;
   if (presorted) {
     W = Wf;
@@ -931,6 +571,12 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
   } else {
     // ---- generic: stable radix sort of each branch by (ts, oid_hi, oid_lo) ----
     tm.begin(ST_GSORT);
+    HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
+    hipLaunchKernelGGL(k_meta_init, dim3(1), dim3(1), 0, st, meta);
+    hipLaunchKernelGGL(k_keymask, dim3(grid_for(n, BLOCK * 8)), dim3(BLOCK), 0, st, ops->ts, ops->oid_hi,
+                       ops->oid_lo, na, n, meta);
+    HIP_TRY(hipMemcpyAsync(&hm, meta, sizeof(ComposeMeta), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     u64* sts = WS(u64, B_STS);
     u64* shi = WS(u64, B_SHI);
     u64* slo = WS(u64, B_SLO);
@@ -948,14 +594,13 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
         int shifts[8], ns = 0;
         for (int dgt = 0; dgt < 8; ++dgt)
           if ((varying >> (8 * dgt)) & 0xffull) shifts[ns++] = 8 * dgt;
-        if (wi == 0)
+        if (wi == 0) {
           hipLaunchKernelGGL(k_gather_init, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi] + off, key,
                              val, cnt);
-        else
+          if (off)  // values are op indices of A||B
+            hipLaunchKernelGGL(k_offset, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, val, cnt, (u32)off);
+        } else {
           hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi], val, key, cnt);
-        if (wi == 0 && off) {
-          // values are op indices of A||B
-          hipLaunchKernelGGL(k_offset, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, val, cnt, (u32)off);
         }
         if (ns) HIP_TRY(radix_sort_pairs(key, val, cnt, shifts, ns, rt, st));
       }
@@ -966,9 +611,13 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
     W = SMX_CEIL_DIV(n, (i64)WIN_CAP);
     hipLaunchKernelGGL(k_gpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, sts, shi, slo, na,
                        nb, W, bnd);
-    hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, ops->kind, perm, bnd, na, W, wcnt, meta, 0);
+    hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, ops->kind, ops->ts, ops->v0, ops->v1, perm, bnd,
+                       na, W, wcnt, meta);
     hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, W, meta);
+    hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&hm, meta, sizeof(ComposeMeta), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     P.kts = sts;
     P.khi = shi;
     P.klo = slo;
@@ -976,13 +625,17 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
     tm.end(ST_GSORT);
   }
   P.W = W;
+  const u64 nMv = hm.kcnt[KMOVE], nR = hm.kcnt[KREN];
+  const u64 nRA = hm.n_ren_side[0], nRB = hm.n_ren_side[1];
+  P.RA = WS(u32, B_RAB);
+  P.RB = WS(u32, B_RAB) + nRA;
 
   // ---- windows -> T-ordered arrays ----
   tm.begin(ST_WINDOW);
   if (presorted)
-    hipLaunchKernelGGL(k_window<true>, dim3(W), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL(k_window_f, dim3(W), dim3(WF_NT), 0, st, P);
   else
-    hipLaunchKernelGGL(k_window<false>, dim3(W), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL(k_window_g, dim3(W), dim3(WG_NT), 0, st, P);
   HIP_TRY(hipGetLastError());
   tm.end(ST_WINDOW);
 
@@ -1033,9 +686,9 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
   HIP_TRY(hipMemsetAsync(tabR, 0, (size_t)n_sym * 8, st));
   if (nMv > 0)
     hipLaunchKernelGGL(k_tab_move, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, P.symT, P.mvA, P.mvF, nMv, tabA,
-                       tabF);
+                       tabF, (u32)(n_sym - 1));
   if (nR > 0)
-    hipLaunchKernelGGL(k_tab_ren, dim3(grid_for(nR)), dim3(BLOCK), 0, st, P.Msym, P.Mstr, skip, nR, tabR);
+    hipLaunchKernelGGL(k_tab_ren, dim3(grid_for(nR)), dim3(BLOCK), 0, st, P.Msym, P.Mstr, skip, nR, tabR, (u32)(n_sym - 1));
   hipLaunchKernelGGL(k_finalize, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, tabA, tabF, tabR, n_sym, fin);
   HIP_TRY(hipGetLastError());
   tm.end(ST_TABLES);
@@ -1065,7 +718,7 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
 
   // ---- compacted output ----
   tm.begin(ST_EMIT);
-  EmitArgs E{P.order, P.symT, prefA, prefF, skip, skipex, fin, meta, (u64)n, nMv, nR,
+  EmitArgs E{P.order, P.symT, prefA, prefF, skip, skipex, fin, meta, (u64)n, nMv, nR, (u32)(n_sym - 1),
              out->order, out->addr, out->file, out->ctx};
   hipLaunchKernelGGL(k_emit, dim3(grid_for(n, BLOCK * 4)), dim3(BLOCK), 0, st, E);
   hipLaunchKernelGGL(k_counts, dim3(1), dim3(1), 0, st, meta, (u64)n, out->counts);
@@ -1094,6 +747,7 @@ extern "C" int smx_set_profiling(int enabled) {
 
 extern "C" int smx_reset_stage_times(void) {
   std::lock_guard<std::mutex> g(g_prof_mu);
+  resolve_pending_locked();
   for (int i = 0; i < ST_N; ++i) {
     g_stage_ms[i] = 0;
     g_stage_calls[i] = 0;
@@ -1103,6 +757,7 @@ extern "C" int smx_reset_stage_times(void) {
 
 extern "C" int smx_stage_times(double* ms, int64_t* calls, int cap) {
   std::lock_guard<std::mutex> g(g_prof_mu);
+  resolve_pending_locked();
   for (int i = 0; i < ST_N && i < cap; ++i) {
     if (ms) ms[i] = g_stage_ms[i];
     if (calls) calls[i] = g_stage_calls[i];

@@ -1,0 +1,453 @@
+// smx_window.h — per-window T-order construction (the dominant kernel).
+//
+// T = stable order of A||B by (precedence, timestamp, id, side, index)
+// (semmerge/compose.py:16-21 sorted() per branch + the A-first merge of :51-56).
+// A window is a pair of contiguous ranges, one per branch, such that every op of
+// the window precedes, in (timestamp, id, side, index) order, every op of the
+// next window.  Inside one window (all in LDS):
+//   1. merge the A part and the B part by timestamp (A first on ties)   -> S
+//   2. stable multisplit of S by precedence rank (wave64 ballots)       -> slots
+//   3. equal-(rank, timestamp) groups are contiguous slot ranges; order each by
+//      (id, side, index) with a counting rank over the group
+//   4. T position = base[rank] + (ops of that rank in earlier windows) + local
+// The presorted kernel (k_window_f) handles branch logs whose timestamps never
+// decrease (lift.ts emits them in order); k_window_g handles branch logs that the
+// generic path pre-sorted by (timestamp, id), where step 3 is not needed.
+#pragma once
+
+#include "smx_common.h"
+
+#define WIN_CAP 2048               // max ops per window held in LDS
+#define WIN_TGT 1024               // target window size, presorted path
+#define NCNT (SMX_N_KINDS + 3)     // kinds, renames per branch, moves with a None value
+#define CNT_REN_A SMX_N_KINDS
+#define CNT_REN_B (SMX_N_KINDS + 1)
+#define CNT_NONE_MV (SMX_N_KINDS + 2)
+#define KMOVE SMX_KIND_MOVE
+#define KREN SMX_KIND_RENAME
+#define NCHUNK (WIN_CAP / WAVE)
+
+struct WinArgs {
+  const u8* kind;
+  const u32* sym;
+  const i32* v0;
+  const i32* v1;
+  // branch view: presorted -> keys at op index j; generic -> sorted copies at j
+  const u64* kts;
+  const u64* khi;
+  const u64* klo;
+  const u32* perm;  // generic only: op index of sorted position (A at [0,na), B at [na,n))
+  i64 na;
+  i64 W;
+  i64 n_sym;
+  const i64* bnd;
+  const u32* woff;  // [NCNT][W] exclusive offsets over windows
+  ComposeMeta* meta;
+  i32* order;
+  u32* symT;
+  i32* mvA;
+  i32* mvF;
+  u32* Msym;
+  i32* Mcls;
+  i32* Mstr;
+  u8* Mside;
+  u32* Mown;
+  u32* RA;
+  u32* RB;
+};
+
+// Writes one op's T-ordered records (registers -> HBM).
+__device__ __forceinline__ void win_emit(const WinArgs& P, const u64* base, i64 w, u32 k, u32 x,
+                                         u32 kb, u32 src, u32 s, i32 a, i32 f, int side, u32 own) {
+  const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (x - kb);
+  P.order[T] = (i32)src;
+  P.symT[T] = s;
+  if (k == KMOVE) {
+    P.mvA[T] = a;
+    P.mvF[T] = f;
+  } else if (k == KREN) {
+    const u64 m = T - base[KREN];
+    P.Msym[m] = s;
+    P.Mcls[m] = a;
+    P.Mstr[m] = f;
+    P.Mside[m] = (u8)side;
+    P.Mown[m] = own;
+    (side ? P.RB : P.RA)[own] = (u32)m;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// presorted windows (timestamps non-decreasing in each branch log)
+
+#define WF_NT 512
+#define WF_WAVES (WF_NT / WAVE)
+#define WF_ITEMS (WIN_CAP / WF_NT)
+
+__global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
+  __shared__ u64 sts[WIN_CAP];        // element space: timestamp keys
+  __shared__ u64 phi[WIN_CAP];        // slot space: oid_hi
+  __shared__ u16 sord[WIN_CAP];       // S order (merge), later the final order
+  __shared__ u16 fin[WIN_CAP];        // slot -> element
+  __shared__ u16 sl[WIN_CAP];         // element -> slot, later element -> final
+  __shared__ u16 rown[WIN_CAP];       // rename rank within its branch (final order)
+  __shared__ u8 skind[WIN_CAP];
+  __shared__ u8 srank[WIN_CAP];
+  __shared__ u64 gbits[NCHUNK];       // group-start bits over slots
+  __shared__ u16 ccnt[NCHUNK][SMX_N_KINDS];
+  __shared__ u16 rc[NCHUNK][2];
+  __shared__ u32 kbase[SMX_N_KINDS + 1];
+  __shared__ u32 wck[SMX_N_KINDS];
+  __shared__ u64 base[SMX_N_KINDS + 1];
+
+  const int t = threadIdx.x;
+  const int lane = t & (WAVE - 1);
+  const int wv = t / WAVE;
+  const i64 w = blockIdx.x;
+  const i64 a0 = P.bnd[2 * w], b0 = P.bnd[2 * w + 1];
+  const int na = (int)(P.bnd[2 * w + 2] - a0);
+  const int nb = (int)(P.bnd[2 * w + 3] - b0);
+  const int sz = na + nb;
+  if (sz == 0) return;
+  const i64 bpos = P.na + b0 - na;  // op index of B element e is bpos + e
+
+  // 1. load: keys to LDS, payload stays in registers
+  u64 hi_r[WF_ITEMS];
+  u32 sym_r[WF_ITEMS];
+  i32 v0_r[WF_ITEMS], v1_r[WF_ITEMS];
+  u32 k_r[WF_ITEMS];
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i) {
+    const int e = t + WF_NT * i;
+    if (e < sz) {
+      const i64 j = e < na ? a0 + e : bpos + e;
+      const u32 k = P.kind[j];
+      const u64 tv = P.kts[j];
+      hi_r[i] = P.khi[j];
+      sym_r[i] = P.sym[j];
+      v0_r[i] = P.v0[j];
+      v1_r[i] = P.v1[j];
+      bad |= (k >= SMX_N_KINDS) || (sym_r[i] >= (u64)P.n_sym);
+      k_r[i] = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
+      sts[e] = tv;
+      skind[e] = (u8)k_r[i];
+    }
+  }
+  if (bad) P.meta->bad_sym = 1;
+  for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
+  if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
+  __syncthreads();
+
+  // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties
+  {
+    const int d0 = t * WF_ITEMS < sz ? t * WF_ITEMS : sz;
+    const int d1 = d0 + WF_ITEMS < sz ? d0 + WF_ITEMS : sz;
+    int lo = d0 - nb > 0 ? d0 - nb : 0, hi = d0 < na ? d0 : na;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sts[mid] <= sts[na + d0 - 1 - mid]) lo = mid + 1;
+      else hi = mid;
+    }
+    int ia = lo, ib = d0 - lo;
+    for (int d = d0; d < d1; ++d) {
+      const bool take_a = ia < na && (ib >= nb || sts[ia] <= sts[na + ib]);
+      sord[d] = (u16)(take_a ? ia++ : na + ib++);
+    }
+  }
+  __syncthreads();
+
+  // 3. stable multisplit of S by rank
+  const int nch = (sz + WAVE - 1) / WAVE;
+  for (int c = wv; c < nch; c += WF_WAVES) {
+    const int m = c * WAVE + lane;
+    const bool valid = m < sz;
+    const int e = valid ? sord[m] : 0;
+    const u32 k = valid ? skind[e] : 0u;
+    const u64 peers = wave_peers<5>(k, valid);
+    const u32 r = __popcll(peers & lanemask_lt());
+    if (valid) {
+      srank[m] = (u8)r;
+      if (r == 0) ccnt[c][k] = (u16)__popcll(peers);
+    }
+  }
+  __syncthreads();
+  for (int k = wv; k < SMX_N_KINDS; k += WF_WAVES) {
+    const u32 x = lane < nch ? ccnt[lane][k] : 0u;
+    const u32 inc = wave_incl_sum(x);
+    if (lane < nch) ccnt[lane][k] = (u16)(inc - x);
+    if (lane == WAVE - 1) wck[k] = inc;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const u32 x = lane < SMX_N_KINDS ? wck[lane] : 0u;
+    const u32 inc = wave_incl_sum(x);
+    if (lane < SMX_N_KINDS) kbase[lane] = inc - x;
+    if (lane == SMX_N_KINDS - 1) kbase[SMX_N_KINDS] = inc;
+  }
+  __syncthreads();
+  for (int m = t; m < sz; m += WF_NT) {
+    const int e = sord[m];
+    const u32 k = skind[e];
+    const int p = kbase[k] + ccnt[m / WAVE][k] + srank[m];
+    fin[p] = (u16)e;
+    sl[e] = (u16)p;
+  }
+  __syncthreads();
+
+  // 4. slot-space oid_hi and group-start bits: a group = equal (rank, timestamp)
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i) {
+    const int e = t + WF_NT * i;
+    if (e < sz) phi[sl[e]] = hi_r[i];
+  }
+#pragma unroll
+  for (int j = 0; j < WF_ITEMS; ++j) {
+    const int p = t + WF_NT * j;
+    bool f = false;
+    if (p < sz) {
+      const int e = fin[p];
+      f = (p == (int)kbase[skind[e]]) || (sts[fin[p - 1]] != sts[e]);
+    }
+    const u64 b = __ballot(f);
+    if (lane == 0 && (p >> 6) < NCHUNK) gbits[p >> 6] = b;
+  }
+  __syncthreads();
+
+  // 5. order each group by (oid, side, index): counting rank, ties on oid_hi
+  //    resolved on oid_lo (rare), then on slot order (= side, index order)
+#pragma unroll
+  for (int j = 0; j < WF_ITEMS; ++j) {
+    const int p = t + WF_NT * j;
+    if (p >= sz) continue;
+    const int e = fin[p];
+    const int bit = p & 63;
+    int wi = p >> 6;
+    u64 word = gbits[wi] & (bit == 63 ? ~0ull : ((1ull << (bit + 1)) - 1));
+    while (word == 0) word = gbits[--wi];
+    const int gs = wi * 64 + 63 - __clzll(word);
+    wi = p >> 6;
+    word = bit == 63 ? 0ull : (gbits[wi] & ~((1ull << (bit + 1)) - 1));
+    while (word == 0 && ++wi < nch) word = gbits[wi];
+    int ge = word ? wi * 64 + __ffsll((unsigned long long)word) - 1 : sz;
+    ge = ge < sz ? ge : sz;
+    int r = p;
+    if (ge - gs > 1) {
+      const u64 h = phi[p];
+      r = gs;
+      for (int q = gs; q < ge; ++q) {
+        const u64 hq = phi[q];
+        bool lt = hq < h;
+        if (hq == h && q != p) {  // equal oid_hi: compare oid_lo, then slot order
+          const int eq = fin[q];
+          const u64 lq = P.klo[eq < na ? a0 + eq : bpos + eq];
+          const u64 lp = P.klo[e < na ? a0 + e : bpos + e];
+          lt = lq < lp || (lq == lp && q < p);
+        }
+        r += lt;
+      }
+    }
+    sord[r] = (u16)e;
+    sl[e] = (u16)r;
+  }
+  __syncthreads();
+
+  // 6. renames: rank among the window's renames of the same branch (final order)
+  const int R0 = kbase[KREN], RN = wck[KREN];
+  const int nrc = (RN + WAVE - 1) / WAVE;
+  for (int c = wv; c < nrc; c += WF_WAVES) {
+    const int x = c * WAVE + lane;
+    const bool valid = x < RN;
+    const int e = valid ? sord[R0 + x] : 0;
+    const bool sb = valid && e >= na;
+    const u64 bm = __ballot(sb), vm = __ballot(valid);
+    const u64 lt = lanemask_lt();
+    if (valid) rown[x] = (u16)(sb ? __popcll(bm & lt) : __popcll(vm & ~bm & lt));
+    if (lane == 0) {
+      rc[c][0] = (u16)__popcll(vm & ~bm);
+      rc[c][1] = (u16)__popcll(bm);
+    }
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const u32 x0 = lane < nrc ? rc[lane][0] : 0u;
+    const u32 x1 = lane < nrc ? rc[lane][1] : 0u;
+    const u32 i0 = wave_incl_sum(x0), i1 = wave_incl_sum(x1);
+    if (lane < nrc) {
+      rc[lane][0] = (u16)(i0 - x0);
+      rc[lane][1] = (u16)(i1 - x1);
+    }
+  }
+  __syncthreads();
+
+  // 7. write T-ordered records from registers
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i) {
+    const int e = t + WF_NT * i;
+    if (e >= sz) continue;
+    const u32 x = sl[e];
+    const u32 k = k_r[i];
+    const int side = e >= na;
+    u32 own = 0;
+    if (k == KREN) {
+      const int xr = (int)x - R0;
+      own = P.woff[(i64)(CNT_REN_A + side) * P.W + w] + rc[xr / WAVE][side] + rown[xr];
+    }
+    const u32 src = (u32)(e < na ? a0 + e : bpos + e);
+    win_emit(P, base, w, k, x, kbase[k], src, sym_r[i], v0_r[i], v1_r[i], side, own);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// generic windows: branch logs pre-sorted by (timestamp, oid); fixed diagonals
+
+__device__ __forceinline__ bool key_le(u64 ta, u64 ha, u64 la, u64 tb, u64 hb, u64 lb) {
+  if (ta != tb) return ta < tb;
+  if (ha != hb) return ha < hb;
+  return la <= lb;
+}
+
+#define WG_NT 256
+#define WG_ITEMS (WIN_CAP / WG_NT)
+
+__global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
+  __shared__ u64 sts[WIN_CAP];
+  __shared__ u64 shi[WIN_CAP];
+  __shared__ u64 slo[WIN_CAP];
+  __shared__ u32 ssrc[WIN_CAP];
+  __shared__ u16 sord[WIN_CAP];
+  __shared__ u16 fin[WIN_CAP];
+  __shared__ u16 rown[WIN_CAP];
+  __shared__ u8 skind[WIN_CAP];
+  __shared__ u8 srank[WIN_CAP];
+  __shared__ u16 ccnt[NCHUNK][SMX_N_KINDS];
+  __shared__ u16 rc[NCHUNK][2];
+  __shared__ u32 kbase[SMX_N_KINDS + 1];
+  __shared__ u32 wck[SMX_N_KINDS];
+  __shared__ u64 base[SMX_N_KINDS + 1];
+
+  const int t = threadIdx.x;
+  const int lane = t & (WAVE - 1);
+  const int wv = t / WAVE;
+  const i64 w = blockIdx.x;
+  const i64 a0 = P.bnd[2 * w], b0 = P.bnd[2 * w + 1];
+  const int na = (int)(P.bnd[2 * w + 2] - a0);
+  const int nb = (int)(P.bnd[2 * w + 3] - b0);
+  const int sz = na + nb;
+  if (sz == 0) return;
+
+  bool bad = false;
+  for (int e = t; e < sz; e += WG_NT) {
+    const i64 j = e < na ? a0 + e : P.na + b0 + (e - na);
+    const u32 src = P.perm[j];
+    sts[e] = P.kts[j];
+    shi[e] = P.khi[j];
+    slo[e] = P.klo[j];
+    ssrc[e] = src;
+    const u32 k = P.kind[src];
+    bad |= (k >= SMX_N_KINDS) || (P.sym[src] >= (u64)P.n_sym);
+    skind[e] = (u8)(k < SMX_N_KINDS ? k : SMX_N_KINDS - 1);
+  }
+  if (bad) P.meta->bad_sym = 1;
+  for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WG_NT) (&ccnt[0][0])[i] = 0;
+  if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
+  __syncthreads();
+
+  {
+    const int d0 = t * WG_ITEMS < sz ? t * WG_ITEMS : sz;
+    const int d1 = d0 + WG_ITEMS < sz ? d0 + WG_ITEMS : sz;
+    int lo = d0 - nb > 0 ? d0 - nb : 0, hi = d0 < na ? d0 : na;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      const int j = na + d0 - 1 - mid;
+      if (key_le(sts[mid], shi[mid], slo[mid], sts[j], shi[j], slo[j])) lo = mid + 1;
+      else hi = mid;
+    }
+    int ia = lo, ib = d0 - lo;
+    for (int d = d0; d < d1; ++d) {
+      bool take_a;
+      if (ia >= na) take_a = false;
+      else if (ib >= nb) take_a = true;
+      else {
+        const int j = na + ib;
+        take_a = key_le(sts[ia], shi[ia], slo[ia], sts[j], shi[j], slo[j]);
+      }
+      sord[d] = (u16)(take_a ? ia++ : na + ib++);
+    }
+  }
+  __syncthreads();
+
+  const int nch = (sz + WAVE - 1) / WAVE;
+  for (int c = wv; c < nch; c += WG_NT / WAVE) {
+    const int m = c * WAVE + lane;
+    const bool valid = m < sz;
+    const int e = valid ? sord[m] : 0;
+    const u32 k = valid ? skind[e] : 0u;
+    const u64 peers = wave_peers<5>(k, valid);
+    const u32 r = __popcll(peers & lanemask_lt());
+    if (valid) {
+      srank[m] = (u8)r;
+      if (r == 0) ccnt[c][k] = (u16)__popcll(peers);
+    }
+  }
+  __syncthreads();
+  for (int k = wv; k < SMX_N_KINDS; k += WG_NT / WAVE) {
+    const u32 x = lane < nch ? ccnt[lane][k] : 0u;
+    const u32 inc = wave_incl_sum(x);
+    if (lane < nch) ccnt[lane][k] = (u16)(inc - x);
+    if (lane == WAVE - 1) wck[k] = inc;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const u32 x = lane < SMX_N_KINDS ? wck[lane] : 0u;
+    const u32 inc = wave_incl_sum(x);
+    if (lane < SMX_N_KINDS) kbase[lane] = inc - x;
+    if (lane == SMX_N_KINDS - 1) kbase[SMX_N_KINDS] = inc;
+  }
+  __syncthreads();
+  for (int m = t; m < sz; m += WG_NT) {
+    const int e = sord[m];
+    const u32 k = skind[e];
+    fin[kbase[k] + ccnt[m / WAVE][k] + srank[m]] = (u16)e;
+  }
+  __syncthreads();
+
+  const int R0 = kbase[KREN], RN = wck[KREN];
+  const int nrc = (RN + WAVE - 1) / WAVE;
+  for (int c = wv; c < nrc; c += WG_NT / WAVE) {
+    const int x = c * WAVE + lane;
+    const bool valid = x < RN;
+    const int e = valid ? fin[R0 + x] : 0;
+    const bool sb = valid && e >= na;
+    const u64 bm = __ballot(sb), vm = __ballot(valid);
+    const u64 lt = lanemask_lt();
+    if (valid) rown[x] = (u16)(sb ? __popcll(bm & lt) : __popcll(vm & ~bm & lt));
+    if (lane == 0) {
+      rc[c][0] = (u16)__popcll(vm & ~bm);
+      rc[c][1] = (u16)__popcll(bm);
+    }
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const u32 x0 = lane < nrc ? rc[lane][0] : 0u;
+    const u32 x1 = lane < nrc ? rc[lane][1] : 0u;
+    const u32 i0 = wave_incl_sum(x0), i1 = wave_incl_sum(x1);
+    if (lane < nrc) {
+      rc[lane][0] = (u16)(i0 - x0);
+      rc[lane][1] = (u16)(i1 - x1);
+    }
+  }
+  __syncthreads();
+
+  for (int x = t; x < sz; x += WG_NT) {
+    const int e = fin[x];
+    const u32 k = skind[e];
+    const u32 src = ssrc[e];
+    const int side = e >= na;
+    u32 own = 0;
+    if (k == KREN) {
+      const int xr = x - R0;
+      own = P.woff[(i64)(CNT_REN_A + side) * P.W + w] + rc[xr / WAVE][side] + rown[xr];
+    }
+    win_emit(P, base, w, k, (u32)x, kbase[k], src, P.sym[src], P.v0[src], P.v1[src], side, own);
+  }
+}

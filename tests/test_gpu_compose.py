@@ -104,3 +104,15 @@ def test_gpu_repeatable_and_none_moves():
     ref = oracle.compose(soa)
     _eq_soa(first, ref, "none-moves")
     _eq_soa(second, ref, "none-moves rerun")
+
+
+def test_invalid_input_fails_loudly():
+    from semantic_merge_amd._lib import SmxError
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(10_000, 100, 2)))
+    soa.sym[7] = soa.n_sym + 3
+    with pytest.raises(SmxError):
+        compose_soa(soa)
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(10_000, 100, 2)))
+    soa.kind[11] = 40
+    with pytest.raises(SmxError):
+        compose_soa(soa)
