@@ -21,8 +21,8 @@
 //   k_window    per window, in LDS: merge A/B parts, multisplit by kind, sort
 //               equal-timestamp groups by id, write T-ordered arrays
 //   walk        k_flags -> compact -> k_replay_q -> max-scan -> k_cluster ->
-//               scan -> k_replay_write (conflict pairs, skip flags)
-//   tables      per-symbol last writers (packed (T+1)<<32|value atomicMax)
+//               scan -> k_replay_write (conflict pairs, skip flags, sorted skip list)
+//   tables      per-symbol last writers: bucket by symbol range, LDS max-reduce
 //   k_emit      compacted output: order, addr, file, ctx
 #include <mutex>
 #include <string>
@@ -30,6 +30,7 @@
 
 #include "smx_sort.h"
 #include "smx_window.h"
+#include "smx_tables.h"
 
 
 // ---------------------------------------------------------------------------
@@ -142,13 +143,13 @@ __global__ void k_meta_init(ComposeMeta* meta) {
 // Presorted windows: boundary k sits at the merge-path split of diagonal k*WIN_TGT
 // (timestamps, A first on ties), snapped down to the first op of that timestamp on
 // both branches, so every (timestamp) group lands whole in one window.
-__global__ void k_fpart(const u64* __restrict__ ts, i64 na, i64 nb, i64 W, i64* __restrict__ bnd) {
+__global__ void k_fpart(const u64* __restrict__ ts, i64 na, i64 nb, i64 W, i64 tgt, i64* __restrict__ bnd) {
   const i64 k = (i64)blockIdx.x * BLOCK + threadIdx.x;
   if (k > W) return;
   const i64 n = na + nb;
   const u64* A = ts;
   const u64* B = ts + na;
-  const i64 d = k * WIN_TGT;
+  const i64 d = k * tgt;
   if (k == 0) {
     bnd[0] = 0;
     bnd[1] = 0;
@@ -201,42 +202,46 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
   bnd[2 * k + 1] = d - lo;
 }
 
-// Per-window counts: each kind, renames per branch, moves with a None value.
-// perm == nullptr: presorted layout (branch position j is op j); then the kernel
-// also checks what the presorted windows rely on: boundaries non-decreasing,
-// window size <= WIN_CAP, timestamps non-decreasing inside each branch (every
-// adjacent pair is checked by exactly one window).  Column-major [c][W].
-__global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, const u64* __restrict__ ts,
-                                                  const i32* __restrict__ v0, const i32* __restrict__ v1,
-                                                  const u32* __restrict__ perm, const i64* __restrict__ bnd,
-                                                  i64 na, i64 W, u32* __restrict__ wcnt, ComposeMeta* meta) {
+// Per-window counts: each kind and renames per branch (+ moves with a None value
+// in the generic layout).  perm == nullptr: presorted layout (branch position j is
+// op j; reads only kind bytes -- the layout itself is verified by k_window_f).
+// Column-major [c][W].
+__global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, const i32* __restrict__ v0,
+                                                  const i32* __restrict__ v1, const u32* __restrict__ perm,
+                                                  const i64* __restrict__ bnd, i64 na, i64 W,
+                                                  u32* __restrict__ wcnt, ComposeMeta* meta) {
   __shared__ u32 c[NCNT];
-  __shared__ u32 fail;
   const i64 w = blockIdx.x;
   if (threadIdx.x < NCNT) c[threadIdx.x] = 0;
-  if (threadIdx.x == 0) fail = 0;
   __syncthreads();
   const i64 a0 = bnd[2 * w], b0 = bnd[2 * w + 1], a1 = bnd[2 * w + 2], b1 = bnd[2 * w + 3];
   const bool presorted = perm == nullptr;
-  if (presorted && threadIdx.x == 0 && (a1 < a0 || b1 < b0 || (a1 - a0) + (b1 - b0) > WIN_CAP)) fail = 1;
-  bool bad = false, mono_fail = false;
+  bool bad = false;
+  const u64 lt = lanemask_lt();
   for (int side = 0; side < 2; ++side) {
     const i64 lo = side ? b0 : a0, hi = side ? b1 : a1, off = side ? na : 0;
-    for (i64 j = lo + threadIdx.x; j < hi; j += BLOCK) {
-      const u32 src = presorted ? (u32)(off + j) : perm[off + j];
-      const u32 k0 = kind[src];
-      bad |= k0 >= SMX_N_KINDS;
-      const u32 k = k0 < SMX_N_KINDS ? k0 : SMX_N_KINDS - 1;
-      atomicAdd(&c[k], 1u);
-      if (k == KREN) atomicAdd(&c[CNT_REN_A + side], 1u);
-      if (k == KMOVE && (v0[src] < 0 || v1[src] < 0)) atomicAdd(&c[CNT_NONE_MV], 1u);
-      if (presorted && j > 0 && ts[src - 1] > ts[src]) mono_fail = true;
+    // wave-uniform trip count so the ballots below see every lane
+    for (i64 j0 = lo; j0 < hi; j0 += BLOCK) {
+      const i64 j = j0 + threadIdx.x;
+      const bool valid = j < hi;
+      u32 k = 0;
+      bool none_mv = false;
+      if (valid) {
+        const u32 src = presorted ? (u32)(off + j) : perm[off + j];
+        const u32 k0 = kind[src];
+        bad |= k0 >= SMX_N_KINDS;
+        k = k0 < SMX_N_KINDS ? k0 : SMX_N_KINDS - 1;
+        if (!presorted) none_mv = k == KMOVE && (v0[src] < 0 || v1[src] < 0);
+      }
+      const u64 peers = wave_peers<5>(k, valid);
+      if (valid && (peers & lt) == 0) atomicAdd(&c[k], (u32)__popcll(peers));
+      const u64 nm = __ballot(none_mv);
+      if (nm && (threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&c[CNT_NONE_MV], (u32)__popcll(nm));
+      if (valid && k == KREN && (peers & lt) == 0) atomicAdd(&c[CNT_REN_A + side], (u32)__popcll(peers));
     }
   }
-  if (mono_fail) fail = 1;
   if (bad) meta->bad_sym = 1;
   __syncthreads();
-  if (threadIdx.x == 0 && fail) meta->f_fail = 1;
   if (threadIdx.x < NCNT) wcnt[(i64)threadIdx.x * W + w] = c[threadIdx.x];
 }
 
@@ -310,34 +315,8 @@ __global__ void k_offset(u32* __restrict__ v, i64 n, u32 off) {
 // ---------------------------------------------------------------------------
 // kernels: per-symbol last writers and output
 
-// Invalid syms (flagged by the window kernel, reported through counts) are
-// clamped so that every access stays in bounds.
-__global__ void k_tab_move(const u32* __restrict__ symT, const i32* __restrict__ mvA,
-                           const i32* __restrict__ mvF, u64 nMv, u64* __restrict__ tabA,
-                           u64* __restrict__ tabF, u32 smax) {
-  for (u64 T = (u64)blockIdx.x * BLOCK + threadIdx.x; T < nMv; T += (u64)gridDim.x * BLOCK) {
-    const u32 s = min(symT[T], smax);
-    const i32 a = mvA[T], f = mvF[T];
-    if (a >= 0) atomicMax((unsigned long long*)&tabA[s], (unsigned long long)(((T + 1) << 32) | (u32)a));
-    if (f >= 0) atomicMax((unsigned long long*)&tabF[s], (unsigned long long)(((T + 1) << 32) | (u32)f));
-  }
-}
 
-__global__ void k_tab_ren(const u32* __restrict__ Msym, const i32* __restrict__ Mstr,
-                          const u8* __restrict__ skip, u64 nR, u64* __restrict__ tabR, u32 smax) {
-  for (u64 m = (u64)blockIdx.x * BLOCK + threadIdx.x; m < nR; m += (u64)gridDim.x * BLOCK) {
-    if (skip[m]) continue;
-    atomicMax((unsigned long long*)&tabR[min(Msym[m], smax)], (unsigned long long)(((m + 1) << 32) | (u32)Mstr[m]));
-  }
-}
 
-__global__ void k_finalize(const u64* __restrict__ tabA, const u64* __restrict__ tabF,
-                           const u64* __restrict__ tabR, i64 n_sym, int4* __restrict__ fin) {
-  for (i64 s = (i64)blockIdx.x * BLOCK + threadIdx.x; s < n_sym; s += (i64)gridDim.x * BLOCK) {
-    const u64 a = tabA[s], f = tabF[s], r = tabR[s];
-    fin[s] = make_int4(a ? (i32)(u32)a : -1, f ? (i32)(u32)f : -1, r ? (i32)(u32)r : -1, 0);
-  }
-}
 
 __global__ void k_mv_init(const u32* __restrict__ symT, u64 nMv, u64* __restrict__ keys,
                           u32* __restrict__ vals) {
@@ -347,33 +326,17 @@ __global__ void k_mv_init(const u32* __restrict__ symT, u64 nMv, u64* __restrict
   }
 }
 
-// Moves grouped by symbol (T order inside a group): inclusive last-non-None scan.
-__global__ void k_mv_seg(const u64* __restrict__ keys, const u32* __restrict__ vals, u64 nMv,
-                         const i32* __restrict__ mvA, const i32* __restrict__ mvF,
-                         i32* __restrict__ prefA, i32* __restrict__ prefF) {
-  for (u64 j = (u64)blockIdx.x * BLOCK + threadIdx.x; j < nMv; j += (u64)gridDim.x * BLOCK) {
-    if (j != 0 && keys[j - 1] == keys[j]) continue;
-    i32 ra = -1, rf = -1;
-    for (u64 i = j; i < nMv && keys[i] == keys[j]; ++i) {
-      const u32 T = vals[i];
-      if (mvA[T] >= 0) ra = mvA[T];
-      if (mvF[T] >= 0) rf = mvF[T];
-      prefA[T] = ra;
-      prefF[T] = rf;
-    }
-  }
-}
 
 struct EmitArgs {
   const i32* order;
   const u32* symT;
-  const i32* prefA;
-  const i32* prefF;
+  const i32* mvA;
+  const i32* mvF;
   const u8* skip;
-  const u32* skipex;
+  const u32* skiplist;
   const int4* fin;
   const ComposeMeta* meta;
-  u64 n, nMv, nR;
+  u64 n;
   u32 smax;
   i32* out_order;
   i32* out_addr;
@@ -381,36 +344,101 @@ struct EmitArgs {
   i32* out_ctx;
 };
 
+#define EMIT_WT 1024  // T positions per wave
+#define EMIT_B 8      // wave steps whose loads are issued together
+
+// Each wave owns EMIT_WT consecutive T positions.  Output index = T minus the
+// skipped renames before T: a binary search of the sorted skip list at the
+// wave's first position, then ballots over the skip flags.  Moves emit their
+// own values (the None-value prefix case is patched afterwards); every other
+// op reads its symbol's final states from fin.
 __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
-  const u64 nskip = 2 * E.meta->n_conf;
-  for (u64 T = (u64)blockIdx.x * BLOCK + threadIdx.x; T < E.n; T += (u64)gridDim.x * BLOCK) {
-    const i32 src = E.order[T];
-    i32 a, f, c;
-    u64 o;
-    if (T < E.nMv) {
-      o = T;
-      a = E.prefA[T];
-      f = E.prefF[T];
-      c = -1;
-    } else if (T < E.nMv + E.nR) {
-      const u64 m = T - E.nMv;
-      if (E.skip[m]) continue;
-      o = T - E.skipex[m];
-      const int4 F = E.fin[min(E.symT[T], E.smax)];
-      a = F.x;
-      f = F.y;
-      c = -1;
-    } else {
-      o = T - nskip;
-      const int4 F = E.fin[min(E.symT[T], E.smax)];
-      a = F.x;
-      f = F.y;
-      c = F.z;
+  const ComposeMeta* M = E.meta;
+  if (M->f_fail | M->bad_sym) return;
+  const u64 nskip = 2 * M->n_conf;
+  const u64 rs = min(M->kcnt[KMOVE], E.n);
+  const u64 re = min(rs + M->kcnt[KREN], E.n);
+  const int lane = threadIdx.x & (WAVE - 1);
+  const u64 w0 = (((u64)blockIdx.x * BLOCK + threadIdx.x) / WAVE) * EMIT_WT;
+  if (w0 >= E.n) return;
+  u64 run;
+  if (w0 <= rs) {
+    run = 0;
+  } else if (w0 >= re) {
+    run = nskip;
+  } else {
+    const u64 mt = w0 - rs;
+    u64 lo = 0, hi = nskip;
+    while (lo < hi) {
+      const u64 mid = (lo + hi) >> 1;
+      if (E.skiplist[mid] < mt) lo = mid + 1;
+      else hi = mid;
     }
-    E.out_order[o] = src;
-    E.out_addr[o] = a;
-    E.out_file[o] = f;
-    E.out_ctx[o] = c;
+    run = lo;
+  }
+  const u64 lt = lanemask_lt();
+  for (int bt = 0; bt < EMIT_WT / (WAVE * EMIT_B); ++bt) {
+    const u64 t0 = w0 + (u64)bt * WAVE * EMIT_B;
+    if (t0 >= E.n) break;
+    u64 bal[EMIT_B];
+    i32 src[EMIT_B], a[EMIT_B], f[EMIT_B], c[EMIT_B];
+    u32 sy[EMIT_B];
+#pragma unroll
+    for (int j = 0; j < EMIT_B; ++j) {
+      const u64 T = t0 + (u64)j * WAVE + lane;
+      const bool sk = T < E.n && T >= rs && T < re && E.skip[T - rs];
+      bal[j] = __ballot(sk);
+      src[j] = T < E.n ? E.order[T] : 0;
+      if (T < rs) {
+        a[j] = E.mvA[T];
+        f[j] = E.mvF[T];
+        c[j] = -1;
+      } else {
+        sy[j] = T < E.n ? min(E.symT[T], E.smax) : 0u;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < EMIT_B; ++j) {
+      const u64 T = t0 + (u64)j * WAVE + lane;
+      if (T >= rs && T < E.n) {
+        const int4 F = E.fin[sy[j]];
+        a[j] = F.x;
+        f[j] = F.y;
+        c[j] = T < re ? -1 : F.z;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < EMIT_B; ++j) {
+      const u64 T = t0 + (u64)j * WAVE + lane;
+      const bool sk = (bal[j] >> lane) & 1;
+      if (T < E.n && !sk) {
+        const u64 o = T - run - __popcll(bal[j] & lt);
+        E.out_order[o] = src[j];
+        E.out_addr[o] = a[j];
+        E.out_file[o] = f[j];
+        E.out_ctx[o] = c[j];
+      }
+      run += __popcll(bal[j]);
+    }
+  }
+}
+
+// Moves whose newAddress or newFile is None see the symbol's inclusive prefix
+// (compose.py:73-82 + 37-41): moves grouped by symbol in T order, last-non-None
+// scan; the composed output index of move T is T (no skips precede the renames).
+__global__ void k_mv_fix(const u64* __restrict__ keys, const u32* __restrict__ vals, u64 nMv,
+                         const i32* __restrict__ mvA, const i32* __restrict__ mvF,
+                         i32* __restrict__ out_addr, i32* __restrict__ out_file) {
+  for (u64 j = (u64)blockIdx.x * BLOCK + threadIdx.x; j < nMv; j += (u64)gridDim.x * BLOCK) {
+    if (j != 0 && keys[j - 1] == keys[j]) continue;
+    i32 ra = -1, rf = -1;
+    for (u64 i = j; i < nMv && keys[i] == keys[j]; ++i) {
+      const u32 T = vals[i];
+      if (mvA[T] >= 0) ra = mvA[T];
+      if (mvF[T] >= 0) rf = mvF[T];
+      out_addr[T] = ra;
+      out_file[T] = rf;
+    }
   }
 }
 
@@ -436,13 +464,13 @@ enum Buf {
   B_META, B_BND, B_WCNT, B_WOFF, B_STS, B_SHI, B_SLO, B_PERM, B_RKEY, B_RVAL, B_RK2, B_RV2,
   B_RHIST, B_PART, B_ORDER, B_SYMT, B_MVA, B_MVF, B_MSYM, B_MCLS, B_MSTR, B_MSIDE, B_MOWN,
   B_RAB, B_FLAGS, B_FPOS, B_CAND, B_Q, B_PM, B_NCONF, B_NREAL, B_COFF, B_SKIP, B_SKIPEX,
-  B_TABA, B_TABF, B_TABR, B_FIN, B_PREFA, B_PREFF, B_N
+  B_TABA, B_TABF, B_TABR, B_FIN, B_PREFA, B_PREFF, B_REC, B_TBHIST, B_TBTOT, B_N
 };
 
 static Layout layout(i64 na, i64 nb, i64 n_sym) {
   const i64 n = na + nb;
   const i64 nn = n > 0 ? n : 1;
-  const i64 W = SMX_CEIL_DIV(nn, (i64)WIN_TGT) + 2;
+  const i64 W = SMX_CEIL_DIV(nn, (i64)WIN_TGT_MIN) + 2;
   const i64 nblk = SMX_CEIL_DIV(nn, (i64)RADIX_TILE);
   size_t sz[B_N];
   sz[B_META] = sizeof(ComposeMeta);
@@ -468,6 +496,9 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_TABA] = sz[B_TABF] = sz[B_TABR] = (size_t)ns * 8;
   sz[B_FIN] = (size_t)ns * 16;
   sz[B_PREFA] = sz[B_PREFF] = (size_t)nn * 4;
+  sz[B_REC] = (size_t)nn * 16;
+  sz[B_TBHIST] = (size_t)TB_MAXBK * SMX_CEIL_DIV(nn, (i64)TB_TILE) * 4;
+  sz[B_TBTOT] = 16;
   Layout L;
   size_t acc = 0;
   for (int i = 0; i < B_N; ++i) {
@@ -493,6 +524,250 @@ extern "C" int smx_compose_workspace_bytes(int64_t n_a, int64_t n_b, int64_t n_s
   return SMX_OK;
 }
 
+struct Ctx {
+  const smx_ops* ops;
+  const smx_compose_out* out;
+  hipStream_t st;
+  Layout L;
+  char* base;
+  i64 na, nb, n, n_sym;
+  StageTimer* tm;
+  template <typename T>
+  T* ws(int b) const { return (T*)(base + L.off[b]); }
+};
+
+static WinArgs win_args(const Ctx& C) {
+  WinArgs P;
+  P.kind = C.ops->kind;
+  P.sym = C.ops->sym;
+  P.v0 = C.ops->v0;
+  P.v1 = C.ops->v1;
+  P.na = C.na;
+  P.nb = C.nb;
+  P.n_sym = C.n_sym;
+  P.bnd = C.ws<i64>(B_BND);
+  P.woff = C.ws<u32>(B_WOFF);
+  P.meta = C.ws<ComposeMeta>(B_META);
+  P.order = C.ws<i32>(B_ORDER);
+  P.symT = C.ws<u32>(B_SYMT);
+  P.mvA = C.ws<i32>(B_MVA);
+  P.mvF = C.ws<i32>(B_MVF);
+  P.Msym = C.ws<u32>(B_MSYM);
+  P.Mcls = C.ws<i32>(B_MCLS);
+  P.Mstr = C.ws<i32>(B_MSTR);
+  P.Mside = C.ws<u8>(B_MSIDE);
+  P.Mown = C.ws<u32>(B_MOWN);
+  P.RA = C.ws<u32>(B_RAB);
+  P.RB = C.ws<u32>(B_RAB) + C.na;  // A has at most n_a renames
+  return P;
+}
+
+// Walk, tables, emit, counts: every size is read on the device from meta, so the
+// whole tail is enqueued without a host sync.
+static int launch_tail(const Ctx& C, const WinArgs& P) {
+  hipStream_t st = C.st;
+  ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
+  const i64 n = C.n;
+  u8* skip = C.ws<u8>(B_SKIP);
+  u32* skiplist = C.ws<u32>(B_SKIPEX);  // sorted skipped rename positions (2 per conflict)
+  u32* part = C.ws<u32>(B_PART);
+
+  C.tm->begin(ST_WALK);
+  HIP_TRY(hipMemsetAsync(skip, 0, n, st));
+  {
+    WalkArgs Wk{P.Msym, P.Mcls, P.Mside, P.Mown, P.RA, P.RB, meta, (u64)C.na, (u64)C.nb, 0, 0, 0, 0};
+    u8* flags = C.ws<u8>(B_FLAGS);
+    u32* bcnt = C.ws<u32>(B_FPOS);
+    u32* cand = C.ws<u32>(B_CAND);
+    u32* q = C.ws<u32>(B_Q);
+    u32* pm = C.ws<u32>(B_PM);
+    u32* nconf = C.ws<u32>(B_NCONF);
+    u32* nreal = C.ws<u32>(B_NREAL);
+    u32* coff = C.ws<u32>(B_COFF);
+    // n_conf is u64 in meta; the scan writes its u32 total into the low word
+    // (little endian) of the zeroed field.
+    u32* nconf32 = (u32*)&meta->n_conf;
+    const u64* ncand_dev = &meta->n_cand;
+    const u32 nfb = (u32)SMX_CEIL_DIV((u64)n, (u64)FLAG_TILE);  // upper bound; idle blocks exit
+    const int gsmall = 256;  // grid for loops over the (few) candidates
+    hipLaunchKernelGGL(k_flags, dim3(nfb), dim3(BLOCK), 0, st, Wk, flags, bcnt);
+    hipLaunchKernelGGL(k_flag_offsets, dim3(1), dim3(BLOCK), 0, st, Wk, bcnt, meta);
+    hipLaunchKernelGGL(k_compact, dim3(nfb), dim3(BLOCK), 0, st, Wk, flags, bcnt, cand);
+    hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
+    HIP_TRY((scan_excl<OpMax, u32, u32>(q, pm, 0, ncand_dev, part, (u32*)nullptr, st)));
+    hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, cand, q, pm, nconf, meta, nreal);
+    HIP_TRY((scan_excl<OpSum, u32, u32>(nreal, coff, 0, ncand_dev, part, nconf32, st)));
+    hipLaunchKernelGGL(k_replay_write, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, nreal, coff, meta,
+                       P.order, C.out->conflicts, (u64)C.out->conflict_cap, skip, skiplist);
+    HIP_TRY(hipGetLastError());
+  }
+  C.tm->end(ST_WALK);
+
+  C.tm->begin(ST_TABLES);
+  int4* fin = C.ws<int4>(B_FIN);
+  {
+    const i64 n_sym = C.n_sym;
+    TbArgs A{P.symT, P.mvA, P.mvF, P.Msym, P.Mstr, skip, meta, (u64)n, 1u, 1u, (u32)(n_sym - 1), 0, 0};
+    u64 width = SMX_CEIL_DIV((u64)n_sym, (u64)256);
+    if (width < 1) width = 1;
+    if (width > TB_WIDTH) width = TB_WIDTH;
+    const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);
+    if (nbk <= TB_MAXBK) {
+      A.width = (u32)width;
+      A.nbk = (u32)nbk;
+      const int nblk = (int)SMX_CEIL_DIV((u64)n, (u64)TB_TILE);
+      u32* hist = C.ws<u32>(B_TBHIST);
+      u32* total = C.ws<u32>(B_TBTOT);
+      uint4* rec = C.ws<uint4>(B_REC);
+      hipLaunchKernelGGL(k_tb_hist, dim3(nblk), dim3(BLOCK), 0, st, A, hist, nblk);
+      HIP_TRY((scan_excl<OpSum, u32, u32>(hist, hist, (i64)nbk * nblk, nullptr, part, total, st)));
+      hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(BLOCK), 0, st, A, hist, nblk, rec);
+      hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, hist, nblk, total, rec, n_sym, fin);
+    } else {
+      // very large symbol spaces: device-scope atomics on the packed keys
+      u64* tabA = C.ws<u64>(B_TABA);
+      u64* tabF = C.ws<u64>(B_TABF);
+      u64* tabR = C.ws<u64>(B_TABR);
+      HIP_TRY(hipMemsetAsync(tabA, 0, (size_t)n_sym * 8, st));
+      HIP_TRY(hipMemsetAsync(tabF, 0, (size_t)n_sym * 8, st));
+      HIP_TRY(hipMemsetAsync(tabR, 0, (size_t)n_sym * 8, st));
+      hipLaunchKernelGGL(k_tab_atomic, dim3(grid_for(n)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR);
+      hipLaunchKernelGGL(k_finalize, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, tabA, tabF, tabR, n_sym, fin);
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  C.tm->end(ST_TABLES);
+
+  C.tm->begin(ST_EMIT);
+  EmitArgs E{P.order, P.symT, P.mvA, P.mvF, skip, skiplist, fin, meta, (u64)n, (u32)(C.n_sym - 1),
+             C.out->order, C.out->addr, C.out->file, C.out->ctx};
+  const i64 ewaves = SMX_CEIL_DIV(n, (i64)EMIT_WT);
+  hipLaunchKernelGGL(k_emit, dim3(SMX_CEIL_DIV(ewaves, (i64)NWAVES)), dim3(BLOCK), 0, st, E);
+  hipLaunchKernelGGL(k_counts, dim3(1), dim3(1), 0, st, meta, (u64)n, C.out->counts);
+  HIP_TRY(hipGetLastError());
+  C.tm->end(ST_EMIT);
+  return SMX_OK;
+}
+
+// Presorted plan: branch logs with non-decreasing timestamps (what lift.ts
+// emits).  Speculative: k_window_f verifies the layout and flags f_fail.
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
+static int run_presorted(const Ctx& C) {
+  hipStream_t st = C.st;
+  ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
+  i64* bnd = C.ws<i64>(B_BND);
+  u32* wcnt = C.ws<u32>(B_WCNT);
+  u32* woff = C.ws<u32>(B_WOFF);
+  C.tm->begin(ST_PLAN);
+  HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
+  i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
+  if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
+  if (tgt > WIN_CAP) tgt = WIN_CAP;
+  const i64 W = SMX_CEIL_DIV(C.n, tgt);
+  hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts, C.na, C.nb,
+                     W, tgt, bnd);
+  hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, C.ops->kind, C.ops->v0, C.ops->v1,
+                     (const u32*)nullptr, bnd, C.na, W, wcnt, meta);
+  hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, W, meta);
+  hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
+  HIP_TRY(hipGetLastError());
+  C.tm->end(ST_PLAN);
+  WinArgs P = win_args(C);
+  P.kts = C.ops->ts;
+  P.khi = C.ops->oid_hi;
+  P.klo = C.ops->oid_lo;
+  P.perm = nullptr;
+  P.W = W;
+  P.ablate = env_int("SMX_ABLATE", 0);
+  C.tm->begin(ST_WINDOW);
+  hipLaunchKernelGGL(k_window_f, dim3(W), dim3(WF_NT), 0, st, P);
+  HIP_TRY(hipGetLastError());
+  C.tm->end(ST_WINDOW);
+  if (P.ablate) return SMX_OK;  // diagnostics: the T-ordered arrays are invalid, stop here
+  return launch_tail(C, P);
+}
+
+// Generic plan: stable radix sort of each branch by (ts, oid_hi, oid_lo), then
+// fixed windows over the sorted logs.  Used when the presorted plan fails.
+static int run_generic(const Ctx& C) {
+  hipStream_t st = C.st;
+  ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
+  i64* bnd = C.ws<i64>(B_BND);
+  u32* wcnt = C.ws<u32>(B_WCNT);
+  u32* woff = C.ws<u32>(B_WOFF);
+  const i64 na = C.na, nb = C.nb, n = C.n;
+  C.tm->begin(ST_GSORT);
+  HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
+  hipLaunchKernelGGL(k_meta_init, dim3(1), dim3(1), 0, st, meta);
+  hipLaunchKernelGGL(k_keymask, dim3(grid_for(n, BLOCK * 8)), dim3(BLOCK), 0, st, C.ops->ts, C.ops->oid_hi,
+                     C.ops->oid_lo, na, n, meta);
+  ComposeMeta hm;
+  HIP_TRY(hipMemcpyAsync(&hm, meta, sizeof(ComposeMeta), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  u64* sts = C.ws<u64>(B_STS);
+  u64* shi = C.ws<u64>(B_SHI);
+  u64* slo = C.ws<u64>(B_SLO);
+  u32* perm = C.ws<u32>(B_PERM);
+  RadixTemp rt{C.ws<u64>(B_RK2), C.ws<u32>(B_RV2), C.ws<u32>(B_RHIST), C.ws<u32>(B_PART)};
+  const u64* words[3] = {C.ops->oid_lo, C.ops->oid_hi, C.ops->ts};
+  for (int side = 0; side < 2; ++side) {
+    const i64 off = side ? na : 0, cnt = side ? nb : na;
+    if (cnt == 0) continue;
+    u64* key = C.ws<u64>(B_RKEY) + off;
+    u32* val = perm + off;
+    for (int wi = 0; wi < 3; ++wi) {
+      const int q = 2 - wi;  // meta order: 0 = ts, 1 = hi, 2 = lo
+      const u64 varying = hm.key_or[side][q] ^ hm.key_and[side][q];
+      int shifts[8], ns = 0;
+      for (int dgt = 0; dgt < 8; ++dgt)
+        if ((varying >> (8 * dgt)) & 0xffull) shifts[ns++] = 8 * dgt;
+      if (wi == 0) {
+        hipLaunchKernelGGL(k_gather_init, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi] + off, key, val,
+                           cnt);
+        if (off)  // values are op indices of A||B
+          hipLaunchKernelGGL(k_offset, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, val, cnt, (u32)off);
+      } else {
+        hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi], val, key, cnt);
+      }
+      if (ns) HIP_TRY(radix_sort_pairs(key, val, cnt, shifts, ns, rt, st));
+    }
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->ts, val, sts + off, cnt);
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_hi, val, shi + off, cnt);
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_lo, val, slo + off, cnt);
+  }
+  const i64 W = SMX_CEIL_DIV(n, (i64)WIN_CAP);
+  hipLaunchKernelGGL(k_gpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, sts, shi, slo, na, nb,
+                     W, bnd);
+  hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, C.ops->kind, C.ops->v0, C.ops->v1, perm, bnd, na, W,
+                     wcnt, meta);
+  hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, W, meta);
+  hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
+  HIP_TRY(hipGetLastError());
+  C.tm->end(ST_GSORT);
+  WinArgs P = win_args(C);
+  P.kts = sts;
+  P.khi = shi;
+  P.klo = slo;
+  P.perm = perm;
+  P.W = W;
+  P.ablate = 0;
+  C.tm->begin(ST_WINDOW);
+  hipLaunchKernelGGL(k_window_g, dim3(W), dim3(WG_NT), 0, st, P);
+  HIP_TRY(hipGetLastError());
+  C.tm->end(ST_WINDOW);
+  return launch_tail(C, P);
+}
+
+static int read_meta(const Ctx& C, ComposeMeta* hm) {
+  HIP_TRY(hipMemcpyAsync(hm, C.ws<ComposeMeta>(B_META), sizeof(ComposeMeta), hipMemcpyDeviceToHost, C.st));
+  HIP_TRY(hipStreamSynchronize(C.st));
+  return SMX_OK;
+}
+
 static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
                         hipStream_t st) {
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
@@ -510,222 +785,44 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
   const Layout L = layout(na, nb, n_sym);
   if (!ws || ws_bytes < L.total)
     return set_err(SMX_E_WORKSPACE, "workspace too small: need " + std::to_string(L.total));
-  char* base = (char*)ws;
-#define WS(T, b) ((T*)(base + L.off[b]))
-  ComposeMeta* meta = WS(ComposeMeta, B_META);
-  i64* bnd = WS(i64, B_BND);
-  u32* wcnt = WS(u32, B_WCNT);
-  u32* woff = WS(u32, B_WOFF);
-
   int prof;
   {
     std::lock_guard<std::mutex> g(g_prof_mu);
     prof = g_prof;
   }
   StageTimer tm(st, prof != 0);
+  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, &tm};
 
-  // ---- plan: presorted windows + per-window counts/checks (one host sync) ----
-  tm.begin(ST_PLAN);
-  HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
-  const i64 Wf = SMX_CEIL_DIV(n, (i64)WIN_TGT);
-  hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(Wf + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, ops->ts, na, nb,
-                     Wf, bnd);
-  hipLaunchKernelGGL(k_wcount, dim3(Wf), dim3(BLOCK), 0, st, ops->kind, ops->ts, ops->v0, ops->v1,
-                     (const u32*)nullptr, bnd, na, Wf, wcnt, meta);
-  hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, Wf, meta);
-  hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
-  HIP_TRY(hipGetLastError());
+  int rc = run_presorted(C);
+  if (rc) return rc;
+  if (env_int("SMX_ABLATE", 0)) {  // diagnostics: timing of the window stage only
+    tm.flush();
+    return SMX_OK;
+  }
   ComposeMeta hm;
-  HIP_TRY(hipMemcpyAsync(&hm, meta, sizeof(ComposeMeta), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  tm.end(ST_PLAN);
-  if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: kind[i] >= 18");
-  const bool presorted = !hm.f_fail;
-
-  WinArgs P;
-  P.kind = ops->kind;
-  P.sym = ops->sym;
-  P.v0 = ops->v0;
-  P.v1 = ops->v1;
-  P.na = na;
-  P.n_sym = n_sym;
-  P.bnd = bnd;
-  P.woff = woff;
-  P.meta = meta;
-  P.order = WS(i32, B_ORDER);
-  P.symT = WS(u32, B_SYMT);
-  P.mvA = WS(i32, B_MVA);
-  P.mvF = WS(i32, B_MVF);
-  P.Msym = WS(u32, B_MSYM);
-  P.Mcls = WS(i32, B_MCLS);
-  P.Mstr = WS(i32, B_MSTR);
-  P.Mside = WS(u8, B_MSIDE);
-  P.Mown = WS(u32, B_MOWN);
-  i64 W;
-  if (presorted) {
-    W = Wf;
-    P.kts = ops->ts;
-    P.khi = ops->oid_hi;
-    P.klo = ops->oid_lo;
-    P.perm = nullptr;
-  } else {
-    // ---- generic: stable radix sort of each branch by (ts, oid_hi, oid_lo) ----
-    tm.begin(ST_GSORT);
-    HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
-    hipLaunchKernelGGL(k_meta_init, dim3(1), dim3(1), 0, st, meta);
-    hipLaunchKernelGGL(k_keymask, dim3(grid_for(n, BLOCK * 8)), dim3(BLOCK), 0, st, ops->ts, ops->oid_hi,
-                       ops->oid_lo, na, n, meta);
-    HIP_TRY(hipMemcpyAsync(&hm, meta, sizeof(ComposeMeta), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    u64* sts = WS(u64, B_STS);
-    u64* shi = WS(u64, B_SHI);
-    u64* slo = WS(u64, B_SLO);
-    u32* perm = WS(u32, B_PERM);
-    RadixTemp rt{WS(u64, B_RK2), WS(u32, B_RV2), WS(u32, B_RHIST), WS(u32, B_PART)};
-    const u64* words[3] = {ops->oid_lo, ops->oid_hi, ops->ts};
-    for (int side = 0; side < 2; ++side) {
-      const i64 off = side ? na : 0, cnt = side ? nb : na;
-      if (cnt == 0) continue;
-      u64* key = WS(u64, B_RKEY) + off;
-      u32* val = perm + off;
-      for (int wi = 0; wi < 3; ++wi) {
-        const int q = 2 - wi;  // meta order: 0 = ts, 1 = hi, 2 = lo
-        const u64 varying = hm.key_or[side][q] ^ hm.key_and[side][q];
-        int shifts[8], ns = 0;
-        for (int dgt = 0; dgt < 8; ++dgt)
-          if ((varying >> (8 * dgt)) & 0xffull) shifts[ns++] = 8 * dgt;
-        if (wi == 0) {
-          hipLaunchKernelGGL(k_gather_init, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi] + off, key,
-                             val, cnt);
-          if (off)  // values are op indices of A||B
-            hipLaunchKernelGGL(k_offset, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, val, cnt, (u32)off);
-        } else {
-          hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi], val, key, cnt);
-        }
-        if (ns) HIP_TRY(radix_sort_pairs(key, val, cnt, shifts, ns, rt, st));
-      }
-      hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, ops->ts, val, sts + off, cnt);
-      hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, ops->oid_hi, val, shi + off, cnt);
-      hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, ops->oid_lo, val, slo + off, cnt);
-    }
-    W = SMX_CEIL_DIV(n, (i64)WIN_CAP);
-    hipLaunchKernelGGL(k_gpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, sts, shi, slo, na,
-                       nb, W, bnd);
-    hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, ops->kind, ops->ts, ops->v0, ops->v1, perm, bnd,
-                       na, W, wcnt, meta);
-    hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, W, meta);
-    hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(&hm, meta, sizeof(ComposeMeta), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    P.kts = sts;
-    P.khi = shi;
-    P.klo = slo;
-    P.perm = perm;
-    tm.end(ST_GSORT);
+  if ((rc = read_meta(C, &hm))) return rc;
+  if (hm.f_fail && !hm.bad_sym) {  // not presorted: redo on the generic plan
+    if ((rc = run_generic(C))) return rc;
+    if ((rc = read_meta(C, &hm))) return rc;
   }
-  P.W = W;
-  const u64 nMv = hm.kcnt[KMOVE], nR = hm.kcnt[KREN];
-  const u64 nRA = hm.n_ren_side[0], nRB = hm.n_ren_side[1];
-  P.RA = WS(u32, B_RAB);
-  P.RB = WS(u32, B_RAB) + nRA;
-
-  // ---- windows -> T-ordered arrays ----
-  tm.begin(ST_WINDOW);
-  if (presorted)
-    hipLaunchKernelGGL(k_window_f, dim3(W), dim3(WF_NT), 0, st, P);
-  else
-    hipLaunchKernelGGL(k_window_g, dim3(W), dim3(WG_NT), 0, st, P);
-  HIP_TRY(hipGetLastError());
-  tm.end(ST_WINDOW);
-
-  // ---- DivergentRename walk over the rename block ----
-  tm.begin(ST_WALK);
-  u8* skip = WS(u8, B_SKIP);
-  u32* skipex = WS(u32, B_SKIPEX);
-  u32* part = WS(u32, B_PART);
-  const i32* order_ren = P.order + hm.base[KREN];
-  if (nR > 0) {
-    HIP_TRY(hipMemsetAsync(skip, 0, nR, st));
-    WalkArgs Wk{P.Msym, P.Mcls, P.Mside, P.Mown, P.RA, P.RB, nR, nRA, nRB};
-    u8* flags = WS(u8, B_FLAGS);
-    u32* fpos = WS(u32, B_FPOS);
-    u32* cand = WS(u32, B_CAND);
-    u32* q = WS(u32, B_Q);
-    u32* pm = WS(u32, B_PM);
-    u32* nconf = WS(u32, B_NCONF);
-    u32* nreal = WS(u32, B_NREAL);
-    u32* coff = WS(u32, B_COFF);
-    // n_cand / n_conf are u64 in meta; the scans produce u32 totals into the low word
-    // (little endian) of the zeroed u64 fields.
-    u32* ncand32 = (u32*)&meta->n_cand;
-    u32* nconf32 = (u32*)&meta->n_conf;
-    const u64* ncand_dev = &meta->n_cand;
-    hipLaunchKernelGGL(k_flags, dim3(grid_for(nR)), dim3(BLOCK), 0, st, Wk, flags);
-    HIP_TRY((scan_excl<OpSum, u8, u32>(flags, fpos, (i64)nR, nullptr, part, ncand32, st)));
-    hipLaunchKernelGGL(k_compact, dim3(grid_for(nR)), dim3(BLOCK), 0, st, flags, fpos, nR, cand);
-    hipLaunchKernelGGL(k_replay_q, dim3(grid_for(nR)), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
-    HIP_TRY((scan_excl<OpMax, u32, u32>(q, pm, 0, ncand_dev, part, (u32*)nullptr, st)));
-    hipLaunchKernelGGL(k_cluster, dim3(grid_for(nR)), dim3(BLOCK), 0, st, cand, q, pm, nconf, meta, nreal);
-    HIP_TRY((scan_excl<OpSum, u32, u32>(nreal, coff, 0, ncand_dev, part, nconf32, st)));
-    hipLaunchKernelGGL(k_replay_write, dim3(grid_for(nR)), dim3(BLOCK), 0, st, Wk, cand, nreal, coff, meta,
-                       order_ren, out->conflicts, (u64)out->conflict_cap, skip);
-    HIP_TRY((scan_excl<OpSum, u8, u32>(skip, skipex, (i64)nR, nullptr, part, (u32*)nullptr, st)));
-    HIP_TRY(hipGetLastError());
-  }
-  tm.end(ST_WALK);
-
-  // ---- per-symbol final states ----
-  tm.begin(ST_TABLES);
-  u64* tabA = WS(u64, B_TABA);
-  u64* tabF = WS(u64, B_TABF);
-  u64* tabR = WS(u64, B_TABR);
-  int4* fin = WS(int4, B_FIN);
-  HIP_TRY(hipMemsetAsync(tabA, 0, (size_t)n_sym * 8, st));
-  HIP_TRY(hipMemsetAsync(tabF, 0, (size_t)n_sym * 8, st));
-  HIP_TRY(hipMemsetAsync(tabR, 0, (size_t)n_sym * 8, st));
-  if (nMv > 0)
-    hipLaunchKernelGGL(k_tab_move, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, P.symT, P.mvA, P.mvF, nMv, tabA,
-                       tabF, (u32)(n_sym - 1));
-  if (nR > 0)
-    hipLaunchKernelGGL(k_tab_ren, dim3(grid_for(nR)), dim3(BLOCK), 0, st, P.Msym, P.Mstr, skip, nR, tabR, (u32)(n_sym - 1));
-  hipLaunchKernelGGL(k_finalize, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, tabA, tabF, tabR, n_sym, fin);
-  HIP_TRY(hipGetLastError());
-  tm.end(ST_TABLES);
-
-  // ---- moves with a None value need the per-symbol prefix (rare) ----
-  const i32* prefA = P.mvA;
-  const i32* prefF = P.mvF;
+  if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
+  const u64 nMv = hm.kcnt[KMOVE];
   if (hm.n_move_none > 0 && nMv > 0) {
     tm.begin(ST_MVPREFIX);
-    u64* keys = WS(u64, B_RKEY);
-    u32* vals = WS(u32, B_RVAL);
-    RadixTemp rt{WS(u64, B_RK2), WS(u32, B_RV2), WS(u32, B_RHIST), WS(u32, B_PART)};
+    u64* keys = C.ws<u64>(B_RKEY);
+    u32* vals = C.ws<u32>(B_RVAL);
+    RadixTemp rt{C.ws<u64>(B_RK2), C.ws<u32>(B_RV2), C.ws<u32>(B_RHIST), C.ws<u32>(B_PART)};
     int shifts[4], ns = 0;
     for (int dgt = 0; dgt < 4; ++dgt)
       if (((u64)(n_sym - 1) >> (8 * dgt)) != 0) shifts[ns++] = 8 * dgt;
-    hipLaunchKernelGGL(k_mv_init, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, P.symT, nMv, keys, vals);
+    hipLaunchKernelGGL(k_mv_init, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, C.ws<u32>(B_SYMT), nMv, keys, vals);
     if (ns) HIP_TRY(radix_sort_pairs(keys, vals, (i64)nMv, shifts, ns, rt, st));
-    i32* pA = WS(i32, B_PREFA);
-    i32* pF = WS(i32, B_PREFF);
-    hipLaunchKernelGGL(k_mv_seg, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, keys, vals, nMv, P.mvA, P.mvF, pA,
-                       pF);
+    hipLaunchKernelGGL(k_mv_fix, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, keys, vals, nMv, C.ws<i32>(B_MVA),
+                       C.ws<i32>(B_MVF), out->addr, out->file);
     HIP_TRY(hipGetLastError());
-    prefA = pA;
-    prefF = pF;
     tm.end(ST_MVPREFIX);
   }
-
-  // ---- compacted output ----
-  tm.begin(ST_EMIT);
-  EmitArgs E{P.order, P.symT, prefA, prefF, skip, skipex, fin, meta, (u64)n, nMv, nR, (u32)(n_sym - 1),
-             out->order, out->addr, out->file, out->ctx};
-  hipLaunchKernelGGL(k_emit, dim3(grid_for(n, BLOCK * 4)), dim3(BLOCK), 0, st, E);
-  hipLaunchKernelGGL(k_counts, dim3(1), dim3(1), 0, st, meta, (u64)n, out->counts);
-  HIP_TRY(hipGetLastError());
-  tm.end(ST_EMIT);
   tm.flush();
-#undef WS
   return SMX_OK;
 }
 

@@ -18,7 +18,8 @@
 #include "smx_common.h"
 
 #define WIN_CAP 2048               // max ops per window held in LDS
-#define WIN_TGT 1024               // target window size, presorted path
+#define WIN_TGT 1024               // default target window size, presorted path (SMX_WIN_TGT)
+#define WIN_TGT_MIN 256
 #define NCNT (SMX_N_KINDS + 3)     // kinds, renames per branch, moves with a None value
 #define CNT_REN_A SMX_N_KINDS
 #define CNT_REN_B (SMX_N_KINDS + 1)
@@ -38,8 +39,10 @@ struct WinArgs {
   const u64* klo;
   const u32* perm;  // generic only: op index of sorted position (A at [0,na), B at [na,n))
   i64 na;
+  i64 nb;
   i64 W;
   i64 n_sym;
+  int ablate;       // diagnostics only (SMX_ABLATE): skip phases, results invalid
   const i64* bnd;
   const u32* woff;  // [NCNT][W] exclusive offsets over windows
   ComposeMeta* meta;
@@ -60,6 +63,8 @@ struct WinArgs {
 __device__ __forceinline__ void win_emit(const WinArgs& P, const u64* base, i64 w, u32 k, u32 x,
                                          u32 kb, u32 src, u32 s, i32 a, i32 f, int side, u32 own) {
   const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (x - kb);
+  // Bounds guards: only a failed (and later discarded) presorted plan can trip them.
+  if (T >= (u64)(P.na + P.nb) || own >= (u64)(side ? P.nb : P.na)) return;
   P.order[T] = (i32)src;
   P.symT[T] = s;
   if (k == KMOVE) {
@@ -83,13 +88,13 @@ __device__ __forceinline__ void win_emit(const WinArgs& P, const u64* base, i64 
 #define WF_WAVES (WF_NT / WAVE)
 #define WF_ITEMS (WIN_CAP / WF_NT)
 
-__global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
-  __shared__ u64 sts[WIN_CAP];        // element space: timestamp keys
-  __shared__ u64 phi[WIN_CAP];        // slot space: oid_hi
+// LDS ~34 KB (buffers are reused across phases) so 4 workgroups fit a CU: while
+// some workgroups run their LDS phases, others stream their windows from HBM.
+__global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
+  __shared__ u64 sts[WIN_CAP];        // element space: timestamp keys; later slot-space oid prefix
   __shared__ u16 sord[WIN_CAP];       // S order (merge), later the final order
-  __shared__ u16 fin[WIN_CAP];        // slot -> element
+  __shared__ u16 fin[WIN_CAP];        // slot -> element, later rename ranks
   __shared__ u16 sl[WIN_CAP];         // element -> slot, later element -> final
-  __shared__ u16 rown[WIN_CAP];       // rename rank within its branch (final order)
   __shared__ u8 skind[WIN_CAP];
   __shared__ u8 srank[WIN_CAP];
   __shared__ u64 gbits[NCHUNK];       // group-start bits over slots
@@ -98,6 +103,8 @@ __global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
   __shared__ u32 kbase[SMX_N_KINDS + 1];
   __shared__ u32 wck[SMX_N_KINDS];
   __shared__ u64 base[SMX_N_KINDS + 1];
+  u32* phi = (u32*)sts;               // slot space: top 32 bits of oid_hi (after step 4)
+  u16* rown = fin;                    // rename rank within its branch (after step 5)
 
   const int t = threadIdx.x;
   const int lane = t & (WAVE - 1);
@@ -107,11 +114,15 @@ __global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
   const int na = (int)(P.bnd[2 * w + 2] - a0);
   const int nb = (int)(P.bnd[2 * w + 3] - b0);
   const int sz = na + nb;
+  if (na < 0 || nb < 0 || sz > WIN_CAP) {  // the presorted plan does not hold
+    if (threadIdx.x == 0) P.meta->f_fail = 1;
+    return;
+  }
   if (sz == 0) return;
   const i64 bpos = P.na + b0 - na;  // op index of B element e is bpos + e
 
   // 1. load: keys to LDS, payload stays in registers
-  u64 hi_r[WF_ITEMS];
+  u32 hi_r[WF_ITEMS];
   u32 sym_r[WF_ITEMS];
   i32 v0_r[WF_ITEMS], v1_r[WF_ITEMS];
   u32 k_r[WF_ITEMS];
@@ -123,7 +134,7 @@ __global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
       const i64 j = e < na ? a0 + e : bpos + e;
       const u32 k = P.kind[j];
       const u64 tv = P.kts[j];
-      hi_r[i] = P.khi[j];
+      hi_r[i] = (u32)(P.khi[j] >> 32);
       sym_r[i] = P.sym[j];
       v0_r[i] = P.v0[j];
       v1_r[i] = P.v1[j];
@@ -137,6 +148,45 @@ __global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
   __syncthreads();
+
+  // presorted-layout check: every adjacent pair of each branch log is
+  // non-decreasing (the pair straddling a window start is checked here too);
+  // moves with a None value are counted for the prefix fix-up
+  if (!(P.ablate & 1)) {
+    bool dec = false;
+    u32 none_mv = 0;
+#pragma unroll
+    for (int i = 0; i < WF_ITEMS; ++i) {
+      const int e = t + WF_NT * i;
+      if (e >= sz) continue;
+      const u64 cur = sts[e];
+      if (e == 0) {
+        if (a0 > 0 && P.kts[a0 - 1] > cur) dec = true;
+      } else if (e == na) {
+        if (b0 > 0 && P.kts[P.na + b0 - 1] > cur) dec = true;
+      } else if (sts[e - 1] > cur) {
+        dec = true;
+      }
+      none_mv += (k_r[i] == KMOVE && (v0_r[i] < 0 || v1_r[i] < 0));
+    }
+    if (none_mv) atomicAdd((unsigned long long*)&P.meta->n_move_none, (unsigned long long)none_mv);
+    if (__syncthreads_or(dec)) {
+      if (t == 0) P.meta->f_fail = 1;
+      return;
+    }
+  }
+
+  if (P.ablate & 8) {  // load + write only
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < WF_ITEMS; ++i) {
+      const int e = t + WF_NT * i;
+      if (e >= sz) continue;
+      const u32 src = (u32)(e < na ? a0 + e : bpos + e);
+      win_emit(P, base, w, k_r[i], (u32)e, 0, src, sym_r[i], v0_r[i], v1_r[i], e >= na, 0);
+    }
+    return;
+  }
 
   // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties
   {
@@ -194,12 +244,8 @@ __global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
   }
   __syncthreads();
 
-  // 4. slot-space oid_hi and group-start bits: a group = equal (rank, timestamp)
-#pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i) {
-    const int e = t + WF_NT * i;
-    if (e < sz) phi[sl[e]] = hi_r[i];
-  }
+  // 4. group-start bits (a group = equal (rank, timestamp), contiguous in slots),
+  //    then the timestamps are dead and their buffer takes the slot-space oid prefix
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {
     const int p = t + WF_NT * j;
@@ -212,9 +258,16 @@ __global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
     if (lane == 0 && (p >> 6) < NCHUNK) gbits[p >> 6] = b;
   }
   __syncthreads();
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i) {
+    const int e = t + WF_NT * i;
+    if (e < sz) phi[sl[e]] = hi_r[i];
+  }
+  __syncthreads();
 
-  // 5. order each group by (oid, side, index): counting rank, ties on oid_hi
-  //    resolved on oid_lo (rare), then on slot order (= side, index order)
+  // 5. order each group by (oid, side, index): counting rank on the top 32 bits of
+  //    oid_hi; elements sharing that prefix (rare) are resolved on the full oid and
+  //    then on slot order (= side, index order)
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {
     const int p = t + WF_NT * j;
@@ -231,19 +284,25 @@ __global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
     int ge = word ? wi * 64 + __ffsll((unsigned long long)word) - 1 : sz;
     ge = ge < sz ? ge : sz;
     int r = p;
-    if (ge - gs > 1) {
-      const u64 h = phi[p];
-      r = gs;
+    if (ge - gs > 1 && !(P.ablate & 2)) {
+      const u32 h = phi[p];
+      u32 lt = 0, eq = 0;
       for (int q = gs; q < ge; ++q) {
-        const u64 hq = phi[q];
-        bool lt = hq < h;
-        if (hq == h && q != p) {  // equal oid_hi: compare oid_lo, then slot order
-          const int eq = fin[q];
-          const u64 lq = P.klo[eq < na ? a0 + eq : bpos + eq];
-          const u64 lp = P.klo[e < na ? a0 + e : bpos + e];
-          lt = lq < lp || (lq == lp && q < p);
+        const u32 hq = phi[q];
+        lt += hq < h;
+        eq += hq == h;
+      }
+      r = gs + (int)lt;
+      if (eq > 1) {  // shared 32-bit prefix: exact compare on (oid_hi, oid_lo), then slot
+        const i64 jp = e < na ? a0 + e : bpos + e;
+        const u64 hp = P.khi[jp], lp = P.klo[jp];
+        for (int q = gs; q < ge; ++q) {
+          if (q == p || phi[q] != h) continue;
+          const int eq2 = fin[q];
+          const i64 jq = eq2 < na ? a0 + eq2 : bpos + eq2;
+          const u64 hq = P.khi[jq], lq = P.klo[jq];
+          r += hq < hp || (hq == hp && (lq < lp || (lq == lp && q < p)));
         }
-        r += lt;
       }
     }
     sord[r] = (u16)e;
@@ -280,6 +339,7 @@ __global__ void __launch_bounds__(WF_NT) k_window_f(WinArgs P) {
   __syncthreads();
 
   // 7. write T-ordered records from registers
+  if (P.ablate & 4) return;
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
