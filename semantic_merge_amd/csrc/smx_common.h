@@ -122,3 +122,6 @@ __device__ __forceinline__ T block_excl_scan(T v, T* s, T* total) {
 }
 
 #define SMX_CEIL_DIV(a, b) (((a) + (b)-1) / (b))
+
+// Records the thread-local error message returned by smx_last_error(); returns code.
+int smx_set_error(int code, const char* msg);

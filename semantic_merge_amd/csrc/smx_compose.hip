@@ -40,6 +40,7 @@ static int set_err(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+int smx_set_error(int code, const char* msg) { return set_err(code, msg ? msg : ""); }
 #define HIP_TRY(x)                                                                 \
   do {                                                                             \
     hipError_t _e = (x);                                                           \

@@ -12,7 +12,7 @@
 #define RADIX_ITEMS 16
 #define RADIX_TILE (BLOCK * RADIX_ITEMS)
 
-__global__ void __launch_bounds__(BLOCK) k_radix_hist(const u64* __restrict__ keys, i64 n, int shift,
+static __global__ void __launch_bounds__(BLOCK) k_radix_hist(const u64* __restrict__ keys, i64 n, int shift,
                                                       u32* __restrict__ hist, int nblk) {
   __shared__ u32 h[256];
   h[threadIdx.x] = 0;
@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(BLOCK) k_radix_hist(const u64* __restrict__ ke
   hist[(i64)threadIdx.x * nblk + blockIdx.x] = h[threadIdx.x];
 }
 
-__global__ void __launch_bounds__(BLOCK) k_radix_scatter(const u64* __restrict__ kin,
+static __global__ void __launch_bounds__(BLOCK) k_radix_scatter(const u64* __restrict__ kin,
                                                          const u32* __restrict__ vin,
                                                          u64* __restrict__ kout,
                                                          u32* __restrict__ vout, i64 n, int shift,

@@ -257,3 +257,29 @@ def lift_op_dicts(logs: LiftLogs) -> Tuple[List[dict], List[dict]]:
             "provenance": prov,
         })
     return out[: logs.n_a], out[logs.n_a:]
+
+
+def rga_batch(n_ops: int, n_lists: int, seed: int, values_per_list: int = 150,
+              anchors_per_list: int = 20, authors: int = 4):
+    """SURVEY §8(d) config 4 shape: RGA events over many independent lists
+    (insert 0.7, delete 0.2, move 0.1), values from 150 per list, anchors from 20
+    per list, t uniform in [0, 2^40), 4 authors, uuid4 opids.  Returns the
+    ``RgaBatch`` image directly (order-preserving ranks; strings not materialised)."""
+    from .crdt import RgaBatch
+    rng = np.random.default_rng(seed)
+    lid = rng.integers(0, n_lists, size=n_ops, dtype=np.int64)
+    op = rng.choice(3, size=n_ops, p=[0.7, 0.1, 0.2]).astype(np.uint8)  # insert, move, delete
+    val = lid * values_per_list + rng.integers(0, values_per_list, size=n_ops)
+    anchor = rng.integers(0, anchors_per_list, size=n_ops, dtype=np.int64)
+    t = rng.integers(0, 1 << 40, size=n_ops, dtype=np.int64)
+    author = rng.integers(0, authors, size=n_ops, dtype=np.int64)
+    bits = rng.integers(0, 0xFFFFFFFFFFFFFFFF, size=(n_ops, 2), dtype=np.uint64, endpoint=True)
+    hi = (bits[:, 0] & ~np.uint64(0xF000)) | np.uint64(0x4000)
+    lo = (bits[:, 1] & ~np.uint64(0xC000000000000000)) | np.uint64(0x8000000000000000)
+    # value ids interned densely in first-seen order, like marshal_streams
+    _, first, inv = np.unique(val, return_index=True, return_inverse=True)
+    order = np.argsort(first, kind="stable")
+    rank = np.empty_like(order)
+    rank[order] = np.arange(len(order))
+    return RgaBatch(n_lists, lid.astype(np.uint32), op, rank[inv].astype(np.uint32),
+                    anchor.astype(np.uint32), t, author.astype(np.uint32), hi, lo, [])

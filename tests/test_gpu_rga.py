@@ -1,0 +1,50 @@
+"""GPU parity for the batched RGA replay (crdt.py:23-57) through the C ABI."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from semantic_merge_amd import synth
+from semantic_merge_amd._lib import rga_replay_device
+from semantic_merge_amd.crdt import RGA, Key, marshal_streams, replay
+
+from _util import load
+from test_rga_oracle import to_streams
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rga_golden_cases_gpu():
+    cases = load("rga_cases.json")
+    got = replay(to_streams(cases))
+    for i, case in enumerate(cases):
+        assert got[i] == case["out"], f"rga case {i}"
+
+
+def test_rga_class_dropin():
+    r = RGA()
+    r.insert(Key("root", 1, "u1", "o1"), "a")
+    r.insert(Key("root", 0, "u1", "o2"), "b")
+    r.move("a", Key("root", -1, "u2", "o3"))
+    r.insert(Key("root", 5, "u1", "o4"), "c")
+    r.delete("b")
+    assert r.materialize() == ["a", "c"]
+
+
+def _check(batch):
+    gv, gs, go = rga_replay_device(batch)
+    ov, os_, oo = oracle.rga(batch.n_lists, batch.list_id, batch.op, batch.value, batch.anchor,
+                             batch.t, batch.author, batch.opid_hi, batch.opid_lo)
+    assert np.array_equal(go, oo)
+    assert np.array_equal(gs, os_)
+    assert np.array_equal(gv, ov)
+
+
+@pytest.mark.parametrize("n_ops,n_lists,seed", [(200_000, 1_000, 13), (1_000_000, 5_000, 14),
+                                                 (300_000, 30, 15)])
+def test_rga_batch_equals_oracle(n_ops, n_lists, seed):
+    _check(synth.rga_batch(n_ops, n_lists, seed))
+
+
+def test_rga_dense_values_and_big_lists():
+    # few values per list (long per-value chains) and lists beyond the LDS capacity
+    _check(synth.rga_batch(60_000, 8, 16, values_per_list=3, anchors_per_list=2, authors=1))
