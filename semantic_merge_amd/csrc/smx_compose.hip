@@ -657,7 +657,7 @@ static int env_int(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 
-static int run_presorted(const Ctx& C) {
+static int run_presorted(const Ctx& C, i64 tgt) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
@@ -665,7 +665,6 @@ static int run_presorted(const Ctx& C) {
   u32* woff = C.ws<u32>(B_WOFF);
   C.tm->begin(ST_PLAN);
   HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
-  i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
   if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
   if (tgt > WIN_CAP) tgt = WIN_CAP;
   const i64 W = SMX_CEIL_DIV(C.n, tgt);
@@ -794,7 +793,11 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
   StageTimer tm(st, prof != 0);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, &tm};
 
-  int rc = run_presorted(C);
+  // Presorted plan first; a window that overflows LDS (dense timestamp ties)
+  // retries with smaller windows, a log that is not timestamp-ordered goes to the
+  // generic plan.
+  i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
+  int rc = run_presorted(C, tgt);
   if (rc) return rc;
   if (env_int("SMX_ABLATE", 0)) {  // diagnostics: timing of the window stage only
     tm.flush();
@@ -802,6 +805,11 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
   }
   ComposeMeta hm;
   if ((rc = read_meta(C, &hm))) return rc;
+  while (hm.f_fail == 2 && !hm.bad_sym && tgt > 512) {
+    tgt /= 2;
+    if ((rc = run_presorted(C, tgt))) return rc;
+    if ((rc = read_meta(C, &hm))) return rc;
+  }
   if (hm.f_fail && !hm.bad_sym) {  // not presorted: redo on the generic plan
     if ((rc = run_generic(C))) return rc;
     if ((rc = read_meta(C, &hm))) return rc;

@@ -18,7 +18,7 @@
 #include "smx_common.h"
 
 #define WIN_CAP 2048               // max ops per window held in LDS
-#define WIN_TGT 1024               // default target window size, presorted path (SMX_WIN_TGT)
+#define WIN_TGT 1792               // default target window size, presorted path (SMX_WIN_TGT)
 #define WIN_TGT_MIN 256
 #define NCNT (SMX_N_KINDS + 3)     // kinds, renames per branch, moves with a None value
 #define CNT_REN_A SMX_N_KINDS
@@ -115,7 +115,9 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   const int nb = (int)(P.bnd[2 * w + 3] - b0);
   const int sz = na + nb;
   if (na < 0 || nb < 0 || sz > WIN_CAP) {  // the presorted plan does not hold
-    if (threadIdx.x == 0) P.meta->f_fail = 1;
+    // bit 0: branch logs not timestamp-ordered; bit 1: window too large for LDS
+    if (threadIdx.x == 0)
+      atomicOr((unsigned long long*)&P.meta->f_fail, (na < 0 || nb < 0) ? 1ull : 2ull);
     return;
   }
   if (sz == 0) return;
@@ -144,6 +146,10 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       skind[e] = (u8)k_r[i];
     }
   }
+  // timestamps just before the window on each branch (issued with the loads above)
+  u64 prev_a = 0, prev_b = 0;
+  if (t == 0 && a0 > 0) prev_a = P.kts[a0 - 1];
+  if (t == 0 && b0 > 0) prev_b = P.kts[P.na + b0 - 1];
   if (bad) P.meta->bad_sym = 1;
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
@@ -155,23 +161,17 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   if (!(P.ablate & 1)) {
     bool dec = false;
     u32 none_mv = 0;
+    if (t == 0) dec = (a0 > 0 && na > 0 && prev_a > sts[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
 #pragma unroll
     for (int i = 0; i < WF_ITEMS; ++i) {
       const int e = t + WF_NT * i;
       if (e >= sz) continue;
-      const u64 cur = sts[e];
-      if (e == 0) {
-        if (a0 > 0 && P.kts[a0 - 1] > cur) dec = true;
-      } else if (e == na) {
-        if (b0 > 0 && P.kts[P.na + b0 - 1] > cur) dec = true;
-      } else if (sts[e - 1] > cur) {
-        dec = true;
-      }
+      if (e != 0 && e != na && sts[e - 1] > sts[e]) dec = true;
       none_mv += (k_r[i] == KMOVE && (v0_r[i] < 0 || v1_r[i] < 0));
     }
     if (none_mv) atomicAdd((unsigned long long*)&P.meta->n_move_none, (unsigned long long)none_mv);
     if (__syncthreads_or(dec)) {
-      if (t == 0) P.meta->f_fail = 1;
+      if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
       return;
     }
   }
@@ -338,22 +338,60 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   }
   __syncthreads();
 
-  // 7. write T-ordered records from registers
+  // 7. write T-ordered records in final order (consecutive lanes -> consecutive T
+  //    inside each kind: coalesced).  The register payload is staged through the
+  //    now-free timestamp buffer in two rounds (sym + v0, then v1).
   if (P.ablate & 4) return;
+  u32* st_a = (u32*)sts;             // [WIN_CAP] sym
+  i32* st_b = (i32*)sts + WIN_CAP;   // [WIN_CAP] v0, then v1
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
-    if (e >= sz) continue;
-    const u32 x = sl[e];
-    const u32 k = k_r[i];
-    const int side = e >= na;
-    u32 own = 0;
-    if (k == KREN) {
-      const int xr = (int)x - R0;
-      own = P.woff[(i64)(CNT_REN_A + side) * P.W + w] + rc[xr / WAVE][side] + rown[xr];
+    if (e < sz) {
+      st_a[e] = sym_r[i];
+      st_b[e] = v0_r[i];
     }
-    const u32 src = (u32)(e < na ? a0 + e : bpos + e);
-    win_emit(P, base, w, k, x, kbase[k], src, sym_r[i], v0_r[i], v1_r[i], side, own);
+  }
+  __syncthreads();
+  const u64 wofs_ra = P.woff[(i64)CNT_REN_A * P.W + w], wofs_rb = P.woff[(i64)CNT_REN_B * P.W + w];
+  const u64 nall = (u64)(P.na + P.nb);
+  for (int x = t; x < sz; x += WF_NT) {
+    const int e = sord[x];
+    const u32 k = skind[e];
+    const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (u32)(x - kbase[k]);
+    if (T >= nall) continue;  // only a failed (discarded) presorted plan can trip this
+    const u32 s = st_a[e];
+    P.order[T] = (i32)(e < na ? a0 + e : bpos + e);
+    P.symT[T] = s;
+    if (k == KMOVE) {
+      P.mvA[T] = st_b[e];
+    } else if (k == KREN) {
+      const int side = e >= na;
+      const int xr = x - R0;
+      const u32 own = (u32)((side ? wofs_rb : wofs_ra) + rc[xr / WAVE][side] + rown[xr]);
+      const u64 m = T - base[KREN];
+      P.Msym[m] = s;
+      P.Mcls[m] = st_b[e];
+      P.Mside[m] = (u8)side;
+      P.Mown[m] = own;
+      if (own < (u64)(side ? P.nb : P.na)) (side ? P.RB : P.RA)[own] = (u32)m;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i) {
+    const int e = t + WF_NT * i;
+    if (e < sz) st_b[e] = v1_r[i];
+  }
+  __syncthreads();
+  for (int x = t; x < sz; x += WF_NT) {
+    const int e = sord[x];
+    const u32 k = skind[e];
+    if (k != KMOVE && k != KREN) continue;
+    const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (u32)(x - kbase[k]);
+    if (T >= nall) continue;
+    if (k == KMOVE) P.mvF[T] = st_b[e];
+    else P.Mstr[T - base[KREN]] = st_b[e];
   }
 }
 

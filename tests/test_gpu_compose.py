@@ -83,7 +83,8 @@ def test_synthetic_digests_gpu(name):
                    rename_overlap=0.30),                         # config 5 shape
     synth.LiftSpec(1_000_000, 64, 23, ops_per_ms=16, mix=synth.ADVERSARIAL_MIX),  # hot symbols
     synth.LiftSpec(333_333, 1, 29, ops_per_ms=1),               # one symbol, every head collides
-], ids=["c2_1M", "c2_1M_shuffled", "c5_2M", "hot64_1M", "onesym"])
+    synth.LiftSpec(1_000_000, 1_000, 41, ops_per_ms=160),       # windows overflow -> smaller windows
+], ids=["c2_1M", "c2_1M_shuffled", "c5_2M", "hot64_1M", "onesym", "dense160"])
 def test_gpu_equals_oracle_soa(spec):
     soa = synth.lift_soa(synth.lift_logs(spec))
     _eq_soa(compose_soa(soa), oracle.compose(soa), str(spec))
