@@ -39,6 +39,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--n-ops", type=int, default=0, help="override the config's op count")
+    ap.add_argument("--n-sym", type=int, default=0, help="override the config's symbol count")
     ap.add_argument("--cpu-sample", type=int, default=40_000_000,
                     help="ops in the CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -47,10 +48,10 @@ def main() -> None:
 
     import torch
     from semantic_merge_amd import _lib, synth
+    from semantic_merge_amd.dist import job_throughput, max_over_ranks, rank_info, rank_seed
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ri = rank_info()
+    world, rank, local = ri.world, ri.rank, ri.local
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -61,7 +62,9 @@ def main() -> None:
     spec = synth.CONFIGS[args.config]
     if args.n_ops:
         spec = synth.LiftSpec(**{**spec.__dict__, "n_total": args.n_ops})
-    spec = synth.LiftSpec(**{**spec.__dict__, "seed": spec.seed + rank})
+    if args.n_sym:
+        spec = synth.LiftSpec(**{**spec.__dict__, "n_sym": args.n_sym})
+    spec = synth.LiftSpec(**{**spec.__dict__, "seed": rank_seed(spec.seed, rank)})
     t0 = time.time()
     logs = synth.lift_logs(spec)
     soa = synth.lift_soa(logs)
@@ -90,10 +93,7 @@ def main() -> None:
     lib.smx_set_profiling(0)
     stages = _lib.stage_times()
     k, nconf = (int(x) for x in dc.counts.cpu().tolist())
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)
 
     if args.verify:
         from oracle import oracle
@@ -111,7 +111,7 @@ def main() -> None:
 
     n = soa.n
     ms_step = elapsed / args.steps * 1e3
-    value = world * n * args.steps / elapsed
+    value = job_throughput(n, world, args.steps, elapsed)
     win_ms, win_calls = stages.get("window", (0.0, 0))
     win_avg = win_ms / max(win_calls, 1)
     achieved = WINDOW_BYTES_PER_OP * n / (win_avg * 1e-3) / 1e9 if win_avg > 0 else None

@@ -203,10 +203,96 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
   bnd[2 * k + 1] = d - lo;
 }
 
+// Presorted plan, counting: kind histogram of fixed 256-op chunks of each branch
+// (cnt[side][kind][chunk]), then an exclusive scan over chunks per (side, kind).
+// A window derives its T offsets from the chunk prefixes at its start plus the
+// kinds of at most 255 ops before it.  Coalesced: iteration j of a block reads
+// chunk j, lane t its byte t.
+#define CH_PER_BLOCK 16
+
+__global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, i64 na, i64 nb, i64 CM,
+                                                 u32* __restrict__ cnt, ComposeMeta* meta) {
+  __shared__ u32 c[CH_PER_BLOCK][SMX_N_KINDS];
+  const i64 CA = SMX_CEIL_DIV(na, (i64)CH), CB = SMX_CEIL_DIV(nb, (i64)CH);
+  for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += BLOCK) (&c[0][0])[i] = 0;
+  __syncthreads();
+  const u64 lt = lanemask_lt();
+  bool bad = false;
+  for (int j = 0; j < CH_PER_BLOCK; ++j) {
+    const i64 g = (i64)blockIdx.x * CH_PER_BLOCK + j;  // global chunk: A chunks then B chunks
+    if (g >= CA + CB) break;
+    const int side = g >= CA;
+    const i64 cc = side ? g - CA : g;
+    const i64 len = side ? nb : na;
+    const i64 p = cc * CH + threadIdx.x;
+    const bool valid = p < len;
+    u32 k = valid ? kind[(side ? na : 0) + p] : 0u;
+    bad |= valid && k >= SMX_N_KINDS;
+    k = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
+    const u64 peers = wave_peers<5>(k, valid);
+    if (valid && (peers & lt) == 0) atomicAdd(&c[j][k], (u32)__popcll(peers));
+  }
+  if (bad) meta->bad_sym = 1;
+  __syncthreads();
+  for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += BLOCK) {
+    const int j = i / SMX_N_KINDS, k = i % SMX_N_KINDS;
+    const i64 g = (i64)blockIdx.x * CH_PER_BLOCK + j;
+    if (g >= CA + CB) continue;
+    const int side = g >= CA;
+    const i64 cc = side ? g - CA : g;
+    cnt[((i64)side * SMX_N_KINDS + k) * CM + cc] = c[j][k];
+  }
+}
+
+// One block per (side, kind) column: exclusive scan in place; totals into meta.
+__global__ void __launch_bounds__(BLOCK) k_cscan(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
+                                                 ComposeMeta* meta) {
+  __shared__ u32 s[NWAVES + 1];
+  const int side = blockIdx.x / SMX_N_KINDS, k = blockIdx.x % SMX_N_KINDS;
+  const i64 C = SMX_CEIL_DIV(side ? nb : na, (i64)CH);
+  u32* col = cnt + ((i64)side * SMX_N_KINDS + k) * CM;
+  u32 carry = 0;
+  for (i64 r0 = 0; r0 < C; r0 += BLOCK * 8) {
+    const i64 b = r0 + (i64)threadIdx.x * 8;
+    u32 v[8];
+    u32 acc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = b + j < C ? col[b + j] : 0u;
+      acc += v[j];
+    }
+    u32 tot;
+    u32 run = carry + block_excl_scan<OpSum, u32>(acc, s, &tot);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (b + j < C) col[b + j] = run;
+      run += v[j];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) {
+    col[C] = carry;  // prefix at the end of the branch (a window may start there)
+    atomicAdd((unsigned long long*)&meta->kcnt[k], (unsigned long long)carry);
+    if (k == KREN) meta->n_ren_side[side] = carry;
+  }
+}
+
 // Per-window counts: each kind and renames per branch (+ moves with a None value
-// in the generic layout).  perm == nullptr: presorted layout (branch position j is
-// op j; reads only kind bytes -- the layout itself is verified by k_window_f).
-// Column-major [c][W].
+// in the generic layout).  Column-major [c][W].
+//  * presorted layout (perm == nullptr): branch position j is op j; only the kind
+//    bytes are read, 16 per lane (the layout itself is verified by k_window_f);
+//  * generic layout: through the sort permutation, one op per lane.
+__device__ __forceinline__ void wc_add_one(u32 k, u32 (&c)[SMX_N_KINDS], bool& bad) {
+  bad |= k >= SMX_N_KINDS;
+#pragma unroll
+  for (int kk = 0; kk < SMX_N_KINDS; ++kk) c[kk] += (k == (u32)kk);
+}
+
+__device__ __forceinline__ void wc_add_bytes(u32 x, u32 (&c)[SMX_N_KINDS], bool& bad) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wc_add_one((x >> (8 * q)) & 0xffu, c, bad);
+}
+
 __global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, const i32* __restrict__ v0,
                                                   const i32* __restrict__ v1, const u32* __restrict__ perm,
                                                   const i64* __restrict__ bnd, i64 na, i64 W,
@@ -216,29 +302,61 @@ __global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, c
   if (threadIdx.x < NCNT) c[threadIdx.x] = 0;
   __syncthreads();
   const i64 a0 = bnd[2 * w], b0 = bnd[2 * w + 1], a1 = bnd[2 * w + 2], b1 = bnd[2 * w + 3];
-  const bool presorted = perm == nullptr;
   bool bad = false;
-  const u64 lt = lanemask_lt();
-  for (int side = 0; side < 2; ++side) {
-    const i64 lo = side ? b0 : a0, hi = side ? b1 : a1, off = side ? na : 0;
-    // wave-uniform trip count so the ballots below see every lane
-    for (i64 j0 = lo; j0 < hi; j0 += BLOCK) {
-      const i64 j = j0 + threadIdx.x;
-      const bool valid = j < hi;
-      u32 k = 0;
-      bool none_mv = false;
-      if (valid) {
-        const u32 src = presorted ? (u32)(off + j) : perm[off + j];
-        const u32 k0 = kind[src];
-        bad |= k0 >= SMX_N_KINDS;
-        k = k0 < SMX_N_KINDS ? k0 : SMX_N_KINDS - 1;
-        if (!presorted) none_mv = k == KMOVE && (v0[src] < 0 || v1[src] < 0);
+  if (perm == nullptr) {
+    for (int side = 0; side < 2; ++side) {
+      const i64 off = side ? na : 0;
+      const i64 lo = off + (side ? b0 : a0), hi = off + (side ? b1 : a1);
+      if (hi <= lo) continue;
+      u32 cnt[SMX_N_KINDS];
+#pragma unroll
+      for (int kk = 0; kk < SMX_N_KINDS; ++kk) cnt[kk] = 0;
+      const i64 alo = (lo + 15) & ~(i64)15, ahi = hi & ~(i64)15;
+      if (alo >= ahi) {  // short range: bytes
+        for (i64 j = lo + threadIdx.x; j < hi; j += BLOCK) wc_add_one(kind[j], cnt, bad);
+      } else {
+        for (i64 j = lo + threadIdx.x; j < alo; j += BLOCK) wc_add_one(kind[j], cnt, bad);
+        for (i64 j = ahi + threadIdx.x; j < hi; j += BLOCK) wc_add_one(kind[j], cnt, bad);
+        const uint4* v = (const uint4*)(kind + alo);
+        for (i64 q = threadIdx.x; q < (ahi - alo) / 16; q += BLOCK) {
+          const uint4 x = v[q];
+          wc_add_bytes(x.x, cnt, bad);
+          wc_add_bytes(x.y, cnt, bad);
+          wc_add_bytes(x.z, cnt, bad);
+          wc_add_bytes(x.w, cnt, bad);
+        }
       }
-      const u64 peers = wave_peers<5>(k, valid);
-      if (valid && (peers & lt) == 0) atomicAdd(&c[k], (u32)__popcll(peers));
-      const u64 nm = __ballot(none_mv);
-      if (nm && (threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&c[CNT_NONE_MV], (u32)__popcll(nm));
-      if (valid && k == KREN && (peers & lt) == 0) atomicAdd(&c[CNT_REN_A + side], (u32)__popcll(peers));
+#pragma unroll
+      for (int kk = 0; kk < SMX_N_KINDS; ++kk) {
+        const u32 tot = wave_incl_sum(cnt[kk]);
+        if ((threadIdx.x & (WAVE - 1)) == WAVE - 1 && tot) {
+          atomicAdd(&c[kk], tot);
+          if (kk == KREN) atomicAdd(&c[CNT_REN_A + side], tot);
+        }
+      }
+    }
+  } else {
+    const u64 lt = lanemask_lt();
+    for (int side = 0; side < 2; ++side) {
+      const i64 lo = side ? b0 : a0, hi = side ? b1 : a1, off = side ? na : 0;
+      for (i64 j0 = lo; j0 < hi; j0 += BLOCK) {  // wave-uniform trip count for the ballots
+        const i64 j = j0 + threadIdx.x;
+        const bool valid = j < hi;
+        u32 k = 0;
+        bool none_mv = false;
+        if (valid) {
+          const u32 src = perm[off + j];
+          const u32 k0 = kind[src];
+          bad |= k0 >= SMX_N_KINDS;
+          k = k0 < SMX_N_KINDS ? k0 : SMX_N_KINDS - 1;
+          none_mv = k == KMOVE && (v0[src] < 0 || v1[src] < 0);
+        }
+        const u64 peers = wave_peers<5>(k, valid);
+        if (valid && (peers & lt) == 0) atomicAdd(&c[k], (u32)__popcll(peers));
+        const u64 nm = __ballot(none_mv);
+        if (nm && (threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&c[CNT_NONE_MV], (u32)__popcll(nm));
+        if (valid && k == KREN && (peers & lt) == 0) atomicAdd(&c[CNT_REN_A + side], (u32)__popcll(peers));
+      }
     }
   }
   if (bad) meta->bad_sym = 1;
@@ -378,48 +496,44 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
     run = lo;
   }
   const u64 lt = lanemask_lt();
+  const u64 nlast = E.n - 1;
+  const u64 rlast = re > rs ? re - rs - 1 : 0;
   for (int bt = 0; bt < EMIT_WT / (WAVE * EMIT_B); ++bt) {
     const u64 t0 = w0 + (u64)bt * WAVE * EMIT_B;
     if (t0 >= E.n) break;
-    u64 bal[EMIT_B];
-    i32 src[EMIT_B], a[EMIT_B], f[EMIT_B], c[EMIT_B];
+    // every load unconditional (clamped addresses): the batch's loads overlap
+    i32 src[EMIT_B], ma[EMIT_B], mf[EMIT_B];
     u32 sy[EMIT_B];
+    u8 skb[EMIT_B];
 #pragma unroll
     for (int j = 0; j < EMIT_B; ++j) {
       const u64 T = t0 + (u64)j * WAVE + lane;
-      const bool sk = T < E.n && T >= rs && T < re && E.skip[T - rs];
-      bal[j] = __ballot(sk);
-      src[j] = T < E.n ? E.order[T] : 0;
-      if (T < rs) {
-        a[j] = E.mvA[T];
-        f[j] = E.mvF[T];
-        c[j] = -1;
-      } else {
-        sy[j] = T < E.n ? min(E.symT[T], E.smax) : 0u;
-      }
+      const u64 Tc = T < E.n ? T : nlast;
+      src[j] = E.order[Tc];
+      sy[j] = min(E.symT[Tc], E.smax);
+      ma[j] = E.mvA[Tc];
+      mf[j] = E.mvF[Tc];
+      const u64 m = Tc >= rs ? Tc - rs : 0;
+      skb[j] = E.skip[m < rlast ? m : rlast];
     }
+    int4 F[EMIT_B];
+#pragma unroll
+    for (int j = 0; j < EMIT_B; ++j) F[j] = E.fin[sy[j]];
 #pragma unroll
     for (int j = 0; j < EMIT_B; ++j) {
       const u64 T = t0 + (u64)j * WAVE + lane;
-      if (T >= rs && T < E.n) {
-        const int4 F = E.fin[sy[j]];
-        a[j] = F.x;
-        f[j] = F.y;
-        c[j] = T < re ? -1 : F.z;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < EMIT_B; ++j) {
-      const u64 T = t0 + (u64)j * WAVE + lane;
-      const bool sk = (bal[j] >> lane) & 1;
+      const bool in_ren = T >= rs && T < re;
+      const bool sk = T < E.n && in_ren && skb[j];
+      const u64 bal = __ballot(sk);
       if (T < E.n && !sk) {
-        const u64 o = T - run - __popcll(bal[j] & lt);
+        const u64 o = T - run - __popcll(bal & lt);
+        const bool mv = T < rs;
         E.out_order[o] = src[j];
-        E.out_addr[o] = a[j];
-        E.out_file[o] = f[j];
-        E.out_ctx[o] = c[j];
+        E.out_addr[o] = mv ? ma[j] : F[j].x;
+        E.out_file[o] = mv ? mf[j] : F[j].y;
+        E.out_ctx[o] = (mv || in_ren) ? -1 : F[j].z;
       }
-      run += __popcll(bal[j]);
+      run += __popcll(bal);
     }
   }
 }
@@ -465,7 +579,7 @@ enum Buf {
   B_META, B_BND, B_WCNT, B_WOFF, B_STS, B_SHI, B_SLO, B_PERM, B_RKEY, B_RVAL, B_RK2, B_RV2,
   B_RHIST, B_PART, B_ORDER, B_SYMT, B_MVA, B_MVF, B_MSYM, B_MCLS, B_MSTR, B_MSIDE, B_MOWN,
   B_RAB, B_FLAGS, B_FPOS, B_CAND, B_Q, B_PM, B_NCONF, B_NREAL, B_COFF, B_SKIP, B_SKIPEX,
-  B_TABA, B_TABF, B_TABR, B_FIN, B_PREFA, B_PREFF, B_REC, B_TBHIST, B_TBTOT, B_N
+  B_TABA, B_TABF, B_TABR, B_FIN, B_PREFA, B_PREFF, B_REC, B_TBHIST, B_TBTOT, B_CCNT, B_N
 };
 
 static Layout layout(i64 na, i64 nb, i64 n_sym) {
@@ -497,9 +611,10 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_TABA] = sz[B_TABF] = sz[B_TABR] = (size_t)ns * 8;
   sz[B_FIN] = (size_t)ns * 16;
   sz[B_PREFA] = sz[B_PREFF] = (size_t)nn * 4;
-  sz[B_REC] = (size_t)nn * 16;
+  sz[B_REC] = (size_t)nn * 8;
   sz[B_TBHIST] = (size_t)TB_MAXBK * SMX_CEIL_DIV(nn, (i64)TB_TILE) * 4;
   sz[B_TBTOT] = 16;
+  sz[B_CCNT] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)256) + 2) * 4;
   Layout L;
   size_t acc = 0;
   for (int i = 0; i < B_N; ++i) {
@@ -539,6 +654,8 @@ struct Ctx {
 
 static WinArgs win_args(const Ctx& C) {
   WinArgs P;
+  P.cpre = nullptr;
+  P.CM = 0;
   P.kind = C.ops->kind;
   P.sym = C.ops->sym;
   P.v0 = C.ops->v0;
@@ -619,21 +736,21 @@ static int launch_tail(const Ctx& C, const WinArgs& P) {
       const int nblk = (int)SMX_CEIL_DIV((u64)n, (u64)TB_TILE);
       u32* hist = C.ws<u32>(B_TBHIST);
       u32* total = C.ws<u32>(B_TBTOT);
-      uint4* rec = C.ws<uint4>(B_REC);
+      u64* rec = C.ws<u64>(B_REC);
       hipLaunchKernelGGL(k_tb_hist, dim3(nblk), dim3(BLOCK), 0, st, A, hist, nblk);
       HIP_TRY((scan_excl<OpSum, u32, u32>(hist, hist, (i64)nbk * nblk, nullptr, part, total, st)));
       hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(BLOCK), 0, st, A, hist, nblk, rec);
       hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, hist, nblk, total, rec, n_sym, fin);
     } else {
       // very large symbol spaces: device-scope atomics on the packed keys
-      u64* tabA = C.ws<u64>(B_TABA);
-      u64* tabF = C.ws<u64>(B_TABF);
-      u64* tabR = C.ws<u64>(B_TABR);
-      HIP_TRY(hipMemsetAsync(tabA, 0, (size_t)n_sym * 8, st));
-      HIP_TRY(hipMemsetAsync(tabF, 0, (size_t)n_sym * 8, st));
-      HIP_TRY(hipMemsetAsync(tabR, 0, (size_t)n_sym * 8, st));
+      u32* tabA = C.ws<u32>(B_TABA);
+      u32* tabF = C.ws<u32>(B_TABF);
+      u32* tabR = C.ws<u32>(B_TABR);
+      HIP_TRY(hipMemsetAsync(tabA, 0, (size_t)n_sym * 4, st));
+      HIP_TRY(hipMemsetAsync(tabF, 0, (size_t)n_sym * 4, st));
+      HIP_TRY(hipMemsetAsync(tabR, 0, (size_t)n_sym * 4, st));
       hipLaunchKernelGGL(k_tab_atomic, dim3(grid_for(n)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR);
-      hipLaunchKernelGGL(k_finalize, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, tabA, tabF, tabR, n_sym, fin);
+      hipLaunchKernelGGL(k_finalize, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR, n_sym, fin);
     }
   }
   HIP_TRY(hipGetLastError());
@@ -670,13 +787,18 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   const i64 W = SMX_CEIL_DIV(C.n, tgt);
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts, C.na, C.nb,
                      W, tgt, bnd);
-  hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, C.ops->kind, C.ops->v0, C.ops->v1,
-                     (const u32*)nullptr, bnd, C.na, W, wcnt, meta);
-  hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, W, meta);
+  const i64 CM = SMX_CEIL_DIV(C.na > C.nb ? C.na : C.nb, (i64)CH) + 1;
+  const i64 nchunk = SMX_CEIL_DIV(C.na, (i64)CH) + SMX_CEIL_DIV(C.nb, (i64)CH);
+  u32* ccnt = C.ws<u32>(B_CCNT);
+  hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK)), dim3(BLOCK), 0, st, C.ops->kind,
+                     C.na, C.nb, CM, ccnt, meta);
+  hipLaunchKernelGGL(k_cscan, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, meta);
   hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_PLAN);
   WinArgs P = win_args(C);
+  P.cpre = ccnt;
+  P.CM = CM;
   P.kts = C.ops->ts;
   P.khi = C.ops->oid_hi;
   P.klo = C.ops->oid_lo;

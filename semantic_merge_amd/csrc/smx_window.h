@@ -27,6 +27,7 @@
 #define KMOVE SMX_KIND_MOVE
 #define KREN SMX_KIND_RENAME
 #define NCHUNK (WIN_CAP / WAVE)
+#define CH 256                     // chunk of the presorted kind histogram
 
 struct WinArgs {
   const u8* kind;
@@ -44,7 +45,9 @@ struct WinArgs {
   i64 n_sym;
   int ablate;       // diagnostics only (SMX_ABLATE): skip phases, results invalid
   const i64* bnd;
-  const u32* woff;  // [NCNT][W] exclusive offsets over windows
+  const u32* woff;  // [NCNT][W] exclusive offsets over windows (generic plan)
+  const u32* cpre;  // presorted plan: [2][kinds][CM] chunk prefixes (256-op chunks)
+  i64 CM;
   ComposeMeta* meta;
   i32* order;
   u32* symT;
@@ -103,6 +106,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   __shared__ u32 kbase[SMX_N_KINDS + 1];
   __shared__ u32 wck[SMX_N_KINDS];
   __shared__ u64 base[SMX_N_KINDS + 1];
+  __shared__ u32 woffk[SMX_N_KINDS + 2];  // this window's offsets: kinds, renames of A, of B
   u32* phi = (u32*)sts;               // slot space: top 32 bits of oid_hi (after step 4)
   u16* rown = fin;                    // rename rank within its branch (after step 5)
 
@@ -129,20 +133,29 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   i32 v0_r[WF_ITEMS], v1_r[WF_ITEMS];
   u32 k_r[WF_ITEMS];
   bool bad = false;
+  // all loads are issued unconditionally (clamped to a valid op) so that the
+  // WF_ITEMS x 6 loads of a lane are in flight together; the guards apply to the
+  // LDS stores only
+  u64 ts_r[WF_ITEMS];
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i) {
+    const int e = t + WF_NT * i;
+    const int ec = e < sz ? e : 0;
+    const i64 j = ec < na ? a0 + ec : bpos + ec;
+    k_r[i] = P.kind[j];
+    ts_r[i] = P.kts[j];
+    hi_r[i] = (u32)(P.khi[j] >> 32);
+    sym_r[i] = P.sym[j];
+    v0_r[i] = P.v0[j];
+    v1_r[i] = P.v1[j];
+  }
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
     if (e < sz) {
-      const i64 j = e < na ? a0 + e : bpos + e;
-      const u32 k = P.kind[j];
-      const u64 tv = P.kts[j];
-      hi_r[i] = (u32)(P.khi[j] >> 32);
-      sym_r[i] = P.sym[j];
-      v0_r[i] = P.v0[j];
-      v1_r[i] = P.v1[j];
-      bad |= (k >= SMX_N_KINDS) || (sym_r[i] >= (u64)P.n_sym);
-      k_r[i] = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
-      sts[e] = tv;
+      bad |= (k_r[i] >= SMX_N_KINDS) || (sym_r[i] >= (u64)P.n_sym);
+      k_r[i] = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
+      sts[e] = ts_r[i];
       skind[e] = (u8)k_r[i];
     }
   }
@@ -153,6 +166,28 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   if (bad) P.meta->bad_sym = 1;
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
+  // window offsets = chunk prefix at the window start + kinds of the <= 255 ops
+  // between that chunk start and the window start (per branch)
+  if (t < SMX_N_KINDS) {
+    woffk[t] = P.cpre[(i64)t * P.CM + a0 / CH] + P.cpre[(i64)(SMX_N_KINDS + t) * P.CM + b0 / CH];
+  } else if (t < SMX_N_KINDS + 2) {
+    const int sd = t - SMX_N_KINDS;
+    woffk[t] = P.cpre[(i64)(sd * SMX_N_KINDS + KREN) * P.CM + (sd ? b0 : a0) / CH];
+  }
+  __syncthreads();
+  {
+    const int pa = (int)(a0 % CH), pb = (int)(b0 % CH);
+    // lanes 0..255: branch A partial chunk, lanes 256..511: branch B
+    const int side = t >= CH;
+    const int q = t - side * CH;
+    if (q < (side ? pb : pa)) {
+      const i64 j = side ? (P.na + b0 - pb + q) : (a0 - pa + q);
+      u32 k = P.kind[j];
+      k = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
+      atomicAdd(&woffk[k], 1u);
+      if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + side], 1u);
+    }
+  }
   __syncthreads();
 
   // presorted-layout check: every adjacent pair of each branch log is
@@ -353,12 +388,12 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     }
   }
   __syncthreads();
-  const u64 wofs_ra = P.woff[(i64)CNT_REN_A * P.W + w], wofs_rb = P.woff[(i64)CNT_REN_B * P.W + w];
+  const u64 wofs_ra = woffk[SMX_N_KINDS], wofs_rb = woffk[SMX_N_KINDS + 1];
   const u64 nall = (u64)(P.na + P.nb);
   for (int x = t; x < sz; x += WF_NT) {
     const int e = sord[x];
     const u32 k = skind[e];
-    const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (u32)(x - kbase[k]);
+    const u64 T = base[k] + woffk[k] + (u32)(x - kbase[k]);
     if (T >= nall) continue;  // only a failed (discarded) presorted plan can trip this
     const u32 s = st_a[e];
     P.order[T] = (i32)(e < na ? a0 + e : bpos + e);
@@ -388,7 +423,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     const int e = sord[x];
     const u32 k = skind[e];
     if (k != KMOVE && k != KREN) continue;
-    const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (u32)(x - kbase[k]);
+    const u64 T = base[k] + woffk[k] + (u32)(x - kbase[k]);
     if (T >= nall) continue;
     if (k == KMOVE) P.mvF[T] = st_b[e];
     else P.Mstr[T - base[KREN]] = st_b[e];
