@@ -31,8 +31,38 @@ struct ComposeMeta {
   u64 key_and[2][3];
   u64 n_cand;                // DivergentRename candidate starts
   u64 n_conf;                // conflicts (real)
-  u64 pad[8];
+  u32 vbits[4];              // OR of (value + 1) over table values: addr, file, ctx (packing widths)
+  u64 pad[6];
 };
+
+// Per-symbol final states (addr, file, ctx).  When the bit widths of (value + 1)
+// add up to <= 64 they are packed into 8 bytes per symbol (half the gather
+// footprint for k_emit); otherwise int4 entries.
+struct FinPack {
+  u32 wa, wf;
+  bool packed;
+};
+
+__device__ __forceinline__ u32 bit_width32(u32 x) { return x ? 32u - (u32)__clz((int)x) : 0u; }
+
+__device__ __forceinline__ FinPack fin_pack_of(const u32* vbits, bool allow) {
+  const u32 wa = bit_width32(vbits[0]), wf = bit_width32(vbits[1]), wc = bit_width32(vbits[2]);
+  return FinPack{wa, wf, allow && wa + wf + wc <= 64};
+}
+
+__device__ __forceinline__ u64 fin_encode(const FinPack& P, int a, int f, int c) {
+  const u64 x = (u64)(u32)(a + 1) | ((u64)(u32)(f + 1) << P.wa);
+  return P.wa + P.wf >= 64 ? x : x | ((u64)(u32)(c + 1) << (P.wa + P.wf));
+}
+
+__device__ __forceinline__ int4 fin_decode(const FinPack& P, u64 x) {
+  const u64 ma = P.wa >= 64 ? ~0ull : ((1ull << P.wa) - 1), mf = P.wf >= 64 ? ~0ull : ((1ull << P.wf) - 1);
+  const int a = (int)(u32)(x & ma) - 1;
+  const int f = (int)(u32)((x >> P.wa) & mf) - 1;
+  const u32 sc = P.wa + P.wf;
+  const int c = sc >= 64 ? -1 : (int)(u32)(x >> sc) - 1;
+  return make_int4(a, f, c, 0);
+}
 
 __device__ __forceinline__ u64 lanemask_lt() {
   const int lane = threadIdx.x & (WAVE - 1);
@@ -94,8 +124,9 @@ struct OpMax {
 };
 
 // Block-wide exclusive scan of one value per thread; returns the exclusive prefix,
-// writes the block aggregate to *total.  `s` must hold NWAVES+1 entries.
-template <typename Op, typename T>
+// writes the block aggregate to *total.  `s` must hold NW+1 entries (NW = waves
+// per block).
+template <typename Op, typename T, int NW = NWAVES>
 __device__ __forceinline__ T block_excl_scan(T v, T* s, T* total) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x / WAVE;
@@ -104,19 +135,19 @@ __device__ __forceinline__ T block_excl_scan(T v, T* s, T* total) {
   __syncthreads();
   if (threadIdx.x == 0) {
     T acc = Op::template identity<T>();
-    for (int i = 0; i < NWAVES; ++i) {
+    for (int i = 0; i < NW; ++i) {
       T x = s[i];
       s[i] = acc;
       acc = Op::apply(acc, x);
     }
-    s[NWAVES] = acc;
+    s[NW] = acc;
   }
   __syncthreads();
   T wpre = s[w];
   T excl_in_wave = __shfl_up(inc, 1, WAVE);
   if (lane == 0) excl_in_wave = Op::template identity<T>();
   T r = Op::apply(wpre, excl_in_wave);
-  *total = s[NWAVES];
+  *total = s[NW];
   __syncthreads();
   return r;
 }

@@ -141,46 +141,76 @@ __global__ void k_meta_init(ComposeMeta* meta) {
     for (int q = 0; q < 3; ++q) meta->key_and[s][q] = ~0ull;
 }
 
-// Presorted windows: boundary k sits at the merge-path split of diagonal k*WIN_TGT
+// Presorted windows: boundary k sits at the merge-path split of diagonal k*tgt
 // (timestamps, A first on ties), snapped down to the first op of that timestamp on
 // both branches, so every (timestamp) group lands whole in one window.
-__global__ void k_fpart(const u64* __restrict__ ts, i64 na, i64 nb, i64 W, i64 tgt, i64* __restrict__ bnd) {
+// tgt is a multiple of CH, so at split candidates m = CH*i the merge-path test
+// A[m] <= B[d-1-m] reads only chunk samples (sA[i] = A[CH*i], sB[j] =
+// B[CH*j + CH-1]; 1/256 of the keys, cache-resident): the first level of the
+// search runs on them, the second inside one chunk.  The snap gallops back over
+// the (short) run of equal timestamps.
+__global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ sA, const u64* __restrict__ sB,
+                        i64 na, i64 nb, i64 W, i64 tgt, i64* __restrict__ bnd) {
   const i64 k = (i64)blockIdx.x * BLOCK + threadIdx.x;
   if (k > W) return;
   const i64 n = na + nb;
   const u64* A = ts;
   const u64* B = ts + na;
   const i64 d = k * tgt;
-  if (k == 0) {
-    bnd[0] = 0;
-    bnd[1] = 0;
+  if (k == 0 || d >= n || k == W) {
+    bnd[2 * k] = k == 0 ? 0 : na;
+    bnd[2 * k + 1] = k == 0 ? 0 : nb;
     return;
   }
-  if (d >= n || k == W) {
-    bnd[2 * k] = na;
-    bnd[2 * k + 1] = nb;
-    return;
-  }
-  i64 lo = d - nb > 0 ? d - nb : 0, hi = d < na ? d : na;
-  while (lo < hi) {
-    i64 mid = (lo + hi) >> 1;
-    if (A[mid] <= B[d - 1 - mid]) lo = mid + 1;
-    else hi = mid;
+  const i64 lo0 = d - nb > 0 ? d - nb : 0, hi0 = d < na ? d : na;
+  i64 lo = lo0, hi = hi0;
+  if (lo < hi) {
+    const i64 ilo = SMX_CEIL_DIV(lo, (i64)CH), ihi = (hi - 1) / CH;  // samples inside [lo, hi)
+    if (ilo <= ihi) {
+      const i64 dj = d / CH - 1;
+      i64 l = ilo, h = ihi + 1;
+      while (l < h) {
+        const i64 mid = (l + h) >> 1;
+        if (sA[mid] <= sB[dj - mid]) l = mid + 1;
+        else h = mid;
+      }
+      // test true at CH*(l-1) (if l > ilo), false at CH*l (if l <= ihi)
+      if (l > ilo) lo = CH * (l - 1) + 1;
+      if (l <= ihi) hi = CH * l;
+    }
+    while (lo < hi) {
+      const i64 mid = (lo + hi) >> 1;
+      if (A[mid] <= B[d - 1 - mid]) lo = mid + 1;
+      else hi = mid;
+    }
   }
   const i64 a = lo, b = d - lo;
   const u64 tau = (a < na && (b >= nb || A[a] <= B[b])) ? A[a] : B[b];
-  lo = 0; hi = na;
-  while (lo < hi) {
-    i64 mid = (lo + hi) >> 1;
-    if (A[mid] < tau) lo = mid + 1; else hi = mid;
+  // first index of each branch with ts >= tau: at or before the split
+  i64 r[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const u64* X = s ? B : A;
+    i64 h = s ? b : a;  // X[h] >= tau, or h == branch length
+    i64 step = 1, l = 0;
+    while (h > 0) {
+      const i64 cand = h - step > 0 ? h - step : 0;
+      if (X[cand] < tau) {
+        l = cand + 1;
+        break;
+      }
+      h = cand;
+      step *= 2;
+    }
+    while (l < h) {
+      const i64 mid = (l + h) >> 1;
+      if (X[mid] < tau) l = mid + 1;
+      else h = mid;
+    }
+    r[s] = l;
   }
-  bnd[2 * k] = lo;
-  lo = 0; hi = nb;
-  while (lo < hi) {
-    i64 mid = (lo + hi) >> 1;
-    if (B[mid] < tau) lo = mid + 1; else hi = mid;
-  }
-  bnd[2 * k + 1] = lo;
+  bnd[2 * k] = r[0];
+  bnd[2 * k + 1] = r[1];
 }
 
 // Generic windows over branch logs sorted by (ts, oid): fixed diagonals of WIN_CAP.
@@ -208,72 +238,133 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 // A window derives its T offsets from the chunk prefixes at its start plus the
 // kinds of at most 255 ops before it.  Coalesced: iteration j of a block reads
 // chunk j, lane t its byte t.
-#define CH_PER_BLOCK 16
+#define CH_PER_BLOCK (BLOCK / 16)   // 16 lanes x 16 kind bytes per 256-op chunk
+#define KH_COPIES 8                 // counter copies (lane & 7) against LDS atomic conflicts
 
-__global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, i64 na, i64 nb, i64 CM,
-                                                 u32* __restrict__ cnt, ComposeMeta* meta) {
-  __shared__ u32 c[CH_PER_BLOCK][SMX_N_KINDS];
+// Block b counts global chunks [b*CH_PER_BLOCK, ...) (A chunks, then B chunks):
+// lane t reads bytes [16*(t%16), +16) of chunk t/16 (one 16-byte load when
+// aligned) and adds each byte to its (chunk, kind) counter with an LDS atomic
+// into one of KH_COPIES copies.
+__global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, const u64* __restrict__ ts,
+                                                 i64 na, i64 nb, i64 CM, u32* __restrict__ cnt,
+                                                 u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta) {
+  __shared__ u32 c[KH_COPIES][CH_PER_BLOCK][SMX_N_KINDS];
   const i64 CA = SMX_CEIL_DIV(na, (i64)CH), CB = SMX_CEIL_DIV(nb, (i64)CH);
-  for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += BLOCK) (&c[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < KH_COPIES * CH_PER_BLOCK * SMX_N_KINDS; i += BLOCK) (&c[0][0][0])[i] = 0;
+  const int j = threadIdx.x / 16, q = threadIdx.x % 16;
+  const i64 g = (i64)blockIdx.x * CH_PER_BLOCK + j;
+  const int side = g >= CA;
+  const i64 cc = side ? g - CA : g;
+  const i64 len = side ? nb : na;
+  const i64 r0 = cc * CH + q * 16;  // branch position of this lane's first byte
+  const int nv = g < CA + CB ? (int)(len - r0 < 0 ? 0 : (len - r0 < 16 ? len - r0 : 16)) : 0;
+  const u8* src = kind + (side ? na : 0) + r0;
+  // timestamp samples for k_fpart: first op of each A chunk, last op of each full B chunk
+  if (g < CA + CB) {
+    if (!side && q == 0) sA[cc] = ts[cc * CH];
+    if (side && q == 15 && nv == 16) sB[cc] = ts[na + cc * CH + CH - 1];
+  }
+  u32 w[4] = {0u, 0u, 0u, 0u};
+  if (nv == 16 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    const uint4 v = *reinterpret_cast<const uint4*>(src);
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  } else {
+#pragma unroll
+    for (int y = 0; y < 16; ++y)
+      if (y < nv) w[y >> 2] |= (u32)src[y] << (8 * (y & 3));
+  }
   __syncthreads();
-  const u64 lt = lanemask_lt();
+  u32* ck = c[threadIdx.x & (KH_COPIES - 1)][j];
   bool bad = false;
-  for (int j = 0; j < CH_PER_BLOCK; ++j) {
-    const i64 g = (i64)blockIdx.x * CH_PER_BLOCK + j;  // global chunk: A chunks then B chunks
-    if (g >= CA + CB) break;
-    const int side = g >= CA;
-    const i64 cc = side ? g - CA : g;
-    const i64 len = side ? nb : na;
-    const i64 p = cc * CH + threadIdx.x;
-    const bool valid = p < len;
-    u32 k = valid ? kind[(side ? na : 0) + p] : 0u;
-    bad |= valid && k >= SMX_N_KINDS;
+#pragma unroll
+  for (int y = 0; y < 16; ++y) {
+    if (y >= nv) break;
+    u32 k = (w[y >> 2] >> (8 * (y & 3))) & 0xffu;
+    bad |= k >= SMX_N_KINDS;
     k = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
-    const u64 peers = wave_peers<5>(k, valid);
-    if (valid && (peers & lt) == 0) atomicAdd(&c[j][k], (u32)__popcll(peers));
+    atomicAdd(&ck[k], 1u);
   }
   if (bad) meta->bad_sym = 1;
   __syncthreads();
   for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += BLOCK) {
-    const int j = i / SMX_N_KINDS, k = i % SMX_N_KINDS;
-    const i64 g = (i64)blockIdx.x * CH_PER_BLOCK + j;
-    if (g >= CA + CB) continue;
-    const int side = g >= CA;
-    const i64 cc = side ? g - CA : g;
-    cnt[((i64)side * SMX_N_KINDS + k) * CM + cc] = c[j][k];
+    const int jj = i / SMX_N_KINDS, k = i % SMX_N_KINDS;
+    const i64 gg = (i64)blockIdx.x * CH_PER_BLOCK + jj;
+    if (gg >= CA + CB) continue;
+    u32 s = 0;
+#pragma unroll
+    for (int cp = 0; cp < KH_COPIES; ++cp) s += c[cp][jj][k];
+    const int sd = gg >= CA;
+    cnt[((i64)sd * SMX_N_KINDS + k) * CM + (sd ? gg - CA : gg)] = s;
   }
 }
 
-// One block per (side, kind) column: exclusive scan in place; totals into meta.
-__global__ void __launch_bounds__(BLOCK) k_cscan(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
-                                                 ComposeMeta* meta) {
+// Exclusive scan of each (side, kind) column of chunk counts in three fully
+// parallel phases over tiles of CS_TILE chunks: tile sums; scan of the tile sums
+// (+ column totals into meta); tile scans.
+#define CS_TILE (BLOCK * 8)
+
+__global__ void __launch_bounds__(BLOCK) k_cscan_up(const u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
+                                                    i64 NT, u32* __restrict__ tsum) {
   __shared__ u32 s[NWAVES + 1];
-  const int side = blockIdx.x / SMX_N_KINDS, k = blockIdx.x % SMX_N_KINDS;
+  const int col = blockIdx.y;
+  const i64 C = SMX_CEIL_DIV(col >= SMX_N_KINDS ? nb : na, (i64)CH);
+  const i64 t0 = (i64)blockIdx.x * CS_TILE;
+  if (t0 >= C) return;
+  const u32* colp = cnt + (i64)col * CM;
+  const i64 b = t0 + (i64)threadIdx.x * 8;
+  u32 acc = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc += b + j < C ? colp[b + j] : 0u;
+  u32 tot;
+  block_excl_scan<OpSum, u32>(acc, s, &tot);
+  if (threadIdx.x == 0) tsum[(i64)col * NT + blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_cscan_mid(u32* __restrict__ tsum, i64 na, i64 nb, i64 CM, i64 NT,
+                                                     u32* __restrict__ cnt, ComposeMeta* meta) {
+  __shared__ u32 s[NWAVES + 1];
+  const int col = blockIdx.x;
+  const int side = col / SMX_N_KINDS, k = col % SMX_N_KINDS;
   const i64 C = SMX_CEIL_DIV(side ? nb : na, (i64)CH);
-  u32* col = cnt + ((i64)side * SMX_N_KINDS + k) * CM;
+  const i64 nt = SMX_CEIL_DIV(C, (i64)CS_TILE);
   u32 carry = 0;
-  for (i64 r0 = 0; r0 < C; r0 += BLOCK * 8) {
-    const i64 b = r0 + (i64)threadIdx.x * 8;
-    u32 v[8];
-    u32 acc = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      v[j] = b + j < C ? col[b + j] : 0u;
-      acc += v[j];
-    }
+  for (i64 r0 = 0; r0 < nt; r0 += BLOCK) {
+    const i64 r = r0 + threadIdx.x;
+    const u32 v = r < nt ? tsum[(i64)col * NT + r] : 0u;
     u32 tot;
-    u32 run = carry + block_excl_scan<OpSum, u32>(acc, s, &tot);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (b + j < C) col[b + j] = run;
-      run += v[j];
-    }
+    const u32 ex = block_excl_scan<OpSum, u32>(v, s, &tot);
+    if (r < nt) tsum[(i64)col * NT + r] = carry + ex;
     carry += tot;
   }
   if (threadIdx.x == 0) {
-    col[C] = carry;  // prefix at the end of the branch (a window may start there)
+    cnt[(i64)col * CM + C] = carry;  // prefix at the end of the branch (a window may start there)
     atomicAdd((unsigned long long*)&meta->kcnt[k], (unsigned long long)carry);
     if (k == KREN) meta->n_ren_side[side] = carry;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_cscan_down(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM, i64 NT,
+                                                      const u32* __restrict__ tsum) {
+  __shared__ u32 s[NWAVES + 1];
+  const int col = blockIdx.y;
+  const i64 C = SMX_CEIL_DIV(col >= SMX_N_KINDS ? nb : na, (i64)CH);
+  const i64 t0 = (i64)blockIdx.x * CS_TILE;
+  if (t0 >= C) return;
+  u32* colp = cnt + (i64)col * CM;
+  const i64 b = t0 + (i64)threadIdx.x * 8;
+  u32 v[8];
+  u32 acc = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    v[j] = b + j < C ? colp[b + j] : 0u;
+    acc += v[j];
+  }
+  u32 tot;
+  u32 run = tsum[(i64)col * NT + blockIdx.x] + block_excl_scan<OpSum, u32>(acc, s, &tot);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (b + j < C) colp[b + j] = run;
+    run += v[j];
   }
 }
 
@@ -457,6 +548,7 @@ struct EmitArgs {
   const ComposeMeta* meta;
   u64 n;
   u32 smax;
+  int allow_pack;  // the final-state table came from k_tb_reduce (packs when widths fit)
   i32* out_order;
   i32* out_addr;
   i32* out_file;
@@ -475,6 +567,9 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
   const ComposeMeta* M = E.meta;
   if (M->f_fail | M->bad_sym) return;
   const u64 nskip = 2 * M->n_conf;
+  const FinPack FP = fin_pack_of(M->vbits, E.allow_pack != 0);
+  const u64* fin8 = reinterpret_cast<const u64*>(E.fin);
+  auto fin_at = [&](u32 s) -> int4 { return FP.packed ? fin_decode(FP, fin8[s]) : E.fin[s]; };
   const u64 rs = min(M->kcnt[KMOVE], E.n);
   const u64 re = min(rs + M->kcnt[KREN], E.n);
   const int lane = threadIdx.x & (WAVE - 1);
@@ -496,42 +591,129 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
     run = lo;
   }
   const u64 lt = lanemask_lt();
-  const u64 nlast = E.n - 1;
-  const u64 rlast = re > rs ? re - rs - 1 : 0;
   for (int bt = 0; bt < EMIT_WT / (WAVE * EMIT_B); ++bt) {
     const u64 t0 = w0 + (u64)bt * WAVE * EMIT_B;
     if (t0 >= E.n) break;
-    // every load unconditional (clamped addresses): the batch's loads overlap
-    i32 src[EMIT_B], ma[EMIT_B], mf[EMIT_B];
-    u32 sy[EMIT_B];
-    u8 skb[EMIT_B];
+    const u64 t1 = t0 + (u64)WAVE * EMIT_B;  // batch [t0, t1), wave-uniform
+    if (t1 <= rs && t1 <= E.n) {
+      // all moves, no skips: own values
+      i32 src[EMIT_B], ma[EMIT_B], mf[EMIT_B];
 #pragma unroll
-    for (int j = 0; j < EMIT_B; ++j) {
-      const u64 T = t0 + (u64)j * WAVE + lane;
-      const u64 Tc = T < E.n ? T : nlast;
-      src[j] = E.order[Tc];
-      sy[j] = min(E.symT[Tc], E.smax);
-      ma[j] = E.mvA[Tc];
-      mf[j] = E.mvF[Tc];
-      const u64 m = Tc >= rs ? Tc - rs : 0;
-      skb[j] = E.skip[m < rlast ? m : rlast];
+      for (int j = 0; j < EMIT_B; ++j) {
+        const u64 T = t0 + (u64)j * WAVE + lane;
+        src[j] = E.order[T];
+        ma[j] = E.mvA[T];
+        mf[j] = E.mvF[T];
+      }
+#pragma unroll
+      for (int j = 0; j < EMIT_B; ++j) {
+        const u64 T = t0 + (u64)j * WAVE + lane;
+        E.out_order[T] = src[j];
+        E.out_addr[T] = ma[j];
+        E.out_file[T] = mf[j];
+        E.out_ctx[T] = -1;
+      }
+      continue;
     }
-    int4 F[EMIT_B];
+    if (t0 >= re) {
+      // all after the rename block: fixed shift, every op looks its symbol up
+      i32 src[EMIT_B];
+      u32 sy[EMIT_B];
 #pragma unroll
-    for (int j = 0; j < EMIT_B; ++j) F[j] = E.fin[sy[j]];
+      for (int j = 0; j < EMIT_B; ++j) {
+        const u64 T = t0 + (u64)j * WAVE + lane;
+        const u64 Tc = T < E.n ? T : E.n - 1;
+        src[j] = E.order[Tc];
+        sy[j] = min(E.symT[Tc], E.smax);
+      }
+      int4 F[EMIT_B];
+      if (FP.packed) {
+        u64 x[EMIT_B];
+#pragma unroll
+        for (int j = 0; j < EMIT_B; ++j) x[j] = fin8[sy[j]];
+#pragma unroll
+        for (int j = 0; j < EMIT_B; ++j) F[j] = fin_decode(FP, x[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < EMIT_B; ++j) F[j] = E.fin[sy[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < EMIT_B; ++j) {
+        const u64 T = t0 + (u64)j * WAVE + lane;
+        if (T < E.n) {
+          const u64 o = T - nskip;
+          E.out_order[o] = src[j];
+          E.out_addr[o] = F[j].x;
+          E.out_file[o] = F[j].y;
+          E.out_ctx[o] = F[j].z;
+        }
+      }
+      continue;
+    }
+    if (t0 >= rs && t1 <= re) {
+      // all renames: final move state, skipped ones dropped
+      i32 src[EMIT_B];
+      u32 sy[EMIT_B];
+      u8 sk[EMIT_B];
+#pragma unroll
+      for (int j = 0; j < EMIT_B; ++j) {
+        const u64 T = t0 + (u64)j * WAVE + lane;
+        src[j] = E.order[T];
+        sy[j] = min(E.symT[T], E.smax);
+        sk[j] = E.skip[T - rs];
+      }
+      int4 F[EMIT_B];
+      if (FP.packed) {
+        u64 x[EMIT_B];
+#pragma unroll
+        for (int j = 0; j < EMIT_B; ++j) x[j] = fin8[sy[j]];
+#pragma unroll
+        for (int j = 0; j < EMIT_B; ++j) F[j] = fin_decode(FP, x[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < EMIT_B; ++j) F[j] = E.fin[sy[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < EMIT_B; ++j) {
+        const u64 T = t0 + (u64)j * WAVE + lane;
+        const u64 bal = __ballot(sk[j] != 0);
+        if (!sk[j]) {
+          const u64 o = T - run - __popcll(bal & lt);
+          E.out_order[o] = src[j];
+          E.out_addr[o] = F[j].x;
+          E.out_file[o] = F[j].y;
+          E.out_ctx[o] = -1;
+        }
+        run += __popcll(bal);
+      }
+      continue;
+    }
+    // general batch (a block boundary inside the batch)
 #pragma unroll
     for (int j = 0; j < EMIT_B; ++j) {
       const u64 T = t0 + (u64)j * WAVE + lane;
+      const bool valid = T < E.n;
       const bool in_ren = T >= rs && T < re;
-      const bool sk = T < E.n && in_ren && skb[j];
+      const bool sk = valid && in_ren && E.skip[T - rs];
       const u64 bal = __ballot(sk);
-      if (T < E.n && !sk) {
+      if (valid && !sk) {
         const u64 o = T - run - __popcll(bal & lt);
-        const bool mv = T < rs;
-        E.out_order[o] = src[j];
-        E.out_addr[o] = mv ? ma[j] : F[j].x;
-        E.out_file[o] = mv ? mf[j] : F[j].y;
-        E.out_ctx[o] = (mv || in_ren) ? -1 : F[j].z;
+        const i32 src = E.order[T];
+        i32 a, f, cc;
+        if (T < rs) {
+          a = E.mvA[T];
+          f = E.mvF[T];
+          cc = -1;
+        } else {
+          const int4 F = fin_at(min(E.symT[T], E.smax));
+          a = F.x;
+          f = F.y;
+          cc = in_ren ? -1 : F.z;
+        }
+        E.out_order[o] = src;
+        E.out_addr[o] = a;
+        E.out_file[o] = f;
+        E.out_ctx[o] = cc;
       }
       run += __popcll(bal);
     }
@@ -579,7 +761,7 @@ enum Buf {
   B_META, B_BND, B_WCNT, B_WOFF, B_STS, B_SHI, B_SLO, B_PERM, B_RKEY, B_RVAL, B_RK2, B_RV2,
   B_RHIST, B_PART, B_ORDER, B_SYMT, B_MVA, B_MVF, B_MSYM, B_MCLS, B_MSTR, B_MSIDE, B_MOWN,
   B_RAB, B_FLAGS, B_FPOS, B_CAND, B_Q, B_PM, B_NCONF, B_NREAL, B_COFF, B_SKIP, B_SKIPEX,
-  B_TABA, B_TABF, B_TABR, B_FIN, B_PREFA, B_PREFF, B_REC, B_TBHIST, B_TBTOT, B_CCNT, B_N
+  B_TABA, B_TABF, B_TABR, B_FIN, B_PREFA, B_PREFF, B_REC, B_TBHIST, B_TBTOT, B_CCNT, B_TSUM, B_SMP, B_N
 };
 
 static Layout layout(i64 na, i64 nb, i64 n_sym) {
@@ -615,6 +797,8 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_TBHIST] = (size_t)TB_MAXBK * SMX_CEIL_DIV(nn, (i64)TB_TILE) * 4;
   sz[B_TBTOT] = 16;
   sz[B_CCNT] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)256) + 2) * 4;
+  sz[B_SMP] = (size_t)(SMX_CEIL_DIV(nn, (i64)CH) + 4) * 8;
+  sz[B_TSUM] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)CH * CS_TILE) + 2) * 4;
   Layout L;
   size_t acc = 0;
   for (int i = 0; i < B_N; ++i) {
@@ -723,6 +907,7 @@ static int launch_tail(const Ctx& C, const WinArgs& P) {
 
   C.tm->begin(ST_TABLES);
   int4* fin = C.ws<int4>(B_FIN);
+  bool bucketed = false;
   {
     const i64 n_sym = C.n_sym;
     TbArgs A{P.symT, P.mvA, P.mvF, P.Msym, P.Mstr, skip, meta, (u64)n, 1u, 1u, (u32)(n_sym - 1), 0, 0};
@@ -731,15 +916,16 @@ static int launch_tail(const Ctx& C, const WinArgs& P) {
     if (width > TB_WIDTH) width = TB_WIDTH;
     const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);
     if (nbk <= TB_MAXBK) {
+      bucketed = true;
       A.width = (u32)width;
       A.nbk = (u32)nbk;
       const int nblk = (int)SMX_CEIL_DIV((u64)n, (u64)TB_TILE);
       u32* hist = C.ws<u32>(B_TBHIST);
       u32* total = C.ws<u32>(B_TBTOT);
       u64* rec = C.ws<u64>(B_REC);
-      hipLaunchKernelGGL(k_tb_hist, dim3(nblk), dim3(BLOCK), 0, st, A, hist, nblk);
+      hipLaunchKernelGGL(k_tb_hist, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk);
       HIP_TRY((scan_excl<OpSum, u32, u32>(hist, hist, (i64)nbk * nblk, nullptr, part, total, st)));
-      hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(BLOCK), 0, st, A, hist, nblk, rec);
+      hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk, rec);
       hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, hist, nblk, total, rec, n_sym, fin);
     } else {
       // very large symbol spaces: device-scope atomics on the packed keys
@@ -758,7 +944,7 @@ static int launch_tail(const Ctx& C, const WinArgs& P) {
 
   C.tm->begin(ST_EMIT);
   EmitArgs E{P.order, P.symT, P.mvA, P.mvF, skip, skiplist, fin, meta, (u64)n, (u32)(C.n_sym - 1),
-             C.out->order, C.out->addr, C.out->file, C.out->ctx};
+             bucketed ? 1 : 0, C.out->order, C.out->addr, C.out->file, C.out->ctx};
   const i64 ewaves = SMX_CEIL_DIV(n, (i64)EMIT_WT);
   hipLaunchKernelGGL(k_emit, dim3(SMX_CEIL_DIV(ewaves, (i64)NWAVES)), dim3(BLOCK), 0, st, E);
   hipLaunchKernelGGL(k_counts, dim3(1), dim3(1), 0, st, meta, (u64)n, C.out->counts);
@@ -784,15 +970,26 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
   if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
   if (tgt > WIN_CAP) tgt = WIN_CAP;
+  tgt -= tgt % CH;  // chunk-aligned diagonals (k_fpart's sampled first level)
   const i64 W = SMX_CEIL_DIV(C.n, tgt);
-  hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts, C.na, C.nb,
-                     W, tgt, bnd);
   const i64 CM = SMX_CEIL_DIV(C.na > C.nb ? C.na : C.nb, (i64)CH) + 1;
   const i64 nchunk = SMX_CEIL_DIV(C.na, (i64)CH) + SMX_CEIL_DIV(C.nb, (i64)CH);
   u32* ccnt = C.ws<u32>(B_CCNT);
+  u64* sA = C.ws<u64>(B_SMP);
+  u64* sB = sA + SMX_CEIL_DIV(C.na, (i64)CH) + 1;
   hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK)), dim3(BLOCK), 0, st, C.ops->kind,
-                     C.na, C.nb, CM, ccnt, meta);
-  hipLaunchKernelGGL(k_cscan, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, meta);
+                     C.ops->ts, C.na, C.nb, CM, ccnt, sA, sB, meta);
+  hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts, sA, sB, C.na,
+                     C.nb, W, tgt, bnd);
+  {
+    const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);
+    u32* tsum = C.ws<u32>(B_TSUM);
+    hipLaunchKernelGGL(k_cscan_up, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT, tsum);
+    hipLaunchKernelGGL(k_cscan_mid, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, tsum, C.na, C.nb, CM, NT, ccnt,
+                       meta);
+    hipLaunchKernelGGL(k_cscan_down, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT,
+                       tsum);
+  }
   hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_PLAN);
@@ -927,8 +1124,8 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
   }
   ComposeMeta hm;
   if ((rc = read_meta(C, &hm))) return rc;
-  while (hm.f_fail == 2 && !hm.bad_sym && tgt > 512) {
-    tgt /= 2;
+  while (hm.f_fail == 2 && !hm.bad_sym && tgt > WIN_TGT_MIN) {
+    tgt = (tgt / 2) / CH * CH;
     if ((rc = run_presorted(C, tgt))) return rc;
     if ((rc = read_meta(C, &hm))) return rc;
   }

@@ -18,8 +18,10 @@
 
 #define TB_WIDTH 4096       // symbols per bucket
 #define TB_MAXBK 1024       // buckets handled by the bucketed path
-#define TB_ITEMS 16
-#define TB_TILE (BLOCK * TB_ITEMS)
+#define TB_NT 512           // scatter workgroup (49 KB LDS: 3 groups = 6 waves/SIMD)
+#define TB_NW (TB_NT / WAVE)
+#define TB_ITEMS 8
+#define TB_TILE (TB_NT * TB_ITEMS)
 
 struct TbArgs {
   const u32* symT;  // moves: T-ordered symbols (T < nMv)
@@ -60,79 +62,131 @@ __device__ __forceinline__ bool tb_record(const TbArgs& A, u64 r, u32* sym, u32*
   return true;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_tb_hist(TbArgs A0, u32* __restrict__ hist, int nblk) {
+// The TB_ITEMS records of a lane (r = base + it * TB_NT + lane), loads issued
+// together: a tile is all moves, all renames, or (one tile) mixed.
+__device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[TB_ITEMS], u32 (&fl)[TB_ITEMS],
+                                         bool (&ok)[TB_ITEMS]) {
+  const u64 nrec = A.nMv + A.nR;
+  const u64 end = base + (u64)TB_TILE;
+  if (end <= A.nMv) {
+    i32 a[TB_ITEMS], f[TB_ITEMS];
+    u32 s[TB_ITEMS];
+#pragma unroll
+    for (int it = 0; it < TB_ITEMS; ++it) {
+      const u64 r = base + (u64)it * TB_NT + threadIdx.x;
+      s[it] = A.symT[r];
+      a[it] = A.mvA[r];
+      f[it] = A.mvF[r];
+    }
+#pragma unroll
+    for (int it = 0; it < TB_ITEMS; ++it) {
+      ok[it] = a[it] >= 0 || f[it] >= 0;
+      fl[it] = (a[it] >= 0 ? 1u : 0u) | (f[it] >= 0 ? 2u : 0u);
+      sym[it] = min(s[it], A.smax);
+    }
+  } else if (base >= A.nMv && end <= nrec) {
+    u32 s[TB_ITEMS];
+    u8 k[TB_ITEMS];
+#pragma unroll
+    for (int it = 0; it < TB_ITEMS; ++it) {
+      const u64 m = base - A.nMv + (u64)it * TB_NT + threadIdx.x;
+      s[it] = A.Msym[m];
+      k[it] = A.skip[m];
+    }
+#pragma unroll
+    for (int it = 0; it < TB_ITEMS; ++it) {
+      ok[it] = k[it] == 0;
+      fl[it] = 0;
+      sym[it] = min(s[it], A.smax);
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < TB_ITEMS; ++it) {
+      const u64 r = base + (u64)it * TB_NT + threadIdx.x;
+      ok[it] = r < nrec && tb_record(A, r, &sym[it], &fl[it]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(TB_NT) k_tb_hist(TbArgs A0, u32* __restrict__ hist, int nblk) {
   __shared__ u32 h[TB_MAXBK];
   const TbArgs A = tb_load(A0);
-  for (u32 i = threadIdx.x; i < A.nbk; i += BLOCK) h[i] = 0;
+  for (u32 i = threadIdx.x; i < A.nbk; i += TB_NT) h[i] = 0;
   __syncthreads();
   const u64 nrec = A.nMv + A.nR;
   const u64 base = (u64)blockIdx.x * TB_TILE;
-#pragma unroll 4
-  for (int it = 0; it < TB_ITEMS; ++it) {
-    const u64 r = base + (u64)it * BLOCK + threadIdx.x;
-    u32 s, fl;
-    if (r < nrec && tb_record(A, r, &s, &fl)) atomicAdd(&h[s / A.width], 1u);
+  if (base < nrec) {
+    u32 s[TB_ITEMS], fl[TB_ITEMS];
+    bool ok[TB_ITEMS];
+    tb_items(A, base, s, fl, ok);
+#pragma unroll
+    for (int it = 0; it < TB_ITEMS; ++it)
+      if (ok[it]) atomicAdd(&h[s[it] / A.width], 1u);
   }
   __syncthreads();
-  for (u32 i = threadIdx.x; i < A.nbk; i += BLOCK) hist[(u64)i * nblk + blockIdx.x] = h[i];
+  for (u32 i = threadIdx.x; i < A.nbk; i += TB_NT) hist[(u64)i * nblk + blockIdx.x] = h[i];
 }
 
 // Scatter into bucket order.  The block's records are counting-sorted by bucket
 // in LDS, then every bucket's run is written contiguously.
-__global__ void __launch_bounds__(BLOCK) k_tb_scatter(TbArgs A0, const u32* __restrict__ offs, int nblk,
+__global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __restrict__ offs, int nblk,
                                                       u64* __restrict__ rec) {
   __shared__ u64 stage[TB_TILE];        // 32 KB
   __shared__ u32 lstart[TB_MAXBK];      // local bucket starts (then cursors)
   __shared__ u32 gbase[TB_MAXBK];       // global start of this block's run in each bucket
-  __shared__ u32 wsum[NWAVES + 1];
+  __shared__ u32 wsum[TB_NW + 1];
   __shared__ u16 sbk[TB_TILE];          // bucket of each staged record
   const TbArgs A = tb_load(A0);
   const u64 nrec = A.nMv + A.nR;
   const u64 base = (u64)blockIdx.x * TB_TILE;
   if (base >= nrec) return;
   const u32 nbk = A.nbk;
-  for (u32 i = threadIdx.x; i < nbk; i += BLOCK) {
+  for (u32 i = threadIdx.x; i < nbk; i += TB_NT) {
     lstart[i] = 0;
     gbase[i] = offs[(u64)i * nblk + blockIdx.x];
   }
   __syncthreads();
   u64 q[TB_ITEMS];
   u32 bk[TB_ITEMS];
+  {
+    u32 s[TB_ITEMS], fl[TB_ITEMS];
+    bool ok[TB_ITEMS];
+    tb_items(A, base, s, fl, ok);
 #pragma unroll
-  for (int it = 0; it < TB_ITEMS; ++it) {
-    const u64 r = base + (u64)it * BLOCK + threadIdx.x;
-    u32 s, fl;
-    bk[it] = 0xffffffffu;
-    if (r < nrec && tb_record(A, r, &s, &fl)) {
-      const u32 b = s / A.width;
-      bk[it] = b;
-      q[it] = (u64)r | ((u64)(s - b * A.width) << 32) | ((u64)fl << 44);
-      atomicAdd(&lstart[b], 1u);
+    for (int it = 0; it < TB_ITEMS; ++it) {
+      const u64 r = base + (u64)it * TB_NT + threadIdx.x;
+      bk[it] = 0xffffffffu;
+      if (ok[it]) {
+        const u32 b = s[it] / A.width;
+        bk[it] = b;
+        q[it] = (u64)r | ((u64)(s[it] - b * A.width) << 32) | ((u64)fl[it] << 44);
+        atomicAdd(&lstart[b], 1u);
+      }
     }
   }
   __syncthreads();
   {
-    u32 v[TB_MAXBK / BLOCK];
+    u32 v[TB_MAXBK / TB_NT];
     u32 acc = 0;
 #pragma unroll
-    for (int j = 0; j < TB_MAXBK / BLOCK; ++j) {
-      const u32 b = threadIdx.x * (TB_MAXBK / BLOCK) + j;
+    for (int j = 0; j < TB_MAXBK / TB_NT; ++j) {
+      const u32 b = threadIdx.x * (TB_MAXBK / TB_NT) + j;
       v[j] = b < nbk ? lstart[b] : 0u;
       acc += v[j];
     }
     u32 tot;
-    u32 run = block_excl_scan<OpSum, u32>(acc, wsum, &tot);
+    u32 run = block_excl_scan<OpSum, u32, TB_NW>(acc, wsum, &tot);
 #pragma unroll
-    for (int j = 0; j < TB_MAXBK / BLOCK; ++j) {
-      const u32 b = threadIdx.x * (TB_MAXBK / BLOCK) + j;
+    for (int j = 0; j < TB_MAXBK / TB_NT; ++j) {
+      const u32 b = threadIdx.x * (TB_MAXBK / TB_NT) + j;
       if (b < nbk) lstart[b] = run;
       run += v[j];
     }
-    if (threadIdx.x == 0) wsum[NWAVES] = tot;
+    if (threadIdx.x == 0) wsum[TB_NW] = tot;
   }
   __syncthreads();
-  const u32 total = wsum[NWAVES];
-  for (u32 i = threadIdx.x; i < nbk; i += BLOCK) gbase[i] -= lstart[i];
+  const u32 total = wsum[TB_NW];
+  for (u32 i = threadIdx.x; i < nbk; i += TB_NT) gbase[i] -= lstart[i];
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < TB_ITEMS; ++it) {
@@ -142,7 +196,7 @@ __global__ void __launch_bounds__(BLOCK) k_tb_scatter(TbArgs A0, const u32* __re
     sbk[pos] = (u16)bk[it];
   }
   __syncthreads();
-  for (u32 i = threadIdx.x; i < total; i += BLOCK) rec[gbase[sbk[i]] + i] = stage[i];
+  for (u32 i = threadIdx.x; i < total; i += TB_NT) rec[gbase[sbk[i]] + i] = stage[i];
 }
 
 #define TBR_NT 1024
@@ -153,6 +207,8 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
                                                       const u32* __restrict__ nrec_total,
                                                       const u64* __restrict__ rec, i64 n_sym,
                                                       int4* __restrict__ fin) {
+  const FinPack FP = fin_pack_of(A0.meta->vbits, true);
+  u64* fin8 = reinterpret_cast<u64*>(fin);
   __shared__ u32 tA[TB_WIDTH], tF[TB_WIDTH], tC[TB_WIDTH];
   const TbArgs A = tb_load(A0);
   const u32 b = blockIdx.x;
@@ -176,8 +232,10 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
   const u32 s0 = b * A.width;
   for (u32 i = threadIdx.x; i < A.width && (i64)(s0 + i) < n_sym; i += TBR_NT) {
     const u32 a = tA[i], f = tF[i], c = tC[i];
-    fin[s0 + i] = make_int4(a ? A.mvA[a - 1] : -1, f ? A.mvF[f - 1] : -1,
-                            c ? A.Mstr[(u64)(c - 1) - A.nMv] : -1, 0);
+    const int va = a ? A.mvA[a - 1] : -1, vf = f ? A.mvF[f - 1] : -1;
+    const int vc = c ? A.Mstr[(u64)(c - 1) - A.nMv] : -1;
+    if (FP.packed) fin8[s0 + i] = fin_encode(FP, va, vf, vc);
+    else fin[s0 + i] = make_int4(va, vf, vc, 0);
   }
 }
 

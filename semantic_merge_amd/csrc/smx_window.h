@@ -107,6 +107,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   __shared__ u32 wck[SMX_N_KINDS];
   __shared__ u64 base[SMX_N_KINDS + 1];
   __shared__ u32 woffk[SMX_N_KINDS + 2];  // this window's offsets: kinds, renames of A, of B
+  __shared__ u32 vor[3];              // OR of (value + 1): moves' addr, file; renames' name
   u32* phi = (u32*)sts;               // slot space: top 32 bits of oid_hi (after step 4)
   u16* rown = fin;                    // rename rank within its branch (after step 5)
 
@@ -166,6 +167,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   if (bad) P.meta->bad_sym = 1;
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
+  if (t < 3) vor[t] = 0;
   // window offsets = chunk prefix at the window start + kinds of the <= 255 ops
   // between that chunk start and the window start (per branch)
   if (t < SMX_N_KINDS) {
@@ -205,6 +207,29 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       none_mv += (k_r[i] == KMOVE && (v0_r[i] < 0 || v1_r[i] < 0));
     }
     if (none_mv) atomicAdd((unsigned long long*)&P.meta->n_move_none, (unsigned long long)none_mv);
+    // value bit widths for the packed final-state table (smx_common.h FinPack)
+    u32 oa = 0, of = 0, oc = 0;
+#pragma unroll
+    for (int i = 0; i < WF_ITEMS; ++i) {
+      if (t + WF_NT * i >= sz) continue;
+      if (k_r[i] == KMOVE) {
+        oa |= (u32)(v0_r[i] + 1);
+        of |= (u32)(v1_r[i] + 1);
+      } else if (k_r[i] == KREN) {
+        oc |= (u32)(v1_r[i] + 1);
+      }
+    }
+#pragma unroll
+    for (int o = WAVE / 2; o > 0; o >>= 1) {
+      oa |= __shfl_xor(oa, o, WAVE);
+      of |= __shfl_xor(of, o, WAVE);
+      oc |= __shfl_xor(oc, o, WAVE);
+    }
+    if (lane == 0) {
+      if (oa) atomicOr(&vor[0], oa);
+      if (of) atomicOr(&vor[1], of);
+      if (oc) atomicOr(&vor[2], oc);
+    }
     if (__syncthreads_or(dec)) {
       if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
       return;
@@ -345,6 +370,14 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   }
   __syncthreads();
 
+  // the window's value bits: one device atomic per word, only when it adds bits
+  if (t < 3) {
+    u32* vb = P.meta->vbits;
+    const u32 mine = vor[t];
+    const u32 cur = __hip_atomic_load(&vb[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cur | mine) != cur) atomicOr(&vb[t], mine);
+  }
+
   // 6. renames: rank among the window's renames of the same branch (final order)
   const int R0 = kbase[KREN], RN = wck[KREN];
   const int nrc = (RN + WAVE - 1) / WAVE;
@@ -481,6 +514,7 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
     skind[e] = (u8)(k < SMX_N_KINDS ? k : SMX_N_KINDS - 1);
   }
   if (bad) P.meta->bad_sym = 1;
+  if (w == 0 && t < 3) P.meta->vbits[t] = ~0u;  // generic plan: value widths not tracked -> int4 table
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WG_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
   __syncthreads();

@@ -84,10 +84,24 @@ def test_synthetic_digests_gpu(name):
     synth.LiftSpec(1_000_000, 64, 23, ops_per_ms=16, mix=synth.ADVERSARIAL_MIX),  # hot symbols
     synth.LiftSpec(333_333, 1, 29, ops_per_ms=1),               # one symbol, every head collides
     synth.LiftSpec(1_000_000, 1_000, 41, ops_per_ms=160),       # windows overflow -> smaller windows
-], ids=["c2_1M", "c2_1M_shuffled", "c5_2M", "hot64_1M", "onesym", "dense160"])
+    synth.LiftSpec(400_000, 5_000_000, 43),                     # > 4M symbols: atomic tables
+], ids=["c2_1M", "c2_1M_shuffled", "c5_2M", "hot64_1M", "onesym", "dense160", "sym5M"])
 def test_gpu_equals_oracle_soa(spec):
     soa = synth.lift_soa(synth.lift_logs(spec))
     _eq_soa(compose_soa(soa), oracle.compose(soa), str(spec))
+
+
+@pytest.mark.parametrize("bits", [20, 31], ids=["packed", "wide"])
+def test_gpu_value_widths(bits):
+    """Value ids of `bits` bits: 3 x 20 fits the packed 8-byte final-state table,
+    3 x 31 does not (int4 table)."""
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(300_000, 3_000, 47)))
+    rng = np.random.default_rng(bits)
+    hi = np.int64(1) << (bits - 1)
+    for v in (soa.v0, soa.v1):
+        m = v >= 0
+        v[m] = (hi + rng.integers(0, hi, m.sum())).astype(np.int32)
+    _eq_soa(compose_soa(soa), oracle.compose(soa), f"value bits {bits}")
 
 
 def test_gpu_repeatable_and_none_moves():
