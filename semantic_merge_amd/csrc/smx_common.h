@@ -82,27 +82,63 @@ __device__ __forceinline__ u64 wave_peers(u32 d, bool valid) {
   return m;
 }
 
+// Inclusive wave64 prefix scans on the DPP network (VALU only; __shfl_up would be
+// a chain of six ds_bpermute LDS round trips): row_shr 1, 2, 4, 8 inside each
+// 16-lane row, then row_bcast:15 and row_bcast:31 carry across rows.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ u32 dpp_u32(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+
+__device__ __forceinline__ u32 wave_incl_sum_u32(u32 v) {
+  v += dpp_u32<0x111, 0xf>(v);  // row_shr:1
+  v += dpp_u32<0x112, 0xf>(v);  // row_shr:2
+  v += dpp_u32<0x114, 0xf>(v);  // row_shr:4
+  v += dpp_u32<0x118, 0xf>(v);  // row_shr:8
+  v += dpp_u32<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v += dpp_u32<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+
+__device__ __forceinline__ u32 wave_incl_max_u32(u32 v) {
+  v = max(v, dpp_u32<0x111, 0xf>(v));
+  v = max(v, dpp_u32<0x112, 0xf>(v));
+  v = max(v, dpp_u32<0x114, 0xf>(v));
+  v = max(v, dpp_u32<0x118, 0xf>(v));
+  v = max(v, dpp_u32<0x142, 0xa>(v));
+  v = max(v, dpp_u32<0x143, 0xc>(v));
+  return v;
+}
+
 // Inclusive wave prefix sum (64 lanes).
 template <typename T>
 __device__ __forceinline__ T wave_incl_sum(T v) {
-  const int lane = threadIdx.x & (WAVE - 1);
+  if constexpr (sizeof(T) == 4) {
+    return (T)wave_incl_sum_u32((u32)v);
+  } else {
+    const int lane = threadIdx.x & (WAVE - 1);
 #pragma unroll
-  for (int o = 1; o < WAVE; o <<= 1) {
-    T y = __shfl_up(v, o, WAVE);
-    if (lane >= o) v += y;
+    for (int o = 1; o < WAVE; o <<= 1) {
+      T y = __shfl_up(v, o, WAVE);
+      if (lane >= o) v += y;
+    }
+    return v;
   }
-  return v;
 }
 
 template <typename T>
 __device__ __forceinline__ T wave_incl_max(T v) {
-  const int lane = threadIdx.x & (WAVE - 1);
+  if constexpr (sizeof(T) == 4 && (T)(-1) > (T)0) {
+    return (T)wave_incl_max_u32((u32)v);
+  } else {
+    const int lane = threadIdx.x & (WAVE - 1);
 #pragma unroll
-  for (int o = 1; o < WAVE; o <<= 1) {
-    T y = __shfl_up(v, o, WAVE);
-    if (lane >= o) v = v > y ? v : y;
+    for (int o = 1; o < WAVE; o <<= 1) {
+      T y = __shfl_up(v, o, WAVE);
+      if (lane >= o) v = v > y ? v : y;
+    }
+    return v;
   }
-  return v;
 }
 
 struct OpSum {

@@ -836,8 +836,18 @@ struct Ctx {
   T* ws(int b) const { return (T*)(base + L.off[b]); }
 };
 
+// Diagnostics (tools/window_phases.py): a device buffer for k_window_f phase stamps.
+static void* g_phase_dbg = nullptr;
+static size_t g_phase_dbg_bytes = 0;
+extern "C" int smx_debug_phase_buffer(void* p, size_t bytes) {
+  g_phase_dbg = p;
+  g_phase_dbg_bytes = bytes;
+  return SMX_OK;
+}
+
 static WinArgs win_args(const Ctx& C) {
   WinArgs P;
+  P.dbg = nullptr;
   P.cpre = nullptr;
   P.CM = 0;
   P.kind = C.ops->kind;
@@ -1003,7 +1013,12 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   P.W = W;
   P.ablate = env_int("SMX_ABLATE", 0);
   C.tm->begin(ST_WINDOW);
-  hipLaunchKernelGGL(k_window_f, dim3(W), dim3(WF_NT), 0, st, P);
+  if (g_phase_dbg && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
+    P.dbg = (u64*)g_phase_dbg;
+    hipLaunchKernelGGL(k_window_f<true>, dim3(W), dim3(WF_NT), 0, st, P);
+  } else {
+    hipLaunchKernelGGL(k_window_f<false>, dim3(W), dim3(WF_NT), 0, st, P);
+  }
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_WINDOW);
   if (P.ablate) return SMX_OK;  // diagnostics: the T-ordered arrays are invalid, stop here

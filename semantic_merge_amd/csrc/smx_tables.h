@@ -110,8 +110,10 @@ __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[T
 
 __global__ void __launch_bounds__(TB_NT) k_tb_hist(TbArgs A0, u32* __restrict__ hist, int nblk) {
   __shared__ u32 h[TB_MAXBK];
+  __shared__ u32 vb[3];
   const TbArgs A = tb_load(A0);
   for (u32 i = threadIdx.x; i < A.nbk; i += TB_NT) h[i] = 0;
+  if (threadIdx.x < 3) vb[threadIdx.x] = 0;
   __syncthreads();
   const u64 nrec = A.nMv + A.nR;
   const u64 base = (u64)blockIdx.x * TB_TILE;
@@ -122,9 +124,40 @@ __global__ void __launch_bounds__(TB_NT) k_tb_hist(TbArgs A0, u32* __restrict__ 
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it)
       if (ok[it]) atomicAdd(&h[s[it] / A.width], 1u);
+    // value bit widths for the packed final-state table (smx_common.h FinPack):
+    // OR of (value + 1) over moves' addr / file and renames' names (cache hits
+    // except the names)
+    u32 oa = 0, of = 0, oc = 0;
+#pragma unroll
+    for (int it = 0; it < TB_ITEMS; ++it) {
+      const u64 r = base + (u64)it * TB_NT + threadIdx.x;
+      if (r < A.nMv) {
+        oa |= (u32)(A.mvA[r] + 1);
+        of |= (u32)(A.mvF[r] + 1);
+      } else if (r < nrec) {
+        oc |= (u32)(A.Mstr[r - A.nMv] + 1);
+      }
+    }
+#pragma unroll
+    for (int o = WAVE / 2; o > 0; o >>= 1) {
+      oa |= __shfl_xor(oa, o, WAVE);
+      of |= __shfl_xor(of, o, WAVE);
+      oc |= __shfl_xor(oc, o, WAVE);
+    }
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+      if (oa) atomicOr(&vb[0], oa);
+      if (of) atomicOr(&vb[1], of);
+      if (oc) atomicOr(&vb[2], oc);
+    }
   }
   __syncthreads();
   for (u32 i = threadIdx.x; i < A.nbk; i += TB_NT) hist[(u64)i * nblk + blockIdx.x] = h[i];
+  if (threadIdx.x < 3 && vb[threadIdx.x]) {
+    u32* g = const_cast<ComposeMeta*>(A.meta)->vbits;
+    const u32 mine = vb[threadIdx.x];
+    const u32 cur = __hip_atomic_load(&g[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cur | mine) != cur) atomicOr(&g[threadIdx.x], mine);
+  }
 }
 
 // Scatter into bucket order.  The block's records are counting-sorted by bucket

@@ -28,6 +28,37 @@
 #define KREN SMX_KIND_RENAME
 #define NCHUNK (WIN_CAP / WAVE)
 #define CH 256                     // chunk of the presorted kind histogram
+#ifndef SMX_KEY64
+#define SMX_KEY64 1                // group-rank keys: 0 = 21-bit id prefix (u32), 1 = 42-bit (u64)
+#endif
+#ifndef SMX_LATE_PAYLOAD
+#define SMX_LATE_PAYLOAD 0         // 1: load sym/v0/v1 after the rank phase
+#endif
+#if SMX_KEY64
+typedef u64 rkey_t;
+#define RK_PREFIX_SHIFT 22         // hi >> 22: top 42 bits of oid_hi
+#else
+typedef u32 rkey_t;
+#define RK_PREFIX_SHIFT 43         // top 21 bits of oid_hi
+#endif
+#define RK_PER16 (16 / (int)sizeof(rkey_t))   // keys per 16-byte LDS read
+
+// Number of keys < kp among the first m (<= RK_PER16) keys of a 16-byte LDS read.
+__device__ __forceinline__ int rk_count(const uint4 x, u32 kp, int m) {
+  return (m > 0 && x.x < kp) + (m > 1 && x.y < kp) + (m > 2 && x.z < kp) + (m > 3 && x.w < kp);
+}
+__device__ __forceinline__ int rk_count(const ulonglong2 x, u64 kp, int m) {
+  return (m > 0 && x.x < kp) + (m > 1 && x.y < kp);
+}
+__device__ __forceinline__ int rk_count(const uint4 x, u32 kp) {
+  return (x.x < kp) + (x.y < kp) + (x.z < kp) + (x.w < kp);
+}
+__device__ __forceinline__ int rk_count(const ulonglong2 x, u64 kp) { return (x.x < kp) + (x.y < kp); }
+#if SMX_KEY64
+typedef ulonglong2 rkey16_t;
+#else
+typedef uint4 rkey16_t;
+#endif
 
 struct WinArgs {
   const u8* kind;
@@ -60,6 +91,7 @@ struct WinArgs {
   u32* Mown;
   u32* RA;
   u32* RB;
+  u64* dbg;         // diagnostics only: phase timestamps (k_window_f<true>)
 };
 
 // Writes one op's T-ordered records (registers -> HBM).
@@ -93,11 +125,20 @@ __device__ __forceinline__ void win_emit(const WinArgs& P, const u64* base, i64 
 
 // LDS ~34 KB (buffers are reused across phases) so 4 workgroups fit a CU: while
 // some workgroups run their LDS phases, others stream their windows from HBM.
+// DBG: phase timestamps of every window (diagnostics, tools/window_phases.py):
+// lane 0 of wave 0 stores s_memtime after each phase into P.dbg[w * WF_NSTAMP + i].
+#define WF_NSTAMP 24
+#define WSTAMP(i)                                                                  \
+  do {                                                                             \
+    if (DBG && t == 0) P.dbg[w * WF_NSTAMP + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+template <bool DBG>
 __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
-  __shared__ u64 sts[WIN_CAP];        // element space: timestamp keys; later slot-space oid prefix
+  __shared__ __attribute__((aligned(16))) u64 sts[WIN_CAP];  // element space: timestamps; later slot-space rank keys
   __shared__ u16 sord[WIN_CAP];       // S order (merge), later the final order
   __shared__ u16 fin[WIN_CAP];        // slot -> element, later rename ranks
-  __shared__ u16 sl[WIN_CAP];         // element -> slot, later element -> final
+  __shared__ u16 sl[WIN_CAP];         // element -> slot, later rank -> slot
   __shared__ u8 skind[WIN_CAP];
   __shared__ u8 srank[WIN_CAP];
   __shared__ u64 gbits[NCHUNK];       // group-start bits over slots
@@ -107,8 +148,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   __shared__ u32 wck[SMX_N_KINDS];
   __shared__ u64 base[SMX_N_KINDS + 1];
   __shared__ u32 woffk[SMX_N_KINDS + 2];  // this window's offsets: kinds, renames of A, of B
-  __shared__ u32 vor[3];              // OR of (value + 1): moves' addr, file; renames' name
-  u32* phi = (u32*)sts;               // slot space: top 32 bits of oid_hi (after step 4)
+  rkey_t* pkey = (rkey_t*)sts;        // slot space: rank keys (after step 4)
   u16* rown = fin;                    // rename rank within its branch (after step 5)
 
   const int t = threadIdx.x;
@@ -127,38 +167,67 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   }
   if (sz == 0) return;
   const i64 bpos = P.na + b0 - na;  // op index of B element e is bpos + e
+  WSTAMP(0);
 
-  // 1. load: keys to LDS, payload stays in registers
-  u32 hi_r[WF_ITEMS];
+  // 1. load the sort keys (kind, timestamp, top of the id) to LDS.  The payload
+  //    (sym, v0, v1) is loaded after the rank phase, so its HBM latency overlaps
+  //    the later LDS phases and it holds no registers across the rank loop.
+  u64 hi_r[WF_ITEMS];
   u32 sym_r[WF_ITEMS];
   i32 v0_r[WF_ITEMS], v1_r[WF_ITEMS];
   u32 k_r[WF_ITEMS];
   bool bad = false;
   // all loads are issued unconditionally (clamped to a valid op) so that the
-  // WF_ITEMS x 6 loads of a lane are in flight together; the guards apply to the
-  // LDS stores only
+  // loads of a lane are in flight together; the guards apply to the LDS stores only
   u64 ts_r[WF_ITEMS];
+  auto op_index = [&](int e) -> i64 {
+    const int ec = e < sz ? e : 0;
+    return ec < na ? a0 + ec : bpos + ec;
+  };
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
-    const int e = t + WF_NT * i;
-    const int ec = e < sz ? e : 0;
-    const i64 j = ec < na ? a0 + ec : bpos + ec;
+    const i64 j = op_index(t + WF_NT * i);
     k_r[i] = P.kind[j];
     ts_r[i] = P.kts[j];
-    hi_r[i] = (u32)(P.khi[j] >> 32);
+    hi_r[i] = P.khi[j];
+#if !SMX_LATE_PAYLOAD
     sym_r[i] = P.sym[j];
     v0_r[i] = P.v0[j];
     v1_r[i] = P.v1[j];
+#endif
   }
+  auto load_payload = [&]() {
+    if (!SMX_LATE_PAYLOAD) return;
+#pragma unroll
+    for (int i = 0; i < WF_ITEMS; ++i) {
+      // opaque element index: the compiler must not keep the key loads' 64-bit
+      // addresses alive (in registers or scratch) across the LDS phases
+      int e = t + WF_NT * i;
+      asm volatile("" : "+v"(e));
+      const i64 j = op_index(e);
+      sym_r[i] = P.sym[j];
+      v0_r[i] = P.v0[j];
+      v1_r[i] = P.v1[j];
+    }
+  };
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
     if (e < sz) {
-      bad |= (k_r[i] >= SMX_N_KINDS) || (sym_r[i] >= (u64)P.n_sym);
+      bad |= k_r[i] >= SMX_N_KINDS;
       k_r[i] = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
       sts[e] = ts_r[i];
       skind[e] = (u8)k_r[i];
     }
+  }
+  // kinds of the <= 255 ops between each branch's chunk start and the window start
+  // (window offsets below); lanes 0..255 branch A, 256..511 branch B
+  u32 kpart = 0xffffffffu;
+  {
+    const int pa = (int)(a0 % CH), pb = (int)(b0 % CH);
+    const int side = t >= CH;
+    const int q = t - side * CH;
+    if (q < (side ? pb : pa)) kpart = P.kind[side ? (P.na + b0 - pb + q) : (a0 - pa + q)];
   }
   // timestamps just before the window on each branch (issued with the loads above)
   u64 prev_a = 0, prev_b = 0;
@@ -167,7 +236,6 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   if (bad) P.meta->bad_sym = 1;
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
-  if (t < 3) vor[t] = 0;
   // window offsets = chunk prefix at the window start + kinds of the <= 255 ops
   // between that chunk start and the window start (per branch)
   if (t < SMX_N_KINDS) {
@@ -177,66 +245,34 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     woffk[t] = P.cpre[(i64)(sd * SMX_N_KINDS + KREN) * P.CM + (sd ? b0 : a0) / CH];
   }
   __syncthreads();
-  {
-    const int pa = (int)(a0 % CH), pb = (int)(b0 % CH);
-    // lanes 0..255: branch A partial chunk, lanes 256..511: branch B
-    const int side = t >= CH;
-    const int q = t - side * CH;
-    if (q < (side ? pb : pa)) {
-      const i64 j = side ? (P.na + b0 - pb + q) : (a0 - pa + q);
-      u32 k = P.kind[j];
-      k = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
-      atomicAdd(&woffk[k], 1u);
-      if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + side], 1u);
-    }
+  WSTAMP(1);
+  // window offsets: the partial-chunk kinds; presorted-layout check: every adjacent
+  // pair of each branch log is non-decreasing (the pair straddling a window start
+  // is checked here too); moves with a None value are counted for the prefix fix-up
+  if (kpart != 0xffffffffu) {
+    const u32 k = kpart < SMX_N_KINDS ? kpart : SMX_N_KINDS - 1;
+    atomicAdd(&woffk[k], 1u);
+    if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + (t >= CH)], 1u);
   }
-  __syncthreads();
-
-  // presorted-layout check: every adjacent pair of each branch log is
-  // non-decreasing (the pair straddling a window start is checked here too);
-  // moves with a None value are counted for the prefix fix-up
-  if (!(P.ablate & 1)) {
+  {
     bool dec = false;
-    u32 none_mv = 0;
-    if (t == 0) dec = (a0 > 0 && na > 0 && prev_a > sts[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
+    if (t == 0) dec = (a0 > 0 && na > 0 && prev_a > ts_r[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
 #pragma unroll
     for (int i = 0; i < WF_ITEMS; ++i) {
       const int e = t + WF_NT * i;
       if (e >= sz) continue;
-      if (e != 0 && e != na && sts[e - 1] > sts[e]) dec = true;
-      none_mv += (k_r[i] == KMOVE && (v0_r[i] < 0 || v1_r[i] < 0));
+      if (!(P.ablate & 1) && e != 0 && e != na && sts[e - 1] > ts_r[i]) dec = true;
     }
-    if (none_mv) atomicAdd((unsigned long long*)&P.meta->n_move_none, (unsigned long long)none_mv);
-    // value bit widths for the packed final-state table (smx_common.h FinPack)
-    u32 oa = 0, of = 0, oc = 0;
-#pragma unroll
-    for (int i = 0; i < WF_ITEMS; ++i) {
-      if (t + WF_NT * i >= sz) continue;
-      if (k_r[i] == KMOVE) {
-        oa |= (u32)(v0_r[i] + 1);
-        of |= (u32)(v1_r[i] + 1);
-      } else if (k_r[i] == KREN) {
-        oc |= (u32)(v1_r[i] + 1);
-      }
-    }
-#pragma unroll
-    for (int o = WAVE / 2; o > 0; o >>= 1) {
-      oa |= __shfl_xor(oa, o, WAVE);
-      of |= __shfl_xor(of, o, WAVE);
-      oc |= __shfl_xor(oc, o, WAVE);
-    }
-    if (lane == 0) {
-      if (oa) atomicOr(&vor[0], oa);
-      if (of) atomicOr(&vor[1], of);
-      if (oc) atomicOr(&vor[2], oc);
-    }
-    if (__syncthreads_or(dec)) {
+    const bool any_dec = __syncthreads_or(dec);
+    WSTAMP(20);
+    if (any_dec) {
       if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
       return;
     }
   }
 
   if (P.ablate & 8) {  // load + write only
+    load_payload();
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < WF_ITEMS; ++i) {
@@ -265,6 +301,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     }
   }
   __syncthreads();
+  WSTAMP(3);
 
   // 3. stable multisplit of S by rank
   const int nch = (sz + WAVE - 1) / WAVE;
@@ -281,6 +318,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     }
   }
   __syncthreads();
+  WSTAMP(4);
   for (int k = wv; k < SMX_N_KINDS; k += WF_WAVES) {
     const u32 x = lane < nch ? ccnt[lane][k] : 0u;
     const u32 inc = wave_incl_sum(x);
@@ -288,6 +326,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     if (lane == WAVE - 1) wck[k] = inc;
   }
   __syncthreads();
+  WSTAMP(5);
   if (wv == 0) {
     const u32 x = lane < SMX_N_KINDS ? wck[lane] : 0u;
     const u32 inc = wave_incl_sum(x);
@@ -295,6 +334,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     if (lane == SMX_N_KINDS - 1) kbase[SMX_N_KINDS] = inc;
   }
   __syncthreads();
+  WSTAMP(6);
   for (int m = t; m < sz; m += WF_NT) {
     const int e = sord[m];
     const u32 k = skind[e];
@@ -303,6 +343,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     sl[e] = (u16)p;
   }
   __syncthreads();
+  WSTAMP(7);
 
   // 4. group-start bits (a group = equal (rank, timestamp), contiguous in slots),
   //    then the timestamps are dead and their buffer takes the slot-space oid prefix
@@ -318,21 +359,29 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     if (lane == 0 && (p >> 6) < NCHUNK) gbits[p >> 6] = b;
   }
   __syncthreads();
+  WSTAMP(8);
+  // slot-space rank keys: a prefix of oid_hi, then the slot (unique per window)
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
-    if (e < sz) phi[sl[e]] = hi_r[i];
+    if (e < sz) {
+      const int p = sl[e];
+      pkey[p] = ((rkey_t)(hi_r[i] >> RK_PREFIX_SHIFT) << 11) | (rkey_t)p;
+    }
   }
   __syncthreads();
+  WSTAMP(9);
 
-  // 5. order each group by (oid, side, index): counting rank on the top 32 bits of
-  //    oid_hi; elements sharing that prefix (rare) are resolved on the full oid and
-  //    then on slot order (= side, index order)
+  // 5. order each group by (oid, side, index).  Counting rank on 32-bit keys (21-bit
+  //    oid prefix, slot), four per LDS read; slot order is (side, index) order inside
+  //    a group.  If two adjacent ranks share the prefix (about 1 window in 100 on
+  //    random ids; always for duplicate ids) the window is re-ranked exactly on the
+  //    full oid.
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {
     const int p = t + WF_NT * j;
-    if (p >= sz) continue;
-    const int e = fin[p];
+    if (p >= sz) break;
+    int r = p;
     const int bit = p & 63;
     int wi = p >> 6;
     u64 word = gbits[wi] & (bit == 63 ? ~0ull : ((1ull << (bit + 1)) - 1));
@@ -343,39 +392,71 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     while (word == 0 && ++wi < nch) word = gbits[wi];
     int ge = word ? wi * 64 + __ffsll((unsigned long long)word) - 1 : sz;
     ge = ge < sz ? ge : sz;
-    int r = p;
     if (ge - gs > 1 && !(P.ablate & 2)) {
-      const u32 h = phi[p];
-      u32 lt = 0, eq = 0;
-      for (int q = gs; q < ge; ++q) {
-        const u32 hq = phi[q];
-        lt += hq < h;
-        eq += hq == h;
+      const rkey_t kp = pkey[p];
+      const rkey16_t* pv = reinterpret_cast<const rkey16_t*>(pkey);
+      constexpr int K = RK_PER16;
+      const int q0 = gs & ~(K - 1);
+      int c = 0;
+      int q = q0;
+      // 4 x 16 bytes of keys per step: four independent LDS reads in flight
+      for (; q + 4 * K <= ge; q += 4 * K) {
+        const rkey16_t x0 = pv[q / K], x1 = pv[q / K + 1], x2 = pv[q / K + 2], x3 = pv[q / K + 3];
+        c += rk_count(x0, kp) + rk_count(x1, kp) + rk_count(x2, kp) + rk_count(x3, kp);
       }
-      r = gs + (int)lt;
-      if (eq > 1) {  // shared 32-bit prefix: exact compare on (oid_hi, oid_lo), then slot
-        const i64 jp = e < na ? a0 + e : bpos + e;
-        const u64 hp = P.khi[jp], lp = P.klo[jp];
-        for (int q = gs; q < ge; ++q) {
-          if (q == p || phi[q] != h) continue;
-          const int eq2 = fin[q];
-          const i64 jq = eq2 < na ? a0 + eq2 : bpos + eq2;
-          const u64 hq = P.khi[jq], lq = P.klo[jq];
-          r += hq < hp || (hq == hp && (lq < lp || (lq == lp && q < p)));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // fewer left: up to four more reads, masked
+        const int qq = q + K * u;
+        if (qq < ge) c += rk_count(pv[qq / K], kp, ge - qq);
+      }
+      if (q0 < gs) c -= rk_count(pv[q0 / K], kp, gs - q0);  // slots before the group
+      r = gs + c;
+    }
+    sord[r] = fin[p];
+    sl[r] = (u16)p;  // sl now maps rank -> slot
+  }
+  load_payload();
+  __syncthreads();
+  WSTAMP(10);
+  // Ranks are exact unless two elements of a group share the key prefix: then
+  // they sit at adjacent ranks in slot order.  Such runs (rare on random ids;
+  // every duplicate id) are re-sorted on the full oid, stably.
+  auto run_next = [&](int r) -> bool {  // rank r + 1 continues r's prefix run
+    const int r1 = r + 1;
+    if (r1 >= sz || ((gbits[r1 >> 6] >> (r1 & 63)) & 1ull)) return false;  // next group
+    return (pkey[sl[r]] >> 11) == (pkey[sl[r1]] >> 11);
+  };
+  bool tie = false;
+#pragma unroll
+  for (int j = 0; j < WF_ITEMS; ++j) {  // detection: prefixes of adjacent ranks (any group)
+    const int r = t + WF_NT * j;
+    if (r + 1 < sz) tie |= (pkey[sl[r]] >> 11) == (pkey[sl[r + 1]] >> 11);
+  }
+  const bool any_tie = __syncthreads_or(tie);
+  WSTAMP(21);
+  if (any_tie) {
+    for (int r0 = t; r0 + 1 < sz; r0 += WF_NT) {
+      if (!run_next(r0) || (r0 > 0 && run_next(r0 - 1))) continue;  // not a run start
+      int r1 = r0 + 1;
+      while (run_next(r1)) ++r1;
+      // insertion sort of sord[r0..r1] by (oid_hi, oid_lo); equal ids keep slot order
+      for (int x = r0 + 1; x <= r1; ++x) {
+        const int ex = sord[x];
+        const i64 jx = ex < na ? a0 + ex : bpos + ex;
+        const u64 hx = P.khi[jx], lx = P.klo[jx];
+        int y = x - 1;
+        while (y >= r0) {
+          const int ey = sord[y];
+          const i64 jy = ey < na ? a0 + ey : bpos + ey;
+          const u64 hy = P.khi[jy], ly = P.klo[jy];
+          if (hy < hx || (hy == hx && ly <= lx)) break;
+          sord[y + 1] = (u16)ey;
+          --y;
         }
+        sord[y + 1] = (u16)ex;
       }
     }
-    sord[r] = (u16)e;
-    sl[e] = (u16)r;
-  }
-  __syncthreads();
-
-  // the window's value bits: one device atomic per word, only when it adds bits
-  if (t < 3) {
-    u32* vb = P.meta->vbits;
-    const u32 mine = vor[t];
-    const u32 cur = __hip_atomic_load(&vb[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((cur | mine) != cur) atomicOr(&vb[t], mine);
+    __syncthreads();
   }
 
   // 6. renames: rank among the window's renames of the same branch (final order)
@@ -395,6 +476,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     }
   }
   __syncthreads();
+  WSTAMP(11);
   if (wv == 0) {
     const u32 x0 = lane < nrc ? rc[lane][0] : 0u;
     const u32 x1 = lane < nrc ? rc[lane][1] : 0u;
@@ -405,11 +487,24 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     }
   }
   __syncthreads();
+  WSTAMP(12);
 
   // 7. write T-ordered records in final order (consecutive lanes -> consecutive T
   //    inside each kind: coalesced).  The register payload is staged through the
   //    now-free timestamp buffer in two rounds (sym + v0, then v1).
   if (P.ablate & 4) return;
+  {
+    // payload checks: symbols in range; moves with a None value (prefix fix-up)
+    u32 none_mv = 0;
+#pragma unroll
+    for (int i = 0; i < WF_ITEMS; ++i) {
+      if (t + WF_NT * i >= sz) continue;
+      bad |= sym_r[i] >= (u64)P.n_sym;
+      none_mv += (skind[t + WF_NT * i] == KMOVE && (v0_r[i] < 0 || v1_r[i] < 0));
+    }
+    if (bad) P.meta->bad_sym = 1;
+    if (none_mv) atomicAdd((unsigned long long*)&P.meta->n_move_none, (unsigned long long)none_mv);
+  }
   u32* st_a = (u32*)sts;             // [WIN_CAP] sym
   i32* st_b = (i32*)sts + WIN_CAP;   // [WIN_CAP] v0, then v1
 #pragma unroll
@@ -421,6 +516,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     }
   }
   __syncthreads();
+  WSTAMP(13);
   const u64 wofs_ra = woffk[SMX_N_KINDS], wofs_rb = woffk[SMX_N_KINDS + 1];
   const u64 nall = (u64)(P.na + P.nb);
   for (int x = t; x < sz; x += WF_NT) {
@@ -446,12 +542,14 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     }
   }
   __syncthreads();
+  WSTAMP(14);
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
     if (e < sz) st_b[e] = v1_r[i];
   }
   __syncthreads();
+  WSTAMP(15);
   for (int x = t; x < sz; x += WF_NT) {
     const int e = sord[x];
     const u32 k = skind[e];
@@ -460,6 +558,10 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     if (T >= nall) continue;
     if (k == KMOVE) P.mvF[T] = st_b[e];
     else P.Mstr[T - base[KREN]] = st_b[e];
+  }
+  if (DBG) {
+    __syncthreads();
+    WSTAMP(16);
   }
 }
 
@@ -514,7 +616,6 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
     skind[e] = (u8)(k < SMX_N_KINDS ? k : SMX_N_KINDS - 1);
   }
   if (bad) P.meta->bad_sym = 1;
-  if (w == 0 && t < 3) P.meta->vbits[t] = ~0u;  // generic plan: value widths not tracked -> int4 table
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WG_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
   __syncthreads();
