@@ -95,6 +95,73 @@ int smx_compose(const smx_ops* ops, const smx_compose_out* out, void* workspace,
                 size_t workspace_bytes, void* stream);
 
 /*
+ * Sharded single merge: one process per GPU, shard r of G.
+ * Replaces the same reference loop as smx_compose (compose.py:11-114) for a merge
+ * too large for one GPU.  Shard r holds, for both branches, the ops whose
+ * timestamp keys fall in its key range [tau_r, tau_{r+1}): contiguous index
+ * ranges of the global branch logs (branch logs must be timestamp-ordered, as
+ * lift.ts emits them; the host's all-to-all puts them there).  For each kind
+ * the shards' T-ordered segments follow each other in shard order, so the
+ * global composed log is, kind by kind, the shards' outputs concatenated.
+ *
+ * The host drives four steps on the same workspace, exchanging the small
+ * per-shard summaries (and the partial tables) between them with collectives:
+ *   SMX_SHARD_ORDER   plan + window kernels; writes summary[0..21] and the
+ *                     first halo_cap renames of each branch (export_*)
+ *   SMX_SHARD_WALK    DivergentRename walk with the halo (the next shards'
+ *                     exports) and an incoming open region (in_ahead, in_d);
+ *                     may be re-run when the incoming region changes;
+ *                     writes summary[22..27]
+ *   SMX_SHARD_TABLES  this shard's last writers -> part_tab (MAX-reduce them
+ *                     over shards next); writes summary[28..30]
+ *   SMX_SHARD_EMIT    composed output from the reduced tables (fin_tab) and
+ *                     the global value widths (glob[0..2]); mv_prefix (or NULL
+ *                     when no move has a None value) = [2][n_sym] last non-None
+ *                     move values of the lower shards
+ * Source indices in order[] and conflicts are global: local A op j is
+ * src_a + j, local B op j is src_b + j.  summary (int64):
+ *   [0..17] ops per kind  [18..19] renames of A, B  [20] moves with a None value
+ *   [21] plan failure (not timestamp-ordered / invalid input)
+ *   [22] outgoing region open  [23] its ahead branch  [24] its d
+ *   [25] conflicts  [26] skipped renames  [27] halo too short
+ *   [28..30] bit widths of (value + 1) for addr, file, ctx
+ */
+#define SMX_SHARD_ORDER 0
+#define SMX_SHARD_WALK 1
+#define SMX_SHARD_TABLES 2
+#define SMX_SHARD_EMIT 3
+#define SMX_SHARD_SUMMARY 32
+
+typedef struct smx_shard {
+  int32_t rank;
+  int32_t world;
+  int64_t src_a;
+  int64_t src_b;
+  /* walk: the renames of each branch after this shard's (device) */
+  int64_t halo_n[2];
+  int32_t halo_more[2];
+  const uint32_t* halo_sym[2];
+  const int32_t* halo_cls[2];
+  const int32_t* halo_src[2];
+  int32_t in_ahead;
+  int64_t in_d;
+  /* outputs of the steps (device) */
+  int64_t* summary;
+  int64_t halo_cap;
+  uint32_t* export_sym; /* [2][halo_cap] */
+  int32_t* export_cls;
+  int32_t* export_src;
+  uint64_t* part_tab;   /* [3][n_sym] */
+  /* inputs of the emit step (device) */
+  const uint64_t* fin_tab;   /* [3][n_sym], MAX-reduced part_tab */
+  const int64_t* glob;       /* [3] value bit widths, MAX over shards */
+  const uint64_t* mv_prefix; /* [2][n_sym] or NULL */
+} smx_shard;
+
+int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const smx_compose_out* out,
+                   void* workspace, size_t workspace_bytes, void* stream, int step);
+
+/*
  * Per-stage device timing of the last smx_compose calls on this thread, for the
  * benchmark: when enabled, each stage is bracketed by hipEvents on the call's
  * stream and the elapsed milliseconds are accumulated per stage.

@@ -37,6 +37,35 @@ class SmxComposeOut(C.Structure):
     ]
 
 
+class SmxShard(C.Structure):
+    _fields_ = [
+        ("rank", C.c_int32),
+        ("world", C.c_int32),
+        ("src_a", C.c_int64),
+        ("src_b", C.c_int64),
+        ("halo_n", C.c_int64 * 2),
+        ("halo_more", C.c_int32 * 2),
+        ("halo_sym", C.c_void_p * 2),
+        ("halo_cls", C.c_void_p * 2),
+        ("halo_src", C.c_void_p * 2),
+        ("in_ahead", C.c_int32),
+        ("in_d", C.c_int64),
+        ("summary", C.c_void_p),
+        ("halo_cap", C.c_int64),
+        ("export_sym", C.c_void_p),
+        ("export_cls", C.c_void_p),
+        ("export_src", C.c_void_p),
+        ("part_tab", C.c_void_p),
+        ("fin_tab", C.c_void_p),
+        ("glob", C.c_void_p),
+        ("mv_prefix", C.c_void_p),
+    ]
+
+
+SHARD_ORDER, SHARD_WALK, SHARD_TABLES, SHARD_EMIT = 0, 1, 2, 3
+SHARD_SUMMARY = 32
+
+
 class SmxRgaOps(C.Structure):
     _fields_ = [
         ("n_ops", C.c_int64),
@@ -65,6 +94,7 @@ class SmxRgaOut(C.Structure):
 EXPORTS = (
     "smx_compose_workspace_bytes",
     "smx_compose",
+    "smx_shard_step",
     "smx_set_profiling",
     "smx_stage_times",
     "smx_stage_name",
@@ -84,6 +114,9 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.smx_compose.argtypes = [C.POINTER(SmxOps), C.POINTER(SmxComposeOut), C.c_void_p,
                                 C.c_size_t, C.c_void_p]
     lib.smx_compose.restype = C.c_int
+    lib.smx_shard_step.argtypes = [C.POINTER(SmxOps), C.POINTER(SmxShard), C.POINTER(SmxComposeOut),
+                                   C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]
+    lib.smx_shard_step.restype = C.c_int
     lib.smx_set_profiling.argtypes = [C.c_int]
     lib.smx_set_profiling.restype = C.c_int
     lib.smx_stage_times.argtypes = [C.POINTER(C.c_double), c_i64p, C.c_int]

@@ -32,7 +32,14 @@ struct ComposeMeta {
   u64 n_cand;                // DivergentRename candidate starts
   u64 n_conf;                // conflicts (real)
   u32 vbits[4];              // OR of (value + 1) over table values: addr, file, ctx (packing widths)
-  u64 pad[6];
+  u64 n_skip;                // skipped renames (2 per conflict on one GPU; see smx_walk.h)
+  // sharded merge (smx_shard_step): the incoming open region's end and conflicts,
+  // the outgoing open region's state, halo too short
+  u64 q_in, nconf_in;
+  u64 out_open, out_ahead, out_d;
+  u64 halo_overflow;
+  u64 n_conf_loc;            // conflicts of this shard's own regions (scan total)
+  u64 nskip_in;              // skipped renames of the incoming region (head of the skip list)
 };
 
 // Per-symbol final states (addr, file, ctx).  When the bit widths of (value + 1)
@@ -107,6 +114,17 @@ __device__ __forceinline__ u32 wave_incl_max_u32(u32 v) {
   v = max(v, dpp_u32<0x118, 0xf>(v));
   v = max(v, dpp_u32<0x142, 0xa>(v));
   v = max(v, dpp_u32<0x143, 0xc>(v));
+  return v;
+}
+
+// OR over the wave, valid in lane 63 (DPP, VALU only).
+__device__ __forceinline__ u32 wave_or_to_last(u32 v) {
+  v |= dpp_u32<0x111, 0xf>(v);
+  v |= dpp_u32<0x112, 0xf>(v);
+  v |= dpp_u32<0x114, 0xf>(v);
+  v |= dpp_u32<0x118, 0xf>(v);
+  v |= dpp_u32<0x142, 0xa>(v);
+  v |= dpp_u32<0x143, 0xc>(v);
   return v;
 }
 

@@ -549,12 +549,26 @@ struct EmitArgs {
   u64 n;
   u32 smax;
   int allow_pack;  // the final-state table came from k_tb_reduce (packs when widths fit)
+  u64 na_loc;      // source j of this call -> global j < na_loc ? src_a + j : src_b + j - na_loc
+  i64 src_a, src_b;
   i32* out_order;
   i32* out_addr;
   i32* out_file;
   i32* out_ctx;
 };
 
+#ifndef SMX_EMIT_NT
+#define SMX_EMIT_NT 1
+#endif
+// Streams read or written once: non-temporal, so that they do not evict the
+// gathered final-state table from L2.
+#if SMX_EMIT_NT
+#define NTLD(p) __builtin_nontemporal_load(p)
+#define NTST(v, p) __builtin_nontemporal_store((v), (p))
+#else
+#define NTLD(p) (*(p))
+#define NTST(v, p) (*(p) = (v))
+#endif
 #define EMIT_WT 1024  // T positions per wave
 #define EMIT_B 8      // wave steps whose loads are issued together
 
@@ -566,7 +580,10 @@ struct EmitArgs {
 __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
   const ComposeMeta* M = E.meta;
   if (M->f_fail | M->bad_sym) return;
-  const u64 nskip = 2 * M->n_conf;
+  const u64 nskip = M->n_skip;
+  auto gsrc = [&](i32 j) -> i32 {
+    return (u64)j < E.na_loc ? (i32)(E.src_a + j) : (i32)(E.src_b + ((i64)j - (i64)E.na_loc));
+  };
   const FinPack FP = fin_pack_of(M->vbits, E.allow_pack != 0);
   const u64* fin8 = reinterpret_cast<const u64*>(E.fin);
   auto fin_at = [&](u32 s) -> int4 { return FP.packed ? fin_decode(FP, fin8[s]) : E.fin[s]; };
@@ -601,17 +618,17 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
 #pragma unroll
       for (int j = 0; j < EMIT_B; ++j) {
         const u64 T = t0 + (u64)j * WAVE + lane;
-        src[j] = E.order[T];
-        ma[j] = E.mvA[T];
-        mf[j] = E.mvF[T];
+        src[j] = NTLD(&E.order[T]);
+        ma[j] = NTLD(&E.mvA[T]);
+        mf[j] = NTLD(&E.mvF[T]);
       }
 #pragma unroll
       for (int j = 0; j < EMIT_B; ++j) {
         const u64 T = t0 + (u64)j * WAVE + lane;
-        E.out_order[T] = src[j];
-        E.out_addr[T] = ma[j];
-        E.out_file[T] = mf[j];
-        E.out_ctx[T] = -1;
+        NTST(gsrc(src[j]), &E.out_order[T]);
+        NTST(ma[j], &E.out_addr[T]);
+        NTST(mf[j], &E.out_file[T]);
+        NTST(-1, &E.out_ctx[T]);
       }
       continue;
     }
@@ -623,8 +640,8 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
       for (int j = 0; j < EMIT_B; ++j) {
         const u64 T = t0 + (u64)j * WAVE + lane;
         const u64 Tc = T < E.n ? T : E.n - 1;
-        src[j] = E.order[Tc];
-        sy[j] = min(E.symT[Tc], E.smax);
+        src[j] = NTLD(&E.order[Tc]);
+        sy[j] = min(NTLD(&E.symT[Tc]), E.smax);
       }
       int4 F[EMIT_B];
       if (FP.packed) {
@@ -642,10 +659,10 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
         const u64 T = t0 + (u64)j * WAVE + lane;
         if (T < E.n) {
           const u64 o = T - nskip;
-          E.out_order[o] = src[j];
-          E.out_addr[o] = F[j].x;
-          E.out_file[o] = F[j].y;
-          E.out_ctx[o] = F[j].z;
+          NTST(gsrc(src[j]), &E.out_order[o]);
+          NTST(F[j].x, &E.out_addr[o]);
+          NTST(F[j].y, &E.out_file[o]);
+          NTST(F[j].z, &E.out_ctx[o]);
         }
       }
       continue;
@@ -658,9 +675,9 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
 #pragma unroll
       for (int j = 0; j < EMIT_B; ++j) {
         const u64 T = t0 + (u64)j * WAVE + lane;
-        src[j] = E.order[T];
-        sy[j] = min(E.symT[T], E.smax);
-        sk[j] = E.skip[T - rs];
+        src[j] = NTLD(&E.order[T]);
+        sy[j] = min(NTLD(&E.symT[T]), E.smax);
+        sk[j] = NTLD(&E.skip[T - rs]);
       }
       int4 F[EMIT_B];
       if (FP.packed) {
@@ -679,10 +696,10 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
         const u64 bal = __ballot(sk[j] != 0);
         if (!sk[j]) {
           const u64 o = T - run - __popcll(bal & lt);
-          E.out_order[o] = src[j];
-          E.out_addr[o] = F[j].x;
-          E.out_file[o] = F[j].y;
-          E.out_ctx[o] = -1;
+          NTST(gsrc(src[j]), &E.out_order[o]);
+          NTST(F[j].x, &E.out_addr[o]);
+          NTST(F[j].y, &E.out_file[o]);
+          NTST(-1, &E.out_ctx[o]);
         }
         run += __popcll(bal);
       }
@@ -694,26 +711,26 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
       const u64 T = t0 + (u64)j * WAVE + lane;
       const bool valid = T < E.n;
       const bool in_ren = T >= rs && T < re;
-      const bool sk = valid && in_ren && E.skip[T - rs];
+      const bool sk = valid && in_ren && NTLD(&E.skip[T - rs]);
       const u64 bal = __ballot(sk);
       if (valid && !sk) {
         const u64 o = T - run - __popcll(bal & lt);
-        const i32 src = E.order[T];
+        const i32 src = NTLD(&E.order[T]);
         i32 a, f, cc;
         if (T < rs) {
-          a = E.mvA[T];
-          f = E.mvF[T];
+          a = NTLD(&E.mvA[T]);
+          f = NTLD(&E.mvF[T]);
           cc = -1;
         } else {
-          const int4 F = fin_at(min(E.symT[T], E.smax));
+          const int4 F = fin_at(min(NTLD(&E.symT[T]), E.smax));
           a = F.x;
           f = F.y;
           cc = in_ren ? -1 : F.z;
         }
-        E.out_order[o] = src;
-        E.out_addr[o] = a;
-        E.out_file[o] = f;
-        E.out_ctx[o] = cc;
+        NTST(gsrc(src), &E.out_order[o]);
+        NTST(a, &E.out_addr[o]);
+        NTST(f, &E.out_file[o]);
+        NTST(cc, &E.out_ctx[o]);
       }
       run += __popcll(bal);
     }
@@ -723,12 +740,20 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
 // Moves whose newAddress or newFile is None see the symbol's inclusive prefix
 // (compose.py:73-82 + 37-41): moves grouped by symbol in T order, last-non-None
 // scan; the composed output index of move T is T (no skips precede the renames).
+// Sharded merge: mvpre[2][n_sym] = the symbol's last non-None (addr, file) on the
+// lower shards, as (shard + 1) << 32 | (value + 1), 0 = none.
 __global__ void k_mv_fix(const u64* __restrict__ keys, const u32* __restrict__ vals, u64 nMv,
                          const i32* __restrict__ mvA, const i32* __restrict__ mvF,
+                         const u64* __restrict__ mvpre, u64 n_sym,
                          i32* __restrict__ out_addr, i32* __restrict__ out_file) {
   for (u64 j = (u64)blockIdx.x * BLOCK + threadIdx.x; j < nMv; j += (u64)gridDim.x * BLOCK) {
     if (j != 0 && keys[j - 1] == keys[j]) continue;
     i32 ra = -1, rf = -1;
+    if (mvpre && keys[j] < n_sym) {
+      const u64 pa = mvpre[keys[j]], pf = mvpre[n_sym + keys[j]];
+      if (pa) ra = (i32)(u32)pa - 1;
+      if (pf) rf = (i32)(u32)pf - 1;
+    }
     for (u64 i = j; i < nMv && keys[i] == keys[j]; ++i) {
       const u32 T = vals[i];
       if (mvA[T] >= 0) ra = mvA[T];
@@ -745,7 +770,7 @@ __global__ void k_counts(const ComposeMeta* meta, u64 n, i64* counts) {
     counts[1] = -1;
     return;
   }
-  counts[0] = (i64)(n - 2 * meta->n_conf);
+  counts[0] = (i64)(n - meta->n_skip);
   counts[1] = (i64)meta->n_conf;
 }
 
@@ -799,7 +824,7 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_CCNT] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)256) + 2) * 4;
   sz[B_SMP] = (size_t)(SMX_CEIL_DIV(nn, (i64)CH) + 4) * 8;
   sz[B_TSUM] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)CH * CS_TILE) + 2) * 4;
-  Layout L;
+  Layout L{};
   size_t acc = 0;
   for (int i = 0; i < B_N; ++i) {
     L.off[i] = acc;
@@ -828,7 +853,7 @@ struct Ctx {
   const smx_ops* ops;
   const smx_compose_out* out;
   hipStream_t st;
-  Layout L;
+  Layout L{};
   char* base;
   i64 na, nb, n, n_sym;
   StageTimer* tm;
@@ -874,91 +899,164 @@ static WinArgs win_args(const Ctx& C) {
   return P;
 }
 
-// Walk, tables, emit, counts: every size is read on the device from meta, so the
-// whole tail is enqueued without a host sync.
-static int launch_tail(const Ctx& C, const WinArgs& P) {
+// Sharded-merge parameters of the tail stages (none for a single merge).
+struct TailShard {
+  const smx_shard* sh = nullptr;
+};
+
+static WalkArgs walk_args(const Ctx& C, const WinArgs& P, const smx_shard* sh) {
+  WalkArgs Wk{};
+  Wk.Msym = P.Msym;
+  Wk.Mcls = P.Mcls;
+  Wk.Mside = P.Mside;
+  Wk.Mown = P.Mown;
+  Wk.RA = P.RA;
+  Wk.RB = P.RB;
+  Wk.meta = C.ws<ComposeMeta>(B_META);
+  Wk.na_cap = (u64)C.na;
+  Wk.nb_cap = (u64)C.nb;
+  Wk.src_a = sh ? sh->src_a : 0;
+  Wk.src_b = sh ? sh->src_b : C.na;
+  for (int b = 0; b < 2; ++b) {
+    Wk.halo_sym[b] = sh ? sh->halo_sym[b] : nullptr;
+    Wk.halo_cls[b] = sh ? sh->halo_cls[b] : nullptr;
+    Wk.halo_src[b] = sh ? sh->halo_src[b] : nullptr;
+    Wk.halo_n[b] = sh && sh->halo_sym[b] ? (u64)sh->halo_n[b] : 0;
+    Wk.halo_more[b] = sh ? sh->halo_more[b] : 0;
+  }
+  return Wk;
+}
+
+__global__ void k_walk_init(ComposeMeta* meta) {
+  meta->n_cand = 0;
+  meta->n_conf = 0;
+  meta->n_conf_loc = 0;
+  meta->n_skip = 0;
+  meta->q_in = 0;
+  meta->nconf_in = 0;
+  meta->out_open = 0;
+  meta->out_ahead = 0;
+  meta->out_d = 0;
+  meta->halo_overflow = 0;
+  meta->nskip_in = 0;
+}
+
+__global__ void k_walk_done(ComposeMeta* meta) { meta->n_conf = meta->nconf_in + meta->n_conf_loc; }
+
+// DivergentRename walk (smx_walk.h): conflicts, skip flags, sorted skip list.
+// Every size is read on the device from meta: no host sync.
+static int launch_walk(const Ctx& C, const WinArgs& P, const smx_shard* sh) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   const i64 n = C.n;
   u8* skip = C.ws<u8>(B_SKIP);
-  u32* skiplist = C.ws<u32>(B_SKIPEX);  // sorted skipped rename positions (2 per conflict)
+  u32* skiplist = C.ws<u32>(B_SKIPEX);
   u32* part = C.ws<u32>(B_PART);
-
-  C.tm->begin(ST_WALK);
   HIP_TRY(hipMemsetAsync(skip, 0, n, st));
-  {
-    WalkArgs Wk{P.Msym, P.Mcls, P.Mside, P.Mown, P.RA, P.RB, meta, (u64)C.na, (u64)C.nb, 0, 0, 0, 0};
-    u8* flags = C.ws<u8>(B_FLAGS);
-    u32* bcnt = C.ws<u32>(B_FPOS);
-    u32* cand = C.ws<u32>(B_CAND);
-    u32* q = C.ws<u32>(B_Q);
-    u32* pm = C.ws<u32>(B_PM);
-    u32* nconf = C.ws<u32>(B_NCONF);
-    u32* nreal = C.ws<u32>(B_NREAL);
-    u32* coff = C.ws<u32>(B_COFF);
-    // n_conf is u64 in meta; the scan writes its u32 total into the low word
-    // (little endian) of the zeroed field.
-    u32* nconf32 = (u32*)&meta->n_conf;
-    const u64* ncand_dev = &meta->n_cand;
-    const u32 nfb = (u32)SMX_CEIL_DIV((u64)n, (u64)FLAG_TILE);  // upper bound; idle blocks exit
-    const int gsmall = 256;  // grid for loops over the (few) candidates
-    hipLaunchKernelGGL(k_flags, dim3(nfb), dim3(BLOCK), 0, st, Wk, flags, bcnt);
-    hipLaunchKernelGGL(k_flag_offsets, dim3(1), dim3(BLOCK), 0, st, Wk, bcnt, meta);
-    hipLaunchKernelGGL(k_compact, dim3(nfb), dim3(BLOCK), 0, st, Wk, flags, bcnt, cand);
-    hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
-    HIP_TRY((scan_excl<OpMax, u32, u32>(q, pm, 0, ncand_dev, part, (u32*)nullptr, st)));
-    hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, cand, q, pm, nconf, meta, nreal);
-    HIP_TRY((scan_excl<OpSum, u32, u32>(nreal, coff, 0, ncand_dev, part, nconf32, st)));
-    hipLaunchKernelGGL(k_replay_write, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, nreal, coff, meta,
-                       P.order, C.out->conflicts, (u64)C.out->conflict_cap, skip, skiplist);
-    HIP_TRY(hipGetLastError());
-  }
-  C.tm->end(ST_WALK);
+  hipLaunchKernelGGL(k_walk_init, dim3(1), dim3(1), 0, st, meta);
+  const WalkArgs Wk = walk_args(C, P, sh);
+  u8* flags = C.ws<u8>(B_FLAGS);
+  u32* bcnt = C.ws<u32>(B_FPOS);
+  u32* cand = C.ws<u32>(B_CAND);
+  u32* q = C.ws<u32>(B_Q);
+  u32* pm = C.ws<u32>(B_PM);
+  u32* nconf = C.ws<u32>(B_NCONF);
+  u32* nreal = C.ws<u32>(B_NREAL);
+  u32* coff = C.ws<u32>(B_COFF);
+  // u64 counters of meta: the scans write their u32 totals into the low word
+  // (little endian) of the zeroed fields
+  u32* nconf32 = (u32*)&meta->n_conf_loc;
+  const u64* ncand_dev = &meta->n_cand;
+  const u32 nfb = (u32)SMX_CEIL_DIV((u64)n, (u64)FLAG_TILE);  // upper bound; idle blocks exit
+  const int gsmall = 256;  // grid for loops over the (few) candidates
+  if (sh && sh->in_d > 0)
+    hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d, meta, P.order,
+                       C.out->conflicts, (u64)C.out->conflict_cap, skip, skiplist);
+  hipLaunchKernelGGL(k_flags, dim3(nfb), dim3(BLOCK), 0, st, Wk, flags, bcnt);
+  hipLaunchKernelGGL(k_flag_offsets, dim3(1), dim3(BLOCK), 0, st, Wk, bcnt, &meta->n_cand);
+  hipLaunchKernelGGL(k_compact, dim3(nfb), dim3(BLOCK), 0, st, Wk, flags, bcnt, cand);
+  hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
+  HIP_TRY((scan_excl<OpMax, u32, u32>(q, pm, 0, ncand_dev, part, (u32*)nullptr, st)));
+  hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, cand, q, pm, nconf, meta, nreal);
+  HIP_TRY((scan_excl<OpSum, u32, u32>(nreal, coff, 0, ncand_dev, part, nconf32, st)));
+  hipLaunchKernelGGL(k_replay_write, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, nreal, coff, meta, P.order,
+                     C.out->conflicts, (u64)C.out->conflict_cap, skip, skiplist);
+  hipLaunchKernelGGL(k_walk_done, dim3(1), dim3(1), 0, st, meta);
+  HIP_TRY(hipGetLastError());
+  return SMX_OK;
+}
 
-  C.tm->begin(ST_TABLES);
+// Per-symbol last writers.  part == nullptr: the final-state table fin (packed
+// when the value widths allow); otherwise this shard's partial tables.
+static int launch_tables(const Ctx& C, const WinArgs& P, u64* part_tab, u32 tag, bool* bucketed) {
+  hipStream_t st = C.st;
+  ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
+  const i64 n = C.n;
+  u8* skip = C.ws<u8>(B_SKIP);
+  u32* part = C.ws<u32>(B_PART);
   int4* fin = C.ws<int4>(B_FIN);
-  bool bucketed = false;
-  {
-    const i64 n_sym = C.n_sym;
-    TbArgs A{P.symT, P.mvA, P.mvF, P.Msym, P.Mstr, skip, meta, (u64)n, 1u, 1u, (u32)(n_sym - 1), 0, 0};
-    u64 width = SMX_CEIL_DIV((u64)n_sym, (u64)256);
-    if (width < 1) width = 1;
-    if (width > TB_WIDTH) width = TB_WIDTH;
-    const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);
-    if (nbk <= TB_MAXBK) {
-      bucketed = true;
-      A.width = (u32)width;
-      A.nbk = (u32)nbk;
-      const int nblk = (int)SMX_CEIL_DIV((u64)n, (u64)TB_TILE);
-      u32* hist = C.ws<u32>(B_TBHIST);
-      u32* total = C.ws<u32>(B_TBTOT);
-      u64* rec = C.ws<u64>(B_REC);
-      hipLaunchKernelGGL(k_tb_hist, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk);
-      HIP_TRY((scan_excl<OpSum, u32, u32>(hist, hist, (i64)nbk * nblk, nullptr, part, total, st)));
-      hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk, rec);
-      hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, hist, nblk, total, rec, n_sym, fin);
-    } else {
-      // very large symbol spaces: device-scope atomics on the packed keys
-      u32* tabA = C.ws<u32>(B_TABA);
-      u32* tabF = C.ws<u32>(B_TABF);
-      u32* tabR = C.ws<u32>(B_TABR);
-      HIP_TRY(hipMemsetAsync(tabA, 0, (size_t)n_sym * 4, st));
-      HIP_TRY(hipMemsetAsync(tabF, 0, (size_t)n_sym * 4, st));
-      HIP_TRY(hipMemsetAsync(tabR, 0, (size_t)n_sym * 4, st));
-      hipLaunchKernelGGL(k_tab_atomic, dim3(grid_for(n)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR);
-      hipLaunchKernelGGL(k_finalize, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR, n_sym, fin);
-    }
+  *bucketed = false;
+  const i64 n_sym = C.n_sym;
+  TbArgs A{P.symT, P.mvA, P.mvF, P.Msym, P.Mstr, skip, meta, (u64)n, 1u, 1u, (u32)(n_sym - 1), 0, 0};
+  u64 width = SMX_CEIL_DIV((u64)n_sym, (u64)256);
+  if (width < 1) width = 1;
+  if (width > TB_WIDTH) width = TB_WIDTH;
+  const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);
+  if (nbk <= TB_MAXBK) {
+    *bucketed = true;
+    A.width = (u32)width;
+    A.nbk = (u32)nbk;
+    const int nblk = (int)SMX_CEIL_DIV((u64)n, (u64)TB_TILE);
+    u32* hist = C.ws<u32>(B_TBHIST);
+    u32* total = C.ws<u32>(B_TBTOT);
+    u64* rec = C.ws<u64>(B_REC);
+    hipLaunchKernelGGL(k_tb_hist, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk);
+    HIP_TRY((scan_excl<OpSum, u32, u32>(hist, hist, (i64)nbk * nblk, nullptr, part, total, st)));
+    hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk, rec);
+    hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, hist, nblk, total, rec, n_sym, fin,
+                       part_tab, tag);
+  } else {
+    // very large symbol spaces: device-scope atomics on the packed keys
+    u32* tabA = C.ws<u32>(B_TABA);
+    u32* tabF = C.ws<u32>(B_TABF);
+    u32* tabR = C.ws<u32>(B_TABR);
+    HIP_TRY(hipMemsetAsync(tabA, 0, (size_t)n_sym * 4, st));
+    HIP_TRY(hipMemsetAsync(tabF, 0, (size_t)n_sym * 4, st));
+    HIP_TRY(hipMemsetAsync(tabR, 0, (size_t)n_sym * 4, st));
+    hipLaunchKernelGGL(k_tab_atomic, dim3(grid_for(n)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR);
+    hipLaunchKernelGGL(k_finalize, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR, n_sym, fin,
+                       part_tab, tag);
   }
   HIP_TRY(hipGetLastError());
-  C.tm->end(ST_TABLES);
+  return SMX_OK;
+}
 
-  C.tm->begin(ST_EMIT);
-  EmitArgs E{P.order, P.symT, P.mvA, P.mvF, skip, skiplist, fin, meta, (u64)n, (u32)(C.n_sym - 1),
-             bucketed ? 1 : 0, C.out->order, C.out->addr, C.out->file, C.out->ctx};
+static int launch_emit(const Ctx& C, const WinArgs& P, bool packable, const smx_shard* sh) {
+  hipStream_t st = C.st;
+  ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
+  const i64 n = C.n;
+  EmitArgs E{P.order, P.symT, P.mvA, P.mvF, C.ws<u8>(B_SKIP), C.ws<u32>(B_SKIPEX), C.ws<int4>(B_FIN), meta,
+             (u64)n, (u32)(C.n_sym - 1), packable ? 1 : 0, (u64)C.na, sh ? sh->src_a : 0,
+             sh ? sh->src_b : C.na, C.out->order, C.out->addr, C.out->file, C.out->ctx};
   const i64 ewaves = SMX_CEIL_DIV(n, (i64)EMIT_WT);
   hipLaunchKernelGGL(k_emit, dim3(SMX_CEIL_DIV(ewaves, (i64)NWAVES)), dim3(BLOCK), 0, st, E);
   hipLaunchKernelGGL(k_counts, dim3(1), dim3(1), 0, st, meta, (u64)n, C.out->counts);
   HIP_TRY(hipGetLastError());
+  return SMX_OK;
+}
+
+// Walk, tables, emit of a single merge.
+static int launch_tail(const Ctx& C, const WinArgs& P) {
+  C.tm->begin(ST_WALK);
+  int rc = launch_walk(C, P, nullptr);
+  if (rc) return rc;
+  C.tm->end(ST_WALK);
+  C.tm->begin(ST_TABLES);
+  bool bucketed = false;
+  if ((rc = launch_tables(C, P, nullptr, 0, &bucketed))) return rc;
+  C.tm->end(ST_TABLES);
+  C.tm->begin(ST_EMIT);
+  if ((rc = launch_emit(C, P, bucketed, nullptr))) return rc;
   C.tm->end(ST_EMIT);
   return SMX_OK;
 }
@@ -1102,71 +1200,247 @@ static int read_meta(const Ctx& C, ComposeMeta* hm) {
   return SMX_OK;
 }
 
-static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
-                        hipStream_t st) {
+static int check_args(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes, Layout* L) {
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
   if (na < 0 || nb < 0 || n_sym < 0) return set_err(SMX_E_ARG, "negative size");
   if (n >= (i64)0x7fffffff) return set_err(SMX_E_ARG, "n_a + n_b must be < 2^31");
   if (!out || !out->counts) return set_err(SMX_E_ARG, "null output");
-  if (n == 0) {
-    HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
-    return SMX_OK;
-  }
+  if (n == 0) return SMX_OK;
   if (!ops->kind || !ops->ts || !ops->oid_hi || !ops->oid_lo || !ops->sym || !ops->v0 || !ops->v1 ||
       !out->order || !out->addr || !out->file || !out->ctx || (!out->conflicts && out->conflict_cap > 0))
     return set_err(SMX_E_ARG, "null input/output pointer");
   if (n_sym < 1) return set_err(SMX_E_ARG, "n_sym must be >= 1");
-  const Layout L = layout(na, nb, n_sym);
-  if (!ws || ws_bytes < L.total)
-    return set_err(SMX_E_WORKSPACE, "workspace too small: need " + std::to_string(L.total));
-  int prof;
-  {
-    std::lock_guard<std::mutex> g(g_prof_mu);
-    prof = g_prof;
-  }
-  StageTimer tm(st, prof != 0);
-  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, &tm};
+  *L = layout(na, nb, n_sym);
+  if (!ws || ws_bytes < L->total)
+    return set_err(SMX_E_WORKSPACE, "workspace too small: need " + std::to_string(L->total));
+  return SMX_OK;
+}
 
-  // Presorted plan first; a window that overflows LDS (dense timestamp ties)
-  // retries with smaller windows, a log that is not timestamp-ordered goes to the
-  // generic plan.
+static int profiling_on() {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  return g_prof;
+}
+
+// T order of the merge: the presorted plan first; a window that overflows LDS
+// (dense timestamp ties) retries with smaller windows; a log that is not
+// timestamp-ordered goes to the generic plan when allowed.  hm: the meta after it.
+static int run_order(const Ctx& C, bool allow_generic, ComposeMeta* hm) {
   i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
   int rc = run_presorted(C, tgt);
   if (rc) return rc;
+  if ((rc = read_meta(C, hm))) return rc;
+  while (hm->f_fail == 2 && !hm->bad_sym && tgt > WIN_TGT_MIN) {
+    tgt = (tgt / 2) / CH * CH;
+    if ((rc = run_presorted(C, tgt))) return rc;
+    if ((rc = read_meta(C, hm))) return rc;
+  }
+  if (hm->f_fail && !hm->bad_sym && allow_generic) {
+    if ((rc = run_generic(C))) return rc;
+    if ((rc = read_meta(C, hm))) return rc;
+  }
+  return SMX_OK;
+}
+
+// Moves whose newAddress or newFile is None see the symbol's inclusive prefix of
+// non-None values: moves grouped by symbol (radix sort), then a scan per symbol,
+// seeded from the lower shards' values (mvpre) in a sharded merge.
+static int run_mvprefix(const Ctx& C, const ComposeMeta& hm, const u64* mvpre) {
+  hipStream_t st = C.st;
+  const u64 nMv = hm.kcnt[KMOVE];
+  if (hm.n_move_none == 0 || nMv == 0) return SMX_OK;
+  const i64 n_sym = C.n_sym;
+  u64* keys = C.ws<u64>(B_RKEY);
+  u32* vals = C.ws<u32>(B_RVAL);
+  RadixTemp rt{C.ws<u64>(B_RK2), C.ws<u32>(B_RV2), C.ws<u32>(B_RHIST), C.ws<u32>(B_PART)};
+  int shifts[4], ns = 0;
+  for (int dgt = 0; dgt < 4; ++dgt)
+    if (((u64)(n_sym - 1) >> (8 * dgt)) != 0) shifts[ns++] = 8 * dgt;
+  hipLaunchKernelGGL(k_mv_init, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, C.ws<u32>(B_SYMT), nMv, keys, vals);
+  if (ns) HIP_TRY(radix_sort_pairs(keys, vals, (i64)nMv, shifts, ns, rt, st));
+  hipLaunchKernelGGL(k_mv_fix, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, keys, vals, nMv, C.ws<i32>(B_MVA),
+                     C.ws<i32>(B_MVF), mvpre, (u64)n_sym, C.out->addr, C.out->file);
+  HIP_TRY(hipGetLastError());
+  return SMX_OK;
+}
+
+static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
+                        hipStream_t st) {
+  Layout L{};
+  int rc = check_args(ops, out, ws, ws_bytes, &L);
+  if (rc) return rc;
+  const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
+  if (n == 0) {
+    HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
+    return SMX_OK;
+  }
+  StageTimer tm(st, profiling_on() != 0);
+  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, &tm};
   if (env_int("SMX_ABLATE", 0)) {  // diagnostics: timing of the window stage only
+    if ((rc = run_presorted(C, env_int("SMX_WIN_TGT", WIN_TGT)))) return rc;
     tm.flush();
     return SMX_OK;
   }
   ComposeMeta hm;
-  if ((rc = read_meta(C, &hm))) return rc;
-  while (hm.f_fail == 2 && !hm.bad_sym && tgt > WIN_TGT_MIN) {
-    tgt = (tgt / 2) / CH * CH;
-    if ((rc = run_presorted(C, tgt))) return rc;
-    if ((rc = read_meta(C, &hm))) return rc;
-  }
-  if (hm.f_fail && !hm.bad_sym) {  // not presorted: redo on the generic plan
-    if ((rc = run_generic(C))) return rc;
-    if ((rc = read_meta(C, &hm))) return rc;
-  }
+  if ((rc = run_order(C, true, &hm))) return rc;
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
-  const u64 nMv = hm.kcnt[KMOVE];
-  if (hm.n_move_none > 0 && nMv > 0) {
-    tm.begin(ST_MVPREFIX);
-    u64* keys = C.ws<u64>(B_RKEY);
-    u32* vals = C.ws<u32>(B_RVAL);
-    RadixTemp rt{C.ws<u64>(B_RK2), C.ws<u32>(B_RV2), C.ws<u32>(B_RHIST), C.ws<u32>(B_PART)};
-    int shifts[4], ns = 0;
-    for (int dgt = 0; dgt < 4; ++dgt)
-      if (((u64)(n_sym - 1) >> (8 * dgt)) != 0) shifts[ns++] = 8 * dgt;
-    hipLaunchKernelGGL(k_mv_init, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, C.ws<u32>(B_SYMT), nMv, keys, vals);
-    if (ns) HIP_TRY(radix_sort_pairs(keys, vals, (i64)nMv, shifts, ns, rt, st));
-    hipLaunchKernelGGL(k_mv_fix, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, keys, vals, nMv, C.ws<i32>(B_MVA),
-                       C.ws<i32>(B_MVF), out->addr, out->file);
-    HIP_TRY(hipGetLastError());
-    tm.end(ST_MVPREFIX);
+  tm.begin(ST_MVPREFIX);
+  if ((rc = run_mvprefix(C, hm, nullptr))) return rc;
+  tm.end(ST_MVPREFIX);
+  tm.flush();
+  return SMX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// sharded merge (include/smx.h smx_shard_step)
+
+__device__ __forceinline__ i32 shard_gsrc(i32 j, u64 na, i64 src_a, i64 src_b) {
+  return (u64)j < na ? (i32)(src_a + j) : (i32)(src_b + ((i64)j - (i64)na));
+}
+
+// summary[0..21] and the first `cap` renames of each branch (the previous
+// shards' halo).
+__global__ void k_shard_export(const ComposeMeta* meta, const WinArgs P, i64* summary, u32* xsym, i32* xcls,
+                               i32* xsrc, i64 cap, i64 src_a, i64 src_b) {
+  const u64 nr[2] = {meta->n_ren_side[0], meta->n_ren_side[1]};
+  const i32* order_ren = P.order + meta->base[KREN];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (int k = 0; k < SMX_N_KINDS; ++k) summary[k] = (i64)meta->kcnt[k];
+    summary[18] = (i64)nr[0];
+    summary[19] = (i64)nr[1];
+    summary[20] = (i64)meta->n_move_none;
+    summary[21] = (i64)((meta->f_fail ? 1 : 0) | (meta->bad_sym ? 2 : 0));
+  }
+  if (meta->f_fail | meta->bad_sym) return;
+  for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < 2 * cap; i += (i64)gridDim.x * BLOCK) {
+    const int b = i >= cap;
+    const i64 k = b ? i - cap : i;
+    if ((u64)k >= nr[b]) continue;
+    const u32 u = (b ? P.RB : P.RA)[k];
+    xsym[i] = P.Msym[u];
+    xcls[i] = P.Mcls[u];
+    xsrc[i] = shard_gsrc(order_ren[u], (u64)P.na, src_a, src_b);
+  }
+}
+
+__global__ void k_shard_walk_sum(const ComposeMeta* meta, i64* summary) {
+  summary[22] = (i64)meta->out_open;
+  summary[23] = (i64)meta->out_ahead;
+  summary[24] = (i64)meta->out_d;
+  summary[25] = (i64)meta->n_conf;
+  summary[26] = (i64)meta->n_skip;
+  summary[27] = (i64)meta->halo_overflow;
+}
+
+__global__ void k_shard_tab_sum(const ComposeMeta* meta, i64* summary, int bucketed) {
+  for (int i = 0; i < 3; ++i) summary[28 + i] = bucketed ? (i64)bit_width32(meta->vbits[i]) : 32;
+}
+
+// fin from the reduced partial tables: packed with the global widths when they
+// fit in 64 bits (meta->vbits takes the global widths, for k_emit).
+__global__ void k_fin_from_tab(const u64* __restrict__ tab, const i64* __restrict__ glob, i64 n_sym,
+                               ComposeMeta* meta, int4* __restrict__ fin) {
+  u32 w[3];
+  for (int i = 0; i < 3; ++i) w[i] = (u32)min(max(glob[i], (i64)0), (i64)32);
+  const FinPack FP{w[0], w[1], w[0] + w[1] + w[2] <= 64};
+  if (blockIdx.x == 0 && threadIdx.x < 3)
+    meta->vbits[threadIdx.x] = w[threadIdx.x] >= 32 ? ~0u : ((1u << w[threadIdx.x]) - 1u);
+  u64* fin8 = reinterpret_cast<u64*>(fin);
+  for (i64 s = (i64)blockIdx.x * BLOCK + threadIdx.x; s < n_sym; s += (i64)gridDim.x * BLOCK) {
+    const u64 a = tab[s], f = tab[n_sym + s], c = tab[2 * n_sym + s];
+    const int va = a ? (int)(u32)a - 1 : -1, vf = f ? (int)(u32)f - 1 : -1, vc = c ? (int)(u32)c - 1 : -1;
+    if (FP.packed) fin8[s] = fin_encode(FP, va, vf, vc);
+    else fin[s] = make_int4(va, vf, vc, 0);
+  }
+}
+
+static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose_out* out, void* ws,
+                      size_t ws_bytes, hipStream_t st, int step) {
+  if (!sh || !sh->summary) return set_err(SMX_E_ARG, "null shard / summary");
+  Layout L{};
+  int rc = check_args(ops, out, ws, ws_bytes, &L);
+  if (rc) return rc;
+  const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
+  StageTimer tm(st, profiling_on() != 0);
+  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, &tm};
+  if (n == 0) {  // an empty shard: neutral summaries and outputs
+    if (step == SMX_SHARD_ORDER) HIP_TRY(hipMemsetAsync(sh->summary, 0, SMX_SHARD_SUMMARY * 8, st));
+    if (step == SMX_SHARD_WALK && sh->in_d > 0) {
+      // the open region passes through unchanged
+      const i64 pass[3] = {1, sh->in_ahead, sh->in_d};
+      HIP_TRY(hipMemcpyAsync(sh->summary + 22, pass, sizeof(pass), hipMemcpyHostToDevice, st));
+      HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (step == SMX_SHARD_TABLES && sh->part_tab)
+      HIP_TRY(hipMemsetAsync(sh->part_tab, 0, (size_t)3 * n_sym * 8, st));
+    if (step == SMX_SHARD_EMIT) HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
+    return SMX_OK;
+  }
+  const WinArgs P = win_args(C);
+  switch (step) {
+    case SMX_SHARD_ORDER: {
+      if (sh->halo_cap < 0 || (sh->halo_cap > 0 && (!sh->export_sym || !sh->export_cls || !sh->export_src)))
+        return set_err(SMX_E_ARG, "bad export buffers");
+      ComposeMeta hm;
+      tm.begin(ST_PLAN);
+      if ((rc = run_order(C, false, &hm))) return rc;
+      hipLaunchKernelGGL(k_shard_export, dim3(grid_for(2 * sh->halo_cap + 1)), dim3(BLOCK), 0, st,
+                         C.ws<ComposeMeta>(B_META), P, sh->summary, sh->export_sym, sh->export_cls,
+                         sh->export_src, sh->halo_cap, sh->src_a, sh->src_b);
+      HIP_TRY(hipGetLastError());
+      tm.end(ST_PLAN);
+      if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
+      if (hm.f_fail)
+        return set_err(SMX_E_ARG, "sharded merge needs timestamp-ordered branch logs in every shard");
+      break;
+    }
+    case SMX_SHARD_WALK: {
+      tm.begin(ST_WALK);
+      if ((rc = launch_walk(C, P, sh))) return rc;
+      hipLaunchKernelGGL(k_shard_walk_sum, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary);
+      HIP_TRY(hipGetLastError());
+      tm.end(ST_WALK);
+      break;
+    }
+    case SMX_SHARD_TABLES: {
+      if (!sh->part_tab) return set_err(SMX_E_ARG, "null part_tab");
+      tm.begin(ST_TABLES);
+      bool bucketed = false;
+      if ((rc = launch_tables(C, P, sh->part_tab, (u32)sh->rank + 1u, &bucketed))) return rc;
+      hipLaunchKernelGGL(k_shard_tab_sum, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary,
+                         bucketed ? 1 : 0);
+      HIP_TRY(hipGetLastError());
+      tm.end(ST_TABLES);
+      break;
+    }
+    case SMX_SHARD_EMIT: {
+      if (!sh->fin_tab || !sh->glob) return set_err(SMX_E_ARG, "null fin_tab / glob");
+      tm.begin(ST_EMIT);
+      hipLaunchKernelGGL(k_fin_from_tab, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, sh->fin_tab, sh->glob, n_sym,
+                         C.ws<ComposeMeta>(B_META), C.ws<int4>(B_FIN));
+      if ((rc = launch_emit(C, P, true, sh))) return rc;
+      tm.end(ST_EMIT);
+      ComposeMeta hm;
+      if ((rc = read_meta(C, &hm))) return rc;
+      tm.begin(ST_MVPREFIX);
+      if ((rc = run_mvprefix(C, hm, sh->mv_prefix))) return rc;
+      tm.end(ST_MVPREFIX);
+      break;
+    }
+    default:
+      return set_err(SMX_E_ARG, "unknown shard step");
   }
   tm.flush();
   return SMX_OK;
+}
+
+extern "C" int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const smx_compose_out* out,
+                              void* workspace, size_t workspace_bytes, void* stream, int step) {
+  if (!ops) return set_err(SMX_E_ARG, "null ops");
+  try {
+    return shard_impl(ops, shard, out, workspace, workspace_bytes, (hipStream_t)stream, step);
+  } catch (const std::exception& e) {
+    return set_err(SMX_E_HIP, e.what());
+  }
 }
 
 extern "C" int smx_compose(const smx_ops* ops, const smx_compose_out* out, void* workspace,

@@ -64,8 +64,11 @@ __device__ __forceinline__ bool tb_record(const TbArgs& A, u64 r, u32* sym, u32*
 
 // The TB_ITEMS records of a lane (r = base + it * TB_NT + lane), loads issued
 // together: a tile is all moves, all renames, or (one tile) mixed.
+// VB: also OR (value + 1) of the tile's values into vb (addr, file, name) for the
+// packed final-state table widths (k_tb_hist only).
+template <bool VB = false>
 __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[TB_ITEMS], u32 (&fl)[TB_ITEMS],
-                                         bool (&ok)[TB_ITEMS]) {
+                                         bool (&ok)[TB_ITEMS], u32* vb = nullptr) {
   const u64 nrec = A.nMv + A.nR;
   const u64 end = base + (u64)TB_TILE;
   if (end <= A.nMv) {
@@ -83,27 +86,40 @@ __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[T
       ok[it] = a[it] >= 0 || f[it] >= 0;
       fl[it] = (a[it] >= 0 ? 1u : 0u) | (f[it] >= 0 ? 2u : 0u);
       sym[it] = min(s[it], A.smax);
+      if (VB) {
+        vb[0] |= (u32)(a[it] + 1);
+        vb[1] |= (u32)(f[it] + 1);
+      }
     }
   } else if (base >= A.nMv && end <= nrec) {
     u32 s[TB_ITEMS];
     u8 k[TB_ITEMS];
+    i32 c[TB_ITEMS];
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
       const u64 m = base - A.nMv + (u64)it * TB_NT + threadIdx.x;
       s[it] = A.Msym[m];
       k[it] = A.skip[m];
+      if (VB) c[it] = A.Mstr[m];
     }
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
       ok[it] = k[it] == 0;
       fl[it] = 0;
       sym[it] = min(s[it], A.smax);
+      if (VB) vb[2] |= (u32)(c[it] + 1);
     }
   } else {
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
       const u64 r = base + (u64)it * TB_NT + threadIdx.x;
       ok[it] = r < nrec && tb_record(A, r, &sym[it], &fl[it]);
+      if (VB && r < A.nMv) {
+        vb[0] |= (u32)(A.mvA[r] + 1);
+        vb[1] |= (u32)(A.mvF[r] + 1);
+      } else if (VB && r < nrec) {
+        vb[2] |= (u32)(A.Mstr[r - A.nMv] + 1);
+      }
     }
   }
 }
@@ -120,31 +136,17 @@ __global__ void __launch_bounds__(TB_NT) k_tb_hist(TbArgs A0, u32* __restrict__ 
   if (base < nrec) {
     u32 s[TB_ITEMS], fl[TB_ITEMS];
     bool ok[TB_ITEMS];
-    tb_items(A, base, s, fl, ok);
+    u32 v3[3] = {0u, 0u, 0u};
+    tb_items<true>(A, base, s, fl, ok, v3);
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it)
       if (ok[it]) atomicAdd(&h[s[it] / A.width], 1u);
-    // value bit widths for the packed final-state table (smx_common.h FinPack):
-    // OR of (value + 1) over moves' addr / file and renames' names (cache hits
-    // except the names)
-    u32 oa = 0, of = 0, oc = 0;
-#pragma unroll
-    for (int it = 0; it < TB_ITEMS; ++it) {
-      const u64 r = base + (u64)it * TB_NT + threadIdx.x;
-      if (r < A.nMv) {
-        oa |= (u32)(A.mvA[r] + 1);
-        of |= (u32)(A.mvF[r] + 1);
-      } else if (r < nrec) {
-        oc |= (u32)(A.Mstr[r - A.nMv] + 1);
-      }
-    }
-#pragma unroll
-    for (int o = WAVE / 2; o > 0; o >>= 1) {
-      oa |= __shfl_xor(oa, o, WAVE);
-      of |= __shfl_xor(of, o, WAVE);
-      oc |= __shfl_xor(oc, o, WAVE);
-    }
-    if ((threadIdx.x & (WAVE - 1)) == 0) {
+    // value bit widths for the packed final-state table (smx_common.h FinPack)
+    u32 oa = v3[0], of = v3[1], oc = v3[2];
+    oa = wave_or_to_last(oa);
+    of = wave_or_to_last(of);
+    oc = wave_or_to_last(oc);
+    if ((threadIdx.x & (WAVE - 1)) == WAVE - 1) {
       if (oa) atomicOr(&vb[0], oa);
       if (of) atomicOr(&vb[1], of);
       if (oc) atomicOr(&vb[2], oc);
@@ -236,10 +238,13 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __re
 
 // One workgroup per bucket: LDS max over record indices, then each symbol's
 // values are fetched once: fin[sym] = (addr, file, ctx, 0).
+// part != nullptr (sharded merge): instead of fin, write this shard's partial
+// tables part[3][n_sym] = (tag << 32) | (value + 1), 0 = no record; the MAX
+// all-reduce over shards then keeps the last writer (highest shard).
 __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __restrict__ offs, int nblk,
                                                       const u32* __restrict__ nrec_total,
                                                       const u64* __restrict__ rec, i64 n_sym,
-                                                      int4* __restrict__ fin) {
+                                                      int4* __restrict__ fin, u64* __restrict__ part, u32 tag) {
   const FinPack FP = fin_pack_of(A0.meta->vbits, true);
   u64* fin8 = reinterpret_cast<u64*>(fin);
   __shared__ u32 tA[TB_WIDTH], tF[TB_WIDTH], tC[TB_WIDTH];
@@ -267,8 +272,16 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
     const u32 a = tA[i], f = tF[i], c = tC[i];
     const int va = a ? A.mvA[a - 1] : -1, vf = f ? A.mvF[f - 1] : -1;
     const int vc = c ? A.Mstr[(u64)(c - 1) - A.nMv] : -1;
-    if (FP.packed) fin8[s0 + i] = fin_encode(FP, va, vf, vc);
-    else fin[s0 + i] = make_int4(va, vf, vc, 0);
+    if (part) {
+      const u64 tg = (u64)tag << 32;
+      part[s0 + i] = a ? tg | (u32)(va + 1) : 0ull;
+      part[n_sym + s0 + i] = f ? tg | (u32)(vf + 1) : 0ull;
+      part[2 * n_sym + s0 + i] = c ? tg | (u32)(vc + 1) : 0ull;
+    } else if (FP.packed) {
+      fin8[s0 + i] = fin_encode(FP, va, vf, vc);
+    } else {
+      fin[s0 + i] = make_int4(va, vf, vc, 0);
+    }
   }
 }
 
@@ -290,11 +303,20 @@ __global__ void k_tab_atomic(TbArgs A0, u32* __restrict__ tabA, u32* __restrict_
 }
 
 __global__ void k_finalize(TbArgs A0, const u32* __restrict__ tabA, const u32* __restrict__ tabF,
-                           const u32* __restrict__ tabR, i64 n_sym, int4* __restrict__ fin) {
+                           const u32* __restrict__ tabR, i64 n_sym, int4* __restrict__ fin,
+                           u64* __restrict__ part, u32 tag) {
   const TbArgs A = tb_load(A0);
   for (i64 s = (i64)blockIdx.x * BLOCK + threadIdx.x; s < n_sym; s += (i64)gridDim.x * BLOCK) {
     const u32 a = tabA[s], f = tabF[s], c = tabR[s];
-    fin[s] = make_int4(a ? A.mvA[a - 1] : -1, f ? A.mvF[f - 1] : -1,
-                       c ? A.Mstr[(u64)(c - 1) - A.nMv] : -1, 0);
+    const int va = a ? A.mvA[a - 1] : -1, vf = f ? A.mvF[f - 1] : -1;
+    const int vc = c ? A.Mstr[(u64)(c - 1) - A.nMv] : -1;
+    if (part) {
+      const u64 tg = (u64)tag << 32;
+      part[s] = a ? tg | (u32)(va + 1) : 0ull;
+      part[n_sym + s] = f ? tg | (u32)(vf + 1) : 0ull;
+      part[2 * n_sym + s] = c ? tg | (u32)(vc + 1) : 0ull;
+    } else {
+      fin[s] = make_int4(va, vf, vc, 0);
+    }
   }
 }

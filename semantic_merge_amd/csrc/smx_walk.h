@@ -26,7 +26,52 @@ struct WalkArgs {
   u64 na_cap, nb_cap;   // host sizes: bounds for the device-side counts
   u64 nR, nRA, nRB;     // filled on the device by walk_load
   u64 fail;
+  // Sharded merge (smx_shard_step): the renames of each branch that follow this
+  // shard's in the global rename order (halo_n[b] of them; halo_more[b] when the
+  // halo is a strict prefix of the rest), and the global source index of local
+  // op j: j < na_cap ? src_a + j : src_b + (j - na_cap).  Single merge: no halo,
+  // src_a = 0, src_b = na_cap.
+  const u32* halo_sym[2];
+  const i32* halo_cls[2];
+  const i32* halo_src[2];
+  u64 halo_n[2];
+  int halo_more[2];
+  i64 src_a, src_b;
 };
+
+__device__ __forceinline__ i32 walk_gsrc(const WalkArgs& W, i32 j) {
+  return (u64)j < W.na_cap ? (i32)(W.src_a + j) : (i32)(W.src_b + ((i64)j - (i64)W.na_cap));
+}
+
+// The k-th rename (local numbering) of branch o: a local M position, or an entry
+// of the halo (the next shard's renames).  ok = false when branch o has no k-th
+// rename; a halo too short to tell flags meta->halo_overflow.
+struct WalkHead {
+  bool ok, local;
+  u32 sym;
+  i32 cls;
+  u32 u;  // local M position, or halo index
+};
+
+__device__ __forceinline__ WalkHead walk_head(const WalkArgs& W, int o, u64 k) {
+  WalkHead h{false, false, 0u, 0, 0u};
+  const u64 no = o ? W.nRB : W.nRA;
+  if (k < no) {
+    const u32 u = (o ? W.RB : W.RA)[k];
+    return WalkHead{true, true, W.Msym[u], W.Mcls[u], u};
+  }
+  // selects, not W.halo_*[o]: a dynamic index into the argument struct would put
+  // it in scratch memory
+  const u64 x = k - no;
+  const u64 hn = o ? W.halo_n[1] : W.halo_n[0];
+  if (x < hn) {
+    const u32* hs = o ? W.halo_sym[1] : W.halo_sym[0];
+    const i32* hc = o ? W.halo_cls[1] : W.halo_cls[0];
+    return WalkHead{true, false, hs[x], hc[x], (u32)x};
+  }
+  if (o ? W.halo_more[1] : W.halo_more[0]) const_cast<ComposeMeta*>(W.meta)->halo_overflow = 1;
+  return h;
+}
 
 // Sizes come from the device (no host sync before the walk); a failed
 // presorted plan or invalid input turns every walk kernel into a no-op.
@@ -57,12 +102,8 @@ __global__ void __launch_bounds__(BLOCK) k_flags(WalkArgs W0, u8* __restrict__ f
     if (m >= W.nR) break;
     const int s = W.Mside[m];
     const u64 k = m - W.Mown[m];
-    const u64 no = s ? W.nRA : W.nRB;
-    u8 f = 0;
-    if (k < no) {
-      const u32 u = (s ? W.RA : W.RB)[k];
-      f = (W.Msym[u] == W.Msym[m]) && (W.Mcls[u] != W.Mcls[m]);
-    }
+    const WalkHead h = walk_head(W, 1 - s, k);
+    const u8 f = h.ok && h.sym == W.Msym[m] && h.cls != W.Mcls[m];
     flags[m] = f;
     mine += f;
   }
@@ -73,7 +114,7 @@ __global__ void __launch_bounds__(BLOCK) k_flags(WalkArgs W0, u8* __restrict__ f
 
 // Exclusive scan of the per-block flag counts (one block; nb is small) and the
 // candidate total into meta->n_cand.
-__global__ void __launch_bounds__(BLOCK) k_flag_offsets(WalkArgs W0, u32* __restrict__ bcnt, ComposeMeta* meta) {
+__global__ void __launch_bounds__(BLOCK) k_flag_offsets(WalkArgs W0, u32* __restrict__ bcnt, u64* total) {
   const WalkArgs W = walk_load(W0);
   if (W.fail) return;
   const u32 nb = (u32)SMX_CEIL_DIV(W.nR, (u64)FLAG_TILE);
@@ -97,7 +138,7 @@ __global__ void __launch_bounds__(BLOCK) k_flag_offsets(WalkArgs W0, u32* __rest
     }
     carry += tot;
   }
-  if (threadIdx.x == 0) meta->n_cand = carry;
+  if (threadIdx.x == 0) *total = carry;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_compact(WalkArgs W0, const u8* __restrict__ flags,
@@ -126,46 +167,78 @@ __global__ void __launch_bounds__(BLOCK) k_compact(WalkArgs W0, const u8* __rest
   }
 }
 
-// Replays the reference loop restricted to renames from a d = 0 candidate start
-// p: state (ahead branch, d = how many of its next renames were consumed early).
-// Returns the end q (first position after which d is back to 0).
+// Replays the reference loop restricted to renames from position p with state
+// (ahead branch, d = how many of its next renames were consumed early); a
+// candidate start has d = 0.  Returns the end q (the first position after which
+// d is back to 0, or nR if the region is still open at the shard's end; the
+// final state is left in *ahead_io / *d_io).  WRITE: conflict pairs (global
+// source indices) and skip flags of local positions.
 template <bool WRITE>
-__device__ u32 replay_region(const WalkArgs& W, u32 p, u32* nconf, const i32* order_ren,
-                             i32* pairs, u64 pair_cap, u32 pair_off, u8* skip) {
-  int ahead = -1;
-  u32 d = 0;
+__device__ u32 replay_region(const WalkArgs& W, u32 p, int* ahead_io, u32* d_io, u32* nconf,
+                             const i32* order_ren, i32* pairs, u64 pair_cap, u64 pair_off, u8* skip) {
+  int ahead = *ahead_io;
+  u32 d = *d_io;
   u32 m = p;
   u32 nc = 0;
-  do {
+  while (m < W.nR) {
     const int s = W.Mside[m];
     if (d > 0 && s == ahead) {
       --d;  // consumed as the other head of an earlier conflict
+      if (WRITE) skip[m] = 1;
     } else {
       const int o = 1 - s;
       const u64 k = (u64)(m - W.Mown[m]) + (o == ahead ? d : 0u);
-      const u64 no = s ? W.nRA : W.nRB;
-      if (k < no) {
-        const u32 u = (s ? W.RA : W.RB)[k];
-        if (W.Msym[u] == W.Msym[m] && W.Mcls[u] != W.Mcls[m]) {
-          if (WRITE) {
-            const u64 slot = (u64)pair_off + nc;
-            if (slot < pair_cap) {
-              pairs[2 * slot] = order_ren[s ? u : m];
-              pairs[2 * slot + 1] = order_ren[s ? m : u];
-            }
-            skip[m] = 1;
-            skip[u] = 1;
+      const WalkHead h = walk_head(W, o, k);
+      if (h.ok && h.sym == W.Msym[m] && h.cls != W.Mcls[m]) {
+        if (WRITE) {
+          const u64 slot = pair_off + nc;
+          if (slot < pair_cap) {
+            const i32 mu = walk_gsrc(W, order_ren[m]);
+            const i32 hu = h.local ? walk_gsrc(W, order_ren[h.u]) : (o ? W.halo_src[1] : W.halo_src[0])[h.u];
+            pairs[2 * slot] = s ? hu : mu;
+            pairs[2 * slot + 1] = s ? mu : hu;
           }
-          ++nc;
-          ++d;
-          ahead = o;
+          skip[m] = 1;
+          if (h.local) skip[h.u] = 1;
         }
+        ++nc;
+        ++d;
+        ahead = o;
       }
     }
     ++m;
-  } while (d > 0 && m < W.nR);
+    if (d == 0) break;
+  }
+  *ahead_io = ahead;
+  *d_io = d;
   *nconf = nc;
   return m;
+}
+
+// Incoming open region (sharded merge): the previous shards' walk ended with
+// state (ahead, d > 0); continue it from position 0.  Its conflicts come first in
+// this shard's list; candidates before its end are covered.
+__global__ void k_replay_in(WalkArgs W0, int in_ahead, u32 in_d, ComposeMeta* meta, const i32* __restrict__ order,
+                            i32* __restrict__ pairs, u64 pair_cap, u8* __restrict__ skip,
+                            u32* __restrict__ skiplist) {
+  const WalkArgs W = walk_load(W0);
+  if (W.fail || in_d == 0 || threadIdx.x != 0 || blockIdx.x != 0) return;
+  const i32* order_ren = order + meta->base[SMX_KIND_RENAME];
+  int ahead = in_ahead;
+  u32 d = in_d, nc = 0;
+  const u32 q = replay_region<true>(W, 0, &ahead, &d, &nc, order_ren, pairs, pair_cap, 0, skip);
+  meta->q_in = q;
+  meta->nconf_in = nc;
+  u32 o = 0;  // its skips head the sorted skip list
+  for (u32 m = 0; m < q; ++m)
+    if (skip[m]) skiplist[o++] = m;
+  meta->nskip_in = o;
+  atomicAdd((unsigned long long*)&meta->n_skip, (unsigned long long)o);
+  if (d > 0) {  // still open at this shard's end: hand it on
+    meta->out_open = 1;
+    meta->out_ahead = (u64)ahead;
+    meta->out_d = d;
+  }
 }
 
 __global__ void k_replay_q(WalkArgs W0, const u32* __restrict__ cand, const ComposeMeta* meta,
@@ -174,8 +247,9 @@ __global__ void k_replay_q(WalkArgs W0, const u32* __restrict__ cand, const Comp
   if (W.fail) return;
   const u64 nc = meta->n_cand;
   for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
-    u32 k;
-    q[c] = replay_region<false>(W, cand[c], &k, nullptr, nullptr, 0, 0, nullptr);
+    u32 k, d = 0;
+    int ahead = -1;
+    q[c] = replay_region<false>(W, cand[c], &ahead, &d, &k, nullptr, nullptr, 0, 0, nullptr);
     nconf[c] = k;
   }
 }
@@ -188,7 +262,7 @@ __global__ void k_cluster(const u32* __restrict__ cand, const u32* __restrict__ 
   const u64 nc = meta->n_cand;
   for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
     if (pm[c] > cand[c]) continue;  // not a cluster start
-    u32 last_q = 0;
+    u32 last_q = (u32)meta->q_in;   // an incoming region (sharded merge) covers [0, q_in)
     for (u64 j = c; j < nc && (j == c || pm[j] > cand[j]); ++j) {
       if (cand[j] >= last_q) {
         nreal[j] = nconf[j];
@@ -200,25 +274,40 @@ __global__ void k_cluster(const u32* __restrict__ cand, const u32* __restrict__ 
   }
 }
 
-// Writes the conflict pairs of every real region and its skipped positions:
-// a region's skips lie in [p, q) and regions are disjoint and ordered, so
-// listing [p, q) in order yields the globally sorted skip list (2 per conflict).
+// Writes the conflict pairs, skip flags and skip-list entries of every real
+// region.  Regions are disjoint and ordered and a closed region's skips (2 per
+// conflict) lie in [p, q), so listing [p, q) in order yields the sorted skip list
+// after the incoming region's entries.  The last real region may still be open
+// at the shard's end (sharded merge): its heads beyond the end belong to the next
+// shard, its state is handed on, and its entries (fewer) end the list.
 __global__ void k_replay_write(WalkArgs W0, const u32* __restrict__ cand, const u32* __restrict__ nreal,
-                               const u32* __restrict__ coff, const ComposeMeta* meta,
+                               const u32* __restrict__ coff, ComposeMeta* meta,
                                const i32* __restrict__ order, i32* __restrict__ pairs,
                                u64 pair_cap, u8* __restrict__ skip, u32* __restrict__ skiplist) {
   const WalkArgs W = walk_load(W0);
   if (W.fail) return;
   const i32* order_ren = order + meta->base[SMX_KIND_RENAME];
   const u64 nc = meta->n_cand;
+  const u64 off0 = meta->nconf_in, soff0 = meta->nskip_in;
   for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
     if (nreal[c] == 0) continue;
-    u32 k;
+    u32 k, d = 0;
+    int ahead = -1;
     const u32 p = cand[c];
-    const u32 q = replay_region<true>(W, p, &k, order_ren, pairs, pair_cap, coff[c], skip);
-    u32 o = 2 * coff[c];
+    const u32 q = replay_region<true>(W, p, &ahead, &d, &k, order_ren, pairs, pair_cap, off0 + coff[c], skip);
+    if (d > 0) {
+      meta->out_open = 1;
+      meta->out_ahead = (u64)ahead;
+      meta->out_d = d;
+    }
+    u64 o = soff0 + 2 * (u64)coff[c];
+    u32 cnt = 0;
     for (u32 m = p; m < q; ++m)
-      if (skip[m]) skiplist[o++] = m;
+      if (skip[m]) {
+        skiplist[o++] = m;
+        ++cnt;
+      }
+    atomicAdd((unsigned long long*)&meta->n_skip, (unsigned long long)cnt);
   }
 }
 

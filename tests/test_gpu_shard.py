@@ -1,0 +1,150 @@
+"""GPU parity of the sharded single merge (semantic_merge_amd/shard.py): 2-3 ranks on one
+GPU over gloo (collectives through host copies; RCCL runs the same code on a node).
+Each rank starts from an index slice of the global logs; the assembled per-shard outputs
+must equal the CPU oracle's composition of the whole merge, bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _make(case):
+    from semantic_merge_amd import synth
+    kind, n, n_sym, seed = case
+    if kind == "chain":
+        return _chain_soa(n, seed)
+    if kind == "lift":
+        spec = synth.LiftSpec(n, n_sym, seed, ops_per_ms=64)
+    elif kind == "adv":  # rename-heavy, 30% of symbols renamed on both sides: many conflicts
+        spec = synth.LiftSpec(n, n_sym, seed, ops_per_ms=256, mix=synth.ADVERSARIAL_MIX,
+                              rename_overlap=0.30, divergent=0.2)
+    else:
+        raise ValueError(kind)
+    soa = synth.lift_soa(synth.lift_logs(spec))
+    if kind == "lift" and seed % 2 == 1:
+        # moves with a None newAddress / newFile: the prefix fix-up crosses shards
+        rng = np.random.default_rng(seed)
+        mv = np.flatnonzero(soa.kind == 0)
+        soa.v0[mv[rng.random(len(mv)) < 0.3]] = -1
+        soa.v1[mv[rng.random(len(mv)) < 0.2]] = -1
+    return soa
+
+
+def _chain_soa(n_ren, seed):
+    """One long DivergentRename region: branch A renames symbol 0 n_ren times before
+    any of branch B's n_ren renames of it (other names), plus edits.  Every A rename
+    conflicts with the B rename d ahead, so d climbs to n_ren and the region spans
+    both shards: it is open at shard 0's end and handed to shard 1."""
+    from semantic_merge_amd.marshal import SoA
+    rng = np.random.default_rng(seed)
+    n_edit = n_ren // 2
+    na = nb = n_ren + n_edit
+    kind = np.full(na + nb, 10, np.uint8)            # editStmtBlock precedence rank
+    kind[:n_ren] = 1
+    kind[na:na + n_ren] = 1
+    ts = np.concatenate([np.arange(na, dtype=np.uint64) * 2,
+                         np.uint64(10 * na) + np.arange(nb, dtype=np.uint64) * 2])
+    hi = rng.integers(0, 2**63, size=na + nb, dtype=np.int64).astype(np.uint64)
+    lo = rng.integers(0, 2**63, size=na + nb, dtype=np.int64).astype(np.uint64)
+    sym = np.zeros(na + nb, np.uint32)
+    sym[n_ren:na] = rng.integers(1, 5, size=n_edit)
+    sym[na + n_ren:] = rng.integers(1, 5, size=n_edit)
+    v0 = np.full(na + nb, -1, np.int32)
+    v1 = np.full(na + nb, -1, np.int32)
+    v0[:n_ren], v1[:n_ren] = 0, 0
+    v0[na:na + n_ren], v1[na:na + n_ren] = 1, 1
+    return SoA(na, nb, kind, ts, hi, lo, sym, v0, v1, 5, ["a", "b"])
+
+
+def _worker(rank, world, port, case, halo, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from semantic_merge_amd import shard
+        soa = _make(case)
+        a, b, na, nb = shard.slices_from_soa(soa, rank, world, "cuda:0")
+        sc = shard.ShardedCompose(a, b, na, nb, soa.n_sym, shard.Comm(), "cuda:0", halo_cap=halo)
+        sc.run()
+        res = sc.results()
+        q.put((rank, res, sc.in_state, int(sc.sum_walk[:, shard.S_OPEN].sum())))
+    except Exception as e:  # report to the parent instead of hanging the collective
+        q.put((rank, repr(e), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(case, world, halo=4096):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, halo, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, res, st, nopen = q.get(timeout=240)
+        got[r] = (res, st, nopen)
+    for p in procs:
+        p.join(60)
+    for r in range(world):
+        assert not isinstance(got[r][0], str), f"rank {r}: {got[r][0]}"
+    return [got[r][0] for r in range(world)], got
+
+
+def _check(case, world, halo=4096):
+    from oracle import oracle
+    from semantic_merge_amd import shard
+    parts, got = _run(case, world, halo)
+    glob = shard.assemble(parts)
+    ref = oracle.compose(_make(case))
+    names = ("order", "addr", "file", "ctx", "conflicts")
+    for name, g, r in zip(names, glob, ref):
+        assert g.shape == r.shape, f"{case} x{world}: {name} shape {g.shape} vs {r.shape}"
+        assert np.array_equal(g, r), f"{case} x{world}: {name} differs"
+    return got, ref
+
+
+def test_shard_lift_two_ranks():
+    _check(("lift", 200_000, 2_000, 4), 2)
+
+
+def test_shard_lift_none_moves_three_ranks():
+    _check(("lift", 150_000, 1_000, 5), 3)
+
+
+def test_shard_adversarial_conflicts_cross_boundaries():
+    # 8 symbols: natural heads collide constantly, regions are long and cross shards
+    got, ref = _check(("adv", 120_000, 8, 8), 3)
+    assert len(ref[4]) > 1000  # conflict-dense
+    handed = [got[r][1] for r in range(3) if got[r][1] != (0, 0)]
+    print("incoming open regions:", handed)
+
+
+def test_shard_open_region_handed_to_next_shard():
+    got, ref = _check(("chain", 3000, 0, 3), 2)
+    assert len(ref[4]) == 3000
+    assert got[1][1] != (0, 0), "shard 1 must receive the open region"
+
+
+def test_shard_halo_too_short_fails_loudly():
+    with pytest.raises(AssertionError, match="halo"):
+        _check(("chain", 3000, 0, 3), 2, halo=16)
+
+
+def test_shard_tiny_with_empty_shards():
+    _check(("lift", 40, 5, 2), 3)

@@ -1,8 +1,5 @@
 set -o pipefail
-O=gpurun_out/r1s10; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests64.log 2>&1 || { tail -30 $O/tests64.log; exit 1; }
-tail -2 $O/tests64.log
-for v in head cur head cur; do
-  echo "== $v"; SMX_LIB=$PWD/tools/_build/var_$v/libsmx.so timeout -k 10 200 python tools/window_phases.py > $O/phases_$v.txt 2>&1 || exit 1
-  cat $O/phases_$v.txt | grep -v amdgpu.ids | grep -v "woff\|check\|span"
-done
+O=gpurun_out/r1s16; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_shard.py -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -8 $O/tests.log
+timeout -k 10 200 python tools/stage_ab.py 2>&1 | grep -v amdgpu.ids || exit 1

@@ -1,0 +1,40 @@
+"""A/B timing of the compose stages for one library build (SMX_LIB=...):
+median over rounds of per-stage ms on the c3 workload (or argv[1] ops)."""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    import torch
+    from semantic_merge_amd import _lib, synth
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
+    cfg = sys.argv[2] if len(sys.argv) > 2 else "c3"
+    spec = synth.LiftSpec(**{**synth.CONFIGS[cfg].__dict__, "n_total": n})
+    soa = synth.lift_soa(synth.lift_logs(spec))
+    dc = _lib.DeviceCompose(soa)
+    lib = _lib.lib()
+    for _ in range(2):
+        dc.run()
+    torch.cuda.synchronize()
+    res = {}
+    for _ in range(5):
+        lib.smx_reset_stage_times()
+        lib.smx_set_profiling(1)
+        for _ in range(3):
+            dc.run()
+        torch.cuda.synchronize()
+        lib.smx_set_profiling(0)
+        for k, (ms, c) in _lib.stage_times().items():
+            if c:
+                res.setdefault(k, []).append(ms / c)
+    tot = sum(np.median(v) for v in res.values())
+    print("  ".join(f"{k} {np.median(v):.3f}" for k, v in res.items()) + f"  | total {tot:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
