@@ -2,12 +2,16 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--n-ops N]
 
-One step = one smx_compose call (semmerge/compose.py:11-114 restated on the GPU)
-over one merge of SURVEY §8(d) config 3: 100M lift-shaped ops (50M per branch),
-1M symbols, seed 11 (+rank).  Inputs are resident in HBM before timing.  With
-N > 1 (torchrun, one process per GPU) every rank composes its own independent
-merge (weak scaling; the merge itself is not sharded yet) and
-the time is the max over ranks.  Rank 0 prints one JSON line.
+One step = one composition (semmerge/compose.py:11-114 restated on the GPU) of
+SURVEY §8(d) config 3: 100M lift-shaped ops (50M per branch) per GPU, 1M symbols,
+seed 11.  Inputs are resident in HBM before timing.  N = 1: one smx_compose call.
+N > 1 (torchrun, one process per GPU): ONE merge of N x 100M ops sharded by
+timestamp key range (semantic_merge_amd/shard.py): each rank starts from its
+index slices of both branch logs, and a step is the whole sharded composition --
+the RCCL all-to-all that moves ops to their key-range shard, the per-shard
+kernels, the walk hand-off and the MAX all-reduce of the chain tables (weak
+scaling: 100M ops per GPU).  --independent runs N unrelated merges instead.  The
+time is the max over ranks; rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -43,7 +47,9 @@ def main() -> None:
     ap.add_argument("--cpu-sample", type=int, default=40_000_000,
                     help="ops in the CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", action="store_true", help="check GPU == oracle (slow)")
+    ap.add_argument("--verify", action="store_true", help="check GPU == oracle (slow, N = 1)")
+    ap.add_argument("--independent", action="store_true",
+                    help="N > 1: independent merges per rank instead of one sharded merge")
     args = ap.parse_args()
 
     import torch
@@ -53,10 +59,18 @@ def main() -> None:
     ri = rank_info()
     world, rank, local = ri.world, ri.rank, ri.local
     dist = None
+    # SMX_BENCH_BACKEND=gloo: rehearse N ranks on fewer GPUs (collectives through host
+    # copies); the driver's multi-GPU runs use RCCL, one GPU per rank.
+    backend = os.environ.get("SMX_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     spec = synth.CONFIGS[args.config]
@@ -64,17 +78,30 @@ def main() -> None:
         spec = synth.LiftSpec(**{**spec.__dict__, "n_total": args.n_ops})
     if args.n_sym:
         spec = synth.LiftSpec(**{**spec.__dict__, "n_sym": args.n_sym})
-    spec = synth.LiftSpec(**{**spec.__dict__, "seed": rank_seed(spec.seed, rank)})
+    sharded = world > 1 and not args.independent
     t0 = time.time()
-    logs = synth.lift_logs(spec)
-    soa = synth.lift_soa(logs)
-    del logs
-    log(f"[rank {rank}] generated {soa.n:,} ops in {time.time() - t0:.1f}s")
-    dc = _lib.DeviceCompose(soa, f"cuda:{local}")
-    log(f"[rank {rank}] resident on {dev}; workspace {dc.ws_bytes / 2**30:.2f} GiB")
+    sc = dc = None
+    if sharded:
+        from semantic_merge_amd import shard
+        soa, na_g, nb_g = synth.lift_slice_soa(spec, rank, world)
+        sl_a, sl_b, _, _ = shard.slices_from_soa(soa, 0, 1, dev)
+        log(f"[rank {rank}] generated slice of {soa.n:,} ops in {time.time() - t0:.1f}s")
+        sc = shard.ShardedCompose(sl_a, sl_b, na_g, nb_g, soa.n_sym, shard.Comm(), dev)
+        del sl_a, sl_b
+        run = sc.run
+        log(f"[rank {rank}] resident on {dev}; shard buffers with headroom {sc.hd:,}")
+    else:
+        spec = synth.LiftSpec(**{**spec.__dict__, "seed": rank_seed(spec.seed, rank)})
+        logs = synth.lift_logs(spec)
+        soa = synth.lift_soa(logs)
+        del logs
+        log(f"[rank {rank}] generated {soa.n:,} ops in {time.time() - t0:.1f}s")
+        dc = _lib.DeviceCompose(soa, f"cuda:{local}")
+        run = dc.run
+        log(f"[rank {rank}] resident on {dev}; workspace {dc.ws_bytes / 2**30:.2f} GiB")
 
     for _ in range(args.warmup):
-        dc.run()
+        run()
     torch.cuda.synchronize(dev)
 
     lib = _lib.lib()
@@ -85,17 +112,22 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        dc.run()
+        run()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     lib.smx_set_profiling(0)
     stages = _lib.stage_times()
-    k, nconf = (int(x) for x in dc.counts.cpu().tolist())
+    if sharded:
+        fin = sc.sum_final
+        nconf = int(fin[:, shard.S_NCONF].sum())
+        k = world * soa.n - int(fin[:, shard.S_NSKIP].sum())
+    else:
+        k, nconf = (int(x) for x in dc.counts.cpu().tolist())
     elapsed = max_over_ranks(elapsed, dev)
 
-    if args.verify:
+    if args.verify and not sharded:
         from oracle import oracle
         ref = oracle.compose(soa)
         got = dc.results()
@@ -153,13 +185,19 @@ def main() -> None:
         "dtype": "u64",
         "data": "synthetic (lift-shaped op logs generated from a seed, SURVEY §8(d))",
         "config": {
-            "workload": f"{args.config}: {n:,} ops ({soa.n_a:,} per branch), {soa.n_sym:,} symbols,"
-                        f" {spec.ops_per_ms} ops/ms, seed {spec.seed - rank}+rank",
+            "workload": (f"{args.config}: one merge of {world * n:,} ops ({n:,} per GPU, "
+                         f"{soa.n_a:,} per branch per GPU), {soa.n_sym:,} symbols, "
+                         f"{spec.ops_per_ms} ops/ms, seed {spec.seed}"
+                         + (", sharded by timestamp key range" if sharded else "")
+                         + (f", {world} independent merges" if world > 1 and not sharded else "")),
             "n_ops_per_gpu": n,
+            "n_ops_total": world * n,
             "n_sym": soa.n_sym,
             "composed_ops": k,
             "conflicts": nconf,
-            "parallelism": f"independent merges x{world}",
+            "parallelism": (f"key-range shards x{world} (RCCL all-to-all + all-gathers + "
+                            f"MAX all-reduce)" if sharded else
+                            (f"independent merges x{world}" if world > 1 else "single GPU")),
         },
         "roofline": {
             "bound": "hbm",

@@ -65,6 +65,11 @@ typedef struct smx_ops {
   const uint32_t* sym;
   const int32_t* v0;
   const int32_t* v1;
+  /* B op j (j >= n_a) is stored at index j + b_gap of every field array (0: right
+   * after A).  A sharded merge keeps headroom between its A and B ranges so its
+   * exchange moves only the ops that change shard; smx_compose's generic plan
+   * (logs not timestamp-ordered) needs b_gap = 0. */
+  int64_t b_gap;
 } smx_ops;
 
 /*

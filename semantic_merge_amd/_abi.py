@@ -22,6 +22,7 @@ class SmxOps(C.Structure):
         ("sym", C.c_void_p),
         ("v0", C.c_void_p),
         ("v1", C.c_void_p),
+        ("b_gap", C.c_int64),
     ]
 
 

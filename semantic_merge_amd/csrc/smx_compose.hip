@@ -69,18 +69,22 @@ struct StageTimer {
   bool on;
   hipEvent_t open[ST_N];
   std::vector<PendingEv> done;
+  bool is_open[ST_N] = {};
   StageTimer(hipStream_t s, bool enabled) : st(s), on(enabled) {}
   void begin(int i) {
     if (!on) return;
+    if (is_open[i]) (void)hipEventDestroy(open[i]);  // a stage restarted (plan retries)
     (void)hipEventCreate(&open[i]);
     (void)hipEventRecord(open[i], st);
+    is_open[i] = true;
   }
   void end(int i) {
-    if (!on) return;
+    if (!on || !is_open[i]) return;
     hipEvent_t b;
     (void)hipEventCreate(&b);
     (void)hipEventRecord(b, st);
     done.push_back({i, open[i], b});
+    is_open[i] = false;
   }
   void flush() {
     if (!on) return;
@@ -93,6 +97,8 @@ struct StageTimer {
       (void)hipEventDestroy(p.a);
       (void)hipEventDestroy(p.b);
     }
+    for (int i = 0; i < ST_N; ++i)
+      if (is_open[i]) (void)hipEventDestroy(open[i]);
   }
 };
 
@@ -149,13 +155,13 @@ __global__ void k_meta_init(ComposeMeta* meta) {
 // B[CH*j + CH-1]; 1/256 of the keys, cache-resident): the first level of the
 // search runs on them, the second inside one chunk.  The snap gallops back over
 // the (short) run of equal timestamps.
-__global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ sA, const u64* __restrict__ sB,
-                        i64 na, i64 nb, i64 W, i64 tgt, i64* __restrict__ bnd) {
+__global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB, const u64* __restrict__ sA,
+                        const u64* __restrict__ sB, i64 na, i64 nb, i64 W, i64 tgt, i64* __restrict__ bnd) {
   const i64 k = (i64)blockIdx.x * BLOCK + threadIdx.x;
   if (k > W) return;
   const i64 n = na + nb;
   const u64* A = ts;
-  const u64* B = ts + na;
+  const u64* B = tsB;
   const i64 d = k * tgt;
   if (k == 0 || d >= n || k == W) {
     bnd[2 * k] = k == 0 ? 0 : na;
@@ -246,7 +252,7 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 // aligned) and adds each byte to its (chunk, kind) counter with an LDS atomic
 // into one of KH_COPIES copies.
 __global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, const u64* __restrict__ ts,
-                                                 i64 na, i64 nb, i64 CM, u32* __restrict__ cnt,
+                                                 i64 na, i64 nb, i64 bgap, i64 CM, u32* __restrict__ cnt,
                                                  u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta) {
   __shared__ u32 c[KH_COPIES][CH_PER_BLOCK][SMX_N_KINDS];
   const i64 CA = SMX_CEIL_DIV(na, (i64)CH), CB = SMX_CEIL_DIV(nb, (i64)CH);
@@ -258,11 +264,11 @@ __global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, co
   const i64 len = side ? nb : na;
   const i64 r0 = cc * CH + q * 16;  // branch position of this lane's first byte
   const int nv = g < CA + CB ? (int)(len - r0 < 0 ? 0 : (len - r0 < 16 ? len - r0 : 16)) : 0;
-  const u8* src = kind + (side ? na : 0) + r0;
+  const u8* src = kind + (side ? na + bgap : 0) + r0;
   // timestamp samples for k_fpart: first op of each A chunk, last op of each full B chunk
   if (g < CA + CB) {
     if (!side && q == 0) sA[cc] = ts[cc * CH];
-    if (side && q == 15 && nv == 16) sB[cc] = ts[na + cc * CH + CH - 1];
+    if (side && q == 15 && nv == 16) sB[cc] = ts[na + bgap + cc * CH + CH - 1];
   }
   u32 w[4] = {0u, 0u, 0u, 0u};
   if (nv == 16 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
@@ -881,6 +887,7 @@ static WinArgs win_args(const Ctx& C) {
   P.v1 = C.ops->v1;
   P.na = C.na;
   P.nb = C.nb;
+  P.bgap = C.ops->b_gap;
   P.n_sym = C.n_sym;
   P.bnd = C.ws<i64>(B_BND);
   P.woff = C.ws<u32>(B_WOFF);
@@ -1086,8 +1093,9 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   u64* sA = C.ws<u64>(B_SMP);
   u64* sB = sA + SMX_CEIL_DIV(C.na, (i64)CH) + 1;
   hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK)), dim3(BLOCK), 0, st, C.ops->kind,
-                     C.ops->ts, C.na, C.nb, CM, ccnt, sA, sB, meta);
-  hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts, sA, sB, C.na,
+                     C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta);
+  hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
+                     C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na,
                      C.nb, W, tgt, bnd);
   {
     const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);
@@ -1210,6 +1218,7 @@ static int check_args(const smx_ops* ops, const smx_compose_out* out, void* ws, 
       !out->order || !out->addr || !out->file || !out->ctx || (!out->conflicts && out->conflict_cap > 0))
     return set_err(SMX_E_ARG, "null input/output pointer");
   if (n_sym < 1) return set_err(SMX_E_ARG, "n_sym must be >= 1");
+  if (ops->b_gap < 0) return set_err(SMX_E_ARG, "b_gap must be >= 0");
   *L = layout(na, nb, n_sym);
   if (!ws || ws_bytes < L->total)
     return set_err(SMX_E_WORKSPACE, "workspace too small: need " + std::to_string(L->total));
@@ -1235,6 +1244,8 @@ static int run_order(const Ctx& C, bool allow_generic, ComposeMeta* hm) {
     if ((rc = read_meta(C, hm))) return rc;
   }
   if (hm->f_fail && !hm->bad_sym && allow_generic) {
+    if (C.ops->b_gap != 0)
+      return set_err(SMX_E_ARG, "branch logs not timestamp-ordered: the generic plan needs b_gap = 0");
     if ((rc = run_generic(C))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
   }
@@ -1381,13 +1392,11 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       if (sh->halo_cap < 0 || (sh->halo_cap > 0 && (!sh->export_sym || !sh->export_cls || !sh->export_src)))
         return set_err(SMX_E_ARG, "bad export buffers");
       ComposeMeta hm;
-      tm.begin(ST_PLAN);
-      if ((rc = run_order(C, false, &hm))) return rc;
+      if ((rc = run_order(C, false, &hm))) return rc;  // times its own plan / window stages
       hipLaunchKernelGGL(k_shard_export, dim3(grid_for(2 * sh->halo_cap + 1)), dim3(BLOCK), 0, st,
                          C.ws<ComposeMeta>(B_META), P, sh->summary, sh->export_sym, sh->export_cls,
                          sh->export_src, sh->halo_cap, sh->src_a, sh->src_b);
       HIP_TRY(hipGetLastError());
-      tm.end(ST_PLAN);
       if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
       if (hm.f_fail)
         return set_err(SMX_E_ARG, "sharded merge needs timestamp-ordered branch logs in every shard");

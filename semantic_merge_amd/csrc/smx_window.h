@@ -72,6 +72,7 @@ struct WinArgs {
   const u32* perm;  // generic only: op index of sorted position (A at [0,na), B at [na,n))
   i64 na;
   i64 nb;
+  i64 bgap;         // B op j is stored at j + bgap of the field arrays (presorted plan)
   i64 W;
   i64 n_sym;
   int ablate;       // diagnostics only (SMX_ABLATE): skip phases, results invalid
@@ -167,6 +168,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   }
   if (sz == 0) return;
   const i64 bpos = P.na + b0 - na;  // op index of B element e is bpos + e
+  const i64 bld = bpos + P.bgap;    // ... stored at field index bld + e
   WSTAMP(0);
 
   // 1. load the sort keys (kind, timestamp, top of the id) to LDS.  The payload
@@ -182,7 +184,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   u64 ts_r[WF_ITEMS];
   auto op_index = [&](int e) -> i64 {
     const int ec = e < sz ? e : 0;
-    return ec < na ? a0 + ec : bpos + ec;
+    return ec < na ? a0 + ec : bld + ec;
   };
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
@@ -227,12 +229,12 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     const int pa = (int)(a0 % CH), pb = (int)(b0 % CH);
     const int side = t >= CH;
     const int q = t - side * CH;
-    if (q < (side ? pb : pa)) kpart = P.kind[side ? (P.na + b0 - pb + q) : (a0 - pa + q)];
+    if (q < (side ? pb : pa)) kpart = P.kind[side ? (P.na + P.bgap + b0 - pb + q) : (a0 - pa + q)];
   }
   // timestamps just before the window on each branch (issued with the loads above)
   u64 prev_a = 0, prev_b = 0;
   if (t == 0 && a0 > 0) prev_a = P.kts[a0 - 1];
-  if (t == 0 && b0 > 0) prev_b = P.kts[P.na + b0 - 1];
+  if (t == 0 && b0 > 0) prev_b = P.kts[P.na + P.bgap + b0 - 1];
   if (bad) P.meta->bad_sym = 1;
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
@@ -442,12 +444,12 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       // insertion sort of sord[r0..r1] by (oid_hi, oid_lo); equal ids keep slot order
       for (int x = r0 + 1; x <= r1; ++x) {
         const int ex = sord[x];
-        const i64 jx = ex < na ? a0 + ex : bpos + ex;
+        const i64 jx = ex < na ? a0 + ex : bld + ex;
         const u64 hx = P.khi[jx], lx = P.klo[jx];
         int y = x - 1;
         while (y >= r0) {
           const int ey = sord[y];
-          const i64 jy = ey < na ? a0 + ey : bpos + ey;
+          const i64 jy = ey < na ? a0 + ey : bld + ey;
           const u64 hy = P.khi[jy], ly = P.klo[jy];
           if (hy < hx || (hy == hx && ly <= lx)) break;
           sord[y + 1] = (u16)ey;

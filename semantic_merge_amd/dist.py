@@ -1,8 +1,7 @@
-"""Multi-GPU plumbing for independent merges (one process per GPU).
-
-Each rank composes its own merge (weak scaling): the only collectives are the
-barrier around the timed region and a MAX all-reduce of the elapsed time.  The
-backend is RCCL ("nccl") on GPUs; the same helpers run on "gloo" in the CPU tests.
+"""Multi-GPU plumbing shared by bench.py and the tests (one process per GPU):
+rank info from the torchrun environment, the MAX all-reduce of the elapsed time and the
+whole-job throughput.  The sharded merge itself lives in shard.py.  The backend is RCCL
+("nccl") on GPUs; the same helpers run on "gloo" in the CPU tests.
 """
 from __future__ import annotations
 
@@ -33,6 +32,8 @@ def max_over_ranks(value: float, device=None) -> float:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return value
+    if dist.get_backend() != "nccl":
+        device = None  # gloo: host tensor
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -121,40 +121,74 @@ def _u64_key(t):
 
 class ShardedCompose:
     """One rank's part of a sharded merge.  `a`, `b`: this rank's index slices of the
-    global branch logs (timestamp-ordered), na_glob / nb_glob the global branch sizes."""
+    global branch logs (timestamp-ordered), na_glob / nb_glob the global branch sizes.
+
+    The slices are copied once into field buffers with `headroom` free entries on both
+    sides of each branch range; the exchange writes the ops arriving from the
+    neighbouring shards into the headroom, so the ops that stay (nearly all of them on
+    lift-shaped logs) never move, and the shard is handed to the kernels in place:
+    A' at [a_lo, a_hi) and B' at [b_lo, b_hi) of every field buffer, B' after a gap
+    (smx_ops.b_gap)."""
 
     def __init__(self, a: BranchSlice, b: BranchSlice, na_glob: int, nb_glob: int, n_sym: int,
-                 comm: Comm, device, halo_cap: int = 4096) -> None:
+                 comm: Comm, device, halo_cap: int = 4096, headroom: Optional[int] = None,
+                 restore: bool = True) -> None:
         import torch
         self.torch = torch
-        self.a, self.b = a, b
         self.na_glob, self.nb_glob = na_glob, nb_glob
         self.n_sym = n_sym
         self.comm = comm
         self.rank, self.world = comm.rank, comm.world
         self.dev = torch.device(device)
         self.H = halo_cap
+        self.restore = restore
+        self.na_s, self.nb_s = a.n, b.n
+        self.a_start, self.b_start = a.start, b.start
+        hd = headroom if headroom is not None else max(1 << 16, (a.n + b.n) // 32)
+        self._alloc(hd, a, b)
         self._ws = None
         self._ws_bytes = 0
+        self._outn = -1
         self.summary = torch.zeros(_abi.SHARD_SUMMARY, dtype=torch.int64, device=self.dev)
         self.xsym = torch.zeros(2 * self.H, dtype=torch.int32, device=self.dev)
         self.xcls = torch.zeros(2 * self.H, dtype=torch.int32, device=self.dev)
         self.xsrc = torch.zeros(2 * self.H, dtype=torch.int32, device=self.dev)
         self.part = torch.zeros(3 * max(n_sym, 1), dtype=torch.int64, device=self.dev)
         self.glob = torch.zeros(3, dtype=torch.int64, device=self.dev)
-        self.stream = None
+
+    def _alloc(self, hd: int, a, b) -> None:
+        """Field buffers [hd | A slice | 2 hd | B slice | hd]; a, b: BranchSlices or the
+        previous buffers (grow)."""
+        torch = self.torch
+        self.hd = hd
+        self.capA = self.na_s + 2 * hd
+        cap = self.capA + self.nb_s + 2 * hd
+        old = getattr(self, "buf", None)
+        self.buf = {}
+        for f in FIELDS:
+            src_a = getattr(a, f) if old is None else old[f][self._oa: self._oa + self.na_s]
+            src_b = getattr(b, f) if old is None else old[f][self._ob: self._ob + self.nb_s]
+            t = torch.zeros(cap, dtype=src_a.dtype, device=self.dev)
+            t[hd: hd + self.na_s] = src_a
+            t[self.capA + hd: self.capA + hd + self.nb_s] = src_b
+            self.buf[f] = t
+        self._oa, self._ob = hd, self.capA + hd   # original slices in the buffers
 
     # -- 1. exchange ------------------------------------------------------------------
+    def _orig(self, br: int, f: str):
+        return self.buf[f][self._oa: self._oa + self.na_s] if br == 0 else \
+            self.buf[f][self._ob: self._ob + self.nb_s]
+
     def _splitters(self) -> np.ndarray:
         """tau[1..world-1]: shard r owns timestamps in [tau[r], tau[r+1])."""
         torch = self.torch
-        a, b = self.a, self.b
         info = torch.zeros(6, dtype=torch.int64, device=self.dev)
-        info[0], info[1] = a.n, b.n
-        if a.n:
-            info[2], info[3] = _u64_key(a.ts[0]), _u64_key(a.ts[-1])
-        if b.n:
-            info[4], info[5] = _u64_key(b.ts[0]), _u64_key(b.ts[-1])
+        info[0], info[1] = self.na_s, self.nb_s
+        ta, tb = self._orig(0, "ts"), self._orig(1, "ts")
+        if self.na_s:
+            info[2], info[3] = _u64_key(ta[0]), _u64_key(ta[-1])
+        if self.nb_s:
+            info[4], info[5] = _u64_key(tb[0]), _u64_key(tb[-1])
         g = self.comm.all_gather(info).cpu().numpy()
         for side, (ni, fi, li) in enumerate(((0, 2, 3), (1, 4, 5))):
             nz = g[g[:, ni] > 0]
@@ -169,70 +203,103 @@ class ShardedCompose:
         return tau
 
     def exchange(self) -> None:
+        """The all-to-all: every op to the shard owning its timestamp (collective)."""
         torch = self.torch
+        r, W = self.rank, self.world
         tau = torch.from_numpy(self._splitters()[1:]).to(self.dev)
         counts = []
-        for sl in (self.a, self.b):
-            if sl.n:
-                cut = torch.searchsorted(_u64_key(sl.ts).contiguous(), tau, right=False)
+        for br, n in ((0, self.na_s), (1, self.nb_s)):
+            if n:
+                cut = torch.searchsorted(_u64_key(self._orig(br, "ts")).contiguous(), tau, right=False)
                 edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.dev), cut,
-                                   torch.full((1,), sl.n, dtype=torch.int64, device=self.dev)])
+                                   torch.full((1,), n, dtype=torch.int64, device=self.dev)])
                 counts.append(edges[1:] - edges[:-1])
             else:
-                counts.append(torch.zeros(self.world, dtype=torch.int64, device=self.dev))
-        mine = torch.stack(counts)                       # [2 branches, world dests]
-        allc = self.comm.all_gather(mine).cpu().numpy()  # [src, branch, dest]
-        r, W = self.rank, self.world
-        send = allc[r]                                    # [branch, dest]
-        recv = allc[:, :, r]                              # [src, branch]
-        # global index of this shard's first op of each branch: all ops sent to lower shards
+                counts.append(torch.zeros(W, dtype=torch.int64, device=self.dev))
+        allc = self.comm.all_gather(torch.stack(counts)).cpu().numpy()  # [src, branch, dest]
+        send, recv = allc[r], allc[:, :, r]                              # [br, dest], [src, br]
+        lo_s, hi_s = send[:, :r].sum(axis=1), send[:, r + 1:].sum(axis=1)
+        lo_r, hi_r = recv[:r].sum(axis=0), recv[r + 1:].sum(axis=0)
+        need = int(max(0, (lo_r - lo_s).max(), (hi_r - hi_s).max()))
+        if need > self.hd:  # skewed slices: grow the headroom (copies the slices once)
+            self._alloc(need + (self.na_s + self.nb_s) // 32, None, None)
         first = [int(allc[:, br, :r].sum()) for br in range(2)]
         self.src_a = first[0]
         self.src_b = self.na_glob + first[1]
-        in_splits = (send[0] + send[1]).tolist()
-        out_splits = (recv[:, 0] + recv[:, 1]).tolist()
-        # per destination: [A part, B part]; per source: the same
-        a_sel, b_sel = [], []
-        a_off = np.concatenate([[0], np.cumsum(send[0])])
-        b_off = np.concatenate([[0], np.cumsum(send[1])])
-        self.n_a = int(recv[:, 0].sum())
-        self.n_b = int(recv[:, 1].sum())
-        recv_off = np.concatenate([[0], np.cumsum(out_splits)])
-        ia = np.concatenate([np.arange(recv_off[s], recv_off[s] + recv[s, 0]) for s in range(W)]) \
-            if W else np.zeros(0, np.int64)
-        ib = np.concatenate([np.arange(recv_off[s] + recv[s, 0], recv_off[s + 1]) for s in range(W)])
-        ia_t = torch.from_numpy(ia.astype(np.int64)).to(self.dev)
-        ib_t = torch.from_numpy(ib.astype(np.int64)).to(self.dev)
-        for f in FIELDS:
-            xa, xb = getattr(self.a, f), getattr(self.b, f)
-            parts = []
-            for d in range(W):
-                parts.append(xa[a_off[d]:a_off[d + 1]])
-                parts.append(xb[b_off[d]:b_off[d + 1]])
-            got = self.comm.all_to_all(torch.cat(parts), in_splits, out_splits)
-            setattr(self, f, torch.cat([got[ia_t], got[ib_t]]))
+        # ranges of the shard in the buffers
+        n0 = (self.na_s, self.nb_s)
+        base = (self._oa, self._ob)
+        self.rng = [(base[br] + int(lo_s[br] - lo_r[br]), base[br] + n0[br] - int(hi_s[br] - hi_r[br]))
+                    for br in range(2)]
+        in_splits = [0 if d == r else int(send[0, d] + send[1, d]) for d in range(W)]
+        out_splits = [0 if q == r else int(recv[q, 0] + recv[q, 1]) for q in range(W)]
+        self._saved = []
+        moving = int(allc.sum()) - sum(int(allc[q, :, q].sum()) for q in range(W))
+        if moving:  # the same decision on every rank: the all-to-all is collective
+            soff = [np.concatenate([[0], np.cumsum(send[br])]) for br in range(2)]
+            roff = np.concatenate([[0], np.cumsum(out_splits)])
+            # received pieces of each branch from the lower / higher shards, in shard order
+            idx = {}
+            for br in range(2):
+                for part, qs in (("lo", range(r)), ("hi", range(r + 1, W))):
+                    ii = [np.arange(roff[q] + (recv[q, 0] if br else 0),
+                                    roff[q] + (recv[q, 0] if br else 0) + recv[q, br]) for q in qs]
+                    ii = np.concatenate(ii) if ii else np.zeros(0, np.int64)
+                    idx[br, part] = torch.from_numpy(ii.astype(np.int64)).to(self.dev)
+            for f in FIELDS:
+                pieces = []
+                for d in range(W):
+                    if d == r:
+                        continue
+                    for br in range(2):
+                        o = self._orig(br, f)
+                        pieces.append(o[soff[br][d]: soff[br][d + 1]])
+                sendbuf = torch.cat(pieces) if pieces else self.buf[f][:0]
+                got = self.comm.all_to_all(sendbuf, in_splits, out_splits)
+                for br in range(2):
+                    lo, hi = self.rng[br]
+                    o0 = base[br]
+                    for part, dst0 in (("lo", lo), ("hi", o0 + n0[br] - int(hi_s[br]))):
+                        ix = idx[br, part]
+                        if ix.numel() == 0:
+                            continue
+                        if self.restore:  # originals under the arriving ops, put back after the step
+                            self._saved.append((f, dst0, self.buf[f][dst0: dst0 + ix.numel()].clone()))
+                        self.buf[f][dst0: dst0 + ix.numel()] = got[ix]
+        self.n_a = self.rng[0][1] - self.rng[0][0]
+        self.n_b = self.rng[1][1] - self.rng[1][0]
         self._bind()
+
+    def _restore(self) -> None:
+        for f, at, t in reversed(self._saved):
+            self.buf[f][at: at + t.numel()] = t
+        self._saved = []
 
     # -- device structs -----------------------------------------------------------------
     def _bind(self) -> None:
         torch = self.torch
         n = self.n_a + self.n_b
-        nn = max(n, 1)
-        self.order = torch.empty(nn, dtype=torch.int32, device=self.dev)
-        self.addr = torch.empty(nn, dtype=torch.int32, device=self.dev)
-        self.file = torch.empty(nn, dtype=torch.int32, device=self.dev)
-        self.ctx = torch.empty(nn, dtype=torch.int32, device=self.dev)
+        if n > self._outn:
+            nn = max(n, 1)
+            self.order = torch.empty(nn, dtype=torch.int32, device=self.dev)
+            self.addr = torch.empty(nn, dtype=torch.int32, device=self.dev)
+            self.file = torch.empty(nn, dtype=torch.int32, device=self.dev)
+            self.ctx = torch.empty(nn, dtype=torch.int32, device=self.dev)
+            self._outn = n
         self.cap = max(min(self.n_a, self.n_b) + 2 * self.H, 1)
-        self.conf = torch.empty(2 * self.cap, dtype=torch.int32, device=self.dev)
+        if getattr(self, "conf", None) is None or self.conf.numel() < 2 * self.cap:
+            self.conf = torch.empty(2 * self.cap, dtype=torch.int32, device=self.dev)
         self.counts = torch.zeros(2, dtype=torch.int64, device=self.dev)
         ws = C.c_size_t(0)
         check(lib().smx_compose_workspace_bytes(self.n_a, self.n_b, self.n_sym, C.byref(ws)))
         if ws.value > self._ws_bytes:
             self._ws = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=self.dev)
             self._ws_bytes = ws.value
-        self._ops = _abi.SmxOps(self.n_a, self.n_b, self.n_sym, _ptr(self.kind), _ptr(self.ts),
-                                _ptr(self.hi), _ptr(self.lo), _ptr(self.sym), _ptr(self.v0),
-                                _ptr(self.v1))
+        a_lo = self.rng[0][0]
+        gap = self.rng[1][0] - self.rng[0][1]
+        fp = {f: self.buf[f].data_ptr() + a_lo * self.buf[f].element_size() for f in FIELDS}
+        self._ops = _abi.SmxOps(self.n_a, self.n_b, self.n_sym, fp["kind"], fp["ts"], fp["hi"],
+                                fp["lo"], fp["sym"], fp["v0"], fp["v1"], gap)
         self._out = _abi.SmxComposeOut(_ptr(self.order), _ptr(self.addr), _ptr(self.file),
                                        _ptr(self.ctx), _ptr(self.conf), self.cap,
                                        _ptr(self.counts))
@@ -277,6 +344,8 @@ class ShardedCompose:
         self.comm.all_reduce_max(self.part)
         self._step(_abi.SHARD_EMIT)
         self.sum_final = self.comm.all_gather(self.summary).cpu().numpy()
+        if self.restore:
+            self._restore()
 
     def _set_halo(self, summ: np.ndarray, xs) -> None:
         """Halo of branch b: the renames of b on the following shards, first H of them."""

@@ -175,6 +175,46 @@ def lift_logs(spec: LiftSpec) -> LiftLogs:
                     cat([ha, hb]), cat([la, lb]), cat([na_, nb_]), cat([da, db]))
 
 
+def lift_slice_soa(spec: LiftSpec, rank: int, world: int) -> Tuple[SoA, int, int]:
+    """Rank's index slices of a merge of world x spec.n_total lift-shaped ops, generated
+    without the rest of it (sharded benchmark: each rank loads its own slice).  Branch
+    op k of the global logs has timestamp BASE_MS + k // ops_per_ms; rank r holds ops
+    [r * n, (r + 1) * n) of each branch (n = n_total / 2), drawn from rng(seed, r);
+    divergent renames pair A op k with B op k, so they stay inside one slice.
+    Returns (slice SoA: A slice then B slice, global n_a, global n_b)."""
+    if spec.shuffle or spec.rename_overlap is not None:
+        raise ValueError("lift_slice_soa: plain lift-shaped specs only")
+    n_s = spec.n_total // 2
+    start = rank * n_s
+    rng = np.random.default_rng([spec.seed, rank])
+    probs = np.array([p for _, p in spec.mix], dtype=np.float64)
+    probs /= probs.sum()
+    ren = [t for t, _ in spec.mix].index("renameSymbol")
+    parts = []
+    for side in range(2):
+        t = rng.choice(len(spec.mix), size=n_s, p=probs).astype(np.int8)
+        sym = rng.integers(0, spec.n_sym, size=n_s, dtype=np.int64)
+        bits = rng.integers(0, 0xFFFFFFFFFFFFFFFF, size=(n_s, 2), dtype=np.uint64, endpoint=True)
+        hi = (bits[:, 0] & ~np.uint64(0xF000)) | np.uint64(0x4000)
+        lo = (bits[:, 1] & ~np.uint64(0xC000000000000000)) | np.uint64(0x8000000000000000)
+        name = rng.integers(0, spec.names, size=n_s, dtype=np.int32)
+        dst = rng.integers(0, spec.n_files, size=n_s, dtype=np.int32)
+        ts = BASE_MS + (start + np.arange(n_s, dtype=np.int64)) // spec.ops_per_ms
+        parts.append([t, sym, ts, hi, lo, name, dst])
+    (ta, sa), (tb, sb) = parts[0][:2], parts[1][:2]
+    flip = rng.random(n_s) < spec.divergent
+    sel = flip & (ta == ren) & (tb == ren)
+    sb[sel] = sa[sel]
+    cat = np.concatenate
+    logs = LiftLogs(spec, n_s, n_s, *[cat([parts[0][i], parts[1][i]]) for i in range(7)])
+    soa = lift_soa(logs)
+    # move addresses are one string per global op index (like lift_soa on the whole merge)
+    is_mv = soa.kind == KIND_RANK["moveDecl"]
+    gidx = np.concatenate([start + np.arange(n_s), world * n_s + start + np.arange(n_s)])
+    soa.v0[is_mv] = (2 * spec.names + spec.n_files + gidx[is_mv]).astype(np.int32)
+    return soa, world * n_s, world * n_s
+
+
 def _kind_table(spec: LiftSpec) -> np.ndarray:
     return np.array([KIND_RANK[t] for t, _ in spec.mix], dtype=np.uint8)
 
