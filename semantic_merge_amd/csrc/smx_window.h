@@ -238,6 +238,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   if (bad) P.meta->bad_sym = 1;
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
+  if (t < SMX_N_KINDS) wck[t] = 0;
   // window offsets = chunk prefix at the window start + kinds of the <= 255 ops
   // between that chunk start and the window start (per branch)
   if (t < SMX_N_KINDS) {
@@ -286,7 +287,9 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     return;
   }
 
-  // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties
+  // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties:
+  //    merge path, WF_ITEMS outputs per lane.  (Per-element rank searches, four
+  //    interleaved binary searches per lane, measured 2-3x slower: LDS-bound.)
   {
     const int d0 = t * WF_ITEMS < sz ? t * WF_ITEMS : sz;
     const int d1 = d0 + WF_ITEMS < sz ? d0 + WF_ITEMS : sz;
@@ -305,18 +308,31 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   __syncthreads();
   WSTAMP(3);
 
-  // 3. stable multisplit of S by rank
+  // 3. stable multisplit of S by rank (wave ballots); element, kind and rank stay in
+  //    registers for the scatter (m = t + WF_NT * j is chunk wv + WF_WAVES * j)
   const int nch = (sz + WAVE - 1) / WAVE;
-  for (int c = wv; c < nch; c += WF_WAVES) {
-    const int m = c * WAVE + lane;
+  int me[WF_ITEMS];
+  u32 mkr[WF_ITEMS];  // kind | rank << 8
+#pragma unroll
+  for (int j = 0; j < WF_ITEMS; ++j) {
+    const int m = t + WF_NT * j;
+    me[j] = m < sz ? sord[m] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < WF_ITEMS; ++j) mkr[j] = t + WF_NT * j < sz ? skind[me[j]] : 0u;
+  const u64 ltm = lanemask_lt();
+#pragma unroll
+  for (int j = 0; j < WF_ITEMS; ++j) {
+    const int m = t + WF_NT * j;
+    const int c = wv + WF_WAVES * j;
     const bool valid = m < sz;
-    const int e = valid ? sord[m] : 0;
-    const u32 k = valid ? skind[e] : 0u;
+    const u32 k = mkr[j];
     const u64 peers = wave_peers<5>(k, valid);
-    const u32 r = __popcll(peers & lanemask_lt());
-    if (valid) {
-      srank[m] = (u8)r;
-      if (r == 0) ccnt[c][k] = (u16)__popcll(peers);
+    const u32 r = __popcll(peers & ltm);
+    mkr[j] = k | (r << 8);
+    if (valid && r == 0) {
+      ccnt[c][k] = (u16)__popcll(peers);
+      atomicAdd(&wck[k], (u32)__popcll(peers));
     }
   }
   __syncthreads();
@@ -325,24 +341,25 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     const u32 x = lane < nch ? ccnt[lane][k] : 0u;
     const u32 inc = wave_incl_sum(x);
     if (lane < nch) ccnt[lane][k] = (u16)(inc - x);
-    if (lane == WAVE - 1) wck[k] = inc;
   }
-  __syncthreads();
-  WSTAMP(5);
-  if (wv == 0) {
+  if (wv == WF_WAVES - 1) {  // (kinds 7 and 15 only on this wave)
     const u32 x = lane < SMX_N_KINDS ? wck[lane] : 0u;
     const u32 inc = wave_incl_sum(x);
     if (lane < SMX_N_KINDS) kbase[lane] = inc - x;
     if (lane == SMX_N_KINDS - 1) kbase[SMX_N_KINDS] = inc;
   }
   __syncthreads();
+  WSTAMP(5);
   WSTAMP(6);
-  for (int m = t; m < sz; m += WF_NT) {
-    const int e = sord[m];
-    const u32 k = skind[e];
-    const int p = kbase[k] + ccnt[m / WAVE][k] + srank[m];
-    fin[p] = (u16)e;
-    sl[e] = (u16)p;
+#pragma unroll
+  for (int j = 0; j < WF_ITEMS; ++j) {
+    const int m = t + WF_NT * j;
+    if (m < sz) {
+      const u32 k = mkr[j] & 0xffu;
+      const int p = kbase[k] + ccnt[wv + WF_WAVES * j][k] + (mkr[j] >> 8);
+      fin[p] = (u16)me[j];
+      sl[me[j]] = (u16)p;
+    }
   }
   __syncthreads();
   WSTAMP(7);

@@ -20,6 +20,8 @@ def load(dirs):
             for row in csv.DictReader(open(path)):
                 name = row.get("Kernel_Name") or row.get("Kernel-Name") or ""
                 short = name.split("(")[0].split("<")[0].strip()
+                if short.startswith("void "):
+                    short = short[5:]
                 if "k_calib_read" in name or "k_calib_write" in name:
                     short = name.split("(")[0].strip()
                 vals[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
@@ -50,6 +52,17 @@ def main():
         wr = win["WRITE_SIZE"] * 1024 / cal.get("w4", 1.0)
         out["k_window_f_hbm_bytes"] = {"read": rd, "write": wr, "total": rd + wr}
     json.dump(out, sys.stdout, indent=1)
+    n_ops = int(os.environ.get("SMX_PMC_NOPS", "0"))
+    if n_ops and "k_window_f_hbm_bytes" in out:
+        # the per-launch HBM bytes bench.py reports as roofline.traffic
+        hb = out["k_window_f_hbm_bytes"]
+        rec = {"n_ops": n_ops, "kernel": "k_window_f",
+               "hbm_bytes_per_launch": round(hb["total"]),
+               "read_bytes": round(hb["read"]), "write_bytes": round(hb["write"]),
+               "correction": "FETCH_SIZE / calibrated 8-B read factor, WRITE_SIZE / 4-B write "
+                             "factor (tools/pmc_calib.hip; MI355X_MICROARCH.md HBM section)"}
+        with open(os.environ.get("SMX_PMC_OUT", "pmc_window.json"), "w") as fh:
+            json.dump(rec, fh, indent=1)
 
 
 if __name__ == "__main__":
