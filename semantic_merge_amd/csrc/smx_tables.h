@@ -235,6 +235,7 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __re
 }
 
 #define TBR_NT 1024
+#define TBR_U 8             // records per lane per step in k_tb_reduce
 
 // One workgroup per bucket: LDS max over record indices, then each symbol's
 // values are fetched once: fin[sym] = (addr, file, ctx, 0).
@@ -255,8 +256,9 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
   const bool any = A.nMv + A.nR > 0;
   const u32 lo = any ? offs[(u64)b * nblk] : 0u;
   const u32 hi = !any ? 0u : (b + 1 < A.nbk) ? offs[(u64)(b + 1) * nblk] : *nrec_total;
-  for (u32 i = lo + threadIdx.x; i < hi; i += TBR_NT) {
-    const u64 q = rec[i];
+  // TBR_U records per lane per step, loads issued together (one workgroup per
+  // bucket: its record stream needs the memory-level parallelism)
+  auto put = [&](u64 q) {
     const u32 r1 = (u32)(q & 0x7fffffffu) + 1u;
     const u32 ls = (u32)(q >> 32) & 0xfffu;
     if ((u64)(r1 - 1) < A.nMv) {
@@ -265,7 +267,16 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
     } else {
       atomicMax(&tC[ls], r1);
     }
+  };
+  u32 i = lo + threadIdx.x;
+  for (; i + (TBR_U - 1) * TBR_NT < hi; i += TBR_U * TBR_NT) {
+    u64 q[TBR_U];
+#pragma unroll
+    for (int u = 0; u < TBR_U; ++u) q[u] = __builtin_nontemporal_load(&rec[i + u * TBR_NT]);
+#pragma unroll
+    for (int u = 0; u < TBR_U; ++u) put(q[u]);
   }
+  for (; i < hi; i += TBR_NT) put(rec[i]);
   __syncthreads();
   const u32 s0 = b * A.width;
   for (u32 i = threadIdx.x; i < A.width && (i64)(s0 + i) < n_sym; i += TBR_NT) {

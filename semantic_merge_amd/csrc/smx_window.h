@@ -42,6 +42,9 @@ typedef u32 rkey_t;
 #define RK_PREFIX_SHIFT 43         // top 21 bits of oid_hi
 #endif
 #define RK_PER16 (16 / (int)sizeof(rkey_t))   // keys per 16-byte LDS read
+#ifndef RK_NRD
+#define RK_NRD (SMX_KEY64 ? 4 : 2)           // 16-byte reads per rank-loop step
+#endif
 
 // Number of keys < kp among the first m (<= RK_PER16) keys of a 16-byte LDS read.
 __device__ __forceinline__ int rk_count(const uint4 x, u32 kp, int m) {
@@ -418,13 +421,17 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       const int q0 = gs & ~(K - 1);
       int c = 0;
       int q = q0;
-      // 4 x 16 bytes of keys per step: four independent LDS reads in flight
-      for (; q + 4 * K <= ge; q += 4 * K) {
-        const rkey16_t x0 = pv[q / K], x1 = pv[q / K + 1], x2 = pv[q / K + 2], x3 = pv[q / K + 3];
-        c += rk_count(x0, kp) + rk_count(x1, kp) + rk_count(x2, kp) + rk_count(x3, kp);
+      // RK_NRD x 16 bytes of keys per step: independent LDS reads in flight
+      constexpr int NR = RK_NRD;
+      for (; q + NR * K <= ge; q += NR * K) {
+        rkey16_t x[NR];
+#pragma unroll
+        for (int u = 0; u < NR; ++u) x[u] = pv[q / K + u];
+#pragma unroll
+        for (int u = 0; u < NR; ++u) c += rk_count(x[u], kp);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {  // fewer left: up to four more reads, masked
+      for (int u = 0; u < NR; ++u) {  // fewer left: up to NR more reads, masked
         const int qq = q + K * u;
         if (qq < ge) c += rk_count(pv[qq / K], kp, ge - qq);
       }
