@@ -792,7 +792,7 @@ enum Buf {
   B_META, B_BND, B_WCNT, B_WOFF, B_STS, B_SHI, B_SLO, B_PERM, B_RKEY, B_RVAL, B_RK2, B_RV2,
   B_RHIST, B_PART, B_ORDER, B_SYMT, B_MVA, B_MVF, B_MSYM, B_MCLS, B_MSTR, B_MSIDE, B_MOWN,
   B_RAB, B_FLAGS, B_FPOS, B_CAND, B_Q, B_PM, B_NCONF, B_NREAL, B_COFF, B_SKIP, B_SKIPEX,
-  B_TABA, B_TABF, B_TABR, B_FIN, B_PREFA, B_PREFF, B_REC, B_TBHIST, B_TBTOT, B_CCNT, B_TSUM, B_SMP, B_N
+  B_TABA, B_TABF, B_TABR, B_FIN, B_PREFA, B_PREFF, B_REC, B_TBHIST, B_TBTOT, B_HTS, B_CCNT, B_TSUM, B_SMP, B_N
 };
 
 static Layout layout(i64 na, i64 nb, i64 n_sym) {
@@ -826,7 +826,8 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_PREFA] = sz[B_PREFF] = (size_t)nn * 4;
   sz[B_REC] = (size_t)nn * 8;
   sz[B_TBHIST] = (size_t)TB_MAXBK * SMX_CEIL_DIV(nn, (i64)TB_TILE) * 4;
-  sz[B_TBTOT] = 16;
+  sz[B_TBTOT] = (size_t)(TB_MAXBK + 1) * 4;  // bucket starts
+  sz[B_HTS] = (size_t)TB_MAXBK * (SMX_CEIL_DIV(SMX_CEIL_DIV(nn, (i64)TB_TILE), (i64)HS_ROWS) + 1) * 4;
   sz[B_CCNT] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)256) + 2) * 4;
   sz[B_SMP] = (size_t)(SMX_CEIL_DIV(nn, (i64)CH) + 4) * 8;
   sz[B_TSUM] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)CH * CS_TILE) + 2) * 4;
@@ -1018,7 +1019,14 @@ static int launch_tables(const Ctx& C, const WinArgs& P, u64* part_tab, u32 tag,
     u32* total = C.ws<u32>(B_TBTOT);
     u64* rec = C.ws<u64>(B_REC);
     hipLaunchKernelGGL(k_tb_hist, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk);
-    HIP_TRY((scan_excl<OpSum, u32, u32>(hist, hist, (i64)nbk * nblk, nullptr, part, total, st)));
+    {
+      const int ntile = (int)SMX_CEIL_DIV((i64)nblk, (i64)HS_ROWS);
+      const dim3 g(ntile, (unsigned)SMX_CEIL_DIV((u64)nbk, (u64)HS_COLS));
+      u32* tsum = C.ws<u32>(B_HTS);
+      hipLaunchKernelGGL(k_hscan_up, g, dim3(HS_COLS), 0, st, hist, nblk, (u32)nbk, tsum);
+      hipLaunchKernelGGL(k_hscan_mid, dim3(1), dim3(TB_MAXBK), 0, st, tsum, ntile, (u32)nbk, total);
+      hipLaunchKernelGGL(k_hscan_down, g, dim3(HS_COLS), 0, st, hist, nblk, (u32)nbk, tsum, total);
+    }
     hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk, rec);
     hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, hist, nblk, total, rec, n_sym, fin,
                        part_tab, tag);

@@ -153,12 +153,65 @@ __global__ void __launch_bounds__(TB_NT) k_tb_hist(TbArgs A0, u32* __restrict__ 
     }
   }
   __syncthreads();
-  for (u32 i = threadIdx.x; i < A.nbk; i += TB_NT) hist[(u64)i * nblk + blockIdx.x] = h[i];
+  for (u32 i = threadIdx.x; i < A.nbk; i += TB_NT) hist[(u64)blockIdx.x * A.nbk + i] = h[i];
   if (threadIdx.x < 3 && vb[threadIdx.x]) {
     u32* g = const_cast<ComposeMeta*>(A.meta)->vbits;
     const u32 mine = vb[threadIdx.x];
     const u32 cur = __hip_atomic_load(&g[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((cur | mine) != cur) atomicOr(&g[threadIdx.x], mine);
+  }
+}
+
+// Bucket offsets: hist is [block][bucket] (written and read coalesced by the
+// per-block kernels); each entry becomes the global start of that block's run in
+// that bucket, i.e. an exclusive scan in bucket-major order: bstart[bucket] + the
+// counts of the earlier blocks in the same bucket.  Column scan in tiles of
+// HS_ROWS blocks: tile sums, a per-column scan of the tile sums (+ bucket starts),
+// then the tiles.
+#define HS_ROWS 64
+#define HS_COLS 256
+
+__global__ void __launch_bounds__(HS_COLS) k_hscan_up(const u32* __restrict__ hist, int nblk, u32 nbk,
+                                                      u32* __restrict__ tsum) {
+  const u32 col = blockIdx.y * HS_COLS + threadIdx.x;
+  if (col >= nbk) return;
+  const int r0 = blockIdx.x * HS_ROWS, r1 = min(r0 + HS_ROWS, nblk);
+  u32 s = 0;
+#pragma unroll 8
+  for (int r = r0; r < r1; ++r) s += hist[(u64)r * nbk + col];
+  tsum[(u64)blockIdx.x * nbk + col] = s;
+}
+
+__global__ void __launch_bounds__(TB_MAXBK) k_hscan_mid(u32* __restrict__ tsum, int ntile, u32 nbk,
+                                                        u32* __restrict__ bstart) {
+  __shared__ u32 s[TB_MAXBK / WAVE + 1];
+  const u32 col = threadIdx.x;
+  u32 run = 0;
+  if (col < nbk) {
+#pragma unroll 8
+    for (int t = 0; t < ntile; ++t) {
+      const u32 v = tsum[(u64)t * nbk + col];
+      tsum[(u64)t * nbk + col] = run;
+      run += v;
+    }
+  }
+  u32 tot;
+  const u32 ex = block_excl_scan<OpSum, u32, TB_MAXBK / WAVE>(col < nbk ? run : 0u, s, &tot);
+  if (col < nbk) bstart[col] = ex;
+  if (col == 0) bstart[nbk] = tot;
+}
+
+__global__ void __launch_bounds__(HS_COLS) k_hscan_down(u32* __restrict__ hist, int nblk, u32 nbk,
+                                                        const u32* __restrict__ tsum,
+                                                        const u32* __restrict__ bstart) {
+  const u32 col = blockIdx.y * HS_COLS + threadIdx.x;
+  if (col >= nbk) return;
+  const int r0 = blockIdx.x * HS_ROWS, r1 = min(r0 + HS_ROWS, nblk);
+  u32 run = bstart[col] + tsum[(u64)blockIdx.x * nbk + col];
+  for (int r = r0; r < r1; ++r) {
+    const u32 v = hist[(u64)r * nbk + col];
+    hist[(u64)r * nbk + col] = run;
+    run += v;
   }
 }
 
@@ -178,7 +231,7 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __re
   const u32 nbk = A.nbk;
   for (u32 i = threadIdx.x; i < nbk; i += TB_NT) {
     lstart[i] = 0;
-    gbase[i] = offs[(u64)i * nblk + blockIdx.x];
+    gbase[i] = offs[(u64)blockIdx.x * nbk + i];
   }
   __syncthreads();
   u64 q[TB_ITEMS];
@@ -254,8 +307,8 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
   for (u32 i = threadIdx.x; i < A.width; i += TBR_NT) tA[i] = tF[i] = tC[i] = 0;
   __syncthreads();
   const bool any = A.nMv + A.nR > 0;
-  const u32 lo = any ? offs[(u64)b * nblk] : 0u;
-  const u32 hi = !any ? 0u : (b + 1 < A.nbk) ? offs[(u64)(b + 1) * nblk] : *nrec_total;
+  const u32 lo = any ? nrec_total[b] : 0u;  // bucket starts (k_hscan_mid), nbk + 1 entries
+  const u32 hi = any ? nrec_total[b + 1] : 0u;
   // TBR_U records per lane per step, loads issued together (one workgroup per
   // bucket: its record stream needs the memory-level parallelism)
   auto put = [&](u64 q) {
