@@ -133,13 +133,32 @@ __global__ void __launch_bounds__(BLOCK) k_keymask(const u64* __restrict__ ts, c
       ra[s][q] &= v[q];
     }
   }
+  // wave OR of the 12 words (AND = NOT OR NOT) on DPP, then LDS, then one device
+  // atomic per word and block (a device atomic per thread serialised on 12 words)
+  __shared__ u32 sm[24];
+  if (threadIdx.x < 24) sm[threadIdx.x] = 0;
+  __syncthreads();
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      atomicOr((unsigned long long*)&meta->key_or[s][q], (unsigned long long)ro[s][q]);
-      atomicAnd((unsigned long long*)&meta->key_and[s][q], (unsigned long long)ra[s][q]);
+      const u64 w[2] = {ro[s][q], ~ra[s][q]};
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const u32 lo32 = wave_or_to_last((u32)w[x]), hi32 = wave_or_to_last((u32)(w[x] >> 32));
+        if ((threadIdx.x & (WAVE - 1)) == WAVE - 1) {
+          atomicOr(&sm[(s * 3 + q) * 4 + 2 * x], lo32);
+          atomicOr(&sm[(s * 3 + q) * 4 + 2 * x + 1], hi32);
+        }
+      }
     }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int s = threadIdx.x / 3, q = threadIdx.x % 3;
+    const u32* v = &sm[threadIdx.x * 4];
+    atomicOr((unsigned long long*)&meta->key_or[s][q], ((unsigned long long)v[1] << 32) | v[0]);
+    atomicAnd((unsigned long long*)&meta->key_and[s][q], ~(((unsigned long long)v[3] << 32) | v[2]));
+  }
 }
 
 __global__ void k_meta_init(ComposeMeta* meta) {

@@ -24,6 +24,7 @@
   } while (0)
 
 #define RGA_LIST_CAP 2048  // lists up to this many events are ranked in LDS
+#define RGA_LDS_KEYS 512   // ... with their survivors' keys in LDS up to this many survivors
 
 struct RgaKey {
   u32 anchor;
@@ -115,6 +116,7 @@ __global__ void __launch_bounds__(BLOCK) k_rga_list(smx_rga_ops o, const u32* __
                                                     const u32* __restrict__ lcnt, u32* __restrict__ tmp,
                                                     u32* __restrict__ scnt) {
   __shared__ u32 sidx[RGA_LIST_CAP];
+  __shared__ u64 skey[RGA_LDS_KEYS][4];
   __shared__ u32 ns;
   const u32 l = blockIdx.x;
   const u32 s0 = lstart[l], cnt = lcnt[l];
@@ -127,15 +129,44 @@ __global__ void __launch_bounds__(BLOCK) k_rga_list(smx_rga_ops o, const u32* __
     }
     __syncthreads();
     const u32 m = ns;
-    for (u32 a = threadIdx.x; a < m; a += BLOCK) {
-      const u32 ia = sidx[a];
-      const RgaKey ka = rga_key(o, ia);
-      u32 r = 0;
-      for (u32 b = 0; b < m; ++b) {
-        const u32 ib = sidx[b];
-        r += rga_lt(rga_key(o, ib), ib, ka, ia);
+    if (m <= RGA_LDS_KEYS) {
+      // survivors' keys packed once into LDS as four order-preserving words
+      // (anchor | t_hi, t_lo | author, opid_hi, opid_lo); every lane then ranks
+      // its elements against all of them (same b on all lanes: LDS broadcast)
+      for (u32 a = threadIdx.x; a < m; a += BLOCK) {
+        const u32 i = sidx[a];
+        const u64 tt = (u64)o.t[i] ^ 0x8000000000000000ull;  // signed -> unsigned order
+        skey[a][0] = ((u64)o.anchor[i] << 32) | (tt >> 32);
+        skey[a][1] = (tt << 32) | o.author[i];
+        skey[a][2] = o.opid_hi[i];
+        skey[a][3] = o.opid_lo[i];
       }
-      tmp[s0 + r] = ia;
+      __syncthreads();
+      for (u32 a = threadIdx.x; a < m; a += BLOCK) {
+        const u64 k0 = skey[a][0], k1 = skey[a][1], k2 = skey[a][2], k3 = skey[a][3];
+        const u32 ia = sidx[a];
+        u32 r = 0;
+        for (u32 b = 0; b < m; ++b) {
+          const u64 b0 = skey[b][0], b1 = skey[b][1], b2 = skey[b][2], b3 = skey[b][3];
+          const bool lt = b0 != k0 ? b0 < k0
+                        : b1 != k1 ? b1 < k1
+                        : b2 != k2 ? b2 < k2
+                        : b3 != k3 ? b3 < k3 : sidx[b] < ia;
+          r += lt;
+        }
+        tmp[s0 + r] = ia;
+      }
+    } else {
+      for (u32 a = threadIdx.x; a < m; a += BLOCK) {
+        const u32 ia = sidx[a];
+        const RgaKey ka = rga_key(o, ia);
+        u32 r = 0;
+        for (u32 b = 0; b < m; ++b) {
+          const u32 ib = sidx[b];
+          r += rga_lt(rga_key(o, ib), ib, ka, ia);
+        }
+        tmp[s0 + r] = ia;
+      }
     }
     if (threadIdx.x == 0) scnt[l] = m;
   } else {
