@@ -830,7 +830,7 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_RVAL] = (size_t)nn * 4;
   sz[B_RK2] = (size_t)nn * 8;
   sz[B_RV2] = (size_t)nn * 4;
-  sz[B_RHIST] = (size_t)256 * nblk * 4;
+  sz[B_RHIST] = radix_hist_bytes(nn);
   sz[B_PART] = (size_t)SCAN_NB * 8;
   sz[B_ORDER] = sz[B_SYMT] = sz[B_MVA] = sz[B_MVF] = (size_t)nn * 4;
   sz[B_MSYM] = sz[B_MCLS] = sz[B_MSTR] = sz[B_MOWN] = sz[B_RAB] = (size_t)nn * 4;
@@ -1038,14 +1038,7 @@ static int launch_tables(const Ctx& C, const WinArgs& P, u64* part_tab, u32 tag,
     u32* total = C.ws<u32>(B_TBTOT);
     u64* rec = C.ws<u64>(B_REC);
     hipLaunchKernelGGL(k_tb_hist, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk);
-    {
-      const int ntile = (int)SMX_CEIL_DIV((i64)nblk, (i64)HS_ROWS);
-      const dim3 g(ntile, (unsigned)SMX_CEIL_DIV((u64)nbk, (u64)HS_COLS));
-      u32* tsum = C.ws<u32>(B_HTS);
-      hipLaunchKernelGGL(k_hscan_up, g, dim3(HS_COLS), 0, st, hist, nblk, (u32)nbk, tsum);
-      hipLaunchKernelGGL(k_hscan_mid, dim3(1), dim3(TB_MAXBK), 0, st, tsum, ntile, (u32)nbk, total);
-      hipLaunchKernelGGL(k_hscan_down, g, dim3(HS_COLS), 0, st, hist, nblk, (u32)nbk, tsum, total);
-    }
+    hscan(hist, nblk, (u32)nbk, C.ws<u32>(B_HTS), total, st);
     hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk, rec);
     hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, hist, nblk, total, rec, n_sym, fin,
                        part_tab, tag);

@@ -47,17 +47,22 @@ __device__ __forceinline__ bool rga_lt(const RgaKey& a, u32 ia, const RgaKey& b,
   return ia < ib;
 }
 
+// Sort records: key = (list, value), value word = event index | op << 30 (the op
+// travels through the sort, so the group replay reads no per-event array).
+#define RGA_IDX_MASK 0x3fffffffu
 __global__ void k_rga_init(smx_rga_ops o, u64* __restrict__ keys, u32* __restrict__ vals, i32* __restrict__ err) {
   for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < o.n_ops; i += (i64)gridDim.x * BLOCK) {
     const u32 l = o.list[i];
-    if (l >= (u64)o.n_lists || o.op[i] > 2) *err = 1;
+    const u32 op = o.op[i];
+    if (l >= (u64)o.n_lists || op > 2) *err = 1;
     keys[i] = ((u64)(l < (u64)o.n_lists ? l : 0) << 32) | o.value[i];
-    vals[i] = (u32)i;
+    vals[i] = (u32)i | ((op > 2 ? 0u : op) << 30);
   }
 }
 
-// One thread per (list, value) group (events in stream order): replay and mark
-// the fate of every element the group creates.  state: bit0 present, bit1 tombstoned.
+// One thread per (list, value) group (a contiguous range of the sorted events, in
+// stream order): replay and mark the fate of every element the group creates.
+// state is indexed by sorted position: bit0 present, bit1 tombstoned.
 __global__ void k_rga_groups(smx_rga_ops o, const u64* __restrict__ keys, const u32* __restrict__ vals,
                              u8* __restrict__ state) {
   const i64 n = o.n_ops;
@@ -66,46 +71,43 @@ __global__ void k_rga_groups(smx_rga_ops o, const u64* __restrict__ keys, const 
     i64 end = j + 1;
     while (end < n && keys[end] == keys[j]) ++end;
     for (i64 x = j; x < end; ++x) {
-      const u32 i = vals[x];
-      const u8 op = o.op[i];
+      const u32 op = vals[x] >> 30;
       if (op == 2) {  // delete: tombstone every present element of the value
-        for (i64 y = j; y < x; ++y) {
-          const u32 e = vals[y];
-          if (state[e] & 1) state[e] |= 2;
-        }
-        state[i] = 0;
+        for (i64 y = j; y < x; ++y)
+          if (state[y] & 1) state[y] |= 2;
+        state[x] = 0;
         continue;
       }
       if (op == 1) {  // move: pop the live element with the smallest (key, index)
         i64 best = -1;
         RgaKey bk{};
+        u32 bi = 0;
         for (i64 y = j; y < x; ++y) {
-          const u32 e = vals[y];
-          if (state[e] != 1) continue;
+          if (state[y] != 1) continue;
+          const u32 e = vals[y] & RGA_IDX_MASK;
           const RgaKey ke = rga_key(o, e);
-          if (best < 0 || rga_lt(ke, e, bk, vals[best])) {
+          if (best < 0 || rga_lt(ke, e, bk, bi)) {
             best = y;
             bk = ke;
+            bi = e;
           }
         }
-        if (best >= 0) state[vals[best]] = 0;
+        if (best >= 0) state[best] = 0;
       }
-      state[i] = 1;  // insert / move creates a live element
+      state[x] = 1;  // insert / move creates a live element
     }
   }
 }
 
-// Events per list (keys are sorted by list): a thread starts at each run start and
-// at each multiple of RGA_CH, counts to the run end or the next multiple, and adds
-// the count with one atomic.
-#define RGA_CH 1024
-__global__ void k_rga_lcount(const u64* __restrict__ keys, i64 n, u32* __restrict__ lcnt) {
+// lstart[l] = first sorted position of list l (a list without events starts where
+// the next one does); lstart[n_lists] = n.  One pass over the sorted keys.
+__global__ void k_rga_bounds(const u64* __restrict__ keys, i64 n, i64 nl, u32* __restrict__ lstart) {
   for (i64 j = (i64)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (i64)gridDim.x * BLOCK) {
-    const u32 l = (u32)(keys[j] >> 32);
-    if (j % RGA_CH != 0 && (u32)(keys[j - 1] >> 32) == l) continue;
-    i64 e = j + 1;
-    while (e < n && e % RGA_CH != 0 && (u32)(keys[e] >> 32) == l) ++e;
-    atomicAdd(&lcnt[l], (u32)(e - j));
+    const i64 l = (i64)(keys[j] >> 32);
+    const i64 lp = j ? (i64)(keys[j - 1] >> 32) : -1;
+    for (i64 L = lp + 1; L <= l; ++L) lstart[L] = (u32)j;
+    if (j == n - 1)
+      for (i64 L = l + 1; L <= nl; ++L) lstart[L] = (u32)n;
   }
 }
 
@@ -113,20 +115,17 @@ __global__ void k_rga_lcount(const u64* __restrict__ keys, i64 n, u32* __restric
 // write them, in order, at the start of the list's event range of `tmp`.
 __global__ void __launch_bounds__(BLOCK) k_rga_list(smx_rga_ops o, const u32* __restrict__ vals,
                                                     const u8* __restrict__ state, const u32* __restrict__ lstart,
-                                                    const u32* __restrict__ lcnt, u32* __restrict__ tmp,
-                                                    u32* __restrict__ scnt) {
+                                                    u32* __restrict__ tmp, u32* __restrict__ scnt) {
   __shared__ u32 sidx[RGA_LIST_CAP];
   __shared__ u64 skey[RGA_LDS_KEYS][4];
   __shared__ u32 ns;
   const u32 l = blockIdx.x;
-  const u32 s0 = lstart[l], cnt = lcnt[l];
+  const u32 s0 = lstart[l], cnt = lstart[l + 1] - s0;
   if (threadIdx.x == 0) ns = 0;
   __syncthreads();
   if (cnt <= RGA_LIST_CAP) {
-    for (u32 x = threadIdx.x; x < cnt; x += BLOCK) {
-      const u32 i = vals[s0 + x];
-      if (state[i] == 1) sidx[atomicAdd(&ns, 1u)] = i;
-    }
+    for (u32 x = threadIdx.x; x < cnt; x += BLOCK)
+      if (state[s0 + x] == 1) sidx[atomicAdd(&ns, 1u)] = vals[s0 + x] & RGA_IDX_MASK;
     __syncthreads();
     const u32 m = ns;
     if (m <= RGA_LDS_KEYS) {
@@ -172,15 +171,15 @@ __global__ void __launch_bounds__(BLOCK) k_rga_list(smx_rga_ops o, const u32* __
   } else {
     // large list: rank straight from global memory (quadratic; correct for any size)
     u32 m = 0;
-    for (u32 x = 0; x < cnt; ++x) m += state[vals[s0 + x]] == 1;
+    for (u32 x = 0; x < cnt; ++x) m += state[s0 + x] == 1;
     for (u32 a = threadIdx.x; a < cnt; a += BLOCK) {
-      const u32 ia = vals[s0 + a];
-      if (state[ia] != 1) continue;
+      const u32 ia = vals[s0 + a] & RGA_IDX_MASK;
+      if (state[s0 + a] != 1) continue;
       const RgaKey ka = rga_key(o, ia);
       u32 r = 0;
       for (u32 b = 0; b < cnt; ++b) {
-        const u32 ib = vals[s0 + b];
-        if (state[ib] == 1) r += rga_lt(rga_key(o, ib), ib, ka, ia);
+        const u32 ib = vals[s0 + b] & RGA_IDX_MASK;
+        if (state[s0 + b] == 1) r += rga_lt(rga_key(o, ib), ib, ka, ia);
       }
       tmp[s0 + r] = ia;
     }
@@ -222,7 +221,7 @@ static RgaLayout rga_layout(i64 n, i64 nl) {
   size_t sz[R_N];
   sz[R_KEYS] = sz[R_K2] = (size_t)nn * 8;
   sz[R_VALS] = sz[R_V2] = sz[R_TMP] = (size_t)nn * 4;
-  sz[R_HIST] = (size_t)256 * nblk * 4;
+  sz[R_HIST] = radix_hist_bytes(nn);
   sz[R_PART] = SCAN_NB * 8 + 64;  // + error word + totals
   sz[R_STATE] = (size_t)nn;
   sz[R_LCNT] = sz[R_LSTART] = sz[R_SCNT] = (size_t)(nl + 1) * 4 * 2;
@@ -244,7 +243,7 @@ extern "C" int smx_rga_workspace_bytes(int64_t n_ops, int64_t n_lists, size_t* b
 
 static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, size_t wsb, hipStream_t st) {
   const i64 n = ops->n_ops, nl = ops->n_lists;
-  if (n < 0 || nl < 0 || n >= (i64)0x7fffffff || nl >= (i64)0x7fffffff)
+  if (n < 0 || nl < 0 || n > (i64)RGA_IDX_MASK || nl >= (i64)0x7fffffff)
     return smx_set_error(SMX_E_ARG, "bad sizes");
   if (!out || !out->out_offsets || !out->counts) return smx_set_error(SMX_E_ARG, "null output");
   if (n == 0) {
@@ -274,7 +273,6 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
 
   RGA_TRY(hipMemsetAsync(err, 0, 8, st));
   RGA_TRY(hipMemsetAsync(state, 0, (size_t)n, st));
-  RGA_TRY(hipMemsetAsync(lcnt, 0, (size_t)(nl + 1) * 4, st));
   hipLaunchKernelGGL(k_rga_init, dim3(grid), dim3(BLOCK), 0, st, o, keys, vals, err);
   // stable LSD radix on (list, value): value bytes then list bytes
   int shifts[8], ns = 0;
@@ -285,9 +283,8 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   RadixTemp rt{(u64*)(b + L.off[R_K2]), (u32*)(b + L.off[R_V2]), (u32*)(b + L.off[R_HIST]), part};
   RGA_TRY(radix_sort_pairs(keys, vals, n, shifts, ns, rt, st));
   hipLaunchKernelGGL(k_rga_groups, dim3(grid), dim3(BLOCK), 0, st, o, keys, vals, state);
-  hipLaunchKernelGGL(k_rga_lcount, dim3(grid), dim3(BLOCK), 0, st, keys, n, lcnt);
-  RGA_TRY((scan_excl<OpSum, u32, u32>(lcnt, lstart, nl, nullptr, part, (u32*)nullptr, st)));
-  hipLaunchKernelGGL(k_rga_list, dim3(nl), dim3(BLOCK), 0, st, o, vals, state, lstart, lcnt, tmp, scnt);
+  hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, keys, n, nl, lstart);
+  hipLaunchKernelGGL(k_rga_list, dim3(nl), dim3(BLOCK), 0, st, o, vals, state, lstart, tmp, scnt);
   RGA_TRY((scan_excl<OpSum, u32, u32>(scnt, soff, nl, nullptr, part, totals, st)));
   hipLaunchKernelGGL(k_rga_out, dim3(nl), dim3(BLOCK), 0, st, o, tmp, lstart, scnt, soff, *out);
   hipLaunchKernelGGL(k_rga_fin, dim3(1), dim3(1), 0, st, totals, nl, *out);

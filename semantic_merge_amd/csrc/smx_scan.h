@@ -89,3 +89,71 @@ static hipError_t scan_excl(const TI* in, TO* out, i64 n_host, const u64* n_dev,
                      n_dev, partials);
   return hipGetLastError();
 }
+
+// Column scan of a row-major [block][bucket] count matrix (written and read
+// coalesced by the per-block kernels of the table bucketing and the radix sort):
+// each entry becomes the global start of that block's run in that bucket, i.e. an
+// exclusive scan in bucket-major order: bstart[bucket] + the counts of the earlier
+// blocks in the same bucket.  In tiles of HS_ROWS blocks: tile sums, a per-column
+// scan of the tile sums (+ bucket starts, nbk + 1 entries), then the tiles.
+#define HS_ROWS 64
+#define HS_COLS 256
+#define HS_MAXCOLS 1024
+
+static __global__ void __launch_bounds__(HS_COLS) k_hscan_up(const u32* __restrict__ hist, int nblk, u32 nbk,
+                                                      u32* __restrict__ tsum) {
+  const u32 col = blockIdx.y * HS_COLS + threadIdx.x;
+  if (col >= nbk) return;
+  const int r0 = blockIdx.x * HS_ROWS, r1 = min(r0 + HS_ROWS, nblk);
+  u32 s = 0;
+#pragma unroll 8
+  for (int r = r0; r < r1; ++r) s += hist[(u64)r * nbk + col];
+  tsum[(u64)blockIdx.x * nbk + col] = s;
+}
+
+static __global__ void __launch_bounds__(HS_MAXCOLS) k_hscan_mid(u32* __restrict__ tsum, int ntile, u32 nbk,
+                                                        u32* __restrict__ bstart) {
+  __shared__ u32 s[HS_MAXCOLS / WAVE + 1];
+  const u32 col = threadIdx.x;
+  u32 run = 0;
+  if (col < nbk) {
+#pragma unroll 8
+    for (int t = 0; t < ntile; ++t) {
+      const u32 v = tsum[(u64)t * nbk + col];
+      tsum[(u64)t * nbk + col] = run;
+      run += v;
+    }
+  }
+  u32 tot;
+  const u32 ex = block_excl_scan<OpSum, u32, HS_MAXCOLS / WAVE>(col < nbk ? run : 0u, s, &tot);
+  if (col < nbk) bstart[col] = ex;
+  if (col == 0) bstart[nbk] = tot;
+}
+
+static __global__ void __launch_bounds__(HS_COLS) k_hscan_down(u32* __restrict__ hist, int nblk, u32 nbk,
+                                                        const u32* __restrict__ tsum,
+                                                        const u32* __restrict__ bstart) {
+  const u32 col = blockIdx.y * HS_COLS + threadIdx.x;
+  if (col >= nbk) return;
+  const int r0 = blockIdx.x * HS_ROWS, r1 = min(r0 + HS_ROWS, nblk);
+  u32 run = bstart[col] + tsum[(u64)blockIdx.x * nbk + col];
+  for (int r = r0; r < r1; ++r) {
+    const u32 v = hist[(u64)r * nbk + col];
+    hist[(u64)r * nbk + col] = run;
+    run += v;
+  }
+}
+
+static inline size_t hscan_tsum_bytes(i64 nrows, i64 ncols) {
+  return (size_t)ncols * (SMX_CEIL_DIV(nrows, (i64)HS_ROWS) + 1) * 4;
+}
+
+// hist [nrows][ncols] -> bucket-major exclusive offsets in place; bstart[ncols + 1].
+static inline void hscan(u32* hist, int nrows, u32 ncols, u32* tsum, u32* bstart, hipStream_t st) {
+  const int ntile = (int)SMX_CEIL_DIV((i64)nrows, (i64)HS_ROWS);
+  const dim3 g(ntile, (unsigned)SMX_CEIL_DIV((u64)ncols, (u64)HS_COLS));
+  hipLaunchKernelGGL(k_hscan_up, g, dim3(HS_COLS), 0, st, hist, nrows, ncols, tsum);
+  hipLaunchKernelGGL(k_hscan_mid, dim3(1), dim3(HS_MAXCOLS), 0, st, tsum, ntile, ncols, bstart);
+  hipLaunchKernelGGL(k_hscan_down, g, dim3(HS_COLS), 0, st, hist, nrows, ncols, tsum, bstart);
+}
+

@@ -162,59 +162,6 @@ __global__ void __launch_bounds__(TB_NT) k_tb_hist(TbArgs A0, u32* __restrict__ 
   }
 }
 
-// Bucket offsets: hist is [block][bucket] (written and read coalesced by the
-// per-block kernels); each entry becomes the global start of that block's run in
-// that bucket, i.e. an exclusive scan in bucket-major order: bstart[bucket] + the
-// counts of the earlier blocks in the same bucket.  Column scan in tiles of
-// HS_ROWS blocks: tile sums, a per-column scan of the tile sums (+ bucket starts),
-// then the tiles.
-#define HS_ROWS 64
-#define HS_COLS 256
-
-__global__ void __launch_bounds__(HS_COLS) k_hscan_up(const u32* __restrict__ hist, int nblk, u32 nbk,
-                                                      u32* __restrict__ tsum) {
-  const u32 col = blockIdx.y * HS_COLS + threadIdx.x;
-  if (col >= nbk) return;
-  const int r0 = blockIdx.x * HS_ROWS, r1 = min(r0 + HS_ROWS, nblk);
-  u32 s = 0;
-#pragma unroll 8
-  for (int r = r0; r < r1; ++r) s += hist[(u64)r * nbk + col];
-  tsum[(u64)blockIdx.x * nbk + col] = s;
-}
-
-__global__ void __launch_bounds__(TB_MAXBK) k_hscan_mid(u32* __restrict__ tsum, int ntile, u32 nbk,
-                                                        u32* __restrict__ bstart) {
-  __shared__ u32 s[TB_MAXBK / WAVE + 1];
-  const u32 col = threadIdx.x;
-  u32 run = 0;
-  if (col < nbk) {
-#pragma unroll 8
-    for (int t = 0; t < ntile; ++t) {
-      const u32 v = tsum[(u64)t * nbk + col];
-      tsum[(u64)t * nbk + col] = run;
-      run += v;
-    }
-  }
-  u32 tot;
-  const u32 ex = block_excl_scan<OpSum, u32, TB_MAXBK / WAVE>(col < nbk ? run : 0u, s, &tot);
-  if (col < nbk) bstart[col] = ex;
-  if (col == 0) bstart[nbk] = tot;
-}
-
-__global__ void __launch_bounds__(HS_COLS) k_hscan_down(u32* __restrict__ hist, int nblk, u32 nbk,
-                                                        const u32* __restrict__ tsum,
-                                                        const u32* __restrict__ bstart) {
-  const u32 col = blockIdx.y * HS_COLS + threadIdx.x;
-  if (col >= nbk) return;
-  const int r0 = blockIdx.x * HS_ROWS, r1 = min(r0 + HS_ROWS, nblk);
-  u32 run = bstart[col] + tsum[(u64)blockIdx.x * nbk + col];
-  for (int r = r0; r < r1; ++r) {
-    const u32 v = hist[(u64)r * nbk + col];
-    hist[(u64)r * nbk + col] = run;
-    run += v;
-  }
-}
-
 // Scatter into bucket order.  The block's records are counting-sorted by bucket
 // in LDS, then every bucket's run is written contiguously.
 __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __restrict__ offs, int nblk,
