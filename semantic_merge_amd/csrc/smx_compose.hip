@@ -1153,7 +1153,17 @@ static int run_presorted(const Ctx& C, i64 tgt) {
 
 // Generic plan: stable radix sort of each branch by (ts, oid_hi, oid_lo), then
 // fixed windows over the sorted logs.  Used when the presorted plan fails.
-static int run_generic(const Ctx& C) {
+// Adjacent (ts, oid_hi) duplicates in each branch sorted without oid_lo.
+__global__ void k_dupcheck(const u64* __restrict__ sts, const u64* __restrict__ shi, i64 na, i64 n,
+                           ComposeMeta* meta) {
+  for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x + 1; i < n; i += (i64)gridDim.x * BLOCK)
+    if (i != na && sts[i] == sts[i - 1] && shi[i] == shi[i - 1]) meta->dup_key = 1;
+}
+
+// with_lo = false sorts by (ts, oid_hi) only; ids are random (uuid4), so a
+// duplicate (ts, oid_hi) pair -- checked afterwards -- is rare and reruns the
+// sort with oid_lo (run_order).
+static int run_generic(const Ctx& C, bool with_lo) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
@@ -1174,18 +1184,19 @@ static int run_generic(const Ctx& C) {
   u32* perm = C.ws<u32>(B_PERM);
   RadixTemp rt{C.ws<u64>(B_RK2), C.ws<u32>(B_RV2), C.ws<u32>(B_RHIST), C.ws<u32>(B_PART)};
   const u64* words[3] = {C.ops->oid_lo, C.ops->oid_hi, C.ops->ts};
+  const int w0 = with_lo ? 0 : 1;
   for (int side = 0; side < 2; ++side) {
     const i64 off = side ? na : 0, cnt = side ? nb : na;
     if (cnt == 0) continue;
     u64* key = C.ws<u64>(B_RKEY) + off;
     u32* val = perm + off;
-    for (int wi = 0; wi < 3; ++wi) {
+    for (int wi = w0; wi < 3; ++wi) {
       const int q = 2 - wi;  // meta order: 0 = ts, 1 = hi, 2 = lo
       const u64 varying = hm.key_or[side][q] ^ hm.key_and[side][q];
       int shifts[8], ns = 0;
       for (int dgt = 0; dgt < 8; ++dgt)
         if ((varying >> (8 * dgt)) & 0xffull) shifts[ns++] = 8 * dgt;
-      if (wi == 0) {
+      if (wi == w0) {
         hipLaunchKernelGGL(k_gather_init, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi] + off, key, val,
                            cnt);
         if (off)  // values are op indices of A||B
@@ -1199,6 +1210,7 @@ static int run_generic(const Ctx& C) {
     hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_hi, val, shi + off, cnt);
     hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_lo, val, slo + off, cnt);
   }
+  if (!with_lo) hipLaunchKernelGGL(k_dupcheck, dim3(grid_for(n)), dim3(BLOCK), 0, st, sts, shi, na, n, meta);
   const i64 W = SMX_CEIL_DIV(n, (i64)WIN_CAP);
   hipLaunchKernelGGL(k_gpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, sts, shi, slo, na, nb,
                      W, bnd);
@@ -1266,8 +1278,12 @@ static int run_order(const Ctx& C, bool allow_generic, ComposeMeta* hm) {
   if (hm->f_fail && !hm->bad_sym && allow_generic) {
     if (C.ops->b_gap != 0)
       return set_err(SMX_E_ARG, "branch logs not timestamp-ordered: the generic plan needs b_gap = 0");
-    if ((rc = run_generic(C))) return rc;
+    if ((rc = run_generic(C, false))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
+    if (hm->dup_key) {
+      if ((rc = run_generic(C, true))) return rc;
+      if ((rc = read_meta(C, hm))) return rc;
+    }
   }
   return SMX_OK;
 }
