@@ -260,23 +260,6 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     atomicAdd(&woffk[k], 1u);
     if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + (t >= CH)], 1u);
   }
-  {
-    bool dec = false;
-    if (t == 0) dec = (a0 > 0 && na > 0 && prev_a > ts_r[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
-#pragma unroll
-    for (int i = 0; i < WF_ITEMS; ++i) {
-      const int e = t + WF_NT * i;
-      if (e >= sz) continue;
-      if (!(P.ablate & 1) && e != 0 && e != na && sts[e - 1] > ts_r[i]) dec = true;
-    }
-    const bool any_dec = __syncthreads_or(dec);
-    WSTAMP(20);
-    if (any_dec) {
-      if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
-      return;
-    }
-  }
-
   if (P.ablate & 8) {  // load + write only
     load_payload();
     __syncthreads();
@@ -293,6 +276,16 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties:
   //    merge path, WF_ITEMS outputs per lane.  (Per-element rank searches, four
   //    interleaved binary searches per lane, measured 2-3x slower: LDS-bound.)
+  //    Shares its barrier with the layout check: a window that fails the check
+  //    discards the merge.
+  bool dec = false;
+  if (t == 0) dec = (a0 > 0 && na > 0 && prev_a > ts_r[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i) {
+    const int e = t + WF_NT * i;
+    if (e >= sz) continue;
+    if (!(P.ablate & 1) && e != 0 && e != na && sts[e - 1] > ts_r[i]) dec = true;
+  }
   {
     const int d0 = t * WF_ITEMS < sz ? t * WF_ITEMS : sz;
     const int d1 = d0 + WF_ITEMS < sz ? d0 + WF_ITEMS : sz;
@@ -308,7 +301,11 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       sord[d] = (u16)(take_a ? ia++ : na + ib++);
     }
   }
-  __syncthreads();
+  if (__syncthreads_or(dec)) {
+    if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
+    return;
+  }
+  WSTAMP(20);
   WSTAMP(3);
 
   // 3. stable multisplit of S by rank (wave ballots); element, kind and rank stay in
@@ -452,12 +449,32 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     if (r1 >= sz || ((gbits[r1 >> 6] >> (r1 & 63)) & 1ull)) return false;  // next group
     return (pkey[sl[r]] >> 11) == (pkey[sl[r1]] >> 11);
   };
+  // 6. renames: rank among the window's renames of the same branch (final order).
+  //    Computed in the tie-detection phase; redone after a (rare) tie fix.
+  const int R0 = kbase[KREN], RN = wck[KREN];
+  const int nrc = (RN + WAVE - 1) / WAVE;
+  auto rename_ranks = [&]() {
+    for (int c = wv; c < nrc; c += WF_WAVES) {
+      const int x = c * WAVE + lane;
+      const bool valid = x < RN;
+      const int e = valid ? sord[R0 + x] : 0;
+      const bool sb = valid && e >= na;
+      const u64 bm = __ballot(sb), vm = __ballot(valid);
+      const u64 lt = lanemask_lt();
+      if (valid) rown[x] = (u16)(sb ? __popcll(bm & lt) : __popcll(vm & ~bm & lt));
+      if (lane == 0) {
+        rc[c][0] = (u16)__popcll(vm & ~bm);
+        rc[c][1] = (u16)__popcll(bm);
+      }
+    }
+  };
   bool tie = false;
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {  // detection: prefixes of adjacent ranks (any group)
     const int r = t + WF_NT * j;
     if (r + 1 < sz) tie |= (pkey[sl[r]] >> 11) == (pkey[sl[r + 1]] >> 11);
   }
+  rename_ranks();
   const bool any_tie = __syncthreads_or(tie);
   WSTAMP(21);
   if (any_tie) {
@@ -483,25 +500,9 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       }
     }
     __syncthreads();
+    rename_ranks();
+    __syncthreads();
   }
-
-  // 6. renames: rank among the window's renames of the same branch (final order)
-  const int R0 = kbase[KREN], RN = wck[KREN];
-  const int nrc = (RN + WAVE - 1) / WAVE;
-  for (int c = wv; c < nrc; c += WF_WAVES) {
-    const int x = c * WAVE + lane;
-    const bool valid = x < RN;
-    const int e = valid ? sord[R0 + x] : 0;
-    const bool sb = valid && e >= na;
-    const u64 bm = __ballot(sb), vm = __ballot(valid);
-    const u64 lt = lanemask_lt();
-    if (valid) rown[x] = (u16)(sb ? __popcll(bm & lt) : __popcll(vm & ~bm & lt));
-    if (lane == 0) {
-      rc[c][0] = (u16)__popcll(vm & ~bm);
-      rc[c][1] = (u16)__popcll(bm);
-    }
-  }
-  __syncthreads();
   WSTAMP(11);
   if (wv == 0) {
     const u32 x0 = lane < nrc ? rc[lane][0] : 0u;
