@@ -6,7 +6,8 @@ Same signature, same result objects, same exceptions for malformed ops:
 
 Inputs are never mutated; outputs are fresh ``Op`` objects built with
 ``type(op)`` / ``type(op.target)`` (so reference ``Op`` instances round-trip),
-and conflicts are built from the uncloned inputs, as in the reference.  To wire
+and conflicts are built from the uncloned inputs, as in the reference.  Marshal and
+materialise run in the native host module (csrc/smx_host.cpp), the merge on the GPU.  To wire
 it into the reference CLI, rebind the module attribute the CLI looks up
 (``semmerge.__main__.compose_oplogs``).
 """
@@ -15,17 +16,17 @@ from __future__ import annotations
 from typing import Any, List, Sequence, Tuple
 
 from ._lib import compose_soa
-from .marshal import marshal
-from .materialize import materialize_conflicts, materialize_ops
+from .marshal import marshal_native
+from .materialize import materialize_conflicts, materialize_ops_native
 
 
 def compose_oplogs(delta_a: Sequence[Any], delta_b: Sequence[Any]) -> Tuple[List[Any], List[Any]]:
     """Compose two op logs into one deterministic sequence plus DivergentRename conflicts."""
     ops_a = list(delta_a)
     ops_b = list(delta_b)
-    soa = marshal(ops_a, ops_b)
+    soa = marshal_native(ops_a, ops_b)
     order, addr, file, ctx, pairs = compose_soa(soa)
     ops = ops_a + ops_b
-    out = materialize_ops(ops, soa.kind, soa.strings, order, addr, file, ctx)
+    out = materialize_ops_native(ops, soa.kind, soa.strings, order, addr, file, ctx)
     conflicts = materialize_conflicts(ops, pairs)
     return out, conflicts

@@ -88,6 +88,15 @@ def _freeze(v: Any):
     return v
 
 
+def eq_key(v: Any):
+    """Hashable key of a non-scalar newName with ``==`` semantics (``_freeze``)."""
+    try:
+        return _freeze(v)
+    except TypeError as exc:
+        raise TypeError(f"newName of type {type(v).__name__} is not comparable "
+                        "by the device composer") from exc
+
+
 class _EqClasses:
     """Interns values by Python ``==`` (the ``!=`` test of compose.py:66)."""
 
@@ -99,11 +108,7 @@ class _EqClasses:
         if isinstance(v, float) and v != v:  # NaN != NaN, even the same object
             self._next += 1
             return self._next - 1
-        try:
-            key = v if isinstance(v, (str, int, float, type(None))) else _freeze(v)
-        except TypeError as exc:
-            raise TypeError(f"newName of type {type(v).__name__} is not comparable "
-                            "by the device composer") from exc
+        key = v if isinstance(v, (str, int, float, type(None))) else eq_key(v)
         got = self._ids.get(key)
         if got is None:
             got = self._ids[key] = self._next
@@ -220,3 +225,29 @@ def marshal(delta_a: Sequence[Any], delta_b: Sequence[Any]) -> SoA:
     id_mode, hi, lo = _encode_ids(ids)
     return SoA(len(delta_a), len(delta_b), kind, ts, hi, lo, sym, v0, v1, max(len(syms), 1),
                list(strings), ts_mode, id_mode)
+
+
+def marshal_native(delta_a: Sequence[Any], delta_b: Sequence[Any]) -> SoA:
+    """``marshal`` done by the native host module (csrc/smx_host.cpp): same SoA, same
+    exceptions.  Only non-ISO timestamps and ids that are neither canonical UUIDs nor
+    short strings go back to the Python encoders above (dense ranks need a sort)."""
+    from ._host import host
+    ops = list(delta_a) + list(delta_b)
+    n = len(ops)
+    kind = np.empty(n, np.uint8)
+    ts = np.empty(n, np.uint64)
+    hi = np.empty(n, np.uint64)
+    lo = np.empty(n, np.uint64)
+    sym = np.empty(n, np.uint32)
+    v0 = np.empty(n, np.int32)
+    v1 = np.empty(n, np.int32)
+    n_sym, strings, ts_ok, id_mode, ts_str, ids = host().marshal_ops(
+        ops, KIND_RANK, KIND_UNKNOWN, KIND_MOVE, KIND_RENAME, DEFAULT_TIMESTAMP, eq_key,
+        kind, ts, hi, lo, sym, v0, v1)
+    ts_mode = TS_ISO
+    if not ts_ok:
+        ts_mode, ts = _encode_ts(ts_str)
+    if id_mode < 0:
+        id_mode, hi, lo = _encode_ids(ids)
+    return SoA(len(delta_a), len(delta_b), kind, ts, hi, lo, sym, v0, v1, max(n_sym, 1),
+               strings, ts_mode, id_mode)

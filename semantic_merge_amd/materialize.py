@@ -9,8 +9,9 @@ preserving dict key order, so ``to_dict()`` JSON is byte-identical.
 """
 from __future__ import annotations
 
+import dataclasses
 from copy import deepcopy
-from typing import Any, List, Sequence
+from typing import Any, List, Sequence, Tuple
 
 import numpy as np
 
@@ -57,6 +58,44 @@ def materialize_ops(ops: Sequence[Any], kind: np.ndarray, strings: Sequence[str]
             clone.params = {**clone.params, "renameContext": strings[c]}
         out.append(clone)
     return out
+
+
+def materialize_ops_native(ops: Sequence[Any], kind: np.ndarray, strings: Sequence[str],
+                           order: np.ndarray, addr: np.ndarray, file: np.ndarray,
+                           ctx: np.ndarray) -> List[Any]:
+    """``materialize_ops`` done by the native host module (csrc/smx_host.cpp)."""
+    from ._host import host
+
+    def i32(a):
+        return np.ascontiguousarray(a, dtype=np.int32)
+    return host().materialize_ops(list(ops), np.ascontiguousarray(kind, dtype=np.uint8),
+                                  list(strings), i32(order), i32(addr), i32(file), i32(ctx),
+                                  KIND_MOVE, KIND_RENAME, deepcopy, smx_host_ctor_mode)
+
+
+def smx_host_ctor_mode(cls: type, names: Tuple[str, ...]) -> int:
+    """How the native materialiser may build ``cls(**dict(zip(names, values)))``.
+
+    1 (2 when frozen): ``cls`` is a plain dataclass whose ``__init__`` is the one
+    ``dataclasses`` generated for exactly ``names`` (every field in __init__, no
+    ``__post_init__``, ``object.__new__``), so the constructor is ``object.__new__`` plus
+    one ``setattr`` per field in order (``object.__setattr__`` when frozen) — what that
+    generated code does.  0: anything else; the class is called.
+    """
+    if not dataclasses.is_dataclass(cls) or cls.__new__ is not object.__new__:
+        return 0
+    if hasattr(cls, "__post_init__"):
+        return 0
+    code = getattr(cls.__init__, "__code__", None)
+    if code is None or code.co_filename != "<string>" or code.co_name != "__init__":
+        return 0
+    if code.co_kwonlyargcount or code.co_argcount != len(names) + 1:
+        return 0
+    if tuple(code.co_varnames[1:code.co_argcount]) != tuple(names):
+        return 0
+    if tuple(f.name for f in dataclasses.fields(cls)) != tuple(names):
+        return 0
+    return 2 if cls.__dataclass_params__.frozen else 1
 
 
 def materialize_conflicts(ops: Sequence[Any], pairs: np.ndarray) -> List[Any]:

@@ -31,3 +31,10 @@ def test_library_exports_all_symbols():
 def test_code_object_targets_gfx950():
     data = open(LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_native_host_module_loads():
+    from semantic_merge_amd._host import host
+    h = host()
+    for name in ("marshal_ops", "materialize_ops", "deep_copy"):
+        assert callable(getattr(h, name)), name
