@@ -9,12 +9,13 @@
 //    one with the smallest (key, index)) and always inserts a new element;
 //    delete tombstones every present element of that value (crdt.py:33-43).
 //  * materialize = live elements in (key, index) order (crdt.py:45-46).
-// Pipeline: stable radix sort of events by (list, value) -> one sequential replay
-// per (list, value) group -> per list, survivors ranked by (anchor, t, author,
-// opid, index) in LDS -> compaction with per-list offsets.
+// Pipeline: stable LSD radix partition of 40-byte event records by list id (LDS-staged,
+// coalesced) -> list bounds -> one block per list, in LDS: order by (value, index), one
+// sequential replay per value group, survivors ranked by (anchor, t, author, opid,
+// index) -> survivor-count scan -> compaction.
 #include <string>
 
-#include "smx_sort.h"
+#include "smx_scan.h"
 
 #define RGA_TRY(x)                                                                     \
   do {                                                                                 \
@@ -23,178 +24,419 @@
       return smx_set_error(SMX_E_HIP, (std::string(#x) + ": " + hipGetErrorString(_e)).c_str()); \
   } while (0)
 
-#define RGA_LIST_CAP 2048  // lists up to this many events are ranked in LDS
-#define RGA_LDS_KEYS 512   // ... with their survivors' keys in LDS up to this many survivors
-
-struct RgaKey {
-  u32 anchor;
-  i64 t;
-  u32 author;
-  u64 hi, lo;
-};
-
-__device__ __forceinline__ RgaKey rga_key(const smx_rga_ops& o, u32 i) {
-  return RgaKey{o.anchor[i], o.t[i], o.author[i], o.opid_hi[i], o.opid_lo[i]};
-}
-
-// (key, index) order: crdt.py:48-57 tuple compare, creation index breaks ties
-__device__ __forceinline__ bool rga_lt(const RgaKey& a, u32 ia, const RgaKey& b, u32 ib) {
-  if (a.anchor != b.anchor) return a.anchor < b.anchor;
-  if (a.t != b.t) return a.t < b.t;
-  if (a.author != b.author) return a.author < b.author;
-  if (a.hi != b.hi) return a.hi < b.hi;
-  if (a.lo != b.lo) return a.lo < b.lo;
-  return ia < ib;
-}
-
-// Sort records: key = (list, value), value word = event index | op << 30 (the op
-// travels through the sort, so the group replay reads no per-event array).
+// Event record, 5 u64 words, grouped by list by the partition below:
+//   w0 = anchor << 32 | t' >> 32,  w1 = t' << 32 | author   (t' = t with the sign bit flipped)
+//   w2 = opid_hi, w3 = opid_lo                              -> (w0..w3) is the crdt.py:48-57 key order
+//   w4 = value << 32 | op << 30 | event index              (index = creation order, the tie-break)
+#define RGA_REC 5
+#ifndef RGA_ABL
+#define RGA_ABL 0  // timing ablations of k_rga_list (tools/build_variants.sh): 1 no (value, index)
+                   // rank, 2 no replay, 3 no survivor rank, 4 load only — results are wrong
+#endif
 #define RGA_IDX_MASK 0x3fffffffu
-__global__ void k_rga_init(smx_rga_ops o, u64* __restrict__ keys, u32* __restrict__ vals, i32* __restrict__ err) {
-  for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < o.n_ops; i += (i64)gridDim.x * BLOCK) {
-    const u32 l = o.list[i];
-    const u32 op = o.op[i];
-    if (l >= (u64)o.n_lists || op > 2) *err = 1;
-    keys[i] = ((u64)(l < (u64)o.n_lists ? l : 0) << 32) | o.value[i];
-    vals[i] = (u32)i | ((op > 2 ? 0u : op) << 30);
+#define RGA_SMALL 256   // lists up to this many events: k_rga_list<RGA_SMALL, 256>, one block per list
+#define RGA_MID 1536    // ... up to this: k_rga_list<RGA_MID, 512> over the deferred lists; longer: k_rga_big
+
+// Grouping the events by list: a stable LSD radix partition of whole records on the
+// list id, 8 bits per pass (one pass up to 256 lists, two up to 65536, ...).  The first
+// pass reads the input columns and packs the records; each pass stages a tile in LDS
+// in digit order and writes each digit's run of records contiguously, so every byte
+// moves in full cache lines.  Stable: each list's events stay in stream order.
+#define RREC_ITEMS 4
+#define RREC_TILE (BLOCK * RREC_ITEMS)  // 1024 records per block and pass
+#define RREC_SEG (RREC_TILE / NWAVES)   // contiguous records per wave
+
+__device__ __forceinline__ u32 rga_list_of(const smx_rga_ops& o, i64 i, i32* err) {
+  const u32 l = o.list[i];
+  if (l >= (u64)o.n_lists || o.op[i] > 2) {
+    *err = 1;
+    return 0;
   }
+  return l;
 }
 
-// One thread per (list, value) group (a contiguous range of the sorted events, in
-// stream order): replay and mark the fate of every element the group creates.
-// state is indexed by sorted position: bit0 present, bit1 tombstoned.
-__global__ void k_rga_groups(smx_rga_ops o, const u64* __restrict__ keys, const u32* __restrict__ vals,
-                             u8* __restrict__ state) {
-  const i64 n = o.n_ops;
-  for (i64 j = (i64)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (i64)gridDim.x * BLOCK) {
-    if (j != 0 && keys[j - 1] == keys[j]) continue;
-    i64 end = j + 1;
-    while (end < n && keys[end] == keys[j]) ++end;
-    for (i64 x = j; x < end; ++x) {
-      const u32 op = vals[x] >> 30;
-      if (op == 2) {  // delete: tombstone every present element of the value
-        for (i64 y = j; y < x; ++y)
-          if (state[y] & 1) state[y] |= 2;
-        state[x] = 0;
-        continue;
-      }
-      if (op == 1) {  // move: pop the live element with the smallest (key, index)
-        i64 best = -1;
-        RgaKey bk{};
-        u32 bi = 0;
-        for (i64 y = j; y < x; ++y) {
-          if (state[y] != 1) continue;
-          const u32 e = vals[y] & RGA_IDX_MASK;
-          const RgaKey ke = rga_key(o, e);
-          if (best < 0 || rga_lt(ke, e, bk, bi)) {
-            best = y;
-            bk = ke;
-            bi = e;
-          }
-        }
-        if (best >= 0) state[best] = 0;
-      }
-      state[x] = 1;  // insert / move creates a live element
+template <bool FIRST>
+__global__ void __launch_bounds__(BLOCK) k_rrec_hist(smx_rga_ops o, const u32* __restrict__ keys, int shift,
+                                                     u32* __restrict__ hist, i32* __restrict__ err) {
+  __shared__ u32 h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const i64 base = (i64)blockIdx.x * RREC_TILE;
+#pragma unroll
+  for (int it = 0; it < RREC_ITEMS; ++it) {
+    const i64 i = base + it * BLOCK + threadIdx.x;
+    if (i < o.n_ops) atomicAdd(&h[((FIRST ? rga_list_of(o, i, err) : keys[i]) >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  hist[(i64)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+template <bool FIRST>
+__global__ void __launch_bounds__(BLOCK) k_rrec_scatter(smx_rga_ops o, const u32* __restrict__ kin,
+                                                        const u64* __restrict__ rin, u32* __restrict__ kout,
+                                                        u64* __restrict__ rout, int shift,
+                                                        const u32* __restrict__ offs) {
+  __shared__ u64 srec[RREC_TILE * RGA_REC];  // 40 KB
+  __shared__ u32 skey[RREC_TILE];
+  __shared__ u32 wc[NWAVES][256];  // per-wave digit counts, then offsets
+  __shared__ u32 lstart[256];
+  __shared__ u32 gofs[256];
+  const int t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
+  const i64 n = o.n_ops, base = (i64)blockIdx.x * RREC_TILE;
+  i32 dummy = 0;
+#pragma unroll
+  for (int q = 0; q < NWAVES; ++q) wc[q][t] = 0;
+  gofs[t] = offs[(i64)blockIdx.x * 256 + t];
+  __syncthreads();
+  const u64 lt = lanemask_lt();
+  u32 key[RREC_ITEMS], dr[RREC_ITEMS];
+#pragma unroll
+  for (int it = 0; it < RREC_ITEMS; ++it) {
+    const i64 i = base + (i64)w * RREC_SEG + it * WAVE + lane;
+    const bool valid = i < n;
+    key[it] = valid ? (FIRST ? rga_list_of(o, i, &dummy) : kin[i]) : 0u;
+    const u32 d = (key[it] >> shift) & 255u;
+    const u64 peers = wave_peers<8>(d, valid);
+    const u32 before = wc[w][d];
+    dr[it] = d | ((before + (u32)__popcll(peers & lt)) << 8);
+    if (valid && (peers >> lane) == 1ull) wc[w][d] = before + (u32)__popcll(peers);
+  }
+  __syncthreads();
+  {
+    u32 tot = 0;
+#pragma unroll
+    for (int q = 0; q < NWAVES; ++q) tot += wc[q][t];
+    lstart[t] = tot;
+  }
+  __syncthreads();
+  if (t < WAVE) {  // exclusive scan of the 256 digit totals, 4 per lane
+    u32 x[4], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[j] = lstart[4 * t + j];
+      sum += x[j];
+    }
+    u32 run = wave_incl_sum(sum) - sum;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lstart[4 * t + j] = run;
+      run += x[j];
     }
   }
+  __syncthreads();
+  {
+    u32 acc = lstart[t];
+#pragma unroll
+    for (int q = 0; q < NWAVES; ++q) {
+      const u32 c = wc[q][t];
+      wc[q][t] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < RREC_ITEMS; ++it) {
+    const i64 i = base + (i64)w * RREC_SEG + it * WAVE + lane;
+    if (i >= n) continue;
+    const u32 d = dr[it] & 255u, p = wc[w][d] + (dr[it] >> 8);
+    skey[p] = key[it];
+    u64* r = &srec[p * RGA_REC];
+    if (FIRST) {
+      const u64 tt = (u64)o.t[i] ^ 0x8000000000000000ull;
+      r[0] = ((u64)o.anchor[i] << 32) | (tt >> 32);
+      r[1] = (tt << 32) | o.author[i];
+      r[2] = o.opid_hi[i];
+      r[3] = o.opid_lo[i];
+      const u32 op = o.op[i] > 2 ? 0u : o.op[i];
+      r[4] = ((u64)o.value[i] << 32) | (op << 30) | (u32)i;
+    } else {
+      const u64* q = rin + (u64)i * RGA_REC;
+#pragma unroll
+      for (int k = 0; k < RGA_REC; ++k) r[k] = q[k];
+    }
+  }
+  __syncthreads();
+  const u32 cnt = (u32)(n - base < RREC_TILE ? n - base : RREC_TILE);
+  for (u32 p = t; p < cnt; p += BLOCK) {
+    const u32 d = (skey[p] >> shift) & 255u;
+    kout[gofs[d] + p - lstart[d]] = skey[p];
+  }
+  for (u32 x = t; x < cnt * RGA_REC; x += BLOCK) {  // word-wise: consecutive lanes, consecutive words
+    const u32 p = x / RGA_REC, k = x - p * RGA_REC;
+    const u32 d = (skey[p] >> shift) & 255u;
+    rout[(u64)(gofs[d] + p - lstart[d]) * RGA_REC + k] = srec[x];
+  }
 }
 
-// lstart[l] = first sorted position of list l (a list without events starts where
-// the next one does); lstart[n_lists] = n.  One pass over the sorted keys.
-__global__ void k_rga_bounds(const u64* __restrict__ keys, i64 n, i64 nl, u32* __restrict__ lstart) {
+// lstart[l] = first sorted position of list l (an empty list starts where the next
+// one does); one pass over the sorted list ids.
+__global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* __restrict__ lstart) {
   for (i64 j = (i64)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (i64)gridDim.x * BLOCK) {
-    const i64 l = (i64)(keys[j] >> 32);
-    const i64 lp = j ? (i64)(keys[j - 1] >> 32) : -1;
+    const i64 l = keys[j];
+    const i64 lp = j ? (i64)keys[j - 1] : -1;
     for (i64 L = lp + 1; L <= l; ++L) lstart[L] = (u32)j;
     if (j == n - 1)
-      for (i64 L = l + 1; L <= nl; ++L) lstart[L] = (u32)n;
+      for (i64 L = l + 1; L < nl; ++L) lstart[L] = (u32)n;
   }
 }
 
-// One block per list: rank the list's surviving elements by (key, index) and
-// write them, in order, at the start of the list's event range of `tmp`.
-__global__ void __launch_bounds__(BLOCK) k_rga_list(smx_rga_ops o, const u32* __restrict__ vals,
-                                                    const u8* __restrict__ state, const u32* __restrict__ lstart,
-                                                    u32* __restrict__ tmp, u32* __restrict__ scnt) {
-  __shared__ u32 sidx[RGA_LIST_CAP];
-  __shared__ u64 skey[RGA_LDS_KEYS][4];
+__device__ __forceinline__ u32 rga_lend(const u32* lstart, u32 l, i64 nl, i64 n) {
+  return l + 1 < nl ? lstart[l + 1] : (u32)n;
+}
+
+// a before b in (key, creation index) order; records as above
+__device__ __forceinline__ bool rec_lt(const u64* a, const u64* b) {
+  if (a[0] != b[0]) return a[0] < b[0];
+  if (a[1] != b[1]) return a[1] < b[1];
+  if (a[2] != b[2]) return a[2] < b[2];
+  if (a[3] != b[3]) return a[3] < b[3];
+  return (u32)a[4] < (u32)b[4];  // index bits (the op bits above them are fixed per index)
+}
+
+// Lists of at most CAP events, one block each, everything in LDS:
+//  1. load the list's records (contiguous);
+//  2. order the events by (value, index): each is ranked by counting (keys are unique);
+//  3. one thread per value group replays the group in stream order (crdt.py:29-43):
+//     insert creates a live element, move pops the live element with the smallest
+//     (key, index) and creates one, delete tombstones every present element;
+//  4. compact the survivors' keys (wave-aggregated) into contiguous LDS columns;
+//  5. rank them by (key, index) (crdt.py:45-57) — word 0 decides almost every pair, the
+//     rest is read only on a tie — and write (value, index) in list order at the
+//     list's range start; scnt[l] = survivors.
+// Grid: list l = blockIdx.x when `todo` is null, else a loop over todo[0..*ntodo).
+// Longer lists are appended to defer[] for the next kernel.
+template <int CAP, int NT>
+__global__ void __launch_bounds__(NT) k_rga_list(const u64* __restrict__ R, const u32* __restrict__ lstart, i64 n,
+                                                 i64 nl, const u32* __restrict__ todo, const u32* __restrict__ ntodo,
+                                                 u32* __restrict__ defer, u32* __restrict__ ndefer,
+                                                 u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
+                                                 u32* __restrict__ scnt) {
+  __shared__ u64 rec[CAP * RGA_REC];
+  __shared__ u64 gk[CAP];       // value << 30 | index (phase 2-3), then survivors' word 0
+  __shared__ u64 sk[4][CAP];    // survivors' words 1..3 and 4
+  __shared__ u16 perm[CAP];     // (value, index) order -> record
+  __shared__ u8 st[CAP];        // by (value, index) position: bit0 present, bit1 tombstoned
   __shared__ u32 ns;
-  const u32 l = blockIdx.x;
-  const u32 s0 = lstart[l], cnt = lstart[l + 1] - s0;
-  if (threadIdx.x == 0) ns = 0;
-  __syncthreads();
-  if (cnt <= RGA_LIST_CAP) {
-    for (u32 x = threadIdx.x; x < cnt; x += BLOCK)
-      if (state[s0 + x] == 1) sidx[atomicAdd(&ns, 1u)] = vals[s0 + x] & RGA_IDX_MASK;
+  const u32 t = threadIdx.x, lane = t & (WAVE - 1);
+  const u64 lanes_lt = lanemask_lt();
+  const u32 nwork = todo ? *ntodo : (u32)gridDim.x;
+  for (u32 item = todo ? blockIdx.x : blockIdx.x; item < nwork; item += todo ? gridDim.x : nwork) {
+    const u32 l = todo ? todo[item] : item;
+    const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
+    if (cnt > (u32)CAP) {
+      if (t == 0) defer[atomicAdd(ndefer, 1u)] = l;
+      continue;
+    }
+    __syncthreads();  // the previous list's LDS reads are done
+    if (t == 0) ns = 0;
+    for (u32 w = t; w < cnt * RGA_REC; w += NT) rec[w] = R[(u64)s0 * RGA_REC + w];
+    __syncthreads();
+#if RGA_ABL == 4
+    if (t == 0) scnt[l] = 0;  // keeps k_rga_out in bounds
+    continue;
+#endif
+    for (u32 i = t; i < cnt; i += NT) {
+      const u64 w4 = rec[i * RGA_REC + 4];
+      gk[i] = ((w4 >> 32) << 30) | (w4 & RGA_IDX_MASK);
+      st[i] = 0;
+    }
+    __syncthreads();
+    for (u32 i = t; i < cnt; i += NT) {
+      const u64 k = gk[i];
+      u32 r = 0, j = 0;
+#if RGA_ABL == 1
+      r = i;
+#else
+      for (; j + 4 <= cnt; j += 4) r += (gk[j] < k) + (gk[j + 1] < k) + (gk[j + 2] < k) + (gk[j + 3] < k);
+      for (; j < cnt; ++j) r += gk[j] < k;
+#endif
+      perm[r] = (u16)i;
+    }
+    __syncthreads();
+#if RGA_ABL == 2
+    for (u32 j = t; j < cnt; j += NT) st[j] = j % 3 ? 1 : 0;
+    if (0)
+#endif
+    for (u32 j = t; j < cnt; j += NT) {
+      const u64 v = gk[perm[j]] >> 30;
+      if (j != 0 && (gk[perm[j - 1]] >> 30) == v) continue;
+      u32 end = j + 1;
+      while (end < cnt && (gk[perm[end]] >> 30) == v) ++end;
+      for (u32 x = j; x < end; ++x) {
+        const u32 op = (u32)(rec[perm[x] * RGA_REC + 4] >> 30) & 3u;
+        if (op == 2) {
+          for (u32 y = j; y < x; ++y)
+            if (st[y] & 1) st[y] |= 2;
+          continue;  // a delete creates nothing
+        }
+        if (op == 1) {
+          int best = -1;
+          for (u32 y = j; y < x; ++y)
+            if (st[y] == 1 && (best < 0 || rec_lt(&rec[perm[y] * RGA_REC], &rec[perm[best] * RGA_REC])))
+              best = (int)y;
+          if (best >= 0) st[best] = 0;
+        }
+        st[x] = 1;
+      }
+    }
+    __syncthreads();
+    for (u32 j0 = 0; j0 < cnt; j0 += NT) {
+      const u32 j = j0 + t;
+      const bool live = j < cnt && st[j] == 1;
+      const u64 ball = __ballot(live);
+      u32 got = 0;
+      if (lane == 0 && ball) got = atomicAdd(&ns, (u32)__popcll(ball));
+      const u32 base = __shfl(got, 0);
+      if (live) {
+        const u32 a = base + (u32)__popcll(ball & lanes_lt), p = perm[j];
+        gk[a] = rec[p * RGA_REC];  // (value, index) keys are dead from here on
+        sk[0][a] = rec[p * RGA_REC + 1];
+        sk[1][a] = rec[p * RGA_REC + 2];
+        sk[2][a] = rec[p * RGA_REC + 3];
+        sk[3][a] = rec[p * RGA_REC + 4];
+      }
+    }
     __syncthreads();
     const u32 m = ns;
-    if (m <= RGA_LDS_KEYS) {
-      // survivors' keys packed once into LDS as four order-preserving words
-      // (anchor | t_hi, t_lo | author, opid_hi, opid_lo); every lane then ranks
-      // its elements against all of them (same b on all lanes: LDS broadcast)
-      for (u32 a = threadIdx.x; a < m; a += BLOCK) {
-        const u32 i = sidx[a];
-        const u64 tt = (u64)o.t[i] ^ 0x8000000000000000ull;  // signed -> unsigned order
-        skey[a][0] = ((u64)o.anchor[i] << 32) | (tt >> 32);
-        skey[a][1] = (tt << 32) | o.author[i];
-        skey[a][2] = o.opid_hi[i];
-        skey[a][3] = o.opid_lo[i];
-      }
-      __syncthreads();
-      for (u32 a = threadIdx.x; a < m; a += BLOCK) {
-        const u64 k0 = skey[a][0], k1 = skey[a][1], k2 = skey[a][2], k3 = skey[a][3];
-        const u32 ia = sidx[a];
-        u32 r = 0;
-        for (u32 b = 0; b < m; ++b) {
-          const u64 b0 = skey[b][0], b1 = skey[b][1], b2 = skey[b][2], b3 = skey[b][3];
-          const bool lt = b0 != k0 ? b0 < k0
-                        : b1 != k1 ? b1 < k1
-                        : b2 != k2 ? b2 < k2
-                        : b3 != k3 ? b3 < k3 : sidx[b] < ia;
-          r += lt;
-        }
-        tmp[s0 + r] = ia;
-      }
-    } else {
-      for (u32 a = threadIdx.x; a < m; a += BLOCK) {
-        const u32 ia = sidx[a];
-        const RgaKey ka = rga_key(o, ia);
-        u32 r = 0;
-        for (u32 b = 0; b < m; ++b) {
-          const u32 ib = sidx[b];
-          r += rga_lt(rga_key(o, ib), ib, ka, ia);
-        }
-        tmp[s0 + r] = ia;
-      }
-    }
-    if (threadIdx.x == 0) scnt[l] = m;
-  } else {
-    // large list: rank straight from global memory (quadratic; correct for any size)
-    u32 m = 0;
-    for (u32 x = 0; x < cnt; ++x) m += state[s0 + x] == 1;
-    for (u32 a = threadIdx.x; a < cnt; a += BLOCK) {
-      const u32 ia = vals[s0 + a] & RGA_IDX_MASK;
-      if (state[s0 + a] != 1) continue;
-      const RgaKey ka = rga_key(o, ia);
+    for (u32 a = t; a < m; a += NT) {
+      const u64 k0 = gk[a];
       u32 r = 0;
-      for (u32 b = 0; b < cnt; ++b) {
-        const u32 ib = vals[s0 + b] & RGA_IDX_MASK;
-        if (state[s0 + b] == 1) r += rga_lt(rga_key(o, ib), ib, ka, ia);
+#if RGA_ABL == 3
+      r = a;
+#else
+      u32 eq = 0, b = 0;  // same b on every lane: LDS broadcast; word 0 only
+      for (; b + 4 <= m; b += 4) {
+        const u64 x0 = gk[b], x1 = gk[b + 1], x2 = gk[b + 2], x3 = gk[b + 3];
+        r += (x0 < k0) + (x1 < k0) + (x2 < k0) + (x3 < k0);
+        eq += (x0 == k0) + (x1 == k0) + (x2 == k0) + (x3 == k0);
       }
-      tmp[s0 + r] = ia;
+      for (; b < m; ++b) {
+        r += gk[b] < k0;
+        eq += gk[b] == k0;
+      }
+      if (eq > 1) {  // another survivor ties on word 0 (rare): the rest of the key, then the index
+        const u64 a1 = sk[0][a], a2 = sk[1][a], a3 = sk[2][a];
+        const u32 ia = (u32)sk[3][a] & RGA_IDX_MASK;
+        for (u32 c = 0; c < m; ++c) {
+          if (gk[c] != k0 || c == a) continue;
+          const u64 b1 = sk[0][c], b2 = sk[1][c], b3 = sk[2][c];
+          const u32 ib = (u32)sk[3][c] & RGA_IDX_MASK;
+          r += b1 != a1 ? b1 < a1 : b2 != a2 ? b2 < a2 : b3 != a3 ? b3 < a3 : ib < ia;
+        }
+      }
+#endif
+      const u64 w4 = sk[3][a];
+      tmp_v[s0 + r] = (u32)(w4 >> 32);
+      tmp_s[s0 + r] = (u32)w4 & RGA_IDX_MASK;
     }
-    if (threadIdx.x == 0) scnt[l] = m;
+    if (t == 0) scnt[l] = m;
   }
 }
 
-__global__ void k_rga_out(smx_rga_ops o, const u32* __restrict__ tmp, const u32* __restrict__ lstart,
-                          const u32* __restrict__ scnt, const u32* __restrict__ soff, smx_rga_out out) {
+// Block-wide sort of the record positions p[0..cnt) by `less`, in global memory:
+// the bitonic network in its all-ascending form (first stage of each merge compares
+// i with its mirror i ^ (k - 1)), so positions past cnt act as +infinity and are
+// never touched.
+template <typename Less>
+__device__ void block_sort_positions(u32* p, u32 cnt, Less less) {
+  u32 P = 1;
+  while (P < cnt) P <<= 1;
+  for (u32 k = 2; k <= P; k <<= 1) {
+    for (u32 j = k >> 1; j > 0; j >>= 1) {
+      const u32 mask = j == (k >> 1) ? k - 1 : j;
+      for (u32 i = threadIdx.x; i < P; i += blockDim.x) {
+        const u32 q = i ^ mask;
+        if (q > i && q < cnt && less(p[q], p[i])) {
+          const u32 x = p[i];
+          p[i] = p[q];
+          p[q] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Lists longer than RGA_MID: the same replay from global memory, one block per list
+// (such lists are rare — a whole file's history in one list).  Per list, in its
+// record range: gp = positions sorted by (value, index), bst = state by that order;
+// then the survivors' positions sorted by (key, index).
+__device__ void rga_big_list(const u64* __restrict__ R, u32 l, const u32* __restrict__ lstart, i64 n, i64 nl,
+                             u8* __restrict__ bst, u32* __restrict__ gp, u32* __restrict__ tmp_v,
+                             u32* __restrict__ tmp_s, u32* __restrict__ scnt) {
+  __shared__ u32 ns;
+  const u32 t = threadIdx.x, NT = blockDim.x;
+  const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
+  const u64* L = R + (u64)s0 * RGA_REC;
+  u8* S = bst + s0;
+  u32* G = gp + s0;
+  auto gkey = [&](u32 x) { const u64 w = L[x * RGA_REC + 4]; return ((w >> 32) << 30) | (w & RGA_IDX_MASK); };
+  for (u32 x = t; x < cnt; x += NT) {
+    G[x] = x;
+    S[x] = 0;
+  }
+  __syncthreads();
+  block_sort_positions(G, cnt, [&](u32 a, u32 b) { return gkey(a) < gkey(b); });
+  for (u32 j = t; j < cnt; j += NT) {
+    const u64 v = gkey(G[j]) >> 30;
+    if (j != 0 && (gkey(G[j - 1]) >> 30) == v) continue;
+    u32 end = j + 1;
+    while (end < cnt && (gkey(G[end]) >> 30) == v) ++end;
+    for (u32 x = j; x < end; ++x) {
+      const u32 op = (u32)(L[G[x] * RGA_REC + 4] >> 30) & 3u;
+      if (op == 2) {
+        for (u32 y = j; y < x; ++y)
+          if (S[y] & 1) S[y] |= 2;
+        continue;
+      }
+      if (op == 1) {
+        int best = -1;
+        for (u32 y = j; y < x; ++y)
+          if (S[y] == 1 && (best < 0 || rec_lt(&L[G[y] * RGA_REC], &L[G[best] * RGA_REC]))) best = (int)y;
+        if (best >= 0) S[best] = 0;
+      }
+      S[x] = 1;
+    }
+  }
+  __syncthreads();
+  // survivors' positions to the front of G (their order is fixed by the sort below)
+  if (t == 0) {
+    u32 w = 0;
+    for (u32 j = 0; j < cnt; ++j)
+      if (S[j] == 1) G[w++] = G[j];
+    ns = w;
+  }
+  __syncthreads();
+  const u32 m = ns;
+  block_sort_positions(G, m, [&](u32 a, u32 b) { return rec_lt(&L[a * RGA_REC], &L[b * RGA_REC]); });
+  for (u32 j = t; j < m; j += NT) {
+    const u64 w4 = L[G[j] * RGA_REC + 4];
+    tmp_v[s0 + j] = (u32)(w4 >> 32);
+    tmp_s[s0 + j] = (u32)w4 & RGA_IDX_MASK;
+  }
+  if (t == 0) scnt[l] = m;
+}
+
+__global__ void __launch_bounds__(1024) k_rga_big(const u64* __restrict__ R, const u32* __restrict__ lstart, i64 n,
+                                                  i64 nl, const u32* __restrict__ todo, const u32* __restrict__ ntodo,
+                                                  u8* __restrict__ bst, u32* __restrict__ gp,
+                                                  u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
+                                                  u32* __restrict__ scnt) {
+  for (u32 item = blockIdx.x; item < *ntodo; item += gridDim.x) {
+    __syncthreads();
+    rga_big_list(R, todo[item], lstart, n, nl, bst, gp, tmp_v, tmp_s, scnt);
+  }
+}
+
+// Per list: its survivors, in list order, to their place in the output.
+__global__ void k_rga_out(const u32* __restrict__ tmp_v, const u32* __restrict__ tmp_s,
+                          const u32* __restrict__ lstart, const u32* __restrict__ scnt, const u32* __restrict__ soff,
+                          smx_rga_out out) {
   const u32 l = blockIdx.x;
   const u32 s0 = lstart[l], m = scnt[l], d = soff[l];
   for (u32 x = threadIdx.x; x < m; x += BLOCK) {
-    const u32 i = tmp[s0 + x];
-    out.out_value[d + x] = o.value[i];
-    out.out_src[d + x] = (i32)i;
+    out.out_value[d + x] = tmp_v[s0 + x];
+    out.out_src[d + x] = (i32)tmp_s[s0 + x];
   }
   if (threadIdx.x == 0) out.out_offsets[l] = d;
 }
@@ -209,22 +451,24 @@ static bool o_ok(const smx_rga_ops* o) {
 }
 
 struct RgaLayout {
-  size_t off[12];
+  size_t off[16];
   size_t total;
 };
 
-enum { R_KEYS, R_VALS, R_K2, R_V2, R_HIST, R_PART, R_STATE, R_LCNT, R_LSTART, R_SCNT, R_TMP, R_N };
+enum { R_REC, R_REC2, R_KEYS, R_KEYS2, R_RHIST, R_TV, R_TS, R_BST, R_GP, R_DEF1, R_DEF2, R_PART, R_LSTART, R_SCNT, R_SOFF, R_N };
 
 static RgaLayout rga_layout(i64 n, i64 nl) {
   const i64 nn = n > 0 ? n : 1;
-  const i64 nblk = SMX_CEIL_DIV(nn, (i64)RADIX_TILE);
   size_t sz[R_N];
-  sz[R_KEYS] = sz[R_K2] = (size_t)nn * 8;
-  sz[R_VALS] = sz[R_V2] = sz[R_TMP] = (size_t)nn * 4;
-  sz[R_HIST] = radix_hist_bytes(nn);
+  sz[R_REC] = sz[R_REC2] = (size_t)nn * RGA_REC * 8;
+  sz[R_KEYS] = sz[R_KEYS2] = sz[R_TV] = sz[R_TS] = sz[R_GP] = (size_t)nn * 4;
+  {
+    const i64 nblk = SMX_CEIL_DIV(nn, (i64)RREC_TILE);
+    sz[R_RHIST] = (size_t)256 * nblk * 4 + hscan_tsum_bytes(nblk, 256) + 260 * 4;
+  }
+  sz[R_BST] = (size_t)nn;
   sz[R_PART] = SCAN_NB * 8 + 64;  // + error word + totals
-  sz[R_STATE] = (size_t)nn;
-  sz[R_LCNT] = sz[R_LSTART] = sz[R_SCNT] = (size_t)(nl + 1) * 4 * 2;
+  sz[R_LSTART] = sz[R_SCNT] = sz[R_SOFF] = sz[R_DEF1] = sz[R_DEF2] = (size_t)(nl + 1) * 4;
   RgaLayout L;
   size_t acc = 0;
   for (int i = 0; i < R_N; ++i) {
@@ -257,36 +501,60 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   if (!ws || wsb < L.total)
     return smx_set_error(SMX_E_WORKSPACE, ("workspace too small: need " + std::to_string(L.total)).c_str());
   char* b = (char*)ws;
-  u64* keys = (u64*)(b + L.off[R_KEYS]);
-  u32* vals = (u32*)(b + L.off[R_VALS]);
+  u64* rec = (u64*)(b + L.off[R_REC]);
+  u64* rec2 = (u64*)(b + L.off[R_REC2]);
+  u32* keys = (u32*)(b + L.off[R_KEYS]);
+  u32* keys2 = (u32*)(b + L.off[R_KEYS2]);
+  u32* rhist = (u32*)(b + L.off[R_RHIST]);
+  u32* tmp_v = (u32*)(b + L.off[R_TV]);
+  u32* tmp_s = (u32*)(b + L.off[R_TS]);
+  u8* bst = (u8*)(b + L.off[R_BST]);
+  u32* gp = (u32*)(b + L.off[R_GP]);
   u32* part = (u32*)(b + L.off[R_PART]);
   i32* err = (i32*)(b + L.off[R_PART] + SCAN_NB * 8);
   u32* totals = (u32*)(err + 2);
-  u8* state = (u8*)(b + L.off[R_STATE]);
-  u32* lcnt = (u32*)(b + L.off[R_LCNT]);
   u32* lstart = (u32*)(b + L.off[R_LSTART]);
   u32* scnt = (u32*)(b + L.off[R_SCNT]);
-  u32* soff = scnt + (nl + 1);
-  u32* tmp = (u32*)(b + L.off[R_TMP]);
+  u32* soff = (u32*)(b + L.off[R_SOFF]);
+  u32* def1 = (u32*)(b + L.off[R_DEF1]);
+  u32* def2 = (u32*)(b + L.off[R_DEF2]);
+  u32* ndef = (u32*)(err + 4);  // two deferred-list counters
   const smx_rga_ops o = *ops;
-  const int grid = (int)(SMX_CEIL_DIV(n, (i64)BLOCK) < 4096 ? SMX_CEIL_DIV(n, (i64)BLOCK) : 4096);
+  const int grid = (int)(SMX_CEIL_DIV(n, (i64)BLOCK) < 8192 ? SMX_CEIL_DIV(n, (i64)BLOCK) : 8192);
 
-  RGA_TRY(hipMemsetAsync(err, 0, 8, st));
-  RGA_TRY(hipMemsetAsync(state, 0, (size_t)n, st));
-  hipLaunchKernelGGL(k_rga_init, dim3(grid), dim3(BLOCK), 0, st, o, keys, vals, err);
-  // stable LSD radix on (list, value): value bytes then list bytes
-  int shifts[8], ns = 0;
-  for (int d = 0; d < 4; ++d)
-    if (((u64)(n - 1) >> (8 * d)) != 0 || d == 0) shifts[ns++] = 8 * d;  // values are < n_ops
-  for (int d = 0; d < 4; ++d)
-    if (((u64)(nl - 1) >> (8 * d)) != 0) shifts[ns++] = 32 + 8 * d;
-  RadixTemp rt{(u64*)(b + L.off[R_K2]), (u32*)(b + L.off[R_V2]), (u32*)(b + L.off[R_HIST]), part};
-  RGA_TRY(radix_sort_pairs(keys, vals, n, shifts, ns, rt, st));
-  hipLaunchKernelGGL(k_rga_groups, dim3(grid), dim3(BLOCK), 0, st, o, keys, vals, state);
-  hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, keys, n, nl, lstart);
-  hipLaunchKernelGGL(k_rga_list, dim3(nl), dim3(BLOCK), 0, st, o, vals, state, lstart, tmp, scnt);
+  RGA_TRY(hipMemsetAsync(err, 0, 32, st));
+  {  // records grouped by list: LSD passes over the list id, ping-pong into rec
+    int npass = 1;
+    while (npass < 4 && ((u64)(nl - 1) >> (8 * npass)) != 0) ++npass;
+    const int nblk = (int)SMX_CEIL_DIV(n, (i64)RREC_TILE);
+    u32* tsum = rhist + (size_t)256 * nblk;
+    u32* dstart = tsum + hscan_tsum_bytes(nblk, 256) / 4;
+    u64* rbuf[2] = {npass % 2 ? rec : rec2, npass % 2 ? rec2 : rec};
+    u32* kbuf[2] = {keys, keys2};
+    for (int p = 0; p < npass; ++p) {
+      if (p == 0)
+        hipLaunchKernelGGL(k_rrec_hist<true>, dim3(nblk), dim3(BLOCK), 0, st, o, nullptr, 0, rhist, err);
+      else
+        hipLaunchKernelGGL(k_rrec_hist<false>, dim3(nblk), dim3(BLOCK), 0, st, o, kbuf[(p - 1) & 1], 8 * p, rhist,
+                           err);
+      hscan(rhist, nblk, 256u, tsum, dstart, st);
+      if (p == 0)
+        hipLaunchKernelGGL(k_rrec_scatter<true>, dim3(nblk), dim3(BLOCK), 0, st, o, nullptr, nullptr, kbuf[0],
+                           rbuf[0], 0, rhist);
+      else
+        hipLaunchKernelGGL(k_rrec_scatter<false>, dim3(nblk), dim3(BLOCK), 0, st, o, kbuf[(p - 1) & 1],
+                           rbuf[(p - 1) & 1], kbuf[p & 1], rbuf[p & 1], 8 * p, rhist);
+    }
+    hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, kbuf[(npass - 1) & 1], n, nl, lstart);
+  }
+  hipLaunchKernelGGL((k_rga_list<RGA_SMALL, 256>), dim3(nl), dim3(256), 0, st, rec, lstart, n, nl, nullptr, nullptr,
+                     def1, ndef, tmp_v, tmp_s, scnt);
+  hipLaunchKernelGGL((k_rga_list<RGA_MID, 512>), dim3(512), dim3(512), 0, st, rec, lstart, n, nl, def1, ndef, def2,
+                     ndef + 1, tmp_v, tmp_s, scnt);
+  hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
+                     tmp_s, scnt);
   RGA_TRY((scan_excl<OpSum, u32, u32>(scnt, soff, nl, nullptr, part, totals, st)));
-  hipLaunchKernelGGL(k_rga_out, dim3(nl), dim3(BLOCK), 0, st, o, tmp, lstart, scnt, soff, *out);
+  hipLaunchKernelGGL(k_rga_out, dim3(nl), dim3(BLOCK), 0, st, tmp_v, tmp_s, lstart, scnt, soff, *out);
   hipLaunchKernelGGL(k_rga_fin, dim3(1), dim3(1), 0, st, totals, nl, *out);
   RGA_TRY(hipGetLastError());
   i32 herr = 0;
@@ -301,4 +569,3 @@ extern "C" int smx_rga_replay(const smx_rga_ops* ops, const smx_rga_out* out, vo
   if (!ops) return SMX_E_ARG;
   return rga_impl(ops, out, ws, wsb, (hipStream_t)stream);
 }
-

@@ -48,3 +48,25 @@ def test_rga_batch_equals_oracle(n_ops, n_lists, seed):
 def test_rga_dense_values_and_big_lists():
     # few values per list (long per-value chains) and lists beyond the LDS capacity
     _check(synth.rga_batch(60_000, 8, 16, values_per_list=3, anchors_per_list=2, authors=1))
+
+
+def test_rga_mixed_list_sizes():
+    # empty lists, ~100-event lists (LDS kernel), ~2000-event lists on both sides of the
+    # 2048 boundary (large LDS kernel / global path) and one ~20k-event list (global path)
+    b = synth.rga_batch(400_000, 2_000, 17)
+    lid = b.list_id.astype(np.int64)
+    lid = np.where(lid < 400, lid % 40, lid)
+    lid = np.where(lid >= 1900, 1999, lid)
+    b.list_id = lid.astype(np.uint32)
+    counts = np.bincount(lid, minlength=2000)
+    assert (counts > 2048).any() and ((counts > 512) & (counts <= 2048)).any() and (counts == 0).any()
+    _check(b)
+
+
+def test_rga_hot_list_and_invalid_input():
+    b = synth.rga_batch(300_000, 50, 18)
+    b.list_id[100_000:120_000] = 7  # a run of one list: slot atomics aggregate per wave
+    _check(b)
+    b.list_id[5] = 50
+    with pytest.raises(Exception, match="n_lists"):
+        rga_replay_device(b)

@@ -39,12 +39,15 @@ def main():
     for _ in range(2):
         _lib.check(lib.smx_rga_replay(C.byref(ops), C.byref(out), wst.data_ptr(), ws.value, s))
     torch.cuda.synchronize()
-    steps = 5
+    steps = int(os.environ.get("RGA_STEPS", 5))
     t0 = time.perf_counter()
     for _ in range(steps):
         _lib.check(lib.smx_rga_replay(C.byref(ops), C.byref(out), wst.data_ptr(), ws.value, s))
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    if os.environ.get("RGA_NO_CPU"):  # A/B timing runs: the GPU leg only
+        print(json.dumps({"ms_per_step": round(dt * 1e3, 3), "value": round(n / dt, 1)}))
+        return
     from oracle import oracle
     m = min(n, 1_000_000)
     sel = b.list_id < np.uint32(max(1, nl * m // n))
