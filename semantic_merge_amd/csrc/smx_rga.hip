@@ -30,8 +30,8 @@
 //   w4 = value << 32 | op << 30 | event index              (index = creation order, the tie-break)
 #define RGA_REC 5
 #ifndef RGA_ABL
-#define RGA_ABL 0  // timing ablations of k_rga_list (tools/build_variants.sh): 1 no (value, index)
-                   // rank, 2 no replay, 3 no survivor rank, 4 load only — results are wrong
+#define RGA_ABL 0  // timing ablations of k_rga_list<256> (wrong results, in bounds): bit0 no
+                   // replay, bit1 no survivor sort
 #endif
 #define RGA_IDX_MASK 0x3fffffffu
 #define RGA_SMALL 256   // lists up to this many events: k_rga_list<RGA_SMALL, 256>, one block per list
@@ -193,16 +193,51 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b) {
   return (u32)a[4] < (u32)b[4];  // index bits (the op bits above them are fixed per index)
 }
 
+// Bitonic sort across a 256-thread block, one (key, payload) per thread, ascending by
+// key (all-ascending network: the lower index of each pair keeps the minimum).  Stages
+// whose pairs lie within a wave exchange through cross-lane permutes; the three
+// stages that cross waves go through LDS.
+__device__ __forceinline__ void bitonic_block256(u64& key, u32& pay, u64* lk, u32* lp) {
+  const u32 i = threadIdx.x;
+#pragma unroll
+  for (u32 k = 2; k <= 256; k <<= 1) {
+#pragma unroll
+    for (u32 j = k >> 1; j > 0; j >>= 1) {
+      const u32 mask = j == (k >> 1) ? k - 1 : j;
+      u64 ok;
+      u32 op;
+      if (mask < WAVE) {
+        ok = __shfl_xor(key, (int)mask);
+        op = __shfl_xor(pay, (int)mask);
+      } else {
+        lk[i] = key;
+        lp[i] = pay;
+        __syncthreads();
+        ok = lk[i ^ mask];
+        op = lp[i ^ mask];
+        __syncthreads();
+      }
+      const bool lower = (i & j) == 0;
+      if (lower ? ok < key : key < ok) {
+        key = ok;
+        pay = op;
+      }
+    }
+  }
+}
+
 // Lists of at most CAP events, one block each, everything in LDS:
 //  1. load the list's records (contiguous);
-//  2. order the events by (value, index): each is ranked by counting (keys are unique);
-//  3. one thread per value group replays the group in stream order (crdt.py:29-43):
-//     insert creates a live element, move pops the live element with the smallest
-//     (key, index) and creates one, delete tombstones every present element;
-//  4. compact the survivors' keys (wave-aggregated) into contiguous LDS columns;
-//  5. rank them by (key, index) (crdt.py:45-57) — word 0 decides almost every pair, the
-//     rest is read only on a tie — and write (value, index) in list order at the
-//     list's range start; scnt[l] = survivors.
+//  2. order the events by (value, index) — block bitonic sort when CAP == NT == 256,
+//     ranking by counting for the larger tier — and let one thread per value group
+//     replay the group in stream order (crdt.py:29-43): insert creates a live element,
+//     move pops the live element with the smallest (key, index) and creates one,
+//     delete tombstones every present element;
+//  3. compact the survivors' keys (wave-aggregated) into contiguous LDS columns;
+//  4. order them by (key, index) (crdt.py:45-57): CAP == NT == 256: block bitonic sort
+//     on word 0, then each run of equal word 0 (rare) is insertion-sorted on the rest
+//     of the key and the index; larger tier: rank by counting.  Write (value, index) in
+//     list order at the list's range start; scnt[l] = survivors.
 // Grid: list l = blockIdx.x when `todo` is null, else a loop over todo[0..*ntodo).
 // Longer lists are appended to defer[] for the next kernel.
 template <int CAP, int NT>
@@ -211,16 +246,22 @@ __global__ void __launch_bounds__(NT) k_rga_list(const u64* __restrict__ R, cons
                                                  u32* __restrict__ defer, u32* __restrict__ ndefer,
                                                  u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
                                                  u32* __restrict__ scnt) {
+  constexpr bool SMALL = CAP == 256 && NT == 256;
   __shared__ u64 rec[CAP * RGA_REC];
-  __shared__ u64 gk[CAP];       // value << 30 | index (phase 2-3), then survivors' word 0
-  __shared__ u64 sk[4][CAP];    // survivors' words 1..3 and 4
-  __shared__ u16 perm[CAP];     // (value, index) order -> record
-  __shared__ u8 st[CAP];        // by (value, index) position: bit0 present, bit1 tombstoned
+  // larger tier: (value << 30 | index) by record, then the survivors' words 0 .. 4
+  __shared__ u64 gk[SMALL ? 1 : CAP];
+  __shared__ u64 sk[4][SMALL ? 1 : CAP];
+  __shared__ u16 perm[CAP];              // (value, index) order -> record
+  __shared__ u16 surv[SMALL ? CAP : 1];  // SMALL: surviving records
+  __shared__ u64 gs[SMALL ? CAP : 1];    // SMALL: (value << 30 | index), sorted
+  __shared__ u8 st[CAP];        // bit0 present, bit1 tombstoned (by record, or by (value, index) position)
+  __shared__ u64 lk[SMALL ? 256 : 1];
+  __shared__ u32 lp[SMALL ? 256 : 1];
   __shared__ u32 ns;
   const u32 t = threadIdx.x, lane = t & (WAVE - 1);
   const u64 lanes_lt = lanemask_lt();
   const u32 nwork = todo ? *ntodo : (u32)gridDim.x;
-  for (u32 item = todo ? blockIdx.x : blockIdx.x; item < nwork; item += todo ? gridDim.x : nwork) {
+  for (u32 item = blockIdx.x; item < nwork; item += todo ? gridDim.x : nwork) {
     const u32 l = todo ? todo[item] : item;
     const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
     if (cnt > (u32)CAP) {
@@ -231,52 +272,80 @@ __global__ void __launch_bounds__(NT) k_rga_list(const u64* __restrict__ R, cons
     if (t == 0) ns = 0;
     for (u32 w = t; w < cnt * RGA_REC; w += NT) rec[w] = R[(u64)s0 * RGA_REC + w];
     __syncthreads();
-#if RGA_ABL == 4
-    if (t == 0) scnt[l] = 0;  // keeps k_rga_out in bounds
-    continue;
+    // survivor: record position when SMALL, else (value, index) position -> perm
+    if constexpr (SMALL) {  // (value, index) order by a block bitonic sort; gk, perm by position
+      u64 key = ~0ull;
+      u32 pay = t;
+      if (t < cnt) {
+        const u64 w4 = rec[t * RGA_REC + 4];
+        key = ((w4 >> 32) << 30) | (w4 & RGA_IDX_MASK);
+      }
+      bitonic_block256(key, pay, lk, lp);
+      gs[t] = key;
+      perm[t] = (u16)pay;
+      st[t] = 0;
+      __syncthreads();
+#if RGA_ABL & 1
+      if (t < cnt) st[t] = t % 3 != 0;
+      if (0)
 #endif
-    for (u32 i = t; i < cnt; i += NT) {
-      const u64 w4 = rec[i * RGA_REC + 4];
-      gk[i] = ((w4 >> 32) << 30) | (w4 & RGA_IDX_MASK);
-      st[i] = 0;
-    }
-    __syncthreads();
-    for (u32 i = t; i < cnt; i += NT) {
-      const u64 k = gk[i];
-      u32 r = 0, j = 0;
-#if RGA_ABL == 1
-      r = i;
-#else
-      for (; j + 4 <= cnt; j += 4) r += (gk[j] < k) + (gk[j + 1] < k) + (gk[j + 2] < k) + (gk[j + 3] < k);
-      for (; j < cnt; ++j) r += gk[j] < k;
-#endif
-      perm[r] = (u16)i;
-    }
-    __syncthreads();
-#if RGA_ABL == 2
-    for (u32 j = t; j < cnt; j += NT) st[j] = j % 3 ? 1 : 0;
-    if (0)
-#endif
-    for (u32 j = t; j < cnt; j += NT) {
-      const u64 v = gk[perm[j]] >> 30;
-      if (j != 0 && (gk[perm[j - 1]] >> 30) == v) continue;
-      u32 end = j + 1;
-      while (end < cnt && (gk[perm[end]] >> 30) == v) ++end;
-      for (u32 x = j; x < end; ++x) {
-        const u32 op = (u32)(rec[perm[x] * RGA_REC + 4] >> 30) & 3u;
-        if (op == 2) {
-          for (u32 y = j; y < x; ++y)
-            if (st[y] & 1) st[y] |= 2;
-          continue;  // a delete creates nothing
+      if (t < cnt && (t == 0 || (gs[t - 1] >> 30) != (key >> 30))) {  // group head: replay in stream order
+        const u64 v = key >> 30;
+        u32 end = t + 1;
+        while (end < cnt && (gs[end] >> 30) == v) ++end;
+        for (u32 x = t; x < end; ++x) {
+          const u32 op = (u32)(rec[perm[x] * RGA_REC + 4] >> 30) & 3u;
+          if (op == 2) {
+            for (u32 y = t; y < x; ++y)
+              if (st[y] & 1) st[y] |= 2;
+            continue;  // a delete creates nothing
+          }
+          if (op == 1) {
+            int best = -1;
+            for (u32 y = t; y < x; ++y)
+              if (st[y] == 1 && (best < 0 || rec_lt(&rec[perm[y] * RGA_REC], &rec[perm[best] * RGA_REC])))
+                best = (int)y;
+            if (best >= 0) st[best] = 0;
+          }
+          st[x] = 1;
         }
-        if (op == 1) {
-          int best = -1;
-          for (u32 y = j; y < x; ++y)
-            if (st[y] == 1 && (best < 0 || rec_lt(&rec[perm[y] * RGA_REC], &rec[perm[best] * RGA_REC])))
-              best = (int)y;
-          if (best >= 0) st[best] = 0;
+      }
+    } else {
+      for (u32 i = t; i < cnt; i += NT) {
+        const u64 w4 = rec[i * RGA_REC + 4];
+        gk[i] = ((w4 >> 32) << 30) | (w4 & RGA_IDX_MASK);
+        st[i] = 0;
+      }
+      __syncthreads();
+      for (u32 i = t; i < cnt; i += NT) {
+        const u64 k = gk[i];
+        u32 r = 0, j = 0;
+        for (; j + 4 <= cnt; j += 4) r += (gk[j] < k) + (gk[j + 1] < k) + (gk[j + 2] < k) + (gk[j + 3] < k);
+        for (; j < cnt; ++j) r += gk[j] < k;
+        perm[r] = (u16)i;
+      }
+      __syncthreads();
+      for (u32 j = t; j < cnt; j += NT) {
+        const u64 v = gk[perm[j]] >> 30;
+        if (j != 0 && (gk[perm[j - 1]] >> 30) == v) continue;
+        u32 end = j + 1;
+        while (end < cnt && (gk[perm[end]] >> 30) == v) ++end;
+        for (u32 x = j; x < end; ++x) {
+          const u32 op = (u32)(rec[perm[x] * RGA_REC + 4] >> 30) & 3u;
+          if (op == 2) {
+            for (u32 y = j; y < x; ++y)
+              if (st[y] & 1) st[y] |= 2;
+            continue;
+          }
+          if (op == 1) {
+            int best = -1;
+            for (u32 y = j; y < x; ++y)
+              if (st[y] == 1 && (best < 0 || rec_lt(&rec[perm[y] * RGA_REC], &rec[perm[best] * RGA_REC])))
+                best = (int)y;
+            if (best >= 0) st[best] = 0;
+          }
+          st[x] = 1;
         }
-        st[x] = 1;
       }
     }
     __syncthreads();
@@ -288,46 +357,71 @@ __global__ void __launch_bounds__(NT) k_rga_list(const u64* __restrict__ R, cons
       if (lane == 0 && ball) got = atomicAdd(&ns, (u32)__popcll(ball));
       const u32 base = __shfl(got, 0);
       if (live) {
-        const u32 a = base + (u32)__popcll(ball & lanes_lt), p = perm[j];
-        gk[a] = rec[p * RGA_REC];  // (value, index) keys are dead from here on
-        sk[0][a] = rec[p * RGA_REC + 1];
-        sk[1][a] = rec[p * RGA_REC + 2];
-        sk[2][a] = rec[p * RGA_REC + 3];
-        sk[3][a] = rec[p * RGA_REC + 4];
+        const u32 a = base + (u32)__popcll(ball & lanes_lt);
+        if constexpr (SMALL) {
+          surv[a] = perm[j];
+        } else {
+          const u32 p = perm[j];
+          gk[a] = rec[p * RGA_REC];
+          sk[0][a] = rec[p * RGA_REC + 1];
+          sk[1][a] = rec[p * RGA_REC + 2];
+          sk[2][a] = rec[p * RGA_REC + 3];
+          sk[3][a] = rec[p * RGA_REC + 4];
+        }
       }
     }
     __syncthreads();
     const u32 m = ns;
-    for (u32 a = t; a < m; a += NT) {
-      const u64 k0 = gk[a];
-      u32 r = 0;
-#if RGA_ABL == 3
-      r = a;
-#else
-      u32 eq = 0, b = 0;  // same b on every lane: LDS broadcast; word 0 only
-      for (; b + 4 <= m; b += 4) {
-        const u64 x0 = gk[b], x1 = gk[b + 1], x2 = gk[b + 2], x3 = gk[b + 3];
-        r += (x0 < k0) + (x1 < k0) + (x2 < k0) + (x3 < k0);
-        eq += (x0 == k0) + (x1 == k0) + (x2 == k0) + (x3 == k0);
-      }
-      for (; b < m; ++b) {
-        r += gk[b] < k0;
-        eq += gk[b] == k0;
-      }
-      if (eq > 1) {  // another survivor ties on word 0 (rare): the rest of the key, then the index
-        const u64 a1 = sk[0][a], a2 = sk[1][a], a3 = sk[2][a];
-        const u32 ia = (u32)sk[3][a] & RGA_IDX_MASK;
-        for (u32 c = 0; c < m; ++c) {
-          if (gk[c] != k0 || c == a) continue;
-          const u64 b1 = sk[0][c], b2 = sk[1][c], b3 = sk[2][c];
-          const u32 ib = (u32)sk[3][c] & RGA_IDX_MASK;
-          r += b1 != a1 ? b1 < a1 : b2 != a2 ? b2 < a2 : b3 != a3 ? b3 < a3 : ib < ia;
+    if constexpr (SMALL) {
+      // survivors a, b (record positions) that tie on word 0: the rest of the key, the index
+      auto tail_lt = [&](u32 b, u32 a) {
+        const u64* ka = &rec[a * RGA_REC];
+        const u64* kb = &rec[b * RGA_REC];
+        const u32 ia = (u32)ka[4] & RGA_IDX_MASK, ib = (u32)kb[4] & RGA_IDX_MASK;
+        return kb[1] != ka[1] ? kb[1] < ka[1] : kb[2] != ka[2] ? kb[2] < ka[2] : kb[3] != ka[3] ? kb[3] < ka[3] : ib < ia;
+      };
+      u32 pay = t < m ? surv[t] : 0u;
+      u64 key = t < m ? rec[pay * RGA_REC] : ~0ull;
+      if (!(RGA_ABL & 2)) bitonic_block256(key, pay, lk, lp);
+      lk[t] = key;
+      lp[t] = pay;
+      __syncthreads();
+      if (t < m && t + 1 < m && lk[t + 1] == key && (t == 0 || lk[t - 1] != key)) {
+        u32 e = t + 2;  // run [t, e) of equal word 0: insertion sort on the rest
+        while (e < m && lk[e] == key) ++e;
+        for (u32 x = t + 1; x < e; ++x) {
+          const u32 v = lp[x];
+          u32 y = x;
+          while (y > t && tail_lt(v, lp[y - 1])) {
+            lp[y] = lp[y - 1];
+            --y;
+          }
+          lp[y] = v;
         }
       }
-#endif
-      const u64 w4 = sk[3][a];
-      tmp_v[s0 + r] = (u32)(w4 >> 32);
-      tmp_s[s0 + r] = (u32)w4 & RGA_IDX_MASK;
+      __syncthreads();
+      if (t < m) {
+        const u64 w4 = rec[lp[t] * RGA_REC + 4];
+        tmp_v[s0 + t] = (u32)(w4 >> 32);
+        tmp_s[s0 + t] = (u32)w4 & RGA_IDX_MASK;
+      }
+    } else {
+      auto tail_lt = [&](u32 b, u32 a) {
+        const u64 a1 = sk[0][a], b1 = sk[0][b], a2 = sk[1][a], b2 = sk[1][b], a3 = sk[2][a], b3 = sk[2][b];
+        const u32 ia = (u32)sk[3][a] & RGA_IDX_MASK, ib = (u32)sk[3][b] & RGA_IDX_MASK;
+        return b1 != a1 ? b1 < a1 : b2 != a2 ? b2 < a2 : b3 != a3 ? b3 < a3 : ib < ia;
+      };
+      for (u32 a = t; a < m; a += NT) {
+        const u64 k0 = gk[a];
+        u32 r = 0;
+        for (u32 b = 0; b < m; ++b) {
+          const u64 x = gk[b];
+          r += x < k0 || (x == k0 && b != a && tail_lt(b, a));
+        }
+        const u64 w4 = sk[3][a];
+        tmp_v[s0 + r] = (u32)(w4 >> 32);
+        tmp_s[s0 + r] = (u32)w4 & RGA_IDX_MASK;
+      }
     }
     if (t == 0) scnt[l] = m;
   }
@@ -563,6 +657,7 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   if (herr) return smx_set_error(SMX_E_ARG, "invalid input: list >= n_lists or op > 2");
   return SMX_OK;
 }
+
 
 extern "C" int smx_rga_replay(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, size_t wsb,
                               void* stream) {
