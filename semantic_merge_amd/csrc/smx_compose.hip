@@ -1151,66 +1151,265 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   return launch_tail(C, P);
 }
 
-// Generic plan: stable radix sort of each branch by (ts, oid_hi, oid_lo), then
-// fixed windows over the sorted logs.  Used when the presorted plan fails.
-// Adjacent (ts, oid_hi) duplicates in each branch sorted without oid_lo.
+// Generic plan: each branch sorted by (ts, oid_hi, oid_lo, index), then fixed windows
+// over the sorted logs (k_window_g).  Used when the presorted plan fails.  Two ways to
+// sort a branch:
+//  * segmented (GEN_SEG): the branch's timestamps never decrease but its equal-timestamp
+//    groups are too long for a presorted window (config 5) -- only each group needs
+//    sorting, by oid.  Nominal tiles of SEG_H ops snap back to a group start, so each
+//    tile holds whole groups (fewer than SEG_H + the longest group ops); a block sorts
+//    its tile with a bitonic network on (group, top 38 bits of oid_hi, tile index), and
+//    runs of equal (group, hi38) (rare; every duplicate id) are re-sorted exactly on
+//    (oid_hi, oid_lo, index).  A group longer than SEG_CAP - SEG_H ops or a timestamp that decreases sets
+//    meta->seg_over and the radix sort runs instead.
+//  * radix (GEN_RADIX / GEN_RADIX_LO): stable LSD radix sort on (ts, oid_hi), checked
+//    afterwards for adjacent (ts, oid_hi) duplicates, which rerun it with oid_lo.
+#define SEG_CAP 8192
+#define SEG_H 4096
+#define SEG_NT 1024
+enum { GEN_SEG, GEN_RADIX, GEN_RADIX_LO };
+
 __global__ void k_dupcheck(const u64* __restrict__ sts, const u64* __restrict__ shi, i64 na, i64 n,
                            ComposeMeta* meta) {
   for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x + 1; i < n; i += (i64)gridDim.x * BLOCK)
     if (i != na && sts[i] == sts[i - 1] && shi[i] == shi[i - 1]) meta->dup_key = 1;
 }
 
-// with_lo = false sorts by (ts, oid_hi) only; ids are random (uuid4), so a
-// duplicate (ts, oid_hi) pair -- checked afterwards -- is rare and reruns the
-// sort with oid_lo (run_order).
-static int run_generic(const Ctx& C, bool with_lo) {
+// First index x <= p with ts[x] == ts[p], for ts non-decreasing up to p: gallop back,
+// then binary search.
+__device__ i64 seg_group_start(const u64* __restrict__ ts, i64 p) {
+  const u64 v = ts[p];
+  i64 h = p, step = 1, l = 0;
+  while (h > 0) {
+    const i64 c = h - step > 0 ? h - step : 0;
+    if (ts[c] < v) {
+      l = c + 1;
+      break;
+    }
+    h = c;
+    step *= 2;
+  }
+  while (l < h) {
+    const i64 m = (l + h) >> 1;
+    if (ts[m] < v) l = m + 1;
+    else h = m;
+  }
+  return l;
+}
+
+// Compare-exchange of registers: a keeps the minimum.
+__device__ __forceinline__ void seg_cx(u64& a, u64& b) {
+  const u64 x = a < b ? a : b, y = a < b ? b : a;
+  a = x;
+  b = y;
+}
+
+// Bitonic half-cleaner stages j = 4, 2, 1 on 8 consecutive keys held by one thread.
+__device__ __forceinline__ void seg_tail8(u64 (&v)[8]) {
+#pragma unroll
+  for (int j = 4; j > 0; j >>= 1)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if ((i & j) == 0) seg_cx(v[i], v[i | j]);
+}
+
+// One tile of one branch (ts, hi, lo: the branch's columns; outputs at the branch's
+// offset; off: the branch's first op index in A||B).  Sort key, one u64 per element:
+// group (13 bits) | top 38 bits of oid_hi | tile index (13 bits) -- unique, so the
+// bitonic network needs no payload; equal (group, hi38) pairs (rare on random ids,
+// every duplicate id) are re-sorted exactly afterwards.  Each thread owns 8
+// consecutive keys: the network's stages inside 8-key blocks (the first three merge
+// levels, and the last three stages of every later merge) run in registers, the rest
+// as pair exchanges in LDS.
+__global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, const u64* __restrict__ hi,
+                                                    const u64* __restrict__ lo, i64 cnt, u32 off,
+                                                    u64* __restrict__ sts, u64* __restrict__ shi,
+                                                    u64* __restrict__ slo, u32* __restrict__ perm,
+                                                    ComposeMeta* meta) {
+  constexpr int PER = SEG_CAP / SEG_NT;  // 8 consecutive keys per thread
+  static_assert(PER == 8, "register stages assume 8 keys per thread");
+  __shared__ u64 key[SEG_CAP];
+  __shared__ u32 wsum[SEG_NT / WAVE];
+  __shared__ i64 se[2];
+  const int t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
+  const i64 p0 = (i64)blockIdx.x * SEG_H;
+  // layout: every adjacent pair of the nominal range (the nominal ranges cover the branch)
+  bool bad = false;
+  for (i64 i = p0 + t; i < p0 + SEG_H && i + 1 < cnt; i += SEG_NT) bad |= ts[i + 1] < ts[i];
+  if (t == 0) {
+    se[0] = seg_group_start(ts, p0);
+    se[1] = p0 + SEG_H < cnt ? seg_group_start(ts, p0 + SEG_H) : cnt;
+  }
+  if (__syncthreads_or(bad)) {
+    if (t == 0) meta->seg_over = 1;
+    return;
+  }
+  const i64 s = se[0], size = se[1] - s;
+  if (size <= 0) return;
+  if (size > SEG_CAP) {
+    if (t == 0) meta->seg_over = 1;
+    return;
+  }
+  u32 P = 8;
+  while (P < (u32)size) P <<= 1;
+  const bool own = (u32)t * PER < P;  // this thread's 8 keys are inside the network
+  // group index of each element: inclusive count of group starts after the first
+  u32 f[PER], run = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const i64 x = (i64)t * PER + k;
+    f[k] = x > 0 && x < size && ts[s + x] != ts[s + x - 1];
+    run += f[k];
+  }
+  const u32 inc = wave_incl_sum(run);
+  if (lane == WAVE - 1) wsum[wv] = inc;
+  __syncthreads();
+  u32 g = inc - run;
+  for (int q = 0; q < wv; ++q) g += wsum[q];
+  u64 v[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const u32 x = t * PER + k;
+    g += f[k];
+    v[k] = x < (u32)size ? ((u64)g << 51) | ((hi[s + x] >> 26) << 13) | x : ~0ull;
+  }
+  // merge levels k = 2, 4, 8 inside the thread's block (all-ascending: lower keeps min)
+  seg_cx(v[0], v[1]); seg_cx(v[2], v[3]); seg_cx(v[4], v[5]); seg_cx(v[6], v[7]);
+  seg_cx(v[0], v[3]); seg_cx(v[1], v[2]); seg_cx(v[4], v[7]); seg_cx(v[5], v[6]);
+  seg_cx(v[0], v[1]); seg_cx(v[2], v[3]); seg_cx(v[4], v[5]); seg_cx(v[6], v[7]);
+  seg_cx(v[0], v[7]); seg_cx(v[1], v[6]); seg_cx(v[2], v[5]); seg_cx(v[3], v[4]);
+  seg_cx(v[0], v[2]); seg_cx(v[1], v[3]); seg_cx(v[4], v[6]); seg_cx(v[5], v[7]);
+  seg_cx(v[0], v[1]); seg_cx(v[2], v[3]); seg_cx(v[4], v[5]); seg_cx(v[6], v[7]);
+  if (own)
+#pragma unroll
+    for (int k = 0; k < PER; ++k) key[t * PER + k] = v[k];
+  __syncthreads();
+  for (u32 k = 16; k <= P; k <<= 1) {
+    for (u32 j = k >> 1; j >= 8; j >>= 1) {  // pair exchanges through LDS
+      const u32 mask = j == (k >> 1) ? k - 1 : j;
+      for (u32 r = t; r < P / 2; r += SEG_NT) {
+        const u32 i = ((r & ~(j - 1)) << 1) | (r & (j - 1)), q = i ^ mask;
+        const u64 a = key[i], b = key[q];
+        if (b < a) {
+          key[i] = b;
+          key[q] = a;
+        }
+      }
+      __syncthreads();
+    }
+    if (own) {  // stages j = 4, 2, 1 in registers
+#pragma unroll
+      for (int m = 0; m < PER; ++m) v[m] = key[t * PER + m];
+      seg_tail8(v);
+#pragma unroll
+      for (int m = 0; m < PER; ++m) key[t * PER + m] = v[m];
+    }
+    __syncthreads();
+  }
+  // runs of equal (group, hi38): exact order on (oid_hi, oid_lo, index)
+  for (u32 x = t; x + 1 < (u32)size; x += SEG_NT) {
+    const u64 kx = key[x] >> 13;
+    if ((key[x + 1] >> 13) != kx || (x > 0 && (key[x - 1] >> 13) == kx)) continue;
+    u32 e = x + 2;
+    while (e < (u32)size && (key[e] >> 13) == kx) ++e;
+    for (u32 y = x + 1; y < e; ++y) {
+      const u64 ky = key[y];
+      const u32 vi = (u32)ky & 0x1fffu;
+      const u64 vh = hi[s + vi], vl = lo[s + vi];
+      u32 z = y;
+      while (z > x) {
+        const u64 kw = key[z - 1];
+        const u32 wi = (u32)kw & 0x1fffu;
+        const u64 wh = hi[s + wi], wl = lo[s + wi];
+        if (!(vh < wh || (vh == wh && (vl < wl || (vl == wl && vi < wi))))) break;
+        key[z] = kw;
+        --z;
+      }
+      key[z] = ky;
+    }
+  }
+  __syncthreads();
+  for (u32 x = t; x < (u32)size; x += SEG_NT) {
+    const i64 src = s + (key[x] & 0x1fffu);
+    sts[s + x] = ts[src];
+    shi[s + x] = hi[src];
+    slo[s + x] = lo[src];
+    perm[s + x] = off + (u32)src;
+  }
+}
+
+static int read_meta(const Ctx& C, ComposeMeta* hm);
+
+// *fallback: the segmented sort could not order this log (mode GEN_SEG only); nothing
+// after the sort was launched.
+static int run_generic(const Ctx& C, int mode, bool* fallback) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
   u32* wcnt = C.ws<u32>(B_WCNT);
   u32* woff = C.ws<u32>(B_WOFF);
   const i64 na = C.na, nb = C.nb, n = C.n;
-  C.tm->begin(ST_GSORT);
-  HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
-  hipLaunchKernelGGL(k_meta_init, dim3(1), dim3(1), 0, st, meta);
-  hipLaunchKernelGGL(k_keymask, dim3(grid_for(n, BLOCK * 8)), dim3(BLOCK), 0, st, C.ops->ts, C.ops->oid_hi,
-                     C.ops->oid_lo, na, n, meta);
-  ComposeMeta hm;
-  HIP_TRY(hipMemcpyAsync(&hm, meta, sizeof(ComposeMeta), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
   u64* sts = C.ws<u64>(B_STS);
   u64* shi = C.ws<u64>(B_SHI);
   u64* slo = C.ws<u64>(B_SLO);
   u32* perm = C.ws<u32>(B_PERM);
-  RadixTemp rt{C.ws<u64>(B_RK2), C.ws<u32>(B_RV2), C.ws<u32>(B_RHIST), C.ws<u32>(B_PART)};
-  const u64* words[3] = {C.ops->oid_lo, C.ops->oid_hi, C.ops->ts};
-  const int w0 = with_lo ? 0 : 1;
-  for (int side = 0; side < 2; ++side) {
-    const i64 off = side ? na : 0, cnt = side ? nb : na;
-    if (cnt == 0) continue;
-    u64* key = C.ws<u64>(B_RKEY) + off;
-    u32* val = perm + off;
-    for (int wi = w0; wi < 3; ++wi) {
-      const int q = 2 - wi;  // meta order: 0 = ts, 1 = hi, 2 = lo
-      const u64 varying = hm.key_or[side][q] ^ hm.key_and[side][q];
-      int shifts[8], ns = 0;
-      for (int dgt = 0; dgt < 8; ++dgt)
-        if ((varying >> (8 * dgt)) & 0xffull) shifts[ns++] = 8 * dgt;
-      if (wi == w0) {
-        hipLaunchKernelGGL(k_gather_init, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi] + off, key, val,
-                           cnt);
-        if (off)  // values are op indices of A||B
-          hipLaunchKernelGGL(k_offset, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, val, cnt, (u32)off);
-      } else {
-        hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi], val, key, cnt);
-      }
-      if (ns) HIP_TRY(radix_sort_pairs(key, val, cnt, shifts, ns, rt, st));
+  *fallback = false;
+  C.tm->begin(ST_GSORT);
+  HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
+  if (mode == GEN_SEG) {
+    for (int side = 0; side < 2; ++side) {
+      const i64 off = side ? na : 0, cnt = side ? nb : na;
+      if (cnt == 0) continue;
+      hipLaunchKernelGGL(k_segsort, dim3(SMX_CEIL_DIV(cnt, (i64)SEG_H)), dim3(SEG_NT), 0, st, C.ops->ts + off,
+                         C.ops->oid_hi + off, C.ops->oid_lo + off, cnt, (u32)off, sts + off, shi + off, slo + off,
+                         perm + off, meta);
     }
-    hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->ts, val, sts + off, cnt);
-    hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_hi, val, shi + off, cnt);
-    hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_lo, val, slo + off, cnt);
+    ComposeMeta hm;
+    int rc = read_meta(C, &hm);
+    if (rc) return rc;
+    if (hm.seg_over) {
+      C.tm->end(ST_GSORT);
+      *fallback = true;
+      return SMX_OK;
+    }
+  } else {
+    const bool with_lo = mode == GEN_RADIX_LO;
+    hipLaunchKernelGGL(k_meta_init, dim3(1), dim3(1), 0, st, meta);
+    hipLaunchKernelGGL(k_keymask, dim3(grid_for(n, BLOCK * 8)), dim3(BLOCK), 0, st, C.ops->ts, C.ops->oid_hi,
+                       C.ops->oid_lo, na, n, meta);
+    ComposeMeta hm;
+    HIP_TRY(hipMemcpyAsync(&hm, meta, sizeof(ComposeMeta), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    RadixTemp rt{C.ws<u64>(B_RK2), C.ws<u32>(B_RV2), C.ws<u32>(B_RHIST), C.ws<u32>(B_PART)};
+    const u64* words[3] = {C.ops->oid_lo, C.ops->oid_hi, C.ops->ts};
+    const int w0 = with_lo ? 0 : 1;
+    for (int side = 0; side < 2; ++side) {
+      const i64 off = side ? na : 0, cnt = side ? nb : na;
+      if (cnt == 0) continue;
+      u64* key = C.ws<u64>(B_RKEY) + off;
+      u32* val = perm + off;
+      for (int wi = w0; wi < 3; ++wi) {
+        const int q = 2 - wi;  // meta order: 0 = ts, 1 = hi, 2 = lo
+        const u64 varying = hm.key_or[side][q] ^ hm.key_and[side][q];
+        int shifts[8], ns = 0;
+        for (int dgt = 0; dgt < 8; ++dgt)
+          if ((varying >> (8 * dgt)) & 0xffull) shifts[ns++] = 8 * dgt;
+        if (wi == w0) {
+          hipLaunchKernelGGL(k_gather_init, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi] + off, key, val,
+                             cnt);
+          if (off)  // values are op indices of A||B
+            hipLaunchKernelGGL(k_offset, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, val, cnt, (u32)off);
+        } else {
+          hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, words[wi], val, key, cnt);
+        }
+        if (ns) HIP_TRY(radix_sort_pairs(key, val, cnt, shifts, ns, rt, st));
+      }
+      hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->ts, val, sts + off, cnt);
+      hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_hi, val, shi + off, cnt);
+      hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_lo, val, slo + off, cnt);
+    }
+    if (!with_lo) hipLaunchKernelGGL(k_dupcheck, dim3(grid_for(n)), dim3(BLOCK), 0, st, sts, shi, na, n, meta);
   }
-  if (!with_lo) hipLaunchKernelGGL(k_dupcheck, dim3(grid_for(n)), dim3(BLOCK), 0, st, sts, shi, na, n, meta);
   const i64 W = SMX_CEIL_DIV(n, (i64)WIN_CAP);
   hipLaunchKernelGGL(k_gpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, sts, shi, slo, na, nb,
                      W, bnd);
@@ -1278,12 +1477,14 @@ static int run_order(const Ctx& C, bool allow_generic, ComposeMeta* hm) {
   if (hm->f_fail && !hm->bad_sym && allow_generic) {
     if (C.ops->b_gap != 0)
       return set_err(SMX_E_ARG, "branch logs not timestamp-ordered: the generic plan needs b_gap = 0");
-    if ((rc = run_generic(C, false))) return rc;
-    if ((rc = read_meta(C, hm))) return rc;
-    if (hm->dup_key) {
-      if ((rc = run_generic(C, true))) return rc;
+    bool fallback = true;
+    if (hm->f_fail == 2 && (rc = run_generic(C, GEN_SEG, &fallback))) return rc;  // ordered, long groups
+    if (fallback) {
+      if ((rc = run_generic(C, GEN_RADIX, &fallback))) return rc;
       if ((rc = read_meta(C, hm))) return rc;
+      if (hm->dup_key && (rc = run_generic(C, GEN_RADIX_LO, &fallback))) return rc;
     }
+    if ((rc = read_meta(C, hm))) return rc;
   }
   return SMX_OK;
 }

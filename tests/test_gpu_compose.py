@@ -85,10 +85,30 @@ def test_synthetic_digests_gpu(name):
     synth.LiftSpec(333_333, 1, 29, ops_per_ms=1),               # one symbol, every head collides
     synth.LiftSpec(1_000_000, 1_000, 41, ops_per_ms=160),       # windows overflow -> smaller windows
     synth.LiftSpec(400_000, 5_000_000, 43),                     # > 4M symbols: atomic tables
-], ids=["c2_1M", "c2_1M_shuffled", "c5_2M", "hot64_1M", "onesym", "dense160", "sym5M"])
+    synth.LiftSpec(600_000, 2_000, 61, ops_per_ms=3000, mix=synth.ADVERSARIAL_MIX),  # segmented plan
+    synth.LiftSpec(300_000, 500, 59, ops_per_ms=10_000),        # groups too long: radix plan
+], ids=["c2_1M", "c2_1M_shuffled", "c5_2M", "hot64_1M", "onesym", "dense160", "sym5M", "seg3000",
+        "groups10k"])
 def test_gpu_equals_oracle_soa(spec):
     soa = synth.lift_soa(synth.lift_logs(spec))
     _eq_soa(compose_soa(soa), oracle.compose(soa), str(spec))
+
+
+def test_gpu_segmented_plan_duplicate_ids():
+    """Config-5-shaped log (ordered, 4096-op timestamp groups: the segmented plan) with
+    duplicate ids and ids equal in their top bits inside groups: the tie runs are
+    re-sorted on the full id, then by index."""
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(400_000, 1_000, 67, ops_per_ms=4096,
+                                                         mix=synth.ADVERSARIAL_MIX)))
+    rng = np.random.default_rng(67)
+    n = soa.n
+    dup = rng.choice(n - 1, 3000, replace=False)
+    soa.oid_hi[dup + 1] = soa.oid_hi[dup]            # same top bits (and same hi) as a neighbour
+    both = dup[:1000]
+    soa.oid_lo[both + 1] = soa.oid_lo[both]          # duplicate ids
+    near = rng.choice(n, 2000, replace=False)
+    soa.oid_hi[near] = (soa.oid_hi[near] & ~np.uint64(0x1fff)) | np.uint64(7)  # equal above bit 13
+    _eq_soa(compose_soa(soa), oracle.compose(soa), "segmented plan, duplicate ids")
 
 
 @pytest.mark.parametrize("bits", [20, 31], ids=["packed", "wide"])
