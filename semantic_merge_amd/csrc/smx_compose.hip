@@ -1175,84 +1175,92 @@ __global__ void k_dupcheck(const u64* __restrict__ sts, const u64* __restrict__ 
     if (i != na && sts[i] == sts[i - 1] && shi[i] == shi[i - 1]) meta->dup_key = 1;
 }
 
-// First index x <= p with ts[x] == ts[p], for ts non-decreasing up to p: gallop back,
-// then binary search.
-__device__ i64 seg_group_start(const u64* __restrict__ ts, i64 p) {
-  const u64 v = ts[p];
-  i64 h = p, step = 1, l = 0;
-  while (h > 0) {
-    const i64 c = h - step > 0 ? h - step : 0;
-    if (ts[c] < v) {
-      l = c + 1;
-      break;
+// One pass of the bitonic network over 8 keys per thread: the thread holds keys
+// base | m << b (m = 0..7) and runs the stages whose partner bit is b + 2, b + 1, b
+// (the top `nbits` of them), ascending where bit k of the index is clear.
+__device__ __forceinline__ void seg_pass(u64 (&v)[8], u32 base, u32 b, u32 k, int top, int nbits) {
+#pragma unroll
+  for (int bit = 2; bit >= 0; --bit) {
+    if (bit > top || bit <= top - nbits) continue;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if ((m >> bit) & 1) continue;
+      const int m2 = m | (1 << bit);
+      const bool asc = ((base | ((u32)m << b)) & k) == 0;
+      const u64 x = v[m], y = v[m2];
+      const bool sw = asc ? y < x : x < y;
+      v[m] = sw ? y : x;
+      v[m2] = sw ? x : y;
     }
-    h = c;
-    step *= 2;
   }
-  while (l < h) {
-    const i64 m = (l + h) >> 1;
-    if (ts[m] < v) l = m + 1;
-    else h = m;
-  }
-  return l;
 }
 
-// Compare-exchange of registers: a keeps the minimum.
-__device__ __forceinline__ void seg_cx(u64& a, u64& b) {
-  const u64 x = a < b ? a : b, y = a < b ? b : a;
-  a = x;
-  b = y;
-}
-
-// Bitonic half-cleaner stages j = 4, 2, 1 on 8 consecutive keys held by one thread.
-__device__ __forceinline__ void seg_tail8(u64 (&v)[8]) {
-#pragma unroll
-  for (int j = 4; j > 0; j >>= 1)
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if ((i & j) == 0) seg_cx(v[i], v[i | j]);
-}
+#define SEGPAD(i) ((i) + ((i) >> 3))  // one pad word per 8 keys: spreads a thread's 8 keys over banks
 
 // One tile of one branch (ts, hi, lo: the branch's columns; outputs at the branch's
 // offset; off: the branch's first op index in A||B).  Sort key, one u64 per element:
 // group (13 bits) | top 38 bits of oid_hi | tile index (13 bits) -- unique, so the
 // bitonic network needs no payload; equal (group, hi38) pairs (rare on random ids,
-// every duplicate id) are re-sorted exactly afterwards.  Each thread owns 8
-// consecutive keys: the network's stages inside 8-key blocks (the first three merge
-// levels, and the last three stages of every later merge) run in registers, the rest
-// as pair exchanges in LDS.
+// every duplicate id) are re-sorted exactly afterwards.  Each thread holds 8 keys whose
+// indices differ in three consecutive bits b .. b+2, so three stages of the network run
+// in registers per LDS round trip (33 round trips for 8192 keys instead of 91 stages).
 __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, const u64* __restrict__ hi,
                                                     const u64* __restrict__ lo, i64 cnt, u32 off,
                                                     u64* __restrict__ sts, u64* __restrict__ shi,
                                                     u64* __restrict__ slo, u32* __restrict__ perm,
                                                     ComposeMeta* meta) {
-  constexpr int PER = SEG_CAP / SEG_NT;  // 8 consecutive keys per thread
-  static_assert(PER == 8, "register stages assume 8 keys per thread");
-  __shared__ u64 key[SEG_CAP];
+  constexpr int PER = SEG_CAP / SEG_NT;  // 8 keys per thread
+  static_assert(PER == 8, "the register passes assume 8 keys per thread");
+  __shared__ u64 key[SEGPAD(SEG_CAP)];
   __shared__ u32 wsum[SEG_NT / WAVE];
   __shared__ i64 se[2];
   const int t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
   const i64 p0 = (i64)blockIdx.x * SEG_H;
-  // layout: every adjacent pair of the nominal range (the nominal ranges cover the branch)
+  // Layout: every adjacent pair of the nominal range (the nominal ranges cover the
+  // branch).  Tile bounds: the group of p0 (and of p0 + SEG_H) starts within the
+  // SEG_CAP - SEG_H ops before it, where the ops below its timestamp are counted.
+  constexpr int W = SEG_CAP - SEG_H;
+  const u64 v0 = ts[p0];
+  const bool has_end = p0 + SEG_H < cnt;
+  const u64 v1 = has_end ? ts[p0 + SEG_H] : 0;
   bool bad = false;
-  for (i64 i = p0 + t; i < p0 + SEG_H && i + 1 < cnt; i += SEG_NT) bad |= ts[i + 1] < ts[i];
-  if (t == 0) {
-    se[0] = seg_group_start(ts, p0);
-    se[1] = p0 + SEG_H < cnt ? seg_group_start(ts, p0 + SEG_H) : cnt;
+  u32 c0 = 0, c1 = 0;
+#pragma unroll
+  for (int r = 0; r < SEG_H / SEG_NT; ++r) {
+    const i64 i = p0 + r * SEG_NT + t;
+    if (i + 1 < cnt) bad |= ts[i + 1] < ts[i];
   }
+#pragma unroll
+  for (int r = 0; r < W / SEG_NT; ++r) {
+    const i64 i0 = p0 - W + r * SEG_NT + t, i1 = p0 + SEG_H - W + r * SEG_NT + t;
+    if (i0 >= 0) c0 += ts[i0] < v0;
+    if (has_end) c1 += ts[i1] < v1;
+  }
+  if (t < 2) se[t] = 0;
+  __syncthreads();
+  c0 = wave_incl_sum(c0);
+  c1 = wave_incl_sum(c1);
+  if (lane == WAVE - 1) {
+    atomicAdd((unsigned long long*)&se[0], (unsigned long long)c0);
+    atomicAdd((unsigned long long*)&se[1], (unsigned long long)c1);
+  }
+  const i64 a0 = p0 - W > 0 ? p0 - W : 0, a1 = p0 + SEG_H - W;
+  // a group reaching below its window: longer than the tile scheme allows
+  if (t == 0 && p0 - W > 0 && ts[p0 - W - 1] == v0) bad = true;
+  if (t == 1 && has_end && a1 > 0 && ts[a1 - 1] == v1) bad = true;
   if (__syncthreads_or(bad)) {
     if (t == 0) meta->seg_over = 1;
     return;
   }
-  const i64 s = se[0], size = se[1] - s;
+  const i64 s = a0 + se[0], size = (has_end ? a1 + se[1] : cnt) - s;
   if (size <= 0) return;
   if (size > SEG_CAP) {
     if (t == 0) meta->seg_over = 1;
     return;
   }
-  u32 P = 8;
-  while (P < (u32)size) P <<= 1;
-  const bool own = (u32)t * PER < P;  // this thread's 8 keys are inside the network
+  u32 P = 8, lgP = 3;
+  while (P < (u32)size) P <<= 1, ++lgP;
+  const bool own = (u32)t * PER < P;  // this thread holds 8 keys of the network
   // group index of each element: inclusive count of group starts after the first
   u32 f[PER], run = 0;
 #pragma unroll
@@ -1271,66 +1279,71 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
   for (int k = 0; k < PER; ++k) {
     const u32 x = t * PER + k;
     g += f[k];
-    v[k] = x < (u32)size ? ((u64)g << 51) | ((hi[s + x] >> 26) << 13) | x : ~0ull;
+    v[k] = x < (u32)size ? ((u64)g << 51) | ((hi[s + x] >> 26) << 13) | x : ~0ull;  // padding sorts last
   }
-  // merge levels k = 2, 4, 8 inside the thread's block (all-ascending: lower keeps min)
-  seg_cx(v[0], v[1]); seg_cx(v[2], v[3]); seg_cx(v[4], v[5]); seg_cx(v[6], v[7]);
-  seg_cx(v[0], v[3]); seg_cx(v[1], v[2]); seg_cx(v[4], v[7]); seg_cx(v[5], v[6]);
-  seg_cx(v[0], v[1]); seg_cx(v[2], v[3]); seg_cx(v[4], v[5]); seg_cx(v[6], v[7]);
-  seg_cx(v[0], v[7]); seg_cx(v[1], v[6]); seg_cx(v[2], v[5]); seg_cx(v[3], v[4]);
-  seg_cx(v[0], v[2]); seg_cx(v[1], v[3]); seg_cx(v[4], v[6]); seg_cx(v[5], v[7]);
-  seg_cx(v[0], v[1]); seg_cx(v[2], v[3]); seg_cx(v[4], v[5]); seg_cx(v[6], v[7]);
-  if (own)
+  // merge levels k = 2, 4, 8: keys 8t .. 8t+7 (b = 0)
+  seg_pass(v, (u32)t * 8, 0, 2, 0, 1);
+  seg_pass(v, (u32)t * 8, 0, 4, 1, 2);
+  seg_pass(v, (u32)t * 8, 0, 8, 2, 3);
+  // later levels: a pass per window b of three partner bits; the keys move between
+  // layouts through LDS (write in the old layout, read in the new one)
+  u32 cur = 0;  // layout of v
+  auto base_of = [&](u32 b) { return ((u32)t >> b << (b + 3)) | ((u32)t & ((1u << b) - 1)); };
+  for (u32 lk = 4; lk <= lgP; ++lk) {
+    const u32 k = 1u << lk;
+    for (int jb = (int)lk - 1; jb >= 0;) {
+      const u32 b = jb >= 2 ? (u32)jb - 2 : 0u;
+      if (b != cur) {
+        __syncthreads();  // the previous layout's reads are done
+        if (own) {
+          const u32 bo = base_of(cur);
 #pragma unroll
-    for (int k = 0; k < PER; ++k) key[t * PER + k] = v[k];
-  __syncthreads();
-  for (u32 k = 16; k <= P; k <<= 1) {
-    for (u32 j = k >> 1; j >= 8; j >>= 1) {  // pair exchanges through LDS
-      const u32 mask = j == (k >> 1) ? k - 1 : j;
-      for (u32 r = t; r < P / 2; r += SEG_NT) {
-        const u32 i = ((r & ~(j - 1)) << 1) | (r & (j - 1)), q = i ^ mask;
-        const u64 a = key[i], b = key[q];
-        if (b < a) {
-          key[i] = b;
-          key[q] = a;
+          for (int m = 0; m < PER; ++m) key[SEGPAD(bo | ((u32)m << cur))] = v[m];
         }
+        __syncthreads();
+        if (own) {
+          const u32 bn = base_of(b);
+#pragma unroll
+          for (int m = 0; m < PER; ++m) v[m] = key[SEGPAD(bn | ((u32)m << b))];
+        }
+        cur = b;
       }
-      __syncthreads();
+      if (own) seg_pass(v, base_of(b), b, k, jb - (int)b, jb - (int)b + 1);
+      jb = (int)b - 1;
     }
-    if (own) {  // stages j = 4, 2, 1 in registers
-#pragma unroll
-      for (int m = 0; m < PER; ++m) v[m] = key[t * PER + m];
-      seg_tail8(v);
-#pragma unroll
-      for (int m = 0; m < PER; ++m) key[t * PER + m] = v[m];
-    }
-    __syncthreads();
   }
+  __syncthreads();
+  if (own) {
+    const u32 bo = base_of(cur);
+#pragma unroll
+    for (int m = 0; m < PER; ++m) key[SEGPAD(bo | ((u32)m << cur))] = v[m];
+  }
+  __syncthreads();
   // runs of equal (group, hi38): exact order on (oid_hi, oid_lo, index)
   for (u32 x = t; x + 1 < (u32)size; x += SEG_NT) {
-    const u64 kx = key[x] >> 13;
-    if ((key[x + 1] >> 13) != kx || (x > 0 && (key[x - 1] >> 13) == kx)) continue;
+    const u64 kx = key[SEGPAD(x)] >> 13;
+    if ((key[SEGPAD(x + 1)] >> 13) != kx || (x > 0 && (key[SEGPAD(x - 1)] >> 13) == kx)) continue;
     u32 e = x + 2;
-    while (e < (u32)size && (key[e] >> 13) == kx) ++e;
+    while (e < (u32)size && (key[SEGPAD(e)] >> 13) == kx) ++e;
     for (u32 y = x + 1; y < e; ++y) {
-      const u64 ky = key[y];
+      const u64 ky = key[SEGPAD(y)];
       const u32 vi = (u32)ky & 0x1fffu;
       const u64 vh = hi[s + vi], vl = lo[s + vi];
       u32 z = y;
       while (z > x) {
-        const u64 kw = key[z - 1];
+        const u64 kw = key[SEGPAD(z - 1)];
         const u32 wi = (u32)kw & 0x1fffu;
         const u64 wh = hi[s + wi], wl = lo[s + wi];
         if (!(vh < wh || (vh == wh && (vl < wl || (vl == wl && vi < wi))))) break;
-        key[z] = kw;
+        key[SEGPAD(z)] = kw;
         --z;
       }
-      key[z] = ky;
+      key[SEGPAD(z)] = ky;
     }
   }
   __syncthreads();
   for (u32 x = t; x < (u32)size; x += SEG_NT) {
-    const i64 src = s + (key[x] & 0x1fffu);
+    const i64 src = s + (key[SEGPAD(x)] & 0x1fffu);
     sts[s + x] = ts[src];
     shi[s + x] = hi[src];
     slo[s + x] = lo[src];
@@ -1469,7 +1482,7 @@ static int run_order(const Ctx& C, bool allow_generic, ComposeMeta* hm) {
   int rc = run_presorted(C, tgt);
   if (rc) return rc;
   if ((rc = read_meta(C, hm))) return rc;
-  while (hm->f_fail == 2 && !hm->bad_sym && tgt > WIN_TGT_MIN) {
+  while (hm->f_fail == 2 && !hm->bad_sym && tgt > WIN_TGT_MIN) {  // dense groups: smaller windows
     tgt = (tgt / 2) / CH * CH;
     if ((rc = run_presorted(C, tgt))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
@@ -1478,7 +1491,7 @@ static int run_order(const Ctx& C, bool allow_generic, ComposeMeta* hm) {
     if (C.ops->b_gap != 0)
       return set_err(SMX_E_ARG, "branch logs not timestamp-ordered: the generic plan needs b_gap = 0");
     bool fallback = true;
-    if (hm->f_fail == 2 && (rc = run_generic(C, GEN_SEG, &fallback))) return rc;  // ordered, long groups
+    if (!(hm->f_fail & 1) && (rc = run_generic(C, GEN_SEG, &fallback))) return rc;  // ordered, long groups
     if (fallback) {
       if ((rc = run_generic(C, GEN_RADIX, &fallback))) return rc;
       if ((rc = read_meta(C, hm))) return rc;

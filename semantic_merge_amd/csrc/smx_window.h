@@ -164,9 +164,19 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   const int nb = (int)(P.bnd[2 * w + 3] - b0);
   const int sz = na + nb;
   if (na < 0 || nb < 0 || sz > WIN_CAP) {  // the presorted plan does not hold
-    // bit 0: branch logs not timestamp-ordered; bit 1: window too large for LDS
-    if (threadIdx.x == 0)
-      atomicOr((unsigned long long*)&P.meta->f_fail, (na < 0 || nb < 0) ? 1ull : 2ull);
+    // bit 0: branch logs not timestamp-ordered; bit 1: window too large for LDS;
+    // bit 2: ... and it holds one timestamp only, so smaller windows cannot help
+    if (threadIdx.x == 0) {
+      u64 f = 1;
+      if (na >= 0 && nb >= 0) {
+        const u64* A = P.kts + a0;
+        const u64* B = P.kts + P.na + P.bgap + b0;
+        const u64 v = na ? A[0] : B[0];
+        const bool one = (!na || (A[0] == v && A[na - 1] == v)) && (!nb || (B[0] == v && B[nb - 1] == v));
+        f = one ? 6 : 2;
+      }
+      atomicOr((unsigned long long*)&P.meta->f_fail, (unsigned long long)f);
+    }
     return;
   }
   if (sz == 0) return;

@@ -1,5 +1,7 @@
 """A/B timing of the compose stages for one library build (SMX_LIB=...):
-median over rounds of per-stage ms on the c3 workload (or argv[1] ops)."""
+median over rounds of per-stage ms per merge (all calls of a stage in one merge summed,
+e.g. failed presorted attempts before the generic plan) on the c3 workload (or
+argv[1] ops of config argv[2])."""
 import os
 import sys
 
@@ -22,16 +24,17 @@ def main():
         dc.run()
     torch.cuda.synchronize()
     res = {}
+    runs = 3
     for _ in range(5):
         lib.smx_reset_stage_times()
         lib.smx_set_profiling(1)
-        for _ in range(3):
+        for _ in range(runs):
             dc.run()
         torch.cuda.synchronize()
         lib.smx_set_profiling(0)
         for k, (ms, c) in _lib.stage_times().items():
             if c:
-                res.setdefault(k, []).append(ms / c)
+                res.setdefault(k, []).append(ms / runs)
     tot = sum(np.median(v) for v in res.values())
     print("  ".join(f"{k} {np.median(v):.3f}" for k, v in res.items()) + f"  | total {tot:.3f} ms")
 
