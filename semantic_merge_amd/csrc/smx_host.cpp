@@ -561,7 +561,99 @@ PyObject* materialize_ops(PyObject*, PyObject* args) {
   return out.release();
 }
 
+// ---------------------------------------------------------------- Op.from_dict
+
+// dict(x) (new reference): a copy of an exact dict, else the dict constructor.
+PyObject* dict_of(PyObject* x) {
+  if (PyDict_CheckExact(x)) return PyDict_Copy(x);
+  return PyObject_CallOneArg((PyObject*)&PyDict_Type, x);
+}
+
+// ops_from_dicts(items, op_cls, target_cls, ctor_mode) -> List[Op]: Op.from_dict of every
+// item (ops.py:89-100), in the same evaluation order and with the same coercions:
+//   id=str(d["id"]), schemaVersion=int(d.get("schemaVersion", 1)), type=d["type"],
+//   target=Target(**d["target"]), params/guards/effects/provenance=dict(d.get(k, {}))
+PyObject* ops_from_dicts(PyObject*, PyObject* args) {
+  PyObject *items, *op_cls, *tcls;
+  Ctor ctor;
+  if (!PyArg_ParseTuple(args, "O!O!O!O", &PyList_Type, &items, &PyType_Type, &op_cls, &PyType_Type, &tcls,
+                        &ctor.mode_fn))
+    return nullptr;
+  GcPause gc_pause;
+  const Py_ssize_t n = PyList_GET_SIZE(items);
+  Ref one(PyLong_FromLong(1));
+  if (!one) return nullptr;
+  Ref out(PyList_New(n));
+  if (!out) return nullptr;
+  PyObject* const keys4[4] = {N.params, N.guards, N.effects, N.provenance};
+  for (Py_ssize_t k = 0; k < n; ++k) {
+    PyObject* d = PyList_GET_ITEM(items, k);
+    Ref id_raw(PyObject_GetItem(d, N.id));
+    if (!id_raw) return nullptr;
+    Ref id(PyObject_Str(id_raw.p));
+    if (!id) return nullptr;
+    Ref sv_raw(map_get(d, N.schemaVersion, one.p));
+    if (!sv_raw) return nullptr;
+    Ref sv(PyNumber_Long(sv_raw.p));
+    if (!sv) return nullptr;
+    Ref ty(PyObject_GetItem(d, N.type));
+    if (!ty) return nullptr;
+    Ref tg_raw(PyObject_GetItem(d, N.target));
+    if (!tg_raw) return nullptr;
+    Ref tg;
+    {  // Target(**target): the plain-dataclass fast path needs exactly symbolId and addressId
+      PyObject *sym = nullptr, *addr = nullptr;
+      if (PyDict_CheckExact(tg_raw.p) && PyDict_GET_SIZE(tg_raw.p) == 2) {
+        sym = PyDict_GetItemWithError(tg_raw.p, N.symbolId);
+        if (!sym && PyErr_Occurred()) return nullptr;
+        addr = sym ? PyDict_GetItemWithError(tg_raw.p, N.addressId) : nullptr;
+        if (!addr && PyErr_Occurred()) return nullptr;
+      }
+      const int mode = sym && addr ? ctor.mode((PyTypeObject*)tcls, N.kw_target) : 0;
+      if (mode < 0) return nullptr;
+      if (mode > 0) {
+        PyObject* a[2] = {sym, addr};
+        tg.reset(ctor.make((PyTypeObject*)tcls, a, N.kw_target));
+      } else {
+        Ref kw(PyDict_New());
+        if (!kw) return nullptr;
+        if (PyDict_Update(kw.p, tg_raw.p) < 0) {  // `**` of a non-mapping: the same TypeError text
+          if (PyErr_ExceptionMatches(PyExc_AttributeError)) {
+            PyErr_Clear();
+            PyErr_Format(PyExc_TypeError, "%.200s() argument after ** must be a mapping, not %.200s",
+                         ((PyTypeObject*)tcls)->tp_name, Py_TYPE(tg_raw.p)->tp_name);
+          }
+          return nullptr;
+        }
+        tg.reset(PyObject_Call(tcls, N.empty, kw.p));
+      }
+      if (!tg) return nullptr;
+    }
+    Ref vals[4];
+    for (int q = 0; q < 4; ++q) {  // dict(d.get(k, {}))
+      if (PyDict_CheckExact(d)) {
+        PyObject* v = PyDict_GetItemWithError(d, keys4[q]);
+        if (!v && PyErr_Occurred()) return nullptr;
+        vals[q].reset(v ? dict_of(v) : PyDict_New());
+      } else {
+        Ref dflt(PyDict_New());
+        if (!dflt) return nullptr;
+        Ref raw(PyObject_CallMethodObjArgs(d, N.get, keys4[q], dflt.p, nullptr));
+        if (!raw) return nullptr;
+        vals[q].reset(dict_of(raw.p));
+      }
+      if (!vals[q]) return nullptr;
+    }
+    PyObject* a8[8] = {id.p, sv.p, ty.p, tg.p, vals[0].p, vals[1].p, vals[2].p, vals[3].p};
+    PyObject* op = ctor.make((PyTypeObject*)op_cls, a8, N.kw_op);
+    if (!op) return nullptr;
+    PyList_SET_ITEM(out.p, k, op);
+  }
+  return out.release();
+}
+
 PyMethodDef methods[] = {
+    {"ops_from_dicts", ops_from_dicts, METH_VARARGS, "Op.from_dict over a list (ops.py:89-100)."},
     {"marshal_ops", marshal_ops, METH_VARARGS, "List[Op] -> SoA columns (see marshal.py)."},
     {"materialize_ops", materialize_ops, METH_VARARGS, "device results -> List[Op] (see materialize.py)."},
     {"deep_copy", py_deep_copy, METH_VARARGS, "copy.deepcopy with a native JSON-tree path."},

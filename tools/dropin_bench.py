@@ -4,6 +4,8 @@ shape: a synthetic two-branch lift log), split into its host and device parts.
     python tools/dropin_bench.py [--n-ops 1000000] [--ref] [--gpu] [--out FILE]
 
 Legs (seconds, median of --reps):
+  python_from_dict / native_from_dicts  decoding the worker's op dicts into Op objects
+                                        (Op.from_dict per op vs oplog.ops_from_dicts)
   python_marshal / python_materialize   the Python restatement (marshal.py, materialize.py)
   native_marshal / native_materialize   csrc/smx_host.cpp (what compose_oplogs runs)
   gpu_compose                           compose_soa on cuda:0, SoA already on the host (--gpu)
@@ -53,9 +55,14 @@ def main():
 
     logs = synth.lift_logs(synth.LiftSpec(a.n_ops, a.n_sym, 11))
     A, B = synth.lift_op_dicts(logs)
-    oa, ob = [Op.from_dict(d) for d in A], [Op.from_dict(d) for d in B]
+    res = {"n_ops": len(A) + len(B), "reps": a.reps}
+    res["python_from_dict"], (oa, ob) = timed(
+        lambda: ([Op.from_dict(d) for d in A], [Op.from_dict(d) for d in B]), a.reps)
+    from semantic_merge_amd.oplog import ops_from_dicts
+    res["native_from_dicts"], (na_, nb_) = timed(lambda: (ops_from_dicts(A), ops_from_dicts(B)), a.reps)
+    assert na_ == oa and nb_ == ob
+    del na_, nb_
     ops = oa + ob
-    res = {"n_ops": len(ops), "reps": a.reps}
 
     res["python_marshal"], soa = timed(lambda: marshal(oa, ob), a.reps)
     res["native_marshal"], soa_n = timed(lambda: marshal_native(oa, ob), a.reps)
