@@ -611,7 +611,9 @@ __device__ __forceinline__ bool key_le(u64 ta, u64 ha, u64 la, u64 tb, u64 hb, u
   return la <= lb;
 }
 
-#define WG_NT 256
+#ifndef WG_NT
+#define WG_NT 1024
+#endif
 #define WG_ITEMS (WIN_CAP / WG_NT)
 
 __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
