@@ -594,8 +594,12 @@ struct EmitArgs {
 #define NTLD(p) (*(p))
 #define NTST(v, p) (*(p) = (v))
 #endif
+#ifndef EMIT_WT
 #define EMIT_WT 1024  // T positions per wave
+#endif
+#ifndef EMIT_B
 #define EMIT_B 8      // wave steps whose loads are issued together
+#endif
 
 // Each wave owns EMIT_WT consecutive T positions.  Output index = T minus the
 // skipped renames before T: a binary search of the sorted skip list at the
@@ -1025,7 +1029,7 @@ static int launch_tables(const Ctx& C, const WinArgs& P, u64* part_tab, u32 tag,
   *bucketed = false;
   const i64 n_sym = C.n_sym;
   TbArgs A{P.symT, P.mvA, P.mvF, P.Msym, P.Mstr, skip, meta, (u64)n, 1u, 1u, (u32)(n_sym - 1), 0, 0};
-  u64 width = SMX_CEIL_DIV((u64)n_sym, (u64)256);
+  u64 width = SMX_CEIL_DIV((u64)n_sym, (u64)TB_NBK_TGT);
   if (width < 1) width = 1;
   if (width > TB_WIDTH) width = TB_WIDTH;
   const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);

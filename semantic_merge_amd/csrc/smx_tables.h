@@ -12,15 +12,23 @@
 //   bits  0..30  r: record index (move T < nMv, or nMv + rename position)
 //   bits 32..43  symbol offset inside its bucket
 //   bit  44      the move has a newAddress      bit 45  the move has a newFile
+//   bits 46..55  bucket (k_tb_scatter's staging only; k_tb_reduce ignores them)
 #pragma once
 
 #include "smx_scan.h"
 
 #define TB_WIDTH 4096       // symbols per bucket
 #define TB_MAXBK 1024       // buckets handled by the bucketed path
-#define TB_NT 512           // scatter workgroup (49 KB LDS: 3 groups = 6 waves/SIMD)
+#ifndef TB_NT
+#define TB_NT 1024          // scatter workgroup: one 16384-record tile (136 KB LDS) per CU
+#endif
 #define TB_NW (TB_NT / WAVE)
-#define TB_ITEMS 8
+#ifndef TB_ITEMS
+#define TB_ITEMS 16         // 64-record runs per bucket and tile: full-line writes
+#endif
+#ifndef TB_NBK_TGT
+#define TB_NBK_TGT 256      // target bucket count (width = n_sym / this, <= TB_WIDTH)
+#endif
 #define TB_TILE (TB_NT * TB_ITEMS)
 
 struct TbArgs {
@@ -166,11 +174,10 @@ __global__ void __launch_bounds__(TB_NT) k_tb_hist(TbArgs A0, u32* __restrict__ 
 // in LDS, then every bucket's run is written contiguously.
 __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __restrict__ offs, int nblk,
                                                       u64* __restrict__ rec) {
-  __shared__ u64 stage[TB_TILE];        // 32 KB
+  __shared__ u64 stage[TB_TILE];        // TB_TILE * 8 bytes
   __shared__ u32 lstart[TB_MAXBK];      // local bucket starts (then cursors)
   __shared__ u32 gbase[TB_MAXBK];       // global start of this block's run in each bucket
   __shared__ u32 wsum[TB_NW + 1];
-  __shared__ u16 sbk[TB_TILE];          // bucket of each staged record
   const TbArgs A = tb_load(A0);
   const u64 nrec = A.nMv + A.nR;
   const u64 base = (u64)blockIdx.x * TB_TILE;
@@ -194,7 +201,7 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __re
       if (ok[it]) {
         const u32 b = s[it] / A.width;
         bk[it] = b;
-        q[it] = (u64)r | ((u64)(s[it] - b * A.width) << 32) | ((u64)fl[it] << 44);
+        q[it] = (u64)r | ((u64)(s[it] - b * A.width) << 32) | ((u64)fl[it] << 44) | ((u64)b << 46);
         atomicAdd(&lstart[b], 1u);
       }
     }
@@ -228,10 +235,12 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __re
     if (bk[it] == 0xffffffffu) continue;
     const u32 pos = atomicAdd(&lstart[bk[it]], 1u);
     stage[pos] = q[it];
-    sbk[pos] = (u16)bk[it];
   }
   __syncthreads();
-  for (u32 i = threadIdx.x; i < total; i += TB_NT) rec[gbase[sbk[i]] + i] = stage[i];
+  for (u32 i = threadIdx.x; i < total; i += TB_NT) {
+    const u64 q = stage[i];
+    rec[gbase[(u32)(q >> 46) & 0x3ffu] + i] = q;
+  }
 }
 
 #define TBR_NT 1024
