@@ -42,9 +42,17 @@
 // pass reads the input columns and packs the records; each pass stages a tile in LDS
 // in digit order and writes each digit's run of records contiguously, so every byte
 // moves in full cache lines.  Stable: each list's events stay in stream order.
-#define RREC_ITEMS 4
-#define RREC_TILE (BLOCK * RREC_ITEMS)  // 1024 records per block and pass
-#define RREC_SEG (RREC_TILE / NWAVES)   // contiguous records per wave
+#ifndef RR_NT
+#define RR_NT 1024                        // scatter workgroup
+#endif
+#define RR_NW (RR_NT / WAVE)
+#ifndef RREC_ITEMS
+#define RREC_ITEMS 3
+#endif
+#define RREC_TILE (RR_NT * RREC_ITEMS)    // 3072 records (120 KB) per block and pass
+#define RREC_SEG (RREC_TILE / RR_NW)      // contiguous records per wave
+#define RGA_NDIG 256                      // digits per pass
+static_assert(RREC_TILE % BLOCK == 0 && RREC_TILE <= 65535, "tile: k_rrec_hist blocks, u16 slots");
 
 __device__ __forceinline__ u32 rga_list_of(const smx_rga_ops& o, i64 i, i32* err) {
   const u32 l = o.list[i];
@@ -58,35 +66,41 @@ __device__ __forceinline__ u32 rga_list_of(const smx_rga_ops& o, i64 i, i32* err
 template <bool FIRST>
 __global__ void __launch_bounds__(BLOCK) k_rrec_hist(smx_rga_ops o, const u32* __restrict__ keys, int shift,
                                                      u32* __restrict__ hist, i32* __restrict__ err) {
-  __shared__ u32 h[256];
+  __shared__ u32 h[RGA_NDIG];
   h[threadIdx.x] = 0;
   __syncthreads();
   const i64 base = (i64)blockIdx.x * RREC_TILE;
 #pragma unroll
-  for (int it = 0; it < RREC_ITEMS; ++it) {
+  for (int it = 0; it < RREC_TILE / BLOCK; ++it) {
     const i64 i = base + it * BLOCK + threadIdx.x;
     if (i < o.n_ops) atomicAdd(&h[((FIRST ? rga_list_of(o, i, err) : keys[i]) >> shift) & 255u], 1u);
   }
   __syncthreads();
-  hist[(i64)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+  hist[(i64)blockIdx.x * RGA_NDIG + threadIdx.x] = h[threadIdx.x];
 }
 
+// One tile per block: wave multisplit of the tile's records by digit (ranks and
+// per-wave digit counts), block scan of the digit totals, records staged in LDS in
+// digit order, then every digit's run written contiguously (RREC_TILE / 256 records
+// per run on average: whole cache lines).  Pass 2+ reads the previous pass's records
+// word by word (consecutive lanes, consecutive words) into their staged slots.
 template <bool FIRST>
-__global__ void __launch_bounds__(BLOCK) k_rrec_scatter(smx_rga_ops o, const u32* __restrict__ kin,
+__global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32* __restrict__ kin,
                                                         const u64* __restrict__ rin, u32* __restrict__ kout,
                                                         u64* __restrict__ rout, int shift,
                                                         const u32* __restrict__ offs) {
-  __shared__ u64 srec[RREC_TILE * RGA_REC];  // 40 KB
+  __shared__ u64 srec[RREC_TILE * RGA_REC];  // 120 KB
   __shared__ u32 skey[RREC_TILE];
-  __shared__ u32 wc[NWAVES][256];  // per-wave digit counts, then offsets
-  __shared__ u32 lstart[256];
-  __shared__ u32 gofs[256];
+  __shared__ u16 spos[RREC_TILE];            // tile record -> staged slot (pass 2+)
+  __shared__ u16 wc[RR_NW][RGA_NDIG];        // per-wave digit counts, then offsets
+  __shared__ u32 lstart[RGA_NDIG];
+  __shared__ u32 gofs[RGA_NDIG];
   const int t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
   const i64 n = o.n_ops, base = (i64)blockIdx.x * RREC_TILE;
+  const u32 cnt = (u32)(n - base < RREC_TILE ? n - base : RREC_TILE);
   i32 dummy = 0;
-#pragma unroll
-  for (int q = 0; q < NWAVES; ++q) wc[q][t] = 0;
-  gofs[t] = offs[(i64)blockIdx.x * 256 + t];
+  for (int x = t; x < RR_NW * RGA_NDIG; x += RR_NT) (&wc[0][0])[x] = 0;
+  if (t < RGA_NDIG) gofs[t] = offs[(i64)blockIdx.x * RGA_NDIG + t];
   __syncthreads();
   const u64 lt = lanemask_lt();
   u32 key[RREC_ITEMS], dr[RREC_ITEMS];
@@ -99,13 +113,13 @@ __global__ void __launch_bounds__(BLOCK) k_rrec_scatter(smx_rga_ops o, const u32
     const u64 peers = wave_peers<8>(d, valid);
     const u32 before = wc[w][d];
     dr[it] = d | ((before + (u32)__popcll(peers & lt)) << 8);
-    if (valid && (peers >> lane) == 1ull) wc[w][d] = before + (u32)__popcll(peers);
+    if (valid && (peers >> lane) == 1ull) wc[w][d] = (u16)(before + (u32)__popcll(peers));
   }
   __syncthreads();
-  {
+  if (t < RGA_NDIG) {
     u32 tot = 0;
 #pragma unroll
-    for (int q = 0; q < NWAVES; ++q) tot += wc[q][t];
+    for (int q = 0; q < RR_NW; ++q) tot += wc[q][t];
     lstart[t] = tot;
   }
   __syncthreads();
@@ -124,24 +138,25 @@ __global__ void __launch_bounds__(BLOCK) k_rrec_scatter(smx_rga_ops o, const u32
     }
   }
   __syncthreads();
-  {
+  if (t < RGA_NDIG) {
     u32 acc = lstart[t];
 #pragma unroll
-    for (int q = 0; q < NWAVES; ++q) {
+    for (int q = 0; q < RR_NW; ++q) {
       const u32 c = wc[q][t];
-      wc[q][t] = acc;
+      wc[q][t] = (u16)acc;
       acc += c;
     }
   }
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < RREC_ITEMS; ++it) {
-    const i64 i = base + (i64)w * RREC_SEG + it * WAVE + lane;
+    const u32 li = (u32)(w * RREC_SEG + it * WAVE + lane);
+    const i64 i = base + li;
     if (i >= n) continue;
     const u32 d = dr[it] & 255u, p = wc[w][d] + (dr[it] >> 8);
     skey[p] = key[it];
-    u64* r = &srec[p * RGA_REC];
     if (FIRST) {
+      u64* r = &srec[p * RGA_REC];
       const u64 tt = (u64)o.t[i] ^ 0x8000000000000000ull;
       r[0] = ((u64)o.anchor[i] << 32) | (tt >> 32);
       r[1] = (tt << 32) | o.author[i];
@@ -150,18 +165,23 @@ __global__ void __launch_bounds__(BLOCK) k_rrec_scatter(smx_rga_ops o, const u32
       const u32 op = o.op[i] > 2 ? 0u : o.op[i];
       r[4] = ((u64)o.value[i] << 32) | (op << 30) | (u32)i;
     } else {
-      const u64* q = rin + (u64)i * RGA_REC;
-#pragma unroll
-      for (int k = 0; k < RGA_REC; ++k) r[k] = q[k];
+      spos[li] = (u16)p;
+    }
+  }
+  if (!FIRST) {
+    __syncthreads();
+    const u64* q = rin + (u64)base * RGA_REC;
+    for (u32 x = t; x < cnt * RGA_REC; x += RR_NT) {
+      const u32 r = x / RGA_REC, k = x - r * RGA_REC;
+      srec[spos[r] * RGA_REC + k] = __builtin_nontemporal_load(&q[x]);
     }
   }
   __syncthreads();
-  const u32 cnt = (u32)(n - base < RREC_TILE ? n - base : RREC_TILE);
-  for (u32 p = t; p < cnt; p += BLOCK) {
+  for (u32 p = t; p < cnt; p += RR_NT) {
     const u32 d = (skey[p] >> shift) & 255u;
     kout[gofs[d] + p - lstart[d]] = skey[p];
   }
-  for (u32 x = t; x < cnt * RGA_REC; x += BLOCK) {  // word-wise: consecutive lanes, consecutive words
+  for (u32 x = t; x < cnt * RGA_REC; x += RR_NT) {  // word-wise: consecutive lanes, consecutive words
     const u32 p = x / RGA_REC, k = x - p * RGA_REC;
     const u32 d = (skey[p] >> shift) & 255u;
     rout[(u64)(gofs[d] + p - lstart[d]) * RGA_REC + k] = srec[x];
@@ -633,10 +653,10 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
                            err);
       hscan(rhist, nblk, 256u, tsum, dstart, st);
       if (p == 0)
-        hipLaunchKernelGGL(k_rrec_scatter<true>, dim3(nblk), dim3(BLOCK), 0, st, o, nullptr, nullptr, kbuf[0],
+        hipLaunchKernelGGL(k_rrec_scatter<true>, dim3(nblk), dim3(RR_NT), 0, st, o, nullptr, nullptr, kbuf[0],
                            rbuf[0], 0, rhist);
       else
-        hipLaunchKernelGGL(k_rrec_scatter<false>, dim3(nblk), dim3(BLOCK), 0, st, o, kbuf[(p - 1) & 1],
+        hipLaunchKernelGGL(k_rrec_scatter<false>, dim3(nblk), dim3(RR_NT), 0, st, o, kbuf[(p - 1) & 1],
                            rbuf[(p - 1) & 1], kbuf[p & 1], rbuf[p & 1], 8 * p, rhist);
     }
     hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, kbuf[(npass - 1) & 1], n, nl, lstart);
