@@ -45,23 +45,61 @@ struct ComposeMeta {
 };
 
 // Per-symbol final states (addr, file, ctx).  When the bit widths of (value + 1)
-// add up to <= 64 they are packed into 8 bytes per symbol (half the gather
-// footprint for k_emit); otherwise int4 entries.
+// add up to <= 64 they are packed per symbol (a smaller gather footprint for
+// k_emit, whose lookups are bound by L2 misses); otherwise int4 entries.
+//   <= 48 bits: 6-byte entries, 21 per 128-byte line (6.1 MB at 2^20 symbols); one
+//               4-byte-aligned 8-byte load per lookup, never crossing a line
+//   <= 64 bits: 8-byte entries
+#ifndef SMX_FIN48
+#define SMX_FIN48 1
+#endif
 struct FinPack {
   u32 wa, wf;
-  bool packed;
+  bool packed;  // 6- or 8-byte entries
+  bool p48;     // 6-byte entries
 };
 
 __device__ __forceinline__ u32 bit_width32(u32 x) { return x ? 32u - (u32)__clz((int)x) : 0u; }
 
+__device__ __forceinline__ FinPack fin_pack_make(u32 wa, u32 wf, u32 wc, bool allow) {
+  const bool packed = allow && wa + wf + wc <= 64;
+  return FinPack{wa, wf, packed, SMX_FIN48 && packed && wa + wf + wc <= 48};
+}
+
 __device__ __forceinline__ FinPack fin_pack_of(const u32* vbits, bool allow) {
-  const u32 wa = bit_width32(vbits[0]), wf = bit_width32(vbits[1]), wc = bit_width32(vbits[2]);
-  return FinPack{wa, wf, allow && wa + wf + wc <= 64};
+  return fin_pack_make(bit_width32(vbits[0]), bit_width32(vbits[1]), bit_width32(vbits[2]), allow);
 }
 
 __device__ __forceinline__ u64 fin_encode(const FinPack& P, int a, int f, int c) {
   const u64 x = (u64)(u32)(a + 1) | ((u64)(u32)(f + 1) << P.wa);
   return P.wa + P.wf >= 64 ? x : x | ((u64)(u32)(c + 1) << (P.wa + P.wf));
+}
+
+// byte offset of symbol s's 6-byte entry
+__device__ __forceinline__ u64 fin48_off(u32 s) {
+  const u32 line = s / 21u;
+  return (u64)line * 128u + (u64)(s - line * 21u) * 6u;
+}
+__device__ __forceinline__ void fin48_store(void* fin, u32 s, u64 x) {
+  u16* p = reinterpret_cast<u16*>(reinterpret_cast<u8*>(fin) + fin48_off(s));
+  p[0] = (u16)x;
+  p[1] = (u16)(x >> 16);
+  p[2] = (u16)(x >> 32);
+}
+typedef u64 __attribute__((aligned(4))) u64_a4;
+__device__ __forceinline__ u64 fin48_load(const void* fin, u32 s) {
+  const u64 o = fin48_off(s);
+  const u64 w = *reinterpret_cast<const u64_a4*>(reinterpret_cast<const u8*>(fin) + (o & ~3ull));
+  return (w >> ((o & 2) * 8)) & 0xffffffffffffull;
+}
+// the packed word of symbol s (P.packed)
+__device__ __forceinline__ u64 fin_word(const FinPack& P, const void* fin, u32 s) {
+  return P.p48 ? fin48_load(fin, s) : reinterpret_cast<const u64*>(fin)[s];
+}
+__device__ __forceinline__ void fin_put(const FinPack& P, void* fin, u32 s, int a, int f, int c) {
+  if (P.p48) fin48_store(fin, s, fin_encode(P, a, f, c));
+  else if (P.packed) reinterpret_cast<u64*>(fin)[s] = fin_encode(P, a, f, c);
+  else reinterpret_cast<int4*>(fin)[s] = make_int4(a, f, c, 0);
 }
 
 __device__ __forceinline__ int4 fin_decode(const FinPack& P, u64 x) {

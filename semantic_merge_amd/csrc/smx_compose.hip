@@ -614,8 +614,7 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
     return (u64)j < E.na_loc ? (i32)(E.src_a + j) : (i32)(E.src_b + ((i64)j - (i64)E.na_loc));
   };
   const FinPack FP = fin_pack_of(M->vbits, E.allow_pack != 0);
-  const u64* fin8 = reinterpret_cast<const u64*>(E.fin);
-  auto fin_at = [&](u32 s) -> int4 { return FP.packed ? fin_decode(FP, fin8[s]) : E.fin[s]; };
+  auto fin_at = [&](u32 s) -> int4 { return FP.packed ? fin_decode(FP, fin_word(FP, E.fin, s)) : E.fin[s]; };
   const u64 rs = min(M->kcnt[KMOVE], E.n);
   const u64 re = min(rs + M->kcnt[KREN], E.n);
   const int lane = threadIdx.x & (WAVE - 1);
@@ -676,7 +675,7 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
       if (FP.packed) {
         u64 x[EMIT_B];
 #pragma unroll
-        for (int j = 0; j < EMIT_B; ++j) x[j] = fin8[sy[j]];
+        for (int j = 0; j < EMIT_B; ++j) x[j] = fin_word(FP, E.fin, sy[j]);
 #pragma unroll
         for (int j = 0; j < EMIT_B; ++j) F[j] = fin_decode(FP, x[j]);
       } else {
@@ -712,7 +711,7 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
       if (FP.packed) {
         u64 x[EMIT_B];
 #pragma unroll
-        for (int j = 0; j < EMIT_B; ++j) x[j] = fin8[sy[j]];
+        for (int j = 0; j < EMIT_B; ++j) x[j] = fin_word(FP, E.fin, sy[j]);
 #pragma unroll
         for (int j = 0; j < EMIT_B; ++j) F[j] = fin_decode(FP, x[j]);
       } else {
@@ -1606,15 +1605,13 @@ __global__ void k_fin_from_tab(const u64* __restrict__ tab, const i64* __restric
                                ComposeMeta* meta, int4* __restrict__ fin) {
   u32 w[3];
   for (int i = 0; i < 3; ++i) w[i] = (u32)min(max(glob[i], (i64)0), (i64)32);
-  const FinPack FP{w[0], w[1], w[0] + w[1] + w[2] <= 64};
+  const FinPack FP = fin_pack_make(w[0], w[1], w[2], true);
   if (blockIdx.x == 0 && threadIdx.x < 3)
     meta->vbits[threadIdx.x] = w[threadIdx.x] >= 32 ? ~0u : ((1u << w[threadIdx.x]) - 1u);
-  u64* fin8 = reinterpret_cast<u64*>(fin);
   for (i64 s = (i64)blockIdx.x * BLOCK + threadIdx.x; s < n_sym; s += (i64)gridDim.x * BLOCK) {
     const u64 a = tab[s], f = tab[n_sym + s], c = tab[2 * n_sym + s];
     const int va = a ? (int)(u32)a - 1 : -1, vf = f ? (int)(u32)f - 1 : -1, vc = c ? (int)(u32)c - 1 : -1;
-    if (FP.packed) fin8[s] = fin_encode(FP, va, vf, vc);
-    else fin[s] = make_int4(va, vf, vc, 0);
+    fin_put(FP, fin, (u32)s, va, vf, vc);
   }
 }
 

@@ -256,7 +256,6 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
                                                       const u64* __restrict__ rec, i64 n_sym,
                                                       int4* __restrict__ fin, u64* __restrict__ part, u32 tag) {
   const FinPack FP = fin_pack_of(A0.meta->vbits, true);
-  u64* fin8 = reinterpret_cast<u64*>(fin);
   __shared__ u32 tA[TB_WIDTH], tF[TB_WIDTH], tC[TB_WIDTH];
   const TbArgs A = tb_load(A0);
   const u32 b = blockIdx.x;
@@ -297,10 +296,8 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
       part[s0 + i] = a ? tg | (u32)(va + 1) : 0ull;
       part[n_sym + s0 + i] = f ? tg | (u32)(vf + 1) : 0ull;
       part[2 * n_sym + s0 + i] = c ? tg | (u32)(vc + 1) : 0ull;
-    } else if (FP.packed) {
-      fin8[s0 + i] = fin_encode(FP, va, vf, vc);
     } else {
-      fin[s0 + i] = make_int4(va, vf, vc, 0);
+      fin_put(FP, fin, s0 + i, va, vf, vc);
     }
   }
 }

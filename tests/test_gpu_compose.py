@@ -111,10 +111,10 @@ def test_gpu_segmented_plan_duplicate_ids():
     _eq_soa(compose_soa(soa), oracle.compose(soa), "segmented plan, duplicate ids")
 
 
-@pytest.mark.parametrize("bits", [20, 31], ids=["packed", "wide"])
+@pytest.mark.parametrize("bits", [15, 20, 31], ids=["packed48", "packed64", "wide"])
 def test_gpu_value_widths(bits):
-    """Value ids of `bits` bits: 3 x 20 fits the packed 8-byte final-state table,
-    3 x 31 does not (int4 table)."""
+    """Value ids of `bits` bits: 3 x 15 fits the 6-byte final-state table entries,
+    3 x 20 the 8-byte ones, 3 x 31 neither (int4 table)."""
     soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(300_000, 3_000, 47)))
     rng = np.random.default_rng(bits)
     hi = np.int64(1) << (bits - 1)
