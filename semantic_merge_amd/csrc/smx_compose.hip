@@ -838,7 +838,7 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_ORDER] = sz[B_SYMT] = sz[B_MVA] = sz[B_MVF] = (size_t)nn * 4;
   sz[B_MSYM] = sz[B_MCLS] = sz[B_MSTR] = sz[B_MOWN] = sz[B_RAB] = (size_t)nn * 4;
   sz[B_MSIDE] = (size_t)nn;
-  sz[B_FLAGS] = (size_t)nn;
+  sz[B_FLAGS] = (size_t)nn * 4;  // k_flags slots
   sz[B_FPOS] = sz[B_CAND] = sz[B_Q] = sz[B_PM] = sz[B_NCONF] = sz[B_NREAL] = sz[B_COFF] = (size_t)nn * 4;
   sz[B_SKIP] = (size_t)nn;
   sz[B_SKIPEX] = (size_t)nn * 4;
@@ -982,10 +982,13 @@ static int launch_walk(const Ctx& C, const WinArgs& P, const smx_shard* sh) {
   u8* skip = C.ws<u8>(B_SKIP);
   u32* skiplist = C.ws<u32>(B_SKIPEX);
   u32* part = C.ws<u32>(B_PART);
-  HIP_TRY(hipMemsetAsync(skip, 0, n, st));
+  // skip flags: cleared by k_flags over the rename block, unless an incoming
+  // region (sharded merge) writes some of them first
+  const bool zero_first = sh && sh->in_d > 0;
+  if (zero_first) HIP_TRY(hipMemsetAsync(skip, 0, n, st));
   hipLaunchKernelGGL(k_walk_init, dim3(1), dim3(1), 0, st, meta);
   const WalkArgs Wk = walk_args(C, P, sh);
-  u8* flags = C.ws<u8>(B_FLAGS);
+  u32* slots = C.ws<u32>(B_FLAGS);
   u32* bcnt = C.ws<u32>(B_FPOS);
   u32* cand = C.ws<u32>(B_CAND);
   u32* q = C.ws<u32>(B_Q);
@@ -1002,9 +1005,10 @@ static int launch_walk(const Ctx& C, const WinArgs& P, const smx_shard* sh) {
   if (sh && sh->in_d > 0)
     hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d, meta, P.order,
                        C.out->conflicts, (u64)C.out->conflict_cap, skip, skiplist);
-  hipLaunchKernelGGL(k_flags, dim3(nfb), dim3(BLOCK), 0, st, Wk, flags, bcnt);
+  hipLaunchKernelGGL(k_flags, dim3(nfb), dim3(BLOCK), 0, st, Wk, slots, bcnt, zero_first ? nullptr : skip);
   hipLaunchKernelGGL(k_flag_offsets, dim3(1), dim3(BLOCK), 0, st, Wk, bcnt, &meta->n_cand);
-  hipLaunchKernelGGL(k_compact, dim3(nfb), dim3(BLOCK), 0, st, Wk, flags, bcnt, cand);
+  hipLaunchKernelGGL(k_compact, dim3(SMX_CEIL_DIV(nfb, (u32)NWAVES)), dim3(BLOCK), 0, st, Wk, slots, bcnt, ncand_dev,
+                     cand);
   hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
   HIP_TRY((scan_excl<OpMax, u32, u32>(q, pm, 0, ncand_dev, part, (u32*)nullptr, st)));
   hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, cand, q, pm, nconf, meta, nreal);

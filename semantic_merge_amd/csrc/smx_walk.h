@@ -89,27 +89,46 @@ __device__ __forceinline__ WalkArgs walk_load(WalkArgs W) {
 // contiguous range of FLAG_TILE renames and also reports how many it flagged.
 #define FLAG_TILE (BLOCK * 8)
 
-__global__ void __launch_bounds__(BLOCK) k_flags(WalkArgs W0, u8* __restrict__ flags, u32* __restrict__ bcnt) {
+// The block's flagged positions go, in order, to its FLAG_TILE-slot range of
+// slots[] (k_compact then moves the few of them to their scanned offsets).
+// zskip != null: also clears the skip flags of the block's positions.
+__global__ void __launch_bounds__(BLOCK) k_flags(WalkArgs W0, u32* __restrict__ slots, u32* __restrict__ bcnt,
+                                                 u8* __restrict__ zskip) {
   const WalkArgs W = walk_load(W0);
   if (W.fail || (u64)blockIdx.x * FLAG_TILE >= W.nR) return;
-  __shared__ u32 c;
-  if (threadIdx.x == 0) c = 0;
-  __syncthreads();
+  constexpr int NI = FLAG_TILE / BLOCK;
+  __shared__ u32 wc[NI][NWAVES];
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   const u64 base = (u64)blockIdx.x * FLAG_TILE;
-  u32 mine = 0;
-  for (int it = 0; it < FLAG_TILE / BLOCK; ++it) {
+  u64 fb[NI];  // this wave's flag ballots
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
     const u64 m = base + (u64)it * BLOCK + threadIdx.x;
-    if (m >= W.nR) break;
-    const int s = W.Mside[m];
-    const u64 k = m - W.Mown[m];
-    const WalkHead h = walk_head(W, 1 - s, k);
-    const u8 f = h.ok && h.sym == W.Msym[m] && h.cls != W.Mcls[m];
-    flags[m] = f;
-    mine += f;
+    bool f = false;
+    if (m < W.nR) {
+      if (zskip) zskip[m] = 0;
+      const int s = W.Mside[m];
+      const u64 k = m - W.Mown[m];
+      const WalkHead h = walk_head(W, 1 - s, k);
+      f = h.ok && h.sym == W.Msym[m] && h.cls != W.Mcls[m];
+    }
+    fb[it] = __ballot(f);
+    if (lane == 0) wc[it][w] = (u32)__popcll(fb[it]);
   }
-  if (mine) atomicAdd(&c, mine);
   __syncthreads();
-  if (threadIdx.x == 0) bcnt[blockIdx.x] = c;
+  u32 before = 0;  // flags of this block before (it, wave w)
+  const u64 lt = lanemask_lt();
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    if ((fb[it] >> lane) & 1ull) {
+      u32 r = before + (u32)__popcll(fb[it] & lt);
+      for (int q = 0; q < w; ++q) r += wc[it][q];
+      slots[base + r] = (u32)(base + (u64)it * BLOCK + threadIdx.x);
+    }
+#pragma unroll
+    for (int q = 0; q < NWAVES; ++q) before += wc[it][q];
+  }
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = before;
 }
 
 // Exclusive scan of the per-block flag counts (one block; nb is small) and the
@@ -141,30 +160,18 @@ __global__ void __launch_bounds__(BLOCK) k_flag_offsets(WalkArgs W0, u32* __rest
   if (threadIdx.x == 0) *total = carry;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_compact(WalkArgs W0, const u8* __restrict__ flags,
-                                                   const u32* __restrict__ boff, u32* __restrict__ out) {
+// One wave per k_flags block: its slots[] run -> cand[] at the block's offset
+// (boff = exclusive scan of the counts; the total is meta->n_cand).
+__global__ void __launch_bounds__(BLOCK) k_compact(WalkArgs W0, const u32* __restrict__ slots,
+                                                   const u32* __restrict__ boff, const u64* __restrict__ total,
+                                                   u32* __restrict__ out) {
   const WalkArgs W = walk_load(W0);
-  const u64 n = W.nR;
-  if (W.fail || (u64)blockIdx.x * FLAG_TILE >= n) return;
-  __shared__ u32 wbase[NWAVES + 1];
-  const u64 base = (u64)blockIdx.x * FLAG_TILE;
-  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-  u32 run = boff[blockIdx.x];
-  for (int it = 0; it < FLAG_TILE / BLOCK; ++it) {
-    const u64 m = base + (u64)it * BLOCK + threadIdx.x;
-    const bool f = m < n && flags[m];
-    const u64 b = __ballot(f);
-    if (lane == 0) wbase[w] = __popcll(b);
-    __syncthreads();
-    u32 before = 0, tot = 0;
-    for (int q = 0; q < NWAVES; ++q) {
-      before += q < w ? wbase[q] : 0u;
-      tot += wbase[q];
-    }
-    if (f) out[run + before + __popcll(b & lanemask_lt())] = (u32)m;
-    run += tot;
-    __syncthreads();
-  }
+  const u64 fbk = (u64)blockIdx.x * NWAVES + threadIdx.x / WAVE;
+  const u64 nfb = SMX_CEIL_DIV(W.nR, (u64)FLAG_TILE);
+  if (W.fail || fbk >= nfb) return;
+  const u32 o = boff[fbk];
+  const u32 e = fbk + 1 < nfb ? boff[fbk + 1] : (u32)*total;
+  for (u32 i = threadIdx.x & (WAVE - 1); o + i < e; i += WAVE) out[o + i] = slots[fbk * FLAG_TILE + i];
 }
 
 // Replays the reference loop restricted to renames from position p with state
