@@ -847,7 +847,7 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_FIN] = (size_t)ns * 16;
   sz[B_PREFA] = sz[B_PREFF] = (size_t)nn * 4;
   sz[B_REC] = (size_t)nn * 8;
-  sz[B_TBHIST] = (size_t)TB_MAXBK * SMX_CEIL_DIV(nn, (i64)TB_TILE) * 4;
+  sz[B_TBHIST] = (size_t)(TB_MAXBK + 1) * SMX_CEIL_DIV(nn, (i64)TB_TILE) * 4;  // k_tb_scatter's lst
   sz[B_TBTOT] = (size_t)(TB_MAXBK + 1) * 4;  // bucket starts
   sz[B_HTS] = (size_t)TB_MAXBK * (SMX_CEIL_DIV(SMX_CEIL_DIV(nn, (i64)TB_TILE), (i64)HS_ROWS) + 1) * 4;
   sz[B_CCNT] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)256) + 2) * 4;
@@ -1006,7 +1006,7 @@ static int launch_walk(const Ctx& C, const WinArgs& P, const smx_shard* sh) {
     hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d, meta, P.order,
                        C.out->conflicts, (u64)C.out->conflict_cap, skip, skiplist);
   hipLaunchKernelGGL(k_flags, dim3(nfb), dim3(BLOCK), 0, st, Wk, slots, bcnt, zero_first ? nullptr : skip);
-  hipLaunchKernelGGL(k_flag_offsets, dim3(1), dim3(BLOCK), 0, st, Wk, bcnt, &meta->n_cand);
+  hipLaunchKernelGGL(k_flag_offsets, dim3(1), dim3(FO_NT), 0, st, Wk, bcnt, &meta->n_cand);
   hipLaunchKernelGGL(k_compact, dim3(SMX_CEIL_DIV(nfb, (u32)NWAVES)), dim3(BLOCK), 0, st, Wk, slots, bcnt, ncand_dev,
                      cand);
   hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
@@ -1041,14 +1041,10 @@ static int launch_tables(const Ctx& C, const WinArgs& P, u64* part_tab, u32 tag,
     A.width = (u32)width;
     A.nbk = (u32)nbk;
     const int nblk = (int)SMX_CEIL_DIV((u64)n, (u64)TB_TILE);
-    u32* hist = C.ws<u32>(B_TBHIST);
-    u32* total = C.ws<u32>(B_TBTOT);
+    u32* lst = C.ws<u32>(B_TBHIST);
     u64* rec = C.ws<u64>(B_REC);
-    hipLaunchKernelGGL(k_tb_hist, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk);
-    hscan(hist, nblk, (u32)nbk, C.ws<u32>(B_HTS), total, st);
-    hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, hist, nblk, rec);
-    hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, hist, nblk, total, rec, n_sym, fin,
-                       part_tab, tag);
+    hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, lst, rec);
+    hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, lst, rec, n_sym, fin, part_tab, tag);
   } else {
     // very large symbol spaces: device-scope atomics on the packed keys
     u32* tabA = C.ws<u32>(B_TABA);

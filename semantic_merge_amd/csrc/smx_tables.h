@@ -5,14 +5,15 @@
 // non-rename sees the last non-skipped rename.  "Last in T order" = max T.
 //
 // Scattered 64-bit device atomics run at ~26 G/s on MI355X; instead the
-// records are bucketed by symbol range (one counting pass + one LDS-staged
-// scatter pass, no global atomics) and each bucket is reduced by one workgroup
-// with 32-bit LDS max over record indices; the values are fetched once per
-// symbol at the end.  A record is 8 bytes:
+// records are bucketed by symbol range and each bucket is reduced by one
+// workgroup with 32-bit LDS max over record indices; the values are fetched once
+// per symbol at the end.  Bucketing needs no counting pass: k_tb_scatter sorts
+// each tile of TB_TILE records by bucket in LDS and writes the tile back in place
+// (fully coalesced) with its bucket starts lst[tile][0..nbk]; k_tb_reduce of
+// bucket b then reads that bucket's run of every tile.  A record is 8 bytes:
 //   bits  0..30  r: record index (move T < nMv, or nMv + rename position)
 //   bits 32..43  symbol offset inside its bucket
 //   bit  44      the move has a newAddress      bit 45  the move has a newFile
-//   bits 46..55  bucket (k_tb_scatter's staging only; k_tb_reduce ignores them)
 #pragma once
 
 #include "smx_scan.h"
@@ -73,7 +74,7 @@ __device__ __forceinline__ bool tb_record(const TbArgs& A, u64 r, u32* sym, u32*
 // The TB_ITEMS records of a lane (r = base + it * TB_NT + lane), loads issued
 // together: a tile is all moves, all renames, or (one tile) mixed.
 // VB: also OR (value + 1) of the tile's values into vb (addr, file, name) for the
-// packed final-state table widths (k_tb_hist only).
+// packed final-state table widths (k_tb_scatter only).
 template <bool VB = false>
 __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[TB_ITEMS], u32 (&fl)[TB_ITEMS],
                                          bool (&ok)[TB_ITEMS], u32* vb = nullptr) {
@@ -132,68 +133,30 @@ __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[T
   }
 }
 
-__global__ void __launch_bounds__(TB_NT) k_tb_hist(TbArgs A0, u32* __restrict__ hist, int nblk) {
-  __shared__ u32 h[TB_MAXBK];
-  __shared__ u32 vb[3];
-  const TbArgs A = tb_load(A0);
-  for (u32 i = threadIdx.x; i < A.nbk; i += TB_NT) h[i] = 0;
-  if (threadIdx.x < 3) vb[threadIdx.x] = 0;
-  __syncthreads();
-  const u64 nrec = A.nMv + A.nR;
-  const u64 base = (u64)blockIdx.x * TB_TILE;
-  if (base < nrec) {
-    u32 s[TB_ITEMS], fl[TB_ITEMS];
-    bool ok[TB_ITEMS];
-    u32 v3[3] = {0u, 0u, 0u};
-    tb_items<true>(A, base, s, fl, ok, v3);
-#pragma unroll
-    for (int it = 0; it < TB_ITEMS; ++it)
-      if (ok[it]) atomicAdd(&h[s[it] / A.width], 1u);
-    // value bit widths for the packed final-state table (smx_common.h FinPack)
-    u32 oa = v3[0], of = v3[1], oc = v3[2];
-    oa = wave_or_to_last(oa);
-    of = wave_or_to_last(of);
-    oc = wave_or_to_last(oc);
-    if ((threadIdx.x & (WAVE - 1)) == WAVE - 1) {
-      if (oa) atomicOr(&vb[0], oa);
-      if (of) atomicOr(&vb[1], of);
-      if (oc) atomicOr(&vb[2], oc);
-    }
-  }
-  __syncthreads();
-  for (u32 i = threadIdx.x; i < A.nbk; i += TB_NT) hist[(u64)blockIdx.x * A.nbk + i] = h[i];
-  if (threadIdx.x < 3 && vb[threadIdx.x]) {
-    u32* g = const_cast<ComposeMeta*>(A.meta)->vbits;
-    const u32 mine = vb[threadIdx.x];
-    const u32 cur = __hip_atomic_load(&g[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((cur | mine) != cur) atomicOr(&g[threadIdx.x], mine);
-  }
-}
-
-// Scatter into bucket order.  The block's records are counting-sorted by bucket
-// in LDS, then every bucket's run is written contiguously.
-__global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __restrict__ offs, int nblk,
-                                                      u64* __restrict__ rec) {
+// Tile-local bucket sort: the tile's records are counting-sorted by bucket in
+// LDS and written back to the tile's own range; lst[tile][b] = start of bucket b
+// in the tile, lst[tile][nbk] = the tile's record count.  Also ORs the value
+// widths of the packed final-state table (smx_common.h FinPack) into meta->vbits.
+__global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict__ lst, u64* __restrict__ rec) {
   __shared__ u64 stage[TB_TILE];        // TB_TILE * 8 bytes
   __shared__ u32 lstart[TB_MAXBK];      // local bucket starts (then cursors)
-  __shared__ u32 gbase[TB_MAXBK];       // global start of this block's run in each bucket
   __shared__ u32 wsum[TB_NW + 1];
+  __shared__ u32 vb[3];
   const TbArgs A = tb_load(A0);
   const u64 nrec = A.nMv + A.nR;
   const u64 base = (u64)blockIdx.x * TB_TILE;
   if (base >= nrec) return;
   const u32 nbk = A.nbk;
-  for (u32 i = threadIdx.x; i < nbk; i += TB_NT) {
-    lstart[i] = 0;
-    gbase[i] = offs[(u64)blockIdx.x * nbk + i];
-  }
+  for (u32 i = threadIdx.x; i < nbk; i += TB_NT) lstart[i] = 0;
+  if (threadIdx.x < 3) vb[threadIdx.x] = 0;
   __syncthreads();
   u64 q[TB_ITEMS];
   u32 bk[TB_ITEMS];
   {
     u32 s[TB_ITEMS], fl[TB_ITEMS];
     bool ok[TB_ITEMS];
-    tb_items(A, base, s, fl, ok);
+    u32 v3[3] = {0u, 0u, 0u};
+    tb_items<true>(A, base, s, fl, ok, v3);
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
       const u64 r = base + (u64)it * TB_NT + threadIdx.x;
@@ -201,12 +164,19 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __re
       if (ok[it]) {
         const u32 b = s[it] / A.width;
         bk[it] = b;
-        q[it] = (u64)r | ((u64)(s[it] - b * A.width) << 32) | ((u64)fl[it] << 44) | ((u64)b << 46);
+        q[it] = (u64)r | ((u64)(s[it] - b * A.width) << 32) | ((u64)fl[it] << 44);
         atomicAdd(&lstart[b], 1u);
       }
     }
+    u32 oa = wave_or_to_last(v3[0]), of = wave_or_to_last(v3[1]), oc = wave_or_to_last(v3[2]);
+    if ((threadIdx.x & (WAVE - 1)) == WAVE - 1) {
+      if (oa) atomicOr(&vb[0], oa);
+      if (of) atomicOr(&vb[1], of);
+      if (oc) atomicOr(&vb[2], oc);
+    }
   }
   __syncthreads();
+  u32* lt = lst + (u64)blockIdx.x * (nbk + 1);
   {
     u32 v[TB_MAXBK / TB_NT];
     u32 acc = 0;
@@ -221,15 +191,25 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __re
 #pragma unroll
     for (int j = 0; j < TB_MAXBK / TB_NT; ++j) {
       const u32 b = threadIdx.x * (TB_MAXBK / TB_NT) + j;
-      if (b < nbk) lstart[b] = run;
+      if (b < nbk) {
+        lstart[b] = run;
+        lt[b] = run;
+      }
       run += v[j];
     }
-    if (threadIdx.x == 0) wsum[TB_NW] = tot;
+    if (threadIdx.x == 0) {
+      wsum[TB_NW] = tot;
+      lt[nbk] = tot;
+    }
+  }
+  if (threadIdx.x < 3 && vb[threadIdx.x]) {
+    u32* g = const_cast<ComposeMeta*>(A.meta)->vbits;
+    const u32 mine = vb[threadIdx.x];
+    const u32 cur = __hip_atomic_load(&g[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cur | mine) != cur) atomicOr(&g[threadIdx.x], mine);
   }
   __syncthreads();
   const u32 total = wsum[TB_NW];
-  for (u32 i = threadIdx.x; i < nbk; i += TB_NT) gbase[i] -= lstart[i];
-  __syncthreads();
 #pragma unroll
   for (int it = 0; it < TB_ITEMS; ++it) {
     if (bk[it] == 0xffffffffu) continue;
@@ -237,22 +217,18 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, const u32* __re
     stage[pos] = q[it];
   }
   __syncthreads();
-  for (u32 i = threadIdx.x; i < total; i += TB_NT) {
-    const u64 q = stage[i];
-    rec[gbase[(u32)(q >> 46) & 0x3ffu] + i] = q;
-  }
+  for (u32 i = threadIdx.x; i < total; i += TB_NT) rec[base + i] = stage[i];
 }
 
 #define TBR_NT 1024
-#define TBR_U 8             // records per lane per step in k_tb_reduce
+#define TBR_TK 8            // tiles per wave step in k_tb_reduce
 
 // One workgroup per bucket: LDS max over record indices, then each symbol's
 // values are fetched once: fin[sym] = (addr, file, ctx, 0).
 // part != nullptr (sharded merge): instead of fin, write this shard's partial
 // tables part[3][n_sym] = (tag << 32) | (value + 1), 0 = no record; the MAX
 // all-reduce over shards then keeps the last writer (highest shard).
-__global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __restrict__ offs, int nblk,
-                                                      const u32* __restrict__ nrec_total,
+__global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __restrict__ lst,
                                                       const u64* __restrict__ rec, i64 n_sym,
                                                       int4* __restrict__ fin, u64* __restrict__ part, u32 tag) {
   const FinPack FP = fin_pack_of(A0.meta->vbits, true);
@@ -261,11 +237,6 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
   const u32 b = blockIdx.x;
   for (u32 i = threadIdx.x; i < A.width; i += TBR_NT) tA[i] = tF[i] = tC[i] = 0;
   __syncthreads();
-  const bool any = A.nMv + A.nR > 0;
-  const u32 lo = any ? nrec_total[b] : 0u;  // bucket starts (k_hscan_mid), nbk + 1 entries
-  const u32 hi = any ? nrec_total[b + 1] : 0u;
-  // TBR_U records per lane per step, loads issued together (one workgroup per
-  // bucket: its record stream needs the memory-level parallelism)
   auto put = [&](u64 q) {
     const u32 r1 = (u32)(q & 0x7fffffffu) + 1u;
     const u32 ls = (u32)(q >> 32) & 0xfffu;
@@ -276,15 +247,43 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
       atomicMax(&tC[ls], r1);
     }
   };
-  u32 i = lo + threadIdx.x;
-  for (; i + (TBR_U - 1) * TBR_NT < hi; i += TBR_U * TBR_NT) {
-    u64 q[TBR_U];
+  // bucket b's run in every tile: each wave takes TBR_TK tiles per step, up to
+  // 2 * WAVE records of each in flight together, longer runs finish in a tail loop
+  const u64 nrec = A.nMv + A.nR;
+  const int nt = nrec ? (int)SMX_CEIL_DIV(nrec, (u64)TB_TILE) : 0;
+  const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+  const u32 nb1 = A.nbk + 1;
+  constexpr int NW = TBR_NT / WAVE;
+  for (int t0 = wv * TBR_TK; t0 < nt; t0 += NW * TBR_TK) {
+    u32 lo = 0, hi = 0;
+    if (lane < TBR_TK && t0 + lane < nt) {
+      const u32* lt = lst + (u64)(t0 + lane) * nb1;
+      lo = lt[b];
+      hi = lt[b + 1];
+    }
+    u64 q[TBR_TK][2];
 #pragma unroll
-    for (int u = 0; u < TBR_U; ++u) q[u] = __builtin_nontemporal_load(&rec[i + u * TBR_NT]);
+    for (int k = 0; k < TBR_TK; ++k) {
+      const u32 lk = __builtin_amdgcn_readlane(lo, k), hk = __builtin_amdgcn_readlane(hi, k);
+      const u64 rb = (u64)(t0 + k) * TB_TILE;
 #pragma unroll
-    for (int u = 0; u < TBR_U; ++u) put(q[u]);
+      for (int u = 0; u < 2; ++u) {
+        const u32 i = lk + (u32)lane + (u32)(u * WAVE);
+        q[k][u] = i < hk ? __builtin_nontemporal_load(&rec[rb + i]) : ~0ull;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < TBR_TK; ++k)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (q[k][u] != ~0ull) put(q[k][u]);
+#pragma unroll
+    for (int k = 0; k < TBR_TK; ++k) {
+      const u32 lk = __builtin_amdgcn_readlane(lo, k), hk = __builtin_amdgcn_readlane(hi, k);
+      const u64 rb = (u64)(t0 + k) * TB_TILE;
+      for (u32 i = lk + 2 * WAVE + (u32)lane; i < hk; i += WAVE) put(rec[rb + i]);
+    }
   }
-  for (; i < hi; i += TBR_NT) put(rec[i]);
   __syncthreads();
   const u32 s0 = b * A.width;
   for (u32 i = threadIdx.x; i < A.width && (i64)(s0 + i) < n_sym; i += TBR_NT) {

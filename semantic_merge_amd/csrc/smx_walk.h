@@ -133,25 +133,26 @@ __global__ void __launch_bounds__(BLOCK) k_flags(WalkArgs W0, u32* __restrict__ 
 
 // Exclusive scan of the per-block flag counts (one block; nb is small) and the
 // candidate total into meta->n_cand.
-__global__ void __launch_bounds__(BLOCK) k_flag_offsets(WalkArgs W0, u32* __restrict__ bcnt, u64* total) {
+#define FO_NT 1024  // k_flag_offsets: one block, 16 counts per thread and round
+__global__ void __launch_bounds__(FO_NT) k_flag_offsets(WalkArgs W0, u32* __restrict__ bcnt, u64* total) {
   const WalkArgs W = walk_load(W0);
   if (W.fail) return;
   const u32 nb = (u32)SMX_CEIL_DIV(W.nR, (u64)FLAG_TILE);
-  __shared__ u32 s[NWAVES + 1];
+  __shared__ u32 s[FO_NT / WAVE + 1];
   u32 carry = 0;
-  for (u32 r0 = 0; r0 < nb; r0 += BLOCK * 8) {
-    const u32 b = r0 + threadIdx.x * 8;
-    u32 v[8];
+  for (u32 r0 = 0; r0 < nb; r0 += FO_NT * 16) {
+    const u32 b = r0 + threadIdx.x * 16;
+    u32 v[16];
     u32 acc = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 16; ++j) {
       v[j] = b + j < nb ? bcnt[b + j] : 0u;
       acc += v[j];
     }
     u32 tot;
-    u32 run = carry + block_excl_scan<OpSum, u32>(acc, s, &tot);
+    u32 run = carry + block_excl_scan<OpSum, u32, FO_NT / WAVE>(acc, s, &tot);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 16; ++j) {
       if (b + j < nb) bcnt[b + j] = run;
       run += v[j];
     }
