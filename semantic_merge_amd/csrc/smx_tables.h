@@ -221,7 +221,10 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
 }
 
 #define TBR_NT 1024
-#define TBR_TK 8            // tiles per wave step in k_tb_reduce
+#ifndef TBR_TK
+#define TBR_TK 8
+#endif
+// TBR_TK: tiles per wave step in k_tb_reduce
 
 // One workgroup per bucket: LDS max over record indices, then each symbol's
 // values are fetched once: fin[sym] = (addr, file, ctx, 0).
