@@ -45,6 +45,12 @@ def test_rga_batch_equals_oracle(n_ops, n_lists, seed):
     _check(synth.rga_batch(n_ops, n_lists, seed))
 
 
+@pytest.mark.timeout(300)
+def test_rga_config4_full_size():
+    """SURVEY §8(d) config 4 at its full size: 10M events over 50k lists, seed 13."""
+    _check(synth.rga_batch(10_000_000, 50_000, 13))
+
+
 def test_rga_dense_values_and_big_lists():
     # few values per list (long per-value chains) and lists beyond the LDS capacity
     _check(synth.rga_batch(60_000, 8, 16, values_per_list=3, anchors_per_list=2, authors=1))
