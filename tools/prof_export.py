@@ -15,7 +15,7 @@ def main():
     rows = con.execute("select name, total_calls, total_duration, average, percentage from top_kernels").fetchall()
     with open(dst, "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
+        w.writerow(["Name", "Calls", "TotalDurationUs", "AverageUs", "Percentage"])
         for r in rows:
             w.writerow([r[0], r[1], round(r[2], 1), round(r[3], 1), round(r[4], 3)])
 
