@@ -149,7 +149,7 @@ def main() -> None:
     achieved = WINDOW_BYTES_PER_OP * n / (win_avg * 1e-3) / 1e9 if win_avg > 0 else None
     traffic = None
     prof = os.path.join(REPO, "profiles", "pmc_window.json")
-    if os.path.exists(prof):
+    if os.path.exists(prof) and args.config == "c3":  # measured on the config-3 window kernel
         rec = json.load(open(prof))
         if rec.get("n_ops") == n:
             traffic = rec.get("hbm_bytes_per_launch")

@@ -9,8 +9,10 @@
 
 #include "smx_scan.h"
 
-#define RADIX_ITEMS 8
-#define RADIX_TILE (BLOCK * RADIX_ITEMS)   // 2048 pairs per block and pass
+#ifndef RADIX_ITEMS
+#define RADIX_ITEMS 16
+#endif
+#define RADIX_TILE (BLOCK * RADIX_ITEMS)   // 4096 pairs per block and pass (16-pair digit runs)
 #define RADIX_SEG (RADIX_TILE / NWAVES)     // contiguous elements per wave
 
 // Digit histogram of each block's tile, row-major hist[block][256].

@@ -68,6 +68,10 @@ CONFIGS: Dict[str, LiftSpec] = {
     # >= 64 renames per symbol, 4096 ops per ms (dense ties), seed 17
     "c5": LiftSpec(20_000_000, 100_000, 17, ops_per_ms=4096, mix=ADVERSARIAL_MIX,
                    rename_overlap=0.30),
+    # robustness variants of configs 2 and 3: each branch log randomly permuted, which
+    # forces the generic (radix) plan; reported, not targeted
+    "c2s": LiftSpec(1_000_000, 10_000, 7, shuffle=True),
+    "c3s": LiftSpec(100_000_000, 1_000_000, 11, shuffle=True),
 }
 
 
