@@ -541,6 +541,16 @@ __global__ void k_gather(const u64* __restrict__ key, const u32* __restrict__ id
     kout[i] = key[idx[i]];
 }
 
+// Two columns gathered through one read of the permutation.
+__global__ void k_gather2(const u64* __restrict__ a, const u64* __restrict__ b, const u32* __restrict__ idx,
+                          u64* __restrict__ aout, u64* __restrict__ bout, i64 n) {
+  for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (i64)gridDim.x * BLOCK) {
+    const u32 j = idx[i];
+    aout[i] = a[j];
+    bout[i] = b[j];
+  }
+}
+
 __global__ void k_offset(u32* __restrict__ v, i64 n, u32 off) {
   for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (i64)gridDim.x * BLOCK) v[i] += off;
 }
@@ -1420,9 +1430,10 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
         }
         if (ns) HIP_TRY(radix_sort_pairs(key, val, cnt, shifts, ns, rt, st));
       }
-      hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->ts, val, sts + off, cnt);
-      hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_hi, val, shi + off, cnt);
-      hipLaunchKernelGGL(k_gather, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_lo, val, slo + off, cnt);
+      // the last key word is ts, so the sorted keys are ts in sorted order already
+      HIP_TRY(hipMemcpyAsync(sts + off, key, (size_t)cnt * 8, hipMemcpyDeviceToDevice, st));
+      hipLaunchKernelGGL(k_gather2, dim3(grid_for(cnt)), dim3(BLOCK), 0, st, C.ops->oid_hi, C.ops->oid_lo, val,
+                         shi + off, slo + off, cnt);
     }
     if (!with_lo) hipLaunchKernelGGL(k_dupcheck, dim3(grid_for(n)), dim3(BLOCK), 0, st, sts, shi, na, n, meta);
   }

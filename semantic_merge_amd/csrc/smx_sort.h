@@ -12,6 +12,9 @@
 #ifndef RADIX_ITEMS
 #define RADIX_ITEMS 16
 #endif
+#ifndef RADIX_HIST_AGG
+#define RADIX_HIST_AGG 0
+#endif
 #define RADIX_TILE (BLOCK * RADIX_ITEMS)   // 4096 pairs per block and pass (16-pair digit runs)
 #define RADIX_SEG (RADIX_TILE / NWAVES)     // contiguous elements per wave
 
@@ -28,9 +31,20 @@ static __global__ void __launch_bounds__(BLOCK) k_radix_hist(const u64* __restri
     const i64 i = base + it * BLOCK + threadIdx.x;
     d[it] = i < n ? (u32)(keys[i] >> shift) & 255u : 256u;
   }
+#if RADIX_HIST_AGG
+  // one LDS atomic per distinct digit per wave (slow-varying digits, e.g. timestamp
+  // bytes, would otherwise serialise on one bin)
+  const u64 lt = lanemask_lt();
+#pragma unroll
+  for (int it = 0; it < RADIX_ITEMS; ++it) {
+    const u64 peers = wave_peers<8>(d[it] & 255u, d[it] < 256u);
+    if (d[it] < 256u && (peers & lt) == 0) atomicAdd(&h[d[it]], (u32)__popcll(peers));
+  }
+#else
 #pragma unroll
   for (int it = 0; it < RADIX_ITEMS; ++it)
     if (d[it] < 256u) atomicAdd(&h[d[it]], 1u);
+#endif
   __syncthreads();
   hist[(i64)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
 }
@@ -45,8 +59,8 @@ static __global__ void __launch_bounds__(BLOCK) k_radix_scatter(const u64* __res
                                                                 u64* __restrict__ kout,
                                                                 u32* __restrict__ vout, i64 n, int shift,
                                                                 const u32* __restrict__ offs, int nblk) {
-  __shared__ u64 sk[RADIX_TILE];          // 16 KB
-  __shared__ u32 sv[RADIX_TILE];          // 8 KB
+  __shared__ u64 sk[RADIX_TILE];          // 32 KB at 4096 pairs
+  __shared__ u32 sv[RADIX_TILE];          // 16 KB
   __shared__ u32 wc[NWAVES][256];         // per-wave digit counts, then offsets
   __shared__ u32 lstart[256];             // local digit starts
   __shared__ u32 gofs[256];               // global start of this block's digit runs
