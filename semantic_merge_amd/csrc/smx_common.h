@@ -42,6 +42,7 @@ struct ComposeMeta {
   u64 nskip_in;              // skipped renames of the incoming region (head of the skip list)
   u64 dup_key;               // generic plan: equal (ts, oid_hi) pair seen -> sort with oid_lo
   u64 seg_over;              // segmented plan: a timestamp group too long, or a branch not ordered
+  u64 n_win;                 // windows of the plan that ran
 };
 
 // Per-symbol final states (addr, file, ctx).  When the bit widths of (value + 1)

@@ -19,11 +19,14 @@
 //   k_wscan     window offsets and kind totals  k_bases   T segment starts
 //   [generic]   radix-sort each branch by (ts, oid) and cut fixed windows
 //   k_window    per window, in LDS: merge A/B parts, multisplit by kind, sort
-//               equal-timestamp groups by id, write T-ordered arrays
-//   walk        k_flags -> compact -> k_replay_q -> max-scan -> k_cluster ->
-//               scan -> k_replay_write (conflict pairs, skip flags, sorted skip list)
+//               equal-timestamp groups by id; the moves' final records, the other
+//               ops' (source, symbol) in T order, natural-head DivergentRename flags
+//   walk        k_boundary -> candidate scan/compact -> k_replay_q -> max-scan ->
+//               k_cluster -> scan -> k_replay_write (conflict pairs, skip bits,
+//               sorted skip list)
 //   tables      per-symbol last writers: bucket by symbol range, LDS max-reduce
-//   k_emit      compacted output: order, addr, file, ctx
+//   k_emit      compacted output of every op after the move block: order, addr,
+//               file, ctx
 #include <mutex>
 #include <string>
 #include <vector>
@@ -514,8 +517,9 @@ __global__ void __launch_bounds__(BLOCK) k_wscan(const u32* __restrict__ wcnt, u
   }
 }
 
-// T bases: exclusive prefix of the kind totals.
-__global__ void k_bases(ComposeMeta* meta) {
+// T bases: exclusive prefix of the kind totals; the plan's window count.
+__global__ void k_bases(ComposeMeta* meta, u64 nwin) {
+  meta->n_win = nwin;
   u64 acc = 0;
   for (int k = 0; k < SMX_N_KINDS; ++k) {
     meta->base[k] = acc;
@@ -558,231 +562,173 @@ __global__ void k_offset(u32* __restrict__ v, i64 n, u32 off) {
 #include "smx_walk.h"
 
 // ---------------------------------------------------------------------------
-// kernels: per-symbol last writers and output
-
-
-
-
-__global__ void k_mv_init(const u32* __restrict__ symT, u64 nMv, u64* __restrict__ keys,
-                          u32* __restrict__ vals) {
-  for (u64 j = (u64)blockIdx.x * BLOCK + threadIdx.x; j < nMv; j += (u64)gridDim.x * BLOCK) {
-    keys[j] = symT[j];
-    vals[j] = (u32)j;
-  }
-}
-
+// kernels: output of the renames and the other kinds; None-value moves
 
 struct EmitArgs {
-  const i32* order;
-  const u32* symT;
-  const i32* mvA;
-  const i32* mvF;
-  const u8* skip;
-  const u32* skiplist;
+  const i32* tsrc;     // P = T - nMv: local source op (renames first, then the rest)
+  const u32* tsym;
+  const u64* skipbits; // renames skipped by the walk
+  const u32* skiplist; // ... as a sorted list
   const int4* fin;
   const ComposeMeta* meta;
   u64 n;
   u32 smax;
   int allow_pack;  // the final-state table came from k_tb_reduce (packs when widths fit)
-  u64 na_loc;      // source j of this call -> global j < na_loc ? src_a + j : src_b + j - na_loc
+  u64 na_loc;      // local op j -> global j < na_loc ? src_a + j : src_b + j - na_loc
   i64 src_a, src_b;
   i32* out_order;
   i32* out_addr;
   i32* out_file;
   i32* out_ctx;
+  i64* counts;
 };
 
 #ifndef SMX_EMIT_NT
 #define SMX_EMIT_NT 1
 #endif
-// Streams read or written once: non-temporal, so that they do not evict the
-// gathered final-state table from L2.
+#ifndef SMX_EMIT_NTST
+#define SMX_EMIT_NTST 1
+#endif
+// Streams read once: non-temporal, so that they do not evict the gathered
+// final-state table from L2.  The output stores are plain: an output range starts
+// anywhere (after the skipped renames), so its first and last lines are shared with
+// the neighbouring waves, and non-temporal partial-line stores measured 1.4-1.8x
+// slower than plain ones (tools/_build variants, profiles/r02_*).
 #if SMX_EMIT_NT
 #define NTLD(p) __builtin_nontemporal_load(p)
-#define NTST(v, p) __builtin_nontemporal_store((v), (p))
 #else
 #define NTLD(p) (*(p))
+#endif
+#if SMX_EMIT_NTST
+#define NTST(v, p) __builtin_nontemporal_store((v), (p))
+#else
 #define NTST(v, p) (*(p) = (v))
 #endif
+#ifndef SMX_EMIT_NOGATHER
+#define SMX_EMIT_NOGATHER 0
+#endif
 #ifndef EMIT_WT
-#define EMIT_WT 1024  // T positions per wave
+#define EMIT_WT 1024  // positions per wave
 #endif
 #ifndef EMIT_B
 #define EMIT_B 8      // wave steps whose loads are issued together
 #endif
 
-// Each wave owns EMIT_WT consecutive T positions.  Output index = T minus the
-// skipped renames before T: a binary search of the sorted skip list at the
-// wave's first position, then ballots over the skip flags.  Moves emit their
-// own values (the None-value prefix case is patched afterwards); every other
-// op reads its symbol's final states from fin.
+// Every op after the move block (the moves' records came from the window
+// kernel).  Each wave owns EMIT_WT consecutive OUTPUT indices (aligned: no output
+// line is shared between waves); output o holds the op at position
+//   renames  P = o' + #{skips j : S[j] - j <= o'}   (o' = o - nMv, S = sorted skip list)
+//   others   P = o' + nskip                          (every skip is a rename)
+// found by one binary search per wave and a scalar walk over the (few) skips of
+// each 64-output step.  Renames see their symbol's final move state, the rest
+// also its last rename (compose.py:30-49).  Block 0 writes the call's counts.
 __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
   const ComposeMeta* M = E.meta;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const bool bad = M->bad_sym != 0;  // invalid input (sym >= n_sym or kind >= 18)
+    E.counts[0] = bad ? -1 : (i64)(E.n - M->n_skip);
+    E.counts[1] = bad ? -1 : (i64)M->n_conf;
+  }
   if (M->f_fail | M->bad_sym) return;
   const u64 nskip = M->n_skip;
+  const u64 nmv = min(M->kcnt[KMOVE], E.n);
+  const u64 nP = E.n - nmv;
+  const u64 nR = min(M->kcnt[KREN], nP);
+  const u64 nout = E.n - nskip, nRk = nR - nskip;
   auto gsrc = [&](i32 j) -> i32 {
     return (u64)j < E.na_loc ? (i32)(E.src_a + j) : (i32)(E.src_b + ((i64)j - (i64)E.na_loc));
   };
   const FinPack FP = fin_pack_of(M->vbits, E.allow_pack != 0);
-  auto fin_at = [&](u32 s) -> int4 { return FP.packed ? fin_decode(FP, fin_word(FP, E.fin, s)) : E.fin[s]; };
-  const u64 rs = min(M->kcnt[KMOVE], E.n);
-  const u64 re = min(rs + M->kcnt[KREN], E.n);
   const int lane = threadIdx.x & (WAVE - 1);
-  const u64 w0 = (((u64)blockIdx.x * BLOCK + threadIdx.x) / WAVE) * EMIT_WT;
-  if (w0 >= E.n) return;
-  u64 run;
-  if (w0 <= rs) {
-    run = 0;
-  } else if (w0 >= re) {
-    run = nskip;
-  } else {
-    const u64 mt = w0 - rs;
-    u64 lo = 0, hi = nskip;
-    while (lo < hi) {
-      const u64 mid = (lo + hi) >> 1;
-      if (E.skiplist[mid] < mt) lo = mid + 1;
-      else hi = mid;
+  const u64 w0 = (((u64)blockIdx.x * BLOCK + threadIdx.x) / WAVE) * EMIT_WT;  // output index
+  if (w0 + EMIT_WT <= nmv || w0 >= nout || nP == 0) return;
+  u64 kk = 0;  // skips with S[j] - j below the next step's first rename output
+  {
+    const u64 o0 = w0 > nmv ? w0 - nmv : 0;
+    if (o0 < nRk) {
+      u64 lo = 0, hi = nskip;
+      while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if ((u64)E.skiplist[mid] - mid < o0) lo = mid + 1;
+        else hi = mid;
+      }
+      kk = lo;
     }
-    run = lo;
   }
-  const u64 lt = lanemask_lt();
   for (int bt = 0; bt < EMIT_WT / (WAVE * EMIT_B); ++bt) {
-    const u64 t0 = w0 + (u64)bt * WAVE * EMIT_B;
-    if (t0 >= E.n) break;
-    const u64 t1 = t0 + (u64)WAVE * EMIT_B;  // batch [t0, t1), wave-uniform
-    if (t1 <= rs && t1 <= E.n) {
-      // all moves, no skips: own values
-      i32 src[EMIT_B], ma[EMIT_B], mf[EMIT_B];
-#pragma unroll
-      for (int j = 0; j < EMIT_B; ++j) {
-        const u64 T = t0 + (u64)j * WAVE + lane;
-        src[j] = NTLD(&E.order[T]);
-        ma[j] = NTLD(&E.mvA[T]);
-        mf[j] = NTLD(&E.mvF[T]);
-      }
-#pragma unroll
-      for (int j = 0; j < EMIT_B; ++j) {
-        const u64 T = t0 + (u64)j * WAVE + lane;
-        NTST(gsrc(src[j]), &E.out_order[T]);
-        NTST(ma[j], &E.out_addr[T]);
-        NTST(mf[j], &E.out_file[T]);
-        NTST(-1, &E.out_ctx[T]);
-      }
-      continue;
-    }
-    if (t0 >= re) {
-      // all after the rename block: fixed shift, every op looks its symbol up
-      i32 src[EMIT_B];
-      u32 sy[EMIT_B];
-#pragma unroll
-      for (int j = 0; j < EMIT_B; ++j) {
-        const u64 T = t0 + (u64)j * WAVE + lane;
-        const u64 Tc = T < E.n ? T : E.n - 1;
-        src[j] = NTLD(&E.order[Tc]);
-        sy[j] = min(NTLD(&E.symT[Tc]), E.smax);
-      }
-      int4 F[EMIT_B];
-      if (FP.packed) {
-        u64 x[EMIT_B];
-#pragma unroll
-        for (int j = 0; j < EMIT_B; ++j) x[j] = fin_word(FP, E.fin, sy[j]);
-#pragma unroll
-        for (int j = 0; j < EMIT_B; ++j) F[j] = fin_decode(FP, x[j]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < EMIT_B; ++j) F[j] = E.fin[sy[j]];
-      }
-#pragma unroll
-      for (int j = 0; j < EMIT_B; ++j) {
-        const u64 T = t0 + (u64)j * WAVE + lane;
-        if (T < E.n) {
-          const u64 o = T - nskip;
-          NTST(gsrc(src[j]), &E.out_order[o]);
-          NTST(F[j].x, &E.out_addr[o]);
-          NTST(F[j].y, &E.out_file[o]);
-          NTST(F[j].z, &E.out_ctx[o]);
-        }
-      }
-      continue;
-    }
-    if (t0 >= rs && t1 <= re) {
-      // all renames: final move state, skipped ones dropped
-      i32 src[EMIT_B];
-      u32 sy[EMIT_B];
-      u8 sk[EMIT_B];
-#pragma unroll
-      for (int j = 0; j < EMIT_B; ++j) {
-        const u64 T = t0 + (u64)j * WAVE + lane;
-        src[j] = NTLD(&E.order[T]);
-        sy[j] = min(NTLD(&E.symT[T]), E.smax);
-        sk[j] = NTLD(&E.skip[T - rs]);
-      }
-      int4 F[EMIT_B];
-      if (FP.packed) {
-        u64 x[EMIT_B];
-#pragma unroll
-        for (int j = 0; j < EMIT_B; ++j) x[j] = fin_word(FP, E.fin, sy[j]);
-#pragma unroll
-        for (int j = 0; j < EMIT_B; ++j) F[j] = fin_decode(FP, x[j]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < EMIT_B; ++j) F[j] = E.fin[sy[j]];
-      }
-#pragma unroll
-      for (int j = 0; j < EMIT_B; ++j) {
-        const u64 T = t0 + (u64)j * WAVE + lane;
-        const u64 bal = __ballot(sk[j] != 0);
-        if (!sk[j]) {
-          const u64 o = T - run - __popcll(bal & lt);
-          NTST(gsrc(src[j]), &E.out_order[o]);
-          NTST(F[j].x, &E.out_addr[o]);
-          NTST(F[j].y, &E.out_file[o]);
-          NTST(-1, &E.out_ctx[o]);
-        }
-        run += __popcll(bal);
-      }
-      continue;
-    }
-    // general batch (a block boundary inside the batch)
+    const u64 ob = w0 + (u64)bt * WAVE * EMIT_B;
+    if (ob >= nout) break;
+    u64 pp[EMIT_B];
 #pragma unroll
     for (int j = 0; j < EMIT_B; ++j) {
-      const u64 T = t0 + (u64)j * WAVE + lane;
-      const bool valid = T < E.n;
-      const bool in_ren = T >= rs && T < re;
-      const bool sk = valid && in_ren && NTLD(&E.skip[T - rs]);
-      const u64 bal = __ballot(sk);
-      if (valid && !sk) {
-        const u64 o = T - run - __popcll(bal & lt);
-        const i32 src = NTLD(&E.order[T]);
-        i32 a, f, cc;
-        if (T < rs) {
-          a = NTLD(&E.mvA[T]);
-          f = NTLD(&E.mvF[T]);
-          cc = -1;
-        } else {
-          const int4 F = fin_at(min(NTLD(&E.symT[T]), E.smax));
-          a = F.x;
-          f = F.y;
-          cc = in_ren ? -1 : F.z;
+      const u64 b = ob + (u64)j * WAVE;  // the step's first output (wave-uniform)
+      const u64 o = b + lane;
+      const u64 op = o >= nmv ? o - nmv : 0;
+      const u64 k0 = kk;
+      u64 add = 0;
+      if (b + WAVE > nmv && (b > nmv ? b - nmv : 0) < nRk) {
+        // rename outputs in this step (o' up to b + 63 - nMv): the skips at or below o'
+        const u64 ohi = b + WAVE - 1 - nmv;
+        while (kk < nskip) {
+          const u64 sj = (u64)(u32)__builtin_amdgcn_readfirstlane((int)E.skiplist[kk]) - kk;
+          if (sj > ohi) break;
+          add += op >= sj;
+          ++kk;
         }
-        NTST(gsrc(src), &E.out_order[o]);
-        NTST(a, &E.out_addr[o]);
-        NTST(f, &E.out_file[o]);
-        NTST(cc, &E.out_ctx[o]);
       }
-      run += __popcll(bal);
+      const bool ok = o >= nmv && o < nout;
+      pp[j] = !ok ? 0 : (op < nRk ? op + k0 + add : op + nskip);
+    }
+    i32 src[EMIT_B];
+    u32 sy[EMIT_B];
+#pragma unroll
+    for (int j = 0; j < EMIT_B; ++j) {
+      src[j] = NTLD(&E.tsrc[pp[j]]);
+      sy[j] = min(NTLD(&E.tsym[pp[j]]), E.smax);
+    }
+    int4 F[EMIT_B];
+    if (SMX_EMIT_NOGATHER) {  // diagnostics only: the stream without the table lookups
+#pragma unroll
+      for (int j = 0; j < EMIT_B; ++j) F[j] = make_int4((int)sy[j], 0, 0, 0);
+    } else if (FP.packed) {
+      u64 x[EMIT_B];
+#pragma unroll
+      for (int j = 0; j < EMIT_B; ++j) x[j] = fin_word(FP, E.fin, sy[j]);
+#pragma unroll
+      for (int j = 0; j < EMIT_B; ++j) F[j] = fin_decode(FP, x[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < EMIT_B; ++j) F[j] = E.fin[sy[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < EMIT_B; ++j) {
+      const u64 o = ob + (u64)j * WAVE + lane;
+      if (o >= nmv && o < nout) {
+        const bool ren = o - nmv < nRk;
+        NTST(gsrc(src[j]), &E.out_order[o]);
+        NTST(F[j].x, &E.out_addr[o]);
+        NTST(F[j].y, &E.out_file[o]);
+        NTST(ren ? -1 : F[j].z, &E.out_ctx[o]);
+      }
     }
   }
 }
 
 // Moves whose newAddress or newFile is None see the symbol's inclusive prefix
 // (compose.py:73-82 + 37-41): moves grouped by symbol in T order, last-non-None
-// scan; the composed output index of move T is T (no skips precede the renames).
+// scan over the moves' own values (out_addr / out_file with msym's has-value bits);
+// the composed output index of move T is T.
 // Sharded merge: mvpre[2][n_sym] = the symbol's last non-None (addr, file) on the
 // lower shards, as (shard + 1) << 32 | (value + 1), 0 = none.
+__global__ void k_mv_init(const u32* __restrict__ msym, u64 nMv, u64* __restrict__ keys, u32* __restrict__ vals) {
+  for (u64 j = (u64)blockIdx.x * BLOCK + threadIdx.x; j < nMv; j += (u64)gridDim.x * BLOCK) {
+    keys[j] = msym[j] & SYM_MASK;
+    vals[j] = (u32)j;
+  }
+}
+
 __global__ void k_mv_fix(const u64* __restrict__ keys, const u32* __restrict__ vals, u64 nMv,
-                         const i32* __restrict__ mvA, const i32* __restrict__ mvF,
-                         const u64* __restrict__ mvpre, u64 n_sym,
+                         const u32* __restrict__ msym, const u64* __restrict__ mvpre, u64 n_sym,
                          i32* __restrict__ out_addr, i32* __restrict__ out_file) {
   for (u64 j = (u64)blockIdx.x * BLOCK + threadIdx.x; j < nMv; j += (u64)gridDim.x * BLOCK) {
     if (j != 0 && keys[j - 1] == keys[j]) continue;
@@ -794,22 +740,13 @@ __global__ void k_mv_fix(const u64* __restrict__ keys, const u32* __restrict__ v
     }
     for (u64 i = j; i < nMv && keys[i] == keys[j]; ++i) {
       const u32 T = vals[i];
-      if (mvA[T] >= 0) ra = mvA[T];
-      if (mvF[T] >= 0) rf = mvF[T];
-      out_addr[T] = ra;
-      out_file[T] = rf;
+      const u32 f = msym[T];
+      if (f & MS_HAS_A) ra = out_addr[T];
+      else out_addr[T] = ra;
+      if (f & MS_HAS_F) rf = out_file[T];
+      else out_file[T] = rf;
     }
   }
-}
-
-__global__ void k_counts(const ComposeMeta* meta, u64 n, i64* counts) {
-  if (meta->bad_sym) {  // invalid input (sym >= n_sym or kind >= 18)
-    counts[0] = -1;
-    counts[1] = -1;
-    return;
-  }
-  counts[0] = (i64)(n - meta->n_skip);
-  counts[1] = (i64)meta->n_conf;
 }
 
 // ---------------------------------------------------------------------------
@@ -822,16 +759,17 @@ struct Layout {
 
 enum Buf {
   B_META, B_BND, B_WCNT, B_WOFF, B_STS, B_SHI, B_SLO, B_PERM, B_RKEY, B_RVAL, B_RK2, B_RV2,
-  B_RHIST, B_PART, B_ORDER, B_SYMT, B_MVA, B_MVF, B_MSYM, B_MCLS, B_MSTR, B_MSIDE, B_MOWN,
-  B_RAB, B_FLAGS, B_FPOS, B_CAND, B_Q, B_PM, B_NCONF, B_NREAL, B_COFF, B_SKIP, B_SKIPEX,
-  B_TABA, B_TABF, B_TABR, B_FIN, B_PREFA, B_PREFF, B_REC, B_TBHIST, B_TBTOT, B_HTS, B_CCNT, B_TSUM, B_SMP, B_N
+  B_RHIST, B_PART, B_MSYM, B_TSRC, B_TSYM, B_RSTR, B_WREN, B_WBND, B_CSLOT, B_WCAND, B_WCANDB,
+  B_WCOFF, B_CAND, B_Q, B_PM, B_NCONF, B_NREAL, B_COFF, B_SKIPBITS, B_SKIPLIST,
+  B_TABA, B_TABF, B_TABR, B_FIN, B_REC, B_TBHIST, B_CCNT, B_TSUM, B_SMP, B_N
 };
+
+static i64 max_windows(i64 nn) { return SMX_CEIL_DIV(nn, (i64)WIN_TGT_MIN) + 2; }
 
 static Layout layout(i64 na, i64 nb, i64 n_sym) {
   const i64 n = na + nb;
   const i64 nn = n > 0 ? n : 1;
-  const i64 W = SMX_CEIL_DIV(nn, (i64)WIN_TGT_MIN) + 2;
-  const i64 nblk = SMX_CEIL_DIV(nn, (i64)RADIX_TILE);
+  const i64 W = max_windows(nn);
   size_t sz[B_N];
   sz[B_META] = sizeof(ComposeMeta);
   sz[B_BND] = (size_t)(W + 1) * 2 * 8;
@@ -845,21 +783,17 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_RV2] = (size_t)nn * 4;
   sz[B_RHIST] = radix_hist_bytes(nn);
   sz[B_PART] = (size_t)SCAN_NB * 8;
-  sz[B_ORDER] = sz[B_SYMT] = sz[B_MVA] = sz[B_MVF] = (size_t)nn * 4;
-  sz[B_MSYM] = sz[B_MCLS] = sz[B_MSTR] = sz[B_MOWN] = sz[B_RAB] = (size_t)nn * 4;
-  sz[B_MSIDE] = (size_t)nn;
-  sz[B_FLAGS] = (size_t)nn * 4;  // k_flags slots
-  sz[B_FPOS] = sz[B_CAND] = sz[B_Q] = sz[B_PM] = sz[B_NCONF] = sz[B_NREAL] = sz[B_COFF] = (size_t)nn * 4;
-  sz[B_SKIP] = (size_t)nn;
-  sz[B_SKIPEX] = (size_t)nn * 4;
+  sz[B_MSYM] = sz[B_TSRC] = sz[B_TSYM] = sz[B_RSTR] = (size_t)nn * 4;
+  sz[B_WREN] = (size_t)W * 2 * 4;
+  sz[B_WBND] = sz[B_WCAND] = sz[B_WCANDB] = sz[B_WCOFF] = (size_t)W * 4;
+  sz[B_CSLOT] = sz[B_CAND] = sz[B_Q] = sz[B_PM] = sz[B_NCONF] = sz[B_NREAL] = sz[B_COFF] = (size_t)nn * 4;
+  sz[B_SKIPBITS] = (size_t)(SMX_CEIL_DIV(nn, (i64)64) + 1) * 8;
+  sz[B_SKIPLIST] = (size_t)nn * 4;
   const i64 ns = n_sym > 0 ? n_sym : 1;
-  sz[B_TABA] = sz[B_TABF] = sz[B_TABR] = (size_t)ns * 8;
+  sz[B_TABA] = sz[B_TABF] = sz[B_TABR] = (size_t)ns * 4;
   sz[B_FIN] = (size_t)ns * 16;
-  sz[B_PREFA] = sz[B_PREFF] = (size_t)nn * 4;
-  sz[B_REC] = (size_t)nn * 8;
+  sz[B_REC] = (size_t)nn * 4;
   sz[B_TBHIST] = (size_t)(TB_MAXBK + 1) * SMX_CEIL_DIV(nn, (i64)TB_TILE) * 4;  // k_tb_scatter's lst
-  sz[B_TBTOT] = (size_t)(TB_MAXBK + 1) * 4;  // bucket starts
-  sz[B_HTS] = (size_t)TB_MAXBK * (SMX_CEIL_DIV(SMX_CEIL_DIV(nn, (i64)TB_TILE), (i64)HS_ROWS) + 1) * 4;
   sz[B_CCNT] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)256) + 2) * 4;
   sz[B_SMP] = (size_t)(SMX_CEIL_DIV(nn, (i64)CH) + 4) * 8;
   sz[B_TSUM] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)CH * CS_TILE) + 2) * 4;
@@ -895,6 +829,7 @@ struct Ctx {
   Layout L{};
   char* base;
   i64 na, nb, n, n_sym;
+  i64 src_a, src_b;  // global source index of local op j (see WinArgs)
   StageTimer* tm;
   template <typename T>
   T* ws(int b) const { return (T*)(base + L.off[b]); }
@@ -910,10 +845,7 @@ extern "C" int smx_debug_phase_buffer(void* p, size_t bytes) {
 }
 
 static WinArgs win_args(const Ctx& C) {
-  WinArgs P;
-  P.dbg = nullptr;
-  P.cpre = nullptr;
-  P.CM = 0;
+  WinArgs P{};
   P.kind = C.ops->kind;
   P.sym = C.ops->sym;
   P.v0 = C.ops->v0;
@@ -922,41 +854,39 @@ static WinArgs win_args(const Ctx& C) {
   P.nb = C.nb;
   P.bgap = C.ops->b_gap;
   P.n_sym = C.n_sym;
+  P.src_a = C.src_a;
+  P.src_b = C.src_b;
   P.bnd = C.ws<i64>(B_BND);
   P.woff = C.ws<u32>(B_WOFF);
   P.meta = C.ws<ComposeMeta>(B_META);
-  P.order = C.ws<i32>(B_ORDER);
-  P.symT = C.ws<u32>(B_SYMT);
-  P.mvA = C.ws<i32>(B_MVA);
-  P.mvF = C.ws<i32>(B_MVF);
-  P.Msym = C.ws<u32>(B_MSYM);
-  P.Mcls = C.ws<i32>(B_MCLS);
-  P.Mstr = C.ws<i32>(B_MSTR);
-  P.Mside = C.ws<u8>(B_MSIDE);
-  P.Mown = C.ws<u32>(B_MOWN);
-  P.RA = C.ws<u32>(B_RAB);
-  P.RB = C.ws<u32>(B_RAB) + C.na;  // A has at most n_a renames
+  P.out_order = C.out->order;
+  P.out_addr = C.out->addr;
+  P.out_file = C.out->file;
+  P.out_ctx = C.out->ctx;
+  P.msym = C.ws<u32>(B_MSYM);
+  P.tsrc = C.ws<i32>(B_TSRC);
+  P.tsym = C.ws<u32>(B_TSYM);
+  P.Rstr = C.ws<i32>(B_RSTR);
+  P.wren = C.ws<u32>(B_WREN);
+  P.wbnd = C.ws<u32>(B_WBND);
+  P.cslot = C.ws<u32>(B_CSLOT);
+  P.wcand = C.ws<u32>(B_WCAND);
   return P;
 }
 
-// Sharded-merge parameters of the tail stages (none for a single merge).
-struct TailShard {
-  const smx_shard* sh = nullptr;
-};
-
-static WalkArgs walk_args(const Ctx& C, const WinArgs& P, const smx_shard* sh) {
+static WalkArgs walk_args(const Ctx& C, const smx_shard* sh) {
   WalkArgs Wk{};
-  Wk.Msym = P.Msym;
-  Wk.Mcls = P.Mcls;
-  Wk.Mside = P.Mside;
-  Wk.Mown = P.Mown;
-  Wk.RA = P.RA;
-  Wk.RB = P.RB;
+  Wk.tsrc = C.ws<i32>(B_TSRC);
+  Wk.tsym = C.ws<u32>(B_TSYM);
+  Wk.v0 = C.ops->v0;
+  Wk.wren = C.ws<u32>(B_WREN);
+  Wk.wbnd = C.ws<u32>(B_WBND);
   Wk.meta = C.ws<ComposeMeta>(B_META);
   Wk.na_cap = (u64)C.na;
   Wk.nb_cap = (u64)C.nb;
-  Wk.src_a = sh ? sh->src_a : 0;
-  Wk.src_b = sh ? sh->src_b : C.na;
+  Wk.bgap = C.ops->b_gap;
+  Wk.src_a = C.src_a;
+  Wk.src_b = C.src_b;
   for (int b = 0; b < 2; ++b) {
     Wk.halo_sym[b] = sh ? sh->halo_sym[b] : nullptr;
     Wk.halo_cls[b] = sh ? sh->halo_cls[b] : nullptr;
@@ -983,23 +913,22 @@ __global__ void k_walk_init(ComposeMeta* meta) {
 
 __global__ void k_walk_done(ComposeMeta* meta) { meta->n_conf = meta->nconf_in + meta->n_conf_loc; }
 
-// DivergentRename walk (smx_walk.h): conflicts, skip flags, sorted skip list.
+// DivergentRename walk (smx_walk.h): conflicts, skip bits, sorted skip list.
 // Every size is read on the device from meta: no host sync.
-static int launch_walk(const Ctx& C, const WinArgs& P, const smx_shard* sh) {
+static int launch_walk(const Ctx& C, const smx_shard* sh) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   const i64 n = C.n;
-  u8* skip = C.ws<u8>(B_SKIP);
-  u32* skiplist = C.ws<u32>(B_SKIPEX);
+  u64* skipbits = C.ws<u64>(B_SKIPBITS);
+  u32* skiplist = C.ws<u32>(B_SKIPLIST);
   u32* part = C.ws<u32>(B_PART);
-  // skip flags: cleared by k_flags over the rename block, unless an incoming
-  // region (sharded merge) writes some of them first
-  const bool zero_first = sh && sh->in_d > 0;
-  if (zero_first) HIP_TRY(hipMemsetAsync(skip, 0, n, st));
+  HIP_TRY(hipMemsetAsync(skipbits, 0, (size_t)(SMX_CEIL_DIV(n, (i64)64) + 1) * 8, st));
   hipLaunchKernelGGL(k_walk_init, dim3(1), dim3(1), 0, st, meta);
-  const WalkArgs Wk = walk_args(C, P, sh);
-  u32* slots = C.ws<u32>(B_FLAGS);
-  u32* bcnt = C.ws<u32>(B_FPOS);
+  const WalkArgs Wk = walk_args(C, sh);
+  u32* cslot = C.ws<u32>(B_CSLOT);
+  u32* wcand = C.ws<u32>(B_WCAND);
+  u32* wcandB = C.ws<u32>(B_WCANDB);
+  u32* wcoff = C.ws<u32>(B_WCOFF);
   u32* cand = C.ws<u32>(B_CAND);
   u32* q = C.ws<u32>(B_Q);
   u32* pm = C.ws<u32>(B_PM);
@@ -1010,38 +939,51 @@ static int launch_walk(const Ctx& C, const WinArgs& P, const smx_shard* sh) {
   // (little endian) of the zeroed fields
   u32* nconf32 = (u32*)&meta->n_conf_loc;
   const u64* ncand_dev = &meta->n_cand;
-  const u32 nfb = (u32)SMX_CEIL_DIV((u64)n, (u64)FLAG_TILE);  // upper bound; idle blocks exit
+  const i64 Wmax = max_windows(n);
   const int gsmall = 256;  // grid for loops over the (few) candidates
   if (sh && sh->in_d > 0)
-    hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d, meta, P.order,
-                       C.out->conflicts, (u64)C.out->conflict_cap, skip, skiplist);
-  hipLaunchKernelGGL(k_flags, dim3(nfb), dim3(BLOCK), 0, st, Wk, slots, bcnt, zero_first ? nullptr : skip);
-  hipLaunchKernelGGL(k_flag_offsets, dim3(1), dim3(FO_NT), 0, st, Wk, bcnt, &meta->n_cand);
-  hipLaunchKernelGGL(k_compact, dim3(SMX_CEIL_DIV(nfb, (u32)NWAVES)), dim3(BLOCK), 0, st, Wk, slots, bcnt, ncand_dev,
-                     cand);
+    hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d, meta,
+                       C.out->conflicts, (u64)C.out->conflict_cap, skiplist, skipbits);
+  hipLaunchKernelGGL(k_boundary, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, cslot, wcand, wcandB);
+  hipLaunchKernelGGL(k_cand_offsets, dim3(1), dim3(FO_NT), 0, st, Wk, wcand, wcandB, wcoff, &meta->n_cand);
+  hipLaunchKernelGGL(k_cand_compact, dim3(SMX_CEIL_DIV(Wmax, (i64)NWAVES)), dim3(BLOCK), 0, st, Wk, cslot, wcoff,
+                     ncand_dev, cand);
   hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
   HIP_TRY((scan_excl<OpMax, u32, u32>(q, pm, 0, ncand_dev, part, (u32*)nullptr, st)));
-  hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, cand, q, pm, nconf, meta, nreal);
+  hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, q, pm, nconf, meta, nreal);
   HIP_TRY((scan_excl<OpSum, u32, u32>(nreal, coff, 0, ncand_dev, part, nconf32, st)));
-  hipLaunchKernelGGL(k_replay_write, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, nreal, coff, meta, P.order,
-                     C.out->conflicts, (u64)C.out->conflict_cap, skip, skiplist);
+  hipLaunchKernelGGL(k_replay_write, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, nreal, coff, meta,
+                     C.out->conflicts, (u64)C.out->conflict_cap, skiplist, skipbits);
   hipLaunchKernelGGL(k_walk_done, dim3(1), dim3(1), 0, st, meta);
   HIP_TRY(hipGetLastError());
   return SMX_OK;
 }
 
+static TbArgs tb_args(const Ctx& C) {
+  TbArgs A{};
+  A.msym = C.ws<u32>(B_MSYM);
+  A.tsym = C.ws<u32>(B_TSYM);
+  A.skipbits = C.ws<u64>(B_SKIPBITS);
+  A.mv_addr = C.out->addr;
+  A.mv_file = C.out->file;
+  A.Rstr = C.ws<i32>(B_RSTR);
+  A.meta = C.ws<ComposeMeta>(B_META);
+  A.ncap = (u64)C.n;
+  A.width = 1u;
+  A.nbk = 1u;
+  A.smax = (u32)(C.n_sym - 1);
+  return A;
+}
+
 // Per-symbol last writers.  part == nullptr: the final-state table fin (packed
 // when the value widths allow); otherwise this shard's partial tables.
-static int launch_tables(const Ctx& C, const WinArgs& P, u64* part_tab, u32 tag, bool* bucketed) {
+static int launch_tables(const Ctx& C, u64* part_tab, u32 tag, bool* bucketed) {
   hipStream_t st = C.st;
-  ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   const i64 n = C.n;
-  u8* skip = C.ws<u8>(B_SKIP);
-  u32* part = C.ws<u32>(B_PART);
   int4* fin = C.ws<int4>(B_FIN);
   *bucketed = false;
   const i64 n_sym = C.n_sym;
-  TbArgs A{P.symT, P.mvA, P.mvF, P.Msym, P.Mstr, skip, meta, (u64)n, 1u, 1u, (u32)(n_sym - 1), 0, 0};
+  TbArgs A = tb_args(C);
   u64 width = SMX_CEIL_DIV((u64)n_sym, (u64)TB_NBK_TGT);
   if (width < 1) width = 1;
   if (width > TB_WIDTH) width = TB_WIDTH;
@@ -1052,7 +994,7 @@ static int launch_tables(const Ctx& C, const WinArgs& P, u64* part_tab, u32 tag,
     A.nbk = (u32)nbk;
     const int nblk = (int)SMX_CEIL_DIV((u64)n, (u64)TB_TILE);
     u32* lst = C.ws<u32>(B_TBHIST);
-    u64* rec = C.ws<u64>(B_REC);
+    u32* rec = C.ws<u32>(B_REC);
     hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, lst, rec);
     hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, lst, rec, n_sym, fin, part_tab, tag);
   } else {
@@ -1071,32 +1013,31 @@ static int launch_tables(const Ctx& C, const WinArgs& P, u64* part_tab, u32 tag,
   return SMX_OK;
 }
 
-static int launch_emit(const Ctx& C, const WinArgs& P, bool packable, const smx_shard* sh) {
+static int launch_emit(const Ctx& C, bool packable) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   const i64 n = C.n;
-  EmitArgs E{P.order, P.symT, P.mvA, P.mvF, C.ws<u8>(B_SKIP), C.ws<u32>(B_SKIPEX), C.ws<int4>(B_FIN), meta,
-             (u64)n, (u32)(C.n_sym - 1), packable ? 1 : 0, (u64)C.na, sh ? sh->src_a : 0,
-             sh ? sh->src_b : C.na, C.out->order, C.out->addr, C.out->file, C.out->ctx};
+  EmitArgs E{C.ws<i32>(B_TSRC), C.ws<u32>(B_TSYM), C.ws<u64>(B_SKIPBITS), C.ws<u32>(B_SKIPLIST),
+             C.ws<int4>(B_FIN), meta, (u64)n, (u32)(C.n_sym - 1), packable ? 1 : 0, (u64)C.na, C.src_a,
+             C.src_b, C.out->order, C.out->addr, C.out->file, C.out->ctx, C.out->counts};
   const i64 ewaves = SMX_CEIL_DIV(n, (i64)EMIT_WT);
   hipLaunchKernelGGL(k_emit, dim3(SMX_CEIL_DIV(ewaves, (i64)NWAVES)), dim3(BLOCK), 0, st, E);
-  hipLaunchKernelGGL(k_counts, dim3(1), dim3(1), 0, st, meta, (u64)n, C.out->counts);
   HIP_TRY(hipGetLastError());
   return SMX_OK;
 }
 
 // Walk, tables, emit of a single merge.
-static int launch_tail(const Ctx& C, const WinArgs& P) {
+static int launch_tail(const Ctx& C) {
   C.tm->begin(ST_WALK);
-  int rc = launch_walk(C, P, nullptr);
+  int rc = launch_walk(C, nullptr);
   if (rc) return rc;
   C.tm->end(ST_WALK);
   C.tm->begin(ST_TABLES);
   bool bucketed = false;
-  if ((rc = launch_tables(C, P, nullptr, 0, &bucketed))) return rc;
+  if ((rc = launch_tables(C, nullptr, 0, &bucketed))) return rc;
   C.tm->end(ST_TABLES);
   C.tm->begin(ST_EMIT);
-  if ((rc = launch_emit(C, P, bucketed, nullptr))) return rc;
+  if ((rc = launch_emit(C, bucketed))) return rc;
   C.tm->end(ST_EMIT);
   return SMX_OK;
 }
@@ -1112,8 +1053,6 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
-  u32* wcnt = C.ws<u32>(B_WCNT);
-  u32* woff = C.ws<u32>(B_WOFF);
   C.tm->begin(ST_PLAN);
   HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
   if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
@@ -1139,7 +1078,7 @@ static int run_presorted(const Ctx& C, i64 tgt) {
     hipLaunchKernelGGL(k_cscan_down, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT,
                        tsum);
   }
-  hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
+  hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta, (u64)W);
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_PLAN);
   WinArgs P = win_args(C);
@@ -1160,9 +1099,9 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   }
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_WINDOW);
-  if (P.ablate) return SMX_OK;  // diagnostics: the T-ordered arrays are invalid, stop here
-  return launch_tail(C, P);
+  return SMX_OK;
 }
+
 
 // Generic plan: each branch sorted by (ts, oid_hi, oid_lo, index), then fixed windows
 // over the sorted logs (k_window_g).  Used when the presorted plan fails.  Two ways to
@@ -1364,6 +1303,7 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
   }
 }
 
+
 static int read_meta(const Ctx& C, ComposeMeta* hm);
 
 // *fallback: the segmented sort could not order this log (mode GEN_SEG only); nothing
@@ -1443,7 +1383,7 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
   hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, C.ops->kind, C.ops->v0, C.ops->v1, perm, bnd, na, W,
                      wcnt, meta);
   hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, W, meta);
-  hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta);
+  hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta, (u64)W);
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_GSORT);
   WinArgs P = win_args(C);
@@ -1457,7 +1397,7 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
   hipLaunchKernelGGL(k_window_g, dim3(W), dim3(WG_NT), 0, st, P);
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_WINDOW);
-  return launch_tail(C, P);
+  return SMX_OK;
 }
 
 static int read_meta(const Ctx& C, ComposeMeta* hm) {
@@ -1470,6 +1410,7 @@ static int check_args(const smx_ops* ops, const smx_compose_out* out, void* ws, 
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
   if (na < 0 || nb < 0 || n_sym < 0) return set_err(SMX_E_ARG, "negative size");
   if (n >= (i64)0x7fffffff) return set_err(SMX_E_ARG, "n_a + n_b must be < 2^31");
+  if (n_sym > (i64)SYM_MASK + 1) return set_err(SMX_E_ARG, "n_sym must be <= 2^30");
   if (!out || !out->counts) return set_err(SMX_E_ARG, "null output");
   if (n == 0) return SMX_OK;
   if (!ops->kind || !ops->ts || !ops->oid_hi || !ops->oid_lo || !ops->sym || !ops->v0 || !ops->v1 ||
@@ -1488,17 +1429,21 @@ static int profiling_on() {
   return g_prof;
 }
 
-// T order of the merge: the presorted plan first; a window that overflows LDS
-// (dense timestamp ties) retries with smaller windows; a log that is not
+// T order of the merge (plan + window kernels): the presorted plan first, with
+// the tail (walk, tables, emit) launched behind it when `tail` -- every tail kernel
+// is a no-op if the window kernel flags the plan as failed; a window that overflows
+// LDS (dense timestamp ties) retries with smaller windows; a log that is not
 // timestamp-ordered goes to the generic plan when allowed.  hm: the meta after it.
-static int run_order(const Ctx& C, bool allow_generic, ComposeMeta* hm) {
+static int run_order(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm) {
   i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
   int rc = run_presorted(C, tgt);
   if (rc) return rc;
+  if (tail && (rc = launch_tail(C))) return rc;
   if ((rc = read_meta(C, hm))) return rc;
   while (hm->f_fail == 2 && !hm->bad_sym && tgt > WIN_TGT_MIN) {  // dense groups: smaller windows
     tgt = (tgt / 2) / CH * CH;
     if ((rc = run_presorted(C, tgt))) return rc;
+    if (tail && (rc = launch_tail(C))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
   }
   if (hm->f_fail && !hm->bad_sym && allow_generic) {
@@ -1511,6 +1456,7 @@ static int run_order(const Ctx& C, bool allow_generic, ComposeMeta* hm) {
       if ((rc = read_meta(C, hm))) return rc;
       if (hm->dup_key && (rc = run_generic(C, GEN_RADIX_LO, &fallback))) return rc;
     }
+    if (tail && (rc = launch_tail(C))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
   }
   return SMX_OK;
@@ -1530,10 +1476,10 @@ static int run_mvprefix(const Ctx& C, const ComposeMeta& hm, const u64* mvpre) {
   int shifts[4], ns = 0;
   for (int dgt = 0; dgt < 4; ++dgt)
     if (((u64)(n_sym - 1) >> (8 * dgt)) != 0) shifts[ns++] = 8 * dgt;
-  hipLaunchKernelGGL(k_mv_init, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, C.ws<u32>(B_SYMT), nMv, keys, vals);
+  hipLaunchKernelGGL(k_mv_init, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, C.ws<u32>(B_MSYM), nMv, keys, vals);
   if (ns) HIP_TRY(radix_sort_pairs(keys, vals, (i64)nMv, shifts, ns, rt, st));
-  hipLaunchKernelGGL(k_mv_fix, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, keys, vals, nMv, C.ws<i32>(B_MVA),
-                     C.ws<i32>(B_MVF), mvpre, (u64)n_sym, C.out->addr, C.out->file);
+  hipLaunchKernelGGL(k_mv_fix, dim3(grid_for(nMv)), dim3(BLOCK), 0, st, keys, vals, nMv, C.ws<u32>(B_MSYM), mvpre,
+                     (u64)n_sym, C.out->addr, C.out->file);
   HIP_TRY(hipGetLastError());
   return SMX_OK;
 }
@@ -1549,14 +1495,14 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
     return SMX_OK;
   }
   StageTimer tm(st, profiling_on() != 0);
-  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, &tm};
+  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
   if (env_int("SMX_ABLATE", 0)) {  // diagnostics: timing of the window stage only
     if ((rc = run_presorted(C, env_int("SMX_WIN_TGT", WIN_TGT)))) return rc;
     tm.flush();
     return SMX_OK;
   }
   ComposeMeta hm;
-  if ((rc = run_order(C, true, &hm))) return rc;
+  if ((rc = run_order(C, true, true, &hm))) return rc;
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
   tm.begin(ST_MVPREFIX);
   if ((rc = run_mvprefix(C, hm, nullptr))) return rc;
@@ -1568,33 +1514,13 @@ static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws
 // ---------------------------------------------------------------------------
 // sharded merge (include/smx.h smx_shard_step)
 
-__device__ __forceinline__ i32 shard_gsrc(i32 j, u64 na, i64 src_a, i64 src_b) {
-  return (u64)j < na ? (i32)(src_a + j) : (i32)(src_b + ((i64)j - (i64)na));
-}
-
-// summary[0..21] and the first `cap` renames of each branch (the previous
-// shards' halo).
-__global__ void k_shard_export(const ComposeMeta* meta, const WinArgs P, i64* summary, u32* xsym, i32* xcls,
-                               i32* xsrc, i64 cap, i64 src_a, i64 src_b) {
-  const u64 nr[2] = {meta->n_ren_side[0], meta->n_ren_side[1]};
-  const i32* order_ren = P.order + meta->base[KREN];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    for (int k = 0; k < SMX_N_KINDS; ++k) summary[k] = (i64)meta->kcnt[k];
-    summary[18] = (i64)nr[0];
-    summary[19] = (i64)nr[1];
-    summary[20] = (i64)meta->n_move_none;
-    summary[21] = (i64)((meta->f_fail ? 1 : 0) | (meta->bad_sym ? 2 : 0));
-  }
-  if (meta->f_fail | meta->bad_sym) return;
-  for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < 2 * cap; i += (i64)gridDim.x * BLOCK) {
-    const int b = i >= cap;
-    const i64 k = b ? i - cap : i;
-    if ((u64)k >= nr[b]) continue;
-    const u32 u = (b ? P.RB : P.RA)[k];
-    xsym[i] = P.Msym[u];
-    xcls[i] = P.Mcls[u];
-    xsrc[i] = shard_gsrc(order_ren[u], (u64)P.na, src_a, src_b);
-  }
+// summary[0..21]
+__global__ void k_shard_summary(const ComposeMeta* meta, i64* summary) {
+  for (int k = 0; k < SMX_N_KINDS; ++k) summary[k] = (i64)meta->kcnt[k];
+  summary[18] = (i64)meta->n_ren_side[0];
+  summary[19] = (i64)meta->n_ren_side[1];
+  summary[20] = (i64)meta->n_move_none;
+  summary[21] = (i64)((meta->f_fail ? 1 : 0) | (meta->bad_sym ? 2 : 0));
 }
 
 __global__ void k_shard_walk_sum(const ComposeMeta* meta, i64* summary) {
@@ -1634,12 +1560,14 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
   if (rc) return rc;
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
   StageTimer tm(st, profiling_on() != 0);
-  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, &tm};
+  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, sh->src_a, sh->src_b, &tm};
   if (n == 0) {  // an empty shard: neutral summaries and outputs
     if (step == SMX_SHARD_ORDER) HIP_TRY(hipMemsetAsync(sh->summary, 0, SMX_SHARD_SUMMARY * 8, st));
-    if (step == SMX_SHARD_WALK && sh->in_d > 0) {
-      // the open region passes through unchanged
-      const i64 pass[3] = {1, sh->in_ahead, sh->in_d};
+    if (step == SMX_SHARD_WALK) {
+      // the open region passes through unchanged (or none comes in): always rewrite
+      // the outgoing state, a previous round may have left another one
+      const i64 pass[6] = {sh->in_d > 0 ? 1 : 0, sh->in_d > 0 ? sh->in_ahead : 0, sh->in_d > 0 ? sh->in_d : 0,
+                           0, 0, 0};
       HIP_TRY(hipMemcpyAsync(sh->summary + 22, pass, sizeof(pass), hipMemcpyHostToDevice, st));
       HIP_TRY(hipStreamSynchronize(st));
     }
@@ -1648,16 +1576,16 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
     if (step == SMX_SHARD_EMIT) HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
     return SMX_OK;
   }
-  const WinArgs P = win_args(C);
   switch (step) {
     case SMX_SHARD_ORDER: {
       if (sh->halo_cap < 0 || (sh->halo_cap > 0 && (!sh->export_sym || !sh->export_cls || !sh->export_src)))
         return set_err(SMX_E_ARG, "bad export buffers");
       ComposeMeta hm;
-      if ((rc = run_order(C, false, &hm))) return rc;  // times its own plan / window stages
-      hipLaunchKernelGGL(k_shard_export, dim3(grid_for(2 * sh->halo_cap + 1)), dim3(BLOCK), 0, st,
-                         C.ws<ComposeMeta>(B_META), P, sh->summary, sh->export_sym, sh->export_cls,
-                         sh->export_src, sh->halo_cap, sh->src_a, sh->src_b);
+      if ((rc = run_order(C, false, false, &hm))) return rc;  // times its own plan / window stages
+      hipLaunchKernelGGL(k_shard_summary, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary);
+      if (sh->halo_cap > 0)
+        hipLaunchKernelGGL(k_halo_export, dim3(1), dim3(EX_NT), 0, st, walk_args(C, nullptr), sh->export_sym,
+                           sh->export_cls, sh->export_src, (u64)sh->halo_cap);
       HIP_TRY(hipGetLastError());
       if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
       if (hm.f_fail)
@@ -1666,7 +1594,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
     }
     case SMX_SHARD_WALK: {
       tm.begin(ST_WALK);
-      if ((rc = launch_walk(C, P, sh))) return rc;
+      if ((rc = launch_walk(C, sh))) return rc;
       hipLaunchKernelGGL(k_shard_walk_sum, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary);
       HIP_TRY(hipGetLastError());
       tm.end(ST_WALK);
@@ -1676,7 +1604,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       if (!sh->part_tab) return set_err(SMX_E_ARG, "null part_tab");
       tm.begin(ST_TABLES);
       bool bucketed = false;
-      if ((rc = launch_tables(C, P, sh->part_tab, (u32)sh->rank + 1u, &bucketed))) return rc;
+      if ((rc = launch_tables(C, sh->part_tab, (u32)sh->rank + 1u, &bucketed))) return rc;
       hipLaunchKernelGGL(k_shard_tab_sum, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary,
                          bucketed ? 1 : 0);
       HIP_TRY(hipGetLastError());
@@ -1688,7 +1616,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       tm.begin(ST_EMIT);
       hipLaunchKernelGGL(k_fin_from_tab, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, sh->fin_tab, sh->glob, n_sym,
                          C.ws<ComposeMeta>(B_META), C.ws<int4>(B_FIN));
-      if ((rc = launch_emit(C, P, true, sh))) return rc;
+      if ((rc = launch_emit(C, true))) return rc;
       tm.end(ST_EMIT);
       ComposeMeta hm;
       if ((rc = read_meta(C, &hm))) return rc;
@@ -1754,4 +1682,4 @@ extern "C" const char* smx_stage_name(int i) { return (i >= 0 && i < ST_N) ? kSt
 
 extern "C" const char* smx_last_error(void) { return g_err.c_str(); }
 
-extern "C" const char* smx_version(void) { return "smx 0.1 gfx950"; }
+extern "C" const char* smx_version(void) { return "smx 0.2 gfx950"; }

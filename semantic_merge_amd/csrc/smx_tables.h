@@ -4,16 +4,19 @@
 // non-None newAddress / newFile over its moves, in T order) and every
 // non-rename sees the last non-skipped rename.  "Last in T order" = max T.
 //
-// Scattered 64-bit device atomics run at ~26 G/s on MI355X; instead the
-// records are bucketed by symbol range and each bucket is reduced by one
-// workgroup with 32-bit LDS max over record indices; the values are fetched once
-// per symbol at the end.  Bucketing needs no counting pass: k_tb_scatter sorts
-// each tile of TB_TILE records by bucket in LDS and writes the tile back in place
-// (fully coalesced) with its bucket starts lst[tile][0..nbk]; k_tb_reduce of
-// bucket b then reads that bucket's run of every tile.  A record is 8 bytes:
-//   bits  0..30  r: record index (move T < nMv, or nMv + rename position)
-//   bits 32..43  symbol offset inside its bucket
-//   bit  44      the move has a newAddress      bit 45  the move has a newFile
+// Records: r in [0, nMv) is the move at T = r (msym[r] = symbol | has-address |
+// has-file, written by the window kernel), r = nMv + m the rename at M position m
+// (tsym[m]; skipped renames, skipbits, carry nothing).  Scattered device atomics
+// execute at the memory side; instead the records are bucketed by symbol range
+// and each bucket is reduced by one workgroup with 32-bit LDS max over record
+// indices; the values are fetched once per symbol at the end (the move's own
+// out_addr / out_file, the rename's Rstr).  Bucketing needs no counting pass:
+// k_tb_scatter sorts each tile of TB_TILE records by bucket in LDS and writes the
+// tile back in place (fully coalesced) with its bucket starts lst[tile][0..nbk];
+// k_tb_reduce of bucket b then reads that bucket's run of every tile.  A record
+// is 4 bytes, relative to its tile:
+//   bits  0..13  index inside the tile          bits 14..25 symbol offset in its bucket
+//   bit  26      the move has a newAddress      bit  27     the move has a newFile
 #pragma once
 
 #include "smx_scan.h"
@@ -21,24 +24,27 @@
 #define TB_WIDTH 4096       // symbols per bucket
 #define TB_MAXBK 1024       // buckets handled by the bucketed path
 #ifndef TB_NT
-#define TB_NT 1024          // scatter workgroup: one 16384-record tile (136 KB LDS) per CU
+#define TB_NT 1024          // scatter workgroup: one 16384-record tile (64 KB LDS)
 #endif
 #define TB_NW (TB_NT / WAVE)
 #ifndef TB_ITEMS
-#define TB_ITEMS 16         // 64-record runs per bucket and tile: full-line writes
+#define TB_ITEMS 16         // 64-record runs per bucket and tile
 #endif
 #ifndef TB_NBK_TGT
 #define TB_NBK_TGT 256      // target bucket count (width = n_sym / this, <= TB_WIDTH)
 #endif
 #define TB_TILE (TB_NT * TB_ITEMS)
+static_assert(TB_TILE <= (1 << 14), "tile-relative record index is 14 bits");
+#define REC_HAS_A (1u << 26)
+#define REC_HAS_F (1u << 27)
 
 struct TbArgs {
-  const u32* symT;  // moves: T-ordered symbols (T < nMv)
-  const i32* mvA;
-  const i32* mvF;
-  const u32* Msym;  // renames (rename block order)
-  const i32* Mstr;
-  const u8* skip;
+  const u32* msym;    // moves: T-ordered symbol | has-address << 30 | has-file << 31
+  const u32* tsym;    // renames: symbol at M position
+  const u64* skipbits;
+  const i32* mv_addr;  // the moves' own newAddress / newFile (= out_addr / out_file, T < nMv)
+  const i32* mv_file;
+  const i32* Rstr;
   const ComposeMeta* meta;
   u64 ncap;         // n_a + n_b (bound for device-side counts)
   u32 width;        // symbols per bucket
@@ -55,18 +61,22 @@ __device__ __forceinline__ TbArgs tb_load(TbArgs A) {
   return A;
 }
 
-// Record r (see header); false when it carries nothing (skipped rename, move with
-// both values None).
+__device__ __forceinline__ bool tb_skipped(const TbArgs& A, u64 m) {
+  return (A.skipbits[m >> 6] >> (m & 63)) & 1ull;
+}
+
+// Record r: symbol and flags; false when it carries nothing (skipped rename, move
+// with both values None).
 __device__ __forceinline__ bool tb_record(const TbArgs& A, u64 r, u32* sym, u32* flags) {
   if (r < A.nMv) {
-    const bool a = A.mvA[r] >= 0, f = A.mvF[r] >= 0;
-    *sym = min(A.symT[r], A.smax);
-    *flags = (a ? 1u : 0u) | (f ? 2u : 0u);
-    return a || f;
+    const u32 x = A.msym[r];
+    *sym = min(x & SYM_MASK, A.smax);
+    *flags = (x & MS_HAS_A ? REC_HAS_A : 0u) | (x & MS_HAS_F ? REC_HAS_F : 0u);
+    return (x & (MS_HAS_A | MS_HAS_F)) != 0;
   }
   const u64 m = r - A.nMv;
-  if (A.skip[m]) return false;
-  *sym = min(A.Msym[m], A.smax);
+  if (tb_skipped(A, m)) return false;
+  *sym = min(A.tsym[m], A.smax);
   *flags = 0;
   return true;
 }
@@ -81,20 +91,22 @@ __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[T
   const u64 nrec = A.nMv + A.nR;
   const u64 end = base + (u64)TB_TILE;
   if (end <= A.nMv) {
+    u32 x[TB_ITEMS];
     i32 a[TB_ITEMS], f[TB_ITEMS];
-    u32 s[TB_ITEMS];
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
       const u64 r = base + (u64)it * TB_NT + threadIdx.x;
-      s[it] = A.symT[r];
-      a[it] = A.mvA[r];
-      f[it] = A.mvF[r];
+      x[it] = A.msym[r];
+      if (VB) {
+        a[it] = A.mv_addr[r];
+        f[it] = A.mv_file[r];
+      }
     }
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
-      ok[it] = a[it] >= 0 || f[it] >= 0;
-      fl[it] = (a[it] >= 0 ? 1u : 0u) | (f[it] >= 0 ? 2u : 0u);
-      sym[it] = min(s[it], A.smax);
+      ok[it] = (x[it] & (MS_HAS_A | MS_HAS_F)) != 0;
+      fl[it] = (x[it] & MS_HAS_A ? REC_HAS_A : 0u) | (x[it] & MS_HAS_F ? REC_HAS_F : 0u);
+      sym[it] = min(x[it] & SYM_MASK, A.smax);
       if (VB) {
         vb[0] |= (u32)(a[it] + 1);
         vb[1] |= (u32)(f[it] + 1);
@@ -102,18 +114,19 @@ __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[T
     }
   } else if (base >= A.nMv && end <= nrec) {
     u32 s[TB_ITEMS];
-    u8 k[TB_ITEMS];
     i32 c[TB_ITEMS];
+    const u64 m0 = base - A.nMv;
+    // the tile's 16384 skip bits: 256 words, lanes of a wave step share one
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
-      const u64 m = base - A.nMv + (u64)it * TB_NT + threadIdx.x;
-      s[it] = A.Msym[m];
-      k[it] = A.skip[m];
-      if (VB) c[it] = A.Mstr[m];
+      const u64 m = m0 + (u64)it * TB_NT + threadIdx.x;
+      s[it] = A.tsym[m];
+      if (VB) c[it] = A.Rstr[m];
     }
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
-      ok[it] = k[it] == 0;
+      const u64 m = m0 + (u64)it * TB_NT + threadIdx.x;
+      ok[it] = !tb_skipped(A, m);
       fl[it] = 0;
       sym[it] = min(s[it], A.smax);
       if (VB) vb[2] |= (u32)(c[it] + 1);
@@ -124,10 +137,10 @@ __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[T
       const u64 r = base + (u64)it * TB_NT + threadIdx.x;
       ok[it] = r < nrec && tb_record(A, r, &sym[it], &fl[it]);
       if (VB && r < A.nMv) {
-        vb[0] |= (u32)(A.mvA[r] + 1);
-        vb[1] |= (u32)(A.mvF[r] + 1);
+        vb[0] |= (u32)(A.mv_addr[r] + 1);
+        vb[1] |= (u32)(A.mv_file[r] + 1);
       } else if (VB && r < nrec) {
-        vb[2] |= (u32)(A.Mstr[r - A.nMv] + 1);
+        vb[2] |= (u32)(A.Rstr[r - A.nMv] + 1);
       }
     }
   }
@@ -137,8 +150,8 @@ __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[T
 // LDS and written back to the tile's own range; lst[tile][b] = start of bucket b
 // in the tile, lst[tile][nbk] = the tile's record count.  Also ORs the value
 // widths of the packed final-state table (smx_common.h FinPack) into meta->vbits.
-__global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict__ lst, u64* __restrict__ rec) {
-  __shared__ u64 stage[TB_TILE];        // TB_TILE * 8 bytes
+__global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict__ lst, u32* __restrict__ rec) {
+  __shared__ u32 stage[TB_TILE];        // TB_TILE * 4 bytes
   __shared__ u32 lstart[TB_MAXBK];      // local bucket starts (then cursors)
   __shared__ u32 wsum[TB_NW + 1];
   __shared__ u32 vb[3];
@@ -150,7 +163,7 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
   for (u32 i = threadIdx.x; i < nbk; i += TB_NT) lstart[i] = 0;
   if (threadIdx.x < 3) vb[threadIdx.x] = 0;
   __syncthreads();
-  u64 q[TB_ITEMS];
+  u32 q[TB_ITEMS];
   u32 bk[TB_ITEMS];
   {
     u32 s[TB_ITEMS], fl[TB_ITEMS];
@@ -159,12 +172,12 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
     tb_items<true>(A, base, s, fl, ok, v3);
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
-      const u64 r = base + (u64)it * TB_NT + threadIdx.x;
+      const u32 loc = (u32)(it * TB_NT) + threadIdx.x;
       bk[it] = 0xffffffffu;
       if (ok[it]) {
         const u32 b = s[it] / A.width;
         bk[it] = b;
-        q[it] = (u64)r | ((u64)(s[it] - b * A.width) << 32) | ((u64)fl[it] << 44);
+        q[it] = loc | ((s[it] - b * A.width) << 14) | fl[it];
         atomicAdd(&lstart[b], 1u);
       }
     }
@@ -227,12 +240,12 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
 // TBR_TK: tiles per wave step in k_tb_reduce
 
 // One workgroup per bucket: LDS max over record indices, then each symbol's
-// values are fetched once: fin[sym] = (addr, file, ctx, 0).
+// values are fetched once: fin[sym] = (addr, file, ctx).
 // part != nullptr (sharded merge): instead of fin, write this shard's partial
 // tables part[3][n_sym] = (tag << 32) | (value + 1), 0 = no record; the MAX
 // all-reduce over shards then keeps the last writer (highest shard).
 __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __restrict__ lst,
-                                                      const u64* __restrict__ rec, i64 n_sym,
+                                                      const u32* __restrict__ rec, i64 n_sym,
                                                       int4* __restrict__ fin, u64* __restrict__ part, u32 tag) {
   const FinPack FP = fin_pack_of(A0.meta->vbits, true);
   __shared__ u32 tA[TB_WIDTH], tF[TB_WIDTH], tC[TB_WIDTH];
@@ -240,12 +253,12 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
   const u32 b = blockIdx.x;
   for (u32 i = threadIdx.x; i < A.width; i += TBR_NT) tA[i] = tF[i] = tC[i] = 0;
   __syncthreads();
-  auto put = [&](u64 q) {
-    const u32 r1 = (u32)(q & 0x7fffffffu) + 1u;
-    const u32 ls = (u32)(q >> 32) & 0xfffu;
+  auto put = [&](u32 q, u64 rb) {
+    const u32 r1 = (u32)(rb + (q & 0x3fffu)) + 1u;
+    const u32 ls = (q >> 14) & 0xfffu;
     if ((u64)(r1 - 1) < A.nMv) {
-      if (q & (1ull << 44)) atomicMax(&tA[ls], r1);
-      if (q & (1ull << 45)) atomicMax(&tF[ls], r1);
+      if (q & REC_HAS_A) atomicMax(&tA[ls], r1);
+      if (q & REC_HAS_F) atomicMax(&tF[ls], r1);
     } else {
       atomicMax(&tC[ls], r1);
     }
@@ -264,7 +277,7 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
       lo = lt[b];
       hi = lt[b + 1];
     }
-    u64 q[TBR_TK][2];
+    u32 q[TBR_TK][2];
 #pragma unroll
     for (int k = 0; k < TBR_TK; ++k) {
       const u32 lk = __builtin_amdgcn_readlane(lo, k), hk = __builtin_amdgcn_readlane(hi, k);
@@ -272,27 +285,27 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const u32 i = lk + (u32)lane + (u32)(u * WAVE);
-        q[k][u] = i < hk ? __builtin_nontemporal_load(&rec[rb + i]) : ~0ull;
+        q[k][u] = i < hk ? __builtin_nontemporal_load(&rec[rb + i]) : ~0u;
       }
     }
 #pragma unroll
     for (int k = 0; k < TBR_TK; ++k)
 #pragma unroll
       for (int u = 0; u < 2; ++u)
-        if (q[k][u] != ~0ull) put(q[k][u]);
+        if (q[k][u] != ~0u) put(q[k][u], (u64)(t0 + k) * TB_TILE);
 #pragma unroll
     for (int k = 0; k < TBR_TK; ++k) {
       const u32 lk = __builtin_amdgcn_readlane(lo, k), hk = __builtin_amdgcn_readlane(hi, k);
       const u64 rb = (u64)(t0 + k) * TB_TILE;
-      for (u32 i = lk + 2 * WAVE + (u32)lane; i < hk; i += WAVE) put(rec[rb + i]);
+      for (u32 i = lk + 2 * WAVE + (u32)lane; i < hk; i += WAVE) put(rec[rb + i], rb);
     }
   }
   __syncthreads();
   const u32 s0 = b * A.width;
   for (u32 i = threadIdx.x; i < A.width && (i64)(s0 + i) < n_sym; i += TBR_NT) {
     const u32 a = tA[i], f = tF[i], c = tC[i];
-    const int va = a ? A.mvA[a - 1] : -1, vf = f ? A.mvF[f - 1] : -1;
-    const int vc = c ? A.Mstr[(u64)(c - 1) - A.nMv] : -1;
+    const int va = a ? A.mv_addr[a - 1] : -1, vf = f ? A.mv_file[f - 1] : -1;
+    const int vc = c ? A.Rstr[(u64)(c - 1) - A.nMv] : -1;
     if (part) {
       const u64 tg = (u64)tag << 32;
       part[s0 + i] = a ? tg | (u32)(va + 1) : 0ull;
@@ -313,8 +326,8 @@ __global__ void k_tab_atomic(TbArgs A0, u32* __restrict__ tabA, u32* __restrict_
     if (!tb_record(A, r, &s, &fl)) continue;
     const u32 r1 = (u32)r + 1u;
     if (r < A.nMv) {
-      if (fl & 1u) atomicMax(&tabA[s], r1);
-      if (fl & 2u) atomicMax(&tabF[s], r1);
+      if (fl & REC_HAS_A) atomicMax(&tabA[s], r1);
+      if (fl & REC_HAS_F) atomicMax(&tabF[s], r1);
     } else {
       atomicMax(&tabR[s], r1);
     }
@@ -327,8 +340,8 @@ __global__ void k_finalize(TbArgs A0, const u32* __restrict__ tabA, const u32* _
   const TbArgs A = tb_load(A0);
   for (i64 s = (i64)blockIdx.x * BLOCK + threadIdx.x; s < n_sym; s += (i64)gridDim.x * BLOCK) {
     const u32 a = tabA[s], f = tabF[s], c = tabR[s];
-    const int va = a ? A.mvA[a - 1] : -1, vf = f ? A.mvF[f - 1] : -1;
-    const int vc = c ? A.Mstr[(u64)(c - 1) - A.nMv] : -1;
+    const int va = a ? A.mv_addr[a - 1] : -1, vf = f ? A.mv_file[f - 1] : -1;
+    const int vc = c ? A.Rstr[(u64)(c - 1) - A.nMv] : -1;
     if (part) {
       const u64 tg = (u64)tag << 32;
       part[s] = a ? tg | (u32)(va + 1) : 0ull;

@@ -5,26 +5,37 @@
 // other kind can conflict) the loop is a transducer over M = renames in T order
 // with state (ahead branch, d): d of the ahead branch's next renames were already
 // consumed as "other heads".  From a d = 0 state the walk only depends on the
-// natural-head test of each element, so: flag every natural-head conflict,
-// replay from each flagged start until d returns to 0 (region end q), and keep
-// the starts not covered by an earlier real region (resolved per cluster).
+// natural-head test of each element (its other-branch head is then that branch's
+// next rename), so: flag every natural-head conflict (k_window_* inside a window,
+// k_boundary for the renames whose head lies in a later window), replay from each
+// flagged start until d returns to 0 (region end q), and keep the starts not
+// covered by an earlier real region (resolved per cluster).
+//
+// M is held as tsrc[m] (local source op: its branch and, through v0, its newName
+// equality class) and tsym[m].  A replay keeps one cursor per branch: the first
+// not-yet-consumed rename of that branch after the current position, found by a
+// forward scan of tsrc (short on real logs; a long gap switches to a rank lookup
+// over the per-window rename counts wren, O(log W + window)).
 #pragma once
 
 #include "smx_common.h"
 
-// ---------------------------------------------------------------------------
-// kernels: DivergentRename walk over the rename block M (T order)
+#define WALK_SCAN 256         // forward-scan steps before the rank lookup
+#define REPLAY_CAP 256        // k_replay_q: steps before a region counts as long
+#define CUR_NONE 0xffffffffu  // cursor: no such rename
+#define CUR_HALO 0x80000000u  // cursor: halo index (| h); local positions are < 2^31
+#define Q_LONG 0xffffffffu    // k_replay_q: region not closed within REPLAY_CAP steps
 
 struct WalkArgs {
-  const u32* Msym;
-  const i32* Mcls;
-  const u8* Mside;
-  const u32* Mown;
-  const u32* RA;
-  const u32* RB;
+  const i32* tsrc;      // M position -> local source op (renames are tsrc[0, nR))
+  const u32* tsym;
+  const i32* v0;        // field array: local op j at j (A) or j + bgap (B)
+  const u32* wren;      // [W][2]: renames, A renames before window w
+  const u32* wbnd;      // [W]: boundary start | branch << 31
   const ComposeMeta* meta;
   u64 na_cap, nb_cap;   // host sizes: bounds for the device-side counts
-  u64 nR, nRA, nRB;     // filled on the device by walk_load
+  i64 bgap;
+  u64 nR, nRA, nRB, Wn; // filled on the device by walk_load
   u64 fail;
   // Sharded merge (smx_shard_step): the renames of each branch that follow this
   // shard's in the global rename order (halo_n[b] of them; halo_more[b] when the
@@ -43,36 +54,6 @@ __device__ __forceinline__ i32 walk_gsrc(const WalkArgs& W, i32 j) {
   return (u64)j < W.na_cap ? (i32)(W.src_a + j) : (i32)(W.src_b + ((i64)j - (i64)W.na_cap));
 }
 
-// The k-th rename (local numbering) of branch o: a local M position, or an entry
-// of the halo (the next shard's renames).  ok = false when branch o has no k-th
-// rename; a halo too short to tell flags meta->halo_overflow.
-struct WalkHead {
-  bool ok, local;
-  u32 sym;
-  i32 cls;
-  u32 u;  // local M position, or halo index
-};
-
-__device__ __forceinline__ WalkHead walk_head(const WalkArgs& W, int o, u64 k) {
-  WalkHead h{false, false, 0u, 0, 0u};
-  const u64 no = o ? W.nRB : W.nRA;
-  if (k < no) {
-    const u32 u = (o ? W.RB : W.RA)[k];
-    return WalkHead{true, true, W.Msym[u], W.Mcls[u], u};
-  }
-  // selects, not W.halo_*[o]: a dynamic index into the argument struct would put
-  // it in scratch memory
-  const u64 x = k - no;
-  const u64 hn = o ? W.halo_n[1] : W.halo_n[0];
-  if (x < hn) {
-    const u32* hs = o ? W.halo_sym[1] : W.halo_sym[0];
-    const i32* hc = o ? W.halo_cls[1] : W.halo_cls[0];
-    return WalkHead{true, false, hs[x], hc[x], (u32)x};
-  }
-  if (o ? W.halo_more[1] : W.halo_more[0]) const_cast<ComposeMeta*>(W.meta)->halo_overflow = 1;
-  return h;
-}
-
 // Sizes come from the device (no host sync before the walk); a failed
 // presorted plan or invalid input turns every walk kernel into a no-op.
 __device__ __forceinline__ WalkArgs walk_load(WalkArgs W) {
@@ -81,79 +62,211 @@ __device__ __forceinline__ WalkArgs walk_load(WalkArgs W) {
   W.nRA = min(m->n_ren_side[0], W.na_cap);
   W.nRB = min(m->n_ren_side[1], W.nb_cap);
   W.nR = W.nRA + W.nRB;
+  W.Wn = m->n_win;
   return W;
 }
 
-// Natural-head test: element m against the other branch's head when no skip
-// has happened yet (d = 0): that head is R_other[m - own(m)].  Each block owns a
-// contiguous range of FLAG_TILE renames and also reports how many it flagged.
-#define FLAG_TILE (BLOCK * 8)
-
-// The block's flagged positions go, in order, to its FLAG_TILE-slot range of
-// slots[] (k_compact then moves the few of them to their scanned offsets).
-// zskip != null: also clears the skip flags of the block's positions.
-__global__ void __launch_bounds__(BLOCK) k_flags(WalkArgs W0, u32* __restrict__ slots, u32* __restrict__ bcnt,
-                                                 u8* __restrict__ zskip) {
-  const WalkArgs W = walk_load(W0);
-  if (W.fail || (u64)blockIdx.x * FLAG_TILE >= W.nR) return;
-  constexpr int NI = FLAG_TILE / BLOCK;
-  __shared__ u32 wc[NI][NWAVES];
-  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-  const u64 base = (u64)blockIdx.x * FLAG_TILE;
-  u64 fb[NI];  // this wave's flag ballots
-#pragma unroll
-  for (int it = 0; it < NI; ++it) {
-    const u64 m = base + (u64)it * BLOCK + threadIdx.x;
-    bool f = false;
-    if (m < W.nR) {
-      if (zskip) zskip[m] = 0;
-      const int s = W.Mside[m];
-      const u64 k = m - W.Mown[m];
-      const WalkHead h = walk_head(W, 1 - s, k);
-      f = h.ok && h.sym == W.Msym[m] && h.cls != W.Mcls[m];
-    }
-    fb[it] = __ballot(f);
-    if (lane == 0) wc[it][w] = (u32)__popcll(fb[it]);
-  }
-  __syncthreads();
-  u32 before = 0;  // flags of this block before (it, wave w)
-  const u64 lt = lanemask_lt();
-#pragma unroll
-  for (int it = 0; it < NI; ++it) {
-    if ((fb[it] >> lane) & 1ull) {
-      u32 r = before + (u32)__popcll(fb[it] & lt);
-      for (int q = 0; q < w; ++q) r += wc[it][q];
-      slots[base + r] = (u32)(base + (u64)it * BLOCK + threadIdx.x);
-    }
-#pragma unroll
-    for (int q = 0; q < NWAVES; ++q) before += wc[it][q];
-  }
-  if (threadIdx.x == 0) bcnt[blockIdx.x] = before;
+__device__ __forceinline__ int walk_side(const WalkArgs& W, u64 m) { return (u64)W.tsrc[m] >= W.na_cap; }
+__device__ __forceinline__ i32 walk_cls_of_src(const WalkArgs& W, i32 j) {
+  return W.v0[(u64)j < W.na_cap ? (i64)j : (i64)j + W.bgap];
 }
 
-// Exclusive scan of the per-block flag counts (one block; nb is small) and the
-// candidate total into meta->n_cand.
-#define FO_NT 1024  // k_flag_offsets: one block, 16 counts per thread and round
-__global__ void __launch_bounds__(FO_NT) k_flag_offsets(WalkArgs W0, u32* __restrict__ bcnt, u64* total) {
+// Halo entry h of branch o (or CUR_NONE; a halo too short to tell flags overflow).
+// Selects, not W.halo_*[o]: a dynamic index into the argument struct would put it
+// in scratch memory.
+__device__ __forceinline__ u32 walk_halo(const WalkArgs& W, int o, u64 h) {
+  if (h < (o ? W.halo_n[1] : W.halo_n[0])) return CUR_HALO | (u32)h;
+  if (o ? W.halo_more[1] : W.halo_more[0]) const_cast<ComposeMeta*>(W.meta)->halo_overflow = 1;
+  return CUR_NONE;
+}
+
+// Renames of branch o before window w (w <= Wn; window Wn = the end of M).
+__device__ __forceinline__ u64 walk_before(const WalkArgs& W, int o, u64 w) {
+  if (w >= W.Wn) return o ? W.nRB : W.nRA;
+  const u64 a = W.wren[2 * w + 1];
+  return o ? (u64)W.wren[2 * w] - a : a;
+}
+
+// First rename of branch o at a position >= x, by counts: x's window, o-renames
+// before x, then the window holding the next one.
+__device__ u32 walk_rank_next(const WalkArgs& W, int o, u64 x) {
+  u64 lo = 0, hi = W.Wn;  // largest w with wren[2w] <= x
+  while (hi - lo > 1) {
+    const u64 mid = (lo + hi) >> 1;
+    if (W.wren[2 * mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  u64 c = walk_before(W, o, lo);
+  for (u64 m = W.wren[2 * lo]; m < x; ++m) c += walk_side(W, m) == o;
+  const u64 no = o ? W.nRB : W.nRA;
+  if (c >= no) return walk_halo(W, o, c - no);
+  lo = 0, hi = W.Wn;  // largest w with before(w) <= c: the window holding o-rename c
+  while (hi - lo > 1) {
+    const u64 mid = (lo + hi) >> 1;
+    if (walk_before(W, o, mid) <= c) lo = mid;
+    else hi = mid;
+  }
+  u64 k = c - walk_before(W, o, lo);
+  for (u64 m = W.wren[2 * lo];; ++m)
+    if (walk_side(W, m) == o && k-- == 0) return (u32)m;
+}
+
+// First rename of branch o at a local position >= from, else the halo.
+__device__ __forceinline__ u32 walk_next(const WalkArgs& W, int o, u64 from) {
+  u64 m = from;
+  for (int i = 0; i < WALK_SCAN; ++i, ++m) {
+    if (m >= W.nR) return walk_halo(W, o, 0);
+    if (walk_side(W, m) == o) return (u32)m;
+  }
+  return walk_rank_next(W, o, m);
+}
+
+// The o-rename after cursor c.
+__device__ __forceinline__ u32 walk_adv(const WalkArgs& W, int o, u32 c) {
+  if (c == CUR_NONE) return CUR_NONE;
+  if (c & CUR_HALO) return walk_halo(W, o, (u64)(c & ~CUR_HALO) + 1);
+  return walk_next(W, o, (u64)c + 1);
+}
+
+struct WalkHead {
+  u32 sym;
+  i32 cls;
+};
+__device__ __forceinline__ WalkHead walk_at(const WalkArgs& W, int o, u32 c) {
+  if (c & CUR_HALO) {
+    const u32 h = c & ~CUR_HALO;
+    return WalkHead{(o ? W.halo_sym[1] : W.halo_sym[0])[h], (o ? W.halo_cls[1] : W.halo_cls[0])[h]};
+  }
+  return WalkHead{W.tsym[c], walk_cls_of_src(W, W.tsrc[c])};
+}
+__device__ __forceinline__ i32 walk_src_at(const WalkArgs& W, int o, u32 c) {
+  if (c & CUR_HALO) return (o ? W.halo_src[1] : W.halo_src[0])[c & ~CUR_HALO];
+  return walk_gsrc(W, W.tsrc[c]);
+}
+
+#define CUR_UNSET (CUR_NONE - 1)  // cursor not computed yet
+
+struct ReplayState {
+  int ahead;
+  u32 d;
+  u32 h[2];  // first not-yet-consumed rename of each branch after the position (lazy)
+};
+
+__device__ __forceinline__ ReplayState replay_fresh() { return ReplayState{-1, 0u, {CUR_UNSET, CUR_UNSET}}; }
+
+// Replays the reference loop restricted to renames from position p with state st
+// (a candidate start has d = 0).  Returns the end q (the first position after which
+// d is back to 0, or nR if the region is still open at the shard's end; the final
+// state is left in st), or Q_LONG when CAP and the region is longer than
+// REPLAY_CAP steps.  WRITE: conflict pairs (global source indices) at pair_off..,
+// skipped positions in increasing order at skip_out.., and their skip bits.
+template <bool WRITE, bool CAP>
+__device__ u32 replay_region(const WalkArgs& W, u32 p, ReplayState& st, u32* nconf, i32* pairs, u64 pair_cap,
+                             u64 pair_off, u32* skip_out, u64* skipbits, u32* nskip) {
+  u32 m = p;
+  u32 nc = 0, ns = 0, steps = 0;
+  while (m < W.nR) {
+    const i32 j = W.tsrc[m];
+    const int s = (u64)j >= W.na_cap;
+    if (st.d > 0 && s == st.ahead) {
+      --st.d;  // consumed as the other head of an earlier conflict
+      if (WRITE) {
+        skip_out[ns] = m;
+        atomicOr((unsigned long long*)&skipbits[m >> 6], 1ull << (m & 63));
+      }
+      ++ns;
+    } else {
+      const int o = 1 - s;
+      if (st.h[o] == CUR_UNSET) st.h[o] = walk_next(W, o, (u64)m + 1);
+      const u32 hc = st.h[o];
+      if (hc != CUR_NONE) {
+        const WalkHead hd = walk_at(W, o, hc);
+        if (hd.sym == W.tsym[m] && hd.cls != walk_cls_of_src(W, j)) {
+          if (WRITE) {
+            const u64 slot = pair_off + nc;
+            if (slot < pair_cap) {
+              const i32 mu = walk_gsrc(W, j), hu = walk_src_at(W, o, hc);
+              pairs[2 * slot] = s ? hu : mu;
+              pairs[2 * slot + 1] = s ? mu : hu;
+            }
+            skip_out[ns] = m;
+            atomicOr((unsigned long long*)&skipbits[m >> 6], 1ull << (m & 63));
+          }
+          ++ns;
+          ++nc;
+          if (st.ahead != o) {
+            st.ahead = o;
+            st.d = 0;
+          }
+          ++st.d;
+          st.h[o] = walk_adv(W, o, hc);
+        }
+      }
+      st.h[s] = walk_next(W, s, (u64)m + 1);
+    }
+    ++m;
+    if (st.d == 0) break;
+    if (CAP && ++steps >= REPLAY_CAP) return Q_LONG;
+  }
+  *nconf = nc;
+  if (nskip) *nskip = ns;
+  return m;
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+
+// Renames after the other branch's last rename of their window: their natural
+// head is that branch's first rename after the window.  Flagged ones follow the
+// window's in-window candidates in its slots (wcandB[w] of them).  Re-running it
+// (sharded walk rounds) rewrites the same slots.
+__global__ void __launch_bounds__(BLOCK) k_boundary(WalkArgs W0, u32* __restrict__ cslot,
+                                                    const u32* __restrict__ wcand, u32* __restrict__ wcandB) {
   const WalkArgs W = walk_load(W0);
   if (W.fail) return;
-  const u32 nb = (u32)SMX_CEIL_DIV(W.nR, (u64)FLAG_TILE);
+  for (u64 w = (u64)blockIdx.x * BLOCK + threadIdx.x; w < W.Wn; w += (u64)gridDim.x * BLOCK) {
+    const u64 Mb = W.wren[2 * w], Me = w + 1 < W.Wn ? (u64)W.wren[2 * (w + 1)] : W.nR;
+    u32 cnt = 0;
+    if (Me > Mb) {
+      const u32 wb = W.wbnd[w];
+      const int o = 1 - (int)(wb >> 31);
+      const u32 hc = walk_next(W, o, Me);
+      if (hc != CUR_NONE) {
+        const WalkHead hd = walk_at(W, o, hc);
+        u32* out = cslot + Mb + wcand[w];
+        for (u64 m = Mb + (wb & 0x7fffffffu); m < Me; ++m)
+          if (W.tsym[m] == hd.sym && walk_cls_of_src(W, W.tsrc[m]) != hd.cls) out[cnt++] = (u32)m;
+      }
+    }
+    wcandB[w] = cnt;
+  }
+}
+
+// Exclusive scan of the per-window candidate counts (one block) and the total
+// into meta->n_cand.
+#define FO_NT 1024
+__global__ void __launch_bounds__(FO_NT) k_cand_offsets(WalkArgs W0, const u32* __restrict__ wcand,
+                                                        const u32* __restrict__ wcandB, u32* __restrict__ woff,
+                                                        u64* total) {
+  const WalkArgs W = walk_load(W0);
+  if (W.fail) return;
+  const u64 nw = W.Wn;
   __shared__ u32 s[FO_NT / WAVE + 1];
   u32 carry = 0;
-  for (u32 r0 = 0; r0 < nb; r0 += FO_NT * 16) {
-    const u32 b = r0 + threadIdx.x * 16;
+  for (u64 r0 = 0; r0 < nw; r0 += FO_NT * 16) {
+    const u64 b = r0 + threadIdx.x * 16;
     u32 v[16];
     u32 acc = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      v[j] = b + j < nb ? bcnt[b + j] : 0u;
+      v[j] = b + j < nw ? wcand[b + j] + wcandB[b + j] : 0u;
       acc += v[j];
     }
     u32 tot;
     u32 run = carry + block_excl_scan<OpSum, u32, FO_NT / WAVE>(acc, s, &tot);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      if (b + j < nb) bcnt[b + j] = run;
+      if (b + j < nw) woff[b + j] = run;
       run += v[j];
     }
     carry += tot;
@@ -161,91 +274,44 @@ __global__ void __launch_bounds__(FO_NT) k_flag_offsets(WalkArgs W0, u32* __rest
   if (threadIdx.x == 0) *total = carry;
 }
 
-// One wave per k_flags block: its slots[] run -> cand[] at the block's offset
-// (boff = exclusive scan of the counts; the total is meta->n_cand).
-__global__ void __launch_bounds__(BLOCK) k_compact(WalkArgs W0, const u32* __restrict__ slots,
-                                                   const u32* __restrict__ boff, const u64* __restrict__ total,
-                                                   u32* __restrict__ out) {
+// One wave per window: its candidate slots -> cand[] at the window's offset.
+__global__ void __launch_bounds__(BLOCK) k_cand_compact(WalkArgs W0, const u32* __restrict__ cslot,
+                                                        const u32* __restrict__ woff, const u64* __restrict__ total,
+                                                        u32* __restrict__ out) {
   const WalkArgs W = walk_load(W0);
-  const u64 fbk = (u64)blockIdx.x * NWAVES + threadIdx.x / WAVE;
-  const u64 nfb = SMX_CEIL_DIV(W.nR, (u64)FLAG_TILE);
-  if (W.fail || fbk >= nfb) return;
-  const u32 o = boff[fbk];
-  const u32 e = fbk + 1 < nfb ? boff[fbk + 1] : (u32)*total;
-  for (u32 i = threadIdx.x & (WAVE - 1); o + i < e; i += WAVE) out[o + i] = slots[fbk * FLAG_TILE + i];
-}
-
-// Replays the reference loop restricted to renames from position p with state
-// (ahead branch, d = how many of its next renames were consumed early); a
-// candidate start has d = 0.  Returns the end q (the first position after which
-// d is back to 0, or nR if the region is still open at the shard's end; the
-// final state is left in *ahead_io / *d_io).  WRITE: conflict pairs (global
-// source indices) and skip flags of local positions.
-template <bool WRITE>
-__device__ u32 replay_region(const WalkArgs& W, u32 p, int* ahead_io, u32* d_io, u32* nconf,
-                             const i32* order_ren, i32* pairs, u64 pair_cap, u64 pair_off, u8* skip) {
-  int ahead = *ahead_io;
-  u32 d = *d_io;
-  u32 m = p;
-  u32 nc = 0;
-  while (m < W.nR) {
-    const int s = W.Mside[m];
-    if (d > 0 && s == ahead) {
-      --d;  // consumed as the other head of an earlier conflict
-      if (WRITE) skip[m] = 1;
-    } else {
-      const int o = 1 - s;
-      const u64 k = (u64)(m - W.Mown[m]) + (o == ahead ? d : 0u);
-      const WalkHead h = walk_head(W, o, k);
-      if (h.ok && h.sym == W.Msym[m] && h.cls != W.Mcls[m]) {
-        if (WRITE) {
-          const u64 slot = pair_off + nc;
-          if (slot < pair_cap) {
-            const i32 mu = walk_gsrc(W, order_ren[m]);
-            const i32 hu = h.local ? walk_gsrc(W, order_ren[h.u]) : (o ? W.halo_src[1] : W.halo_src[0])[h.u];
-            pairs[2 * slot] = s ? hu : mu;
-            pairs[2 * slot + 1] = s ? mu : hu;
-          }
-          skip[m] = 1;
-          if (h.local) skip[h.u] = 1;
-        }
-        ++nc;
-        ++d;
-        ahead = o;
-      }
-    }
-    ++m;
-    if (d == 0) break;
-  }
-  *ahead_io = ahead;
-  *d_io = d;
-  *nconf = nc;
-  return m;
+  const u64 w = (u64)blockIdx.x * NWAVES + threadIdx.x / WAVE;
+  if (W.fail || w >= W.Wn) return;
+  const u32 o = woff[w];
+  const u32 e = w + 1 < W.Wn ? woff[w + 1] : (u32)*total;
+  const u64 Mb = W.wren[2 * w];
+  for (u32 i = threadIdx.x & (WAVE - 1); o + i < e; i += WAVE) out[o + i] = cslot[Mb + i];
 }
 
 // Incoming open region (sharded merge): the previous shards' walk ended with
 // state (ahead, d > 0); continue it from position 0.  Its conflicts come first in
 // this shard's list; candidates before its end are covered.
-__global__ void k_replay_in(WalkArgs W0, int in_ahead, u32 in_d, ComposeMeta* meta, const i32* __restrict__ order,
-                            i32* __restrict__ pairs, u64 pair_cap, u8* __restrict__ skip,
-                            u32* __restrict__ skiplist) {
+__global__ void k_replay_in(WalkArgs W0, int in_ahead, u32 in_d, ComposeMeta* meta, i32* __restrict__ pairs,
+                            u64 pair_cap, u32* __restrict__ skiplist, u64* __restrict__ skipbits) {
   const WalkArgs W = walk_load(W0);
   if (W.fail || in_d == 0 || threadIdx.x != 0 || blockIdx.x != 0) return;
-  const i32* order_ren = order + meta->base[SMX_KIND_RENAME];
-  int ahead = in_ahead;
-  u32 d = in_d, nc = 0;
-  const u32 q = replay_region<true>(W, 0, &ahead, &d, &nc, order_ren, pairs, pair_cap, 0, skip);
+  ReplayState st = replay_fresh();
+  st.ahead = in_ahead;
+  st.d = in_d;
+  // the ahead branch's first in_d renames were consumed before this shard
+  u32 c = walk_next(W, in_ahead, 0);
+  for (u32 i = 0; i < in_d && c != CUR_NONE; ++i) c = walk_adv(W, in_ahead, c);
+  st.h[in_ahead] = c;
+  st.h[1 - in_ahead] = walk_next(W, 1 - in_ahead, 0);
+  u32 nc = 0, ns = 0;
+  const u32 q = replay_region<true, false>(W, 0, st, &nc, pairs, pair_cap, 0, skiplist, skipbits, &ns);
   meta->q_in = q;
   meta->nconf_in = nc;
-  u32 o = 0;  // its skips head the sorted skip list
-  for (u32 m = 0; m < q; ++m)
-    if (skip[m]) skiplist[o++] = m;
-  meta->nskip_in = o;
-  atomicAdd((unsigned long long*)&meta->n_skip, (unsigned long long)o);
-  if (d > 0) {  // still open at this shard's end: hand it on
+  meta->nskip_in = ns;
+  atomicAdd((unsigned long long*)&meta->n_skip, (unsigned long long)ns);
+  if (st.d > 0) {  // still open at this shard's end: hand it on
     meta->out_open = 1;
-    meta->out_ahead = (u64)ahead;
-    meta->out_d = d;
+    meta->out_ahead = (u64)st.ahead;
+    meta->out_d = st.d;
   }
 }
 
@@ -255,24 +321,34 @@ __global__ void k_replay_q(WalkArgs W0, const u32* __restrict__ cand, const Comp
   if (W.fail) return;
   const u64 nc = meta->n_cand;
   for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
-    u32 k, d = 0;
-    int ahead = -1;
-    q[c] = replay_region<false>(W, cand[c], &ahead, &d, &k, nullptr, nullptr, 0, 0, nullptr);
+    u32 k = 0;
+    ReplayState st = replay_fresh();
+    q[c] = replay_region<false, true>(W, cand[c], st, &k, nullptr, 0, 0, nullptr, nullptr, nullptr);
     nconf[c] = k;
   }
 }
 
 // Real region starts: the first candidate of each cluster (no earlier candidate's
-// region reaches it) is real; inside a cluster, walk sequentially.
-__global__ void k_cluster(const u32* __restrict__ cand, const u32* __restrict__ q,
-                          const u32* __restrict__ pm, const u32* __restrict__ nconf,
-                          const ComposeMeta* meta, u32* __restrict__ nreal) {
+// region reaches it) is real; inside a cluster, walk sequentially.  A long region
+// (Q_LONG; it joins every later candidate to its cluster) is replayed in full here,
+// once, by the cluster's thread.
+__global__ void k_cluster(WalkArgs W0, const u32* __restrict__ cand, u32* __restrict__ q,
+                          const u32* __restrict__ pm, u32* __restrict__ nconf, const ComposeMeta* meta,
+                          u32* __restrict__ nreal) {
+  const WalkArgs W = walk_load(W0);
+  if (W.fail) return;
   const u64 nc = meta->n_cand;
   for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
     if (pm[c] > cand[c]) continue;  // not a cluster start
     u32 last_q = (u32)meta->q_in;   // an incoming region (sharded merge) covers [0, q_in)
     for (u64 j = c; j < nc && (j == c || pm[j] > cand[j]); ++j) {
       if (cand[j] >= last_q) {
+        if (q[j] == Q_LONG) {
+          u32 k = 0;
+          ReplayState st = replay_fresh();
+          q[j] = replay_region<false, false>(W, cand[j], st, &k, nullptr, 0, 0, nullptr, nullptr, nullptr);
+          nconf[j] = k;
+        }
         nreal[j] = nconf[j];
         last_q = q[j];
       } else {
@@ -282,40 +358,59 @@ __global__ void k_cluster(const u32* __restrict__ cand, const u32* __restrict__ 
   }
 }
 
-// Writes the conflict pairs, skip flags and skip-list entries of every real
+// Writes the conflict pairs, skip-list entries and skip bits of every real
 // region.  Regions are disjoint and ordered and a closed region's skips (2 per
-// conflict) lie in [p, q), so listing [p, q) in order yields the sorted skip list
-// after the incoming region's entries.  The last real region may still be open
-// at the shard's end (sharded merge): its heads beyond the end belong to the next
-// shard, its state is handed on, and its entries (fewer) end the list.
+// conflict) lie in [p, q) in increasing order, so each region writes its entries
+// at 2 x (conflicts before it), after the incoming region's.  The last real region
+// may still be open at the shard's end (sharded merge): its heads beyond the end
+// belong to the next shard, its state is handed on, and its entries (fewer) end
+// the list.
 __global__ void k_replay_write(WalkArgs W0, const u32* __restrict__ cand, const u32* __restrict__ nreal,
-                               const u32* __restrict__ coff, ComposeMeta* meta,
-                               const i32* __restrict__ order, i32* __restrict__ pairs,
-                               u64 pair_cap, u8* __restrict__ skip, u32* __restrict__ skiplist) {
+                               const u32* __restrict__ coff, ComposeMeta* meta, i32* __restrict__ pairs,
+                               u64 pair_cap, u32* __restrict__ skiplist, u64* __restrict__ skipbits) {
   const WalkArgs W = walk_load(W0);
   if (W.fail) return;
-  const i32* order_ren = order + meta->base[SMX_KIND_RENAME];
   const u64 nc = meta->n_cand;
   const u64 off0 = meta->nconf_in, soff0 = meta->nskip_in;
   for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
     if (nreal[c] == 0) continue;
-    u32 k, d = 0;
-    int ahead = -1;
-    const u32 p = cand[c];
-    const u32 q = replay_region<true>(W, p, &ahead, &d, &k, order_ren, pairs, pair_cap, off0 + coff[c], skip);
-    if (d > 0) {
+    u32 k = 0, ns = 0;
+    ReplayState st = replay_fresh();
+    replay_region<true, false>(W, cand[c], st, &k, pairs, pair_cap, off0 + coff[c],
+                               skiplist + soff0 + 2 * (u64)coff[c], skipbits, &ns);
+    if (st.d > 0) {
       meta->out_open = 1;
-      meta->out_ahead = (u64)ahead;
-      meta->out_d = d;
+      meta->out_ahead = (u64)st.ahead;
+      meta->out_d = st.d;
     }
-    u64 o = soff0 + 2 * (u64)coff[c];
-    u32 cnt = 0;
-    for (u32 m = p; m < q; ++m)
-      if (skip[m]) {
-        skiplist[o++] = m;
-        ++cnt;
-      }
-    atomicAdd((unsigned long long*)&meta->n_skip, (unsigned long long)cnt);
+    atomicAdd((unsigned long long*)&meta->n_skip, (unsigned long long)ns);
   }
 }
 
+// Sharded merge: the first `cap` renames of each branch in M order (symbol,
+// newName class, global source) -- the previous shards' halo.  One block scans M.
+#define EX_NT 1024
+__global__ void __launch_bounds__(EX_NT) k_halo_export(WalkArgs W0, u32* __restrict__ xsym,
+                                                       i32* __restrict__ xcls, i32* __restrict__ xsrc, u64 cap) {
+  const WalkArgs W = walk_load(W0);
+  if (W.fail) return;
+  __shared__ u32 s[EX_NT / WAVE + 1];
+  u64 got[2] = {0, 0};
+  for (u64 m0 = 0; m0 < W.nR && (got[0] < cap || got[1] < cap); m0 += EX_NT) {
+    const u64 m = m0 + threadIdx.x;
+    const bool valid = m < W.nR;
+    const int b = valid ? walk_side(W, m) : 0;
+    u32 tot;
+    const u32 rb = block_excl_scan<OpSum, u32, EX_NT / WAVE>(valid && b ? 1u : 0u, s, &tot);
+    const u32 nvalid = (u32)min((u64)EX_NT, W.nR - m0);
+    const u64 k = b ? got[1] + rb : got[0] + (u64)(threadIdx.x - rb);
+    if (valid && k < cap) {
+      const i32 j = W.tsrc[m];
+      xsym[b * cap + k] = W.tsym[m];
+      xcls[b * cap + k] = walk_cls_of_src(W, j);
+      xsrc[b * cap + k] = walk_gsrc(W, j);
+    }
+    got[1] += tot;
+    got[0] += nvalid - tot;
+  }
+}

@@ -13,6 +13,24 @@
 // The presorted kernel (k_window_f) handles branch logs whose timestamps never
 // decrease (lift.ts emits them in order); k_window_g handles branch logs that the
 // generic path pre-sorted by (timestamp, id), where step 3 is not needed.
+//
+// What a window writes, T-ordered:
+//   moves (T < nMv)     the FINAL composed records: no skip precedes the rename
+//                       block, so a move's output index is T, and it carries its own
+//                       newAddress / newFile (compose.py:37-43; a None value is
+//                       patched later from the symbol's prefix, k_mv_fix); plus
+//                       msym[T] = sym | has-address << 30 | has-file << 31 for the
+//                       last-writer tables
+//   every other op      tsrc / tsym at P = T - nMv (renames first, then the rest):
+//                       the source op and the symbol that k_emit needs
+//   renames             Rstr[m] (the rename-chain value, compose.py:71-72), m = P
+//   DivergentRename     the natural-head test (compose.py:60-70, 88-98 at d = 0) of
+//                       each rename against the other branch's next rename inside
+//                       the window; flagged positions go to the window's candidate
+//                       slots; the renames after the other branch's last rename of
+//                       the window are tested by k_boundary (smx_walk.h)
+//   per window          wren (renames / A renames before it), wbnd (where its
+//                       boundary renames start)
 #pragma once
 
 #include "smx_common.h"
@@ -28,40 +46,17 @@
 #define KREN SMX_KIND_RENAME
 #define NCHUNK (WIN_CAP / WAVE)
 #define CH 256                     // chunk of the presorted kind histogram
-#ifndef SMX_KEY64
-#define SMX_KEY64 1                // group-rank keys: 0 = 21-bit id prefix (u32), 1 = 42-bit (u64)
-#endif
-#ifndef SMX_LATE_PAYLOAD
-#define SMX_LATE_PAYLOAD 0         // 1: load sym/v0/v1 after the rank phase
-#endif
-#if SMX_KEY64
-typedef u64 rkey_t;
-#define RK_PREFIX_SHIFT 22         // hi >> 22: top 42 bits of oid_hi
-#else
-typedef u32 rkey_t;
-#define RK_PREFIX_SHIFT 43         // top 21 bits of oid_hi
-#endif
-#define RK_PER16 (16 / (int)sizeof(rkey_t))   // keys per 16-byte LDS read
-#ifndef RK_NRD
-#define RK_NRD (SMX_KEY64 ? 4 : 2)           // 16-byte reads per rank-loop step
-#endif
+#define SYM_MASK 0x3fffffffu       // msym: symbol bits (n_sym <= 2^30)
+#define MS_HAS_A (1u << 30)
+#define MS_HAS_F (1u << 31)
 
-// Number of keys < kp among the first m (<= RK_PER16) keys of a 16-byte LDS read.
-__device__ __forceinline__ int rk_count(const uint4 x, u32 kp, int m) {
-  return (m > 0 && x.x < kp) + (m > 1 && x.y < kp) + (m > 2 && x.z < kp) + (m > 3 && x.w < kp);
-}
-__device__ __forceinline__ int rk_count(const ulonglong2 x, u64 kp, int m) {
-  return (m > 0 && x.x < kp) + (m > 1 && x.y < kp);
-}
-__device__ __forceinline__ int rk_count(const uint4 x, u32 kp) {
+// Keys < kp among the four (or the first m) of a 16-byte LDS read.
+__device__ __forceinline__ int rk4(const uint4 x, u32 kp) {
   return (x.x < kp) + (x.y < kp) + (x.z < kp) + (x.w < kp);
 }
-__device__ __forceinline__ int rk_count(const ulonglong2 x, u64 kp) { return (x.x < kp) + (x.y < kp); }
-#if SMX_KEY64
-typedef ulonglong2 rkey16_t;
-#else
-typedef uint4 rkey16_t;
-#endif
+__device__ __forceinline__ int rk4(const uint4 x, u32 kp, int m) {
+  return (m > 0 && x.x < kp) + (m > 1 && x.y < kp) + (m > 2 && x.z < kp) + (m > 3 && x.w < kp);
+}
 
 struct WinArgs {
   const u8* kind;
@@ -78,52 +73,101 @@ struct WinArgs {
   i64 bgap;         // B op j is stored at j + bgap of the field arrays (presorted plan)
   i64 W;
   i64 n_sym;
+  i64 src_a, src_b; // global source index of local op j (sharded merge; 0 / na otherwise)
   int ablate;       // diagnostics only (SMX_ABLATE): skip phases, results invalid
   const i64* bnd;
   const u32* woff;  // [NCNT][W] exclusive offsets over windows (generic plan)
   const u32* cpre;  // presorted plan: [2][kinds][CM] chunk prefixes (256-op chunks)
   i64 CM;
   ComposeMeta* meta;
-  i32* order;
-  u32* symT;
-  i32* mvA;
-  i32* mvF;
-  u32* Msym;
-  i32* Mcls;
-  i32* Mstr;
-  u8* Mside;
-  u32* Mown;
-  u32* RA;
-  u32* RB;
+  // outputs (module comment)
+  i32* out_order;
+  i32* out_addr;
+  i32* out_file;
+  i32* out_ctx;
+  u32* msym;
+  i32* tsrc;
+  u32* tsym;
+  i32* Rstr;
+  u32* wren;        // [W][2]
+  u32* wbnd;        // [W]: first boundary rename (window-local) | its branch << 31
+  u32* cslot;       // candidate M positions, window w's from M offset wren[2w]
+  u32* wcand;       // [W] in-window candidates
   u64* dbg;         // diagnostics only: phase timestamps (k_window_f<true>)
 };
 
-// Writes one op's T-ordered records (registers -> HBM).
-__device__ __forceinline__ void win_emit(const WinArgs& P, const u64* base, i64 w, u32 k, u32 x,
-                                         u32 kb, u32 src, u32 s, i32 a, i32 f, int side, u32 own) {
-  const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (x - kb);
-  // Bounds guards: only a failed (and later discarded) presorted plan can trip them.
-  if (T >= (u64)(P.na + P.nb) || own >= (u64)(side ? P.nb : P.na)) return;
-  P.order[T] = (i32)src;
-  P.symT[T] = s;
-  if (k == KMOVE) {
-    P.mvA[T] = a;
-    P.mvF[T] = f;
-  } else if (k == KREN) {
-    const u64 m = T - base[KREN];
-    P.Msym[m] = s;
-    P.Mcls[m] = a;
-    P.Mstr[m] = f;
-    P.Mside[m] = (u8)side;
-    P.Mown[m] = own;
-    (side ? P.RB : P.RA)[own] = (u32)m;
+__device__ __forceinline__ i32 win_gsrc(const WinArgs& P, i64 j) {
+  return j < P.na ? (i32)(P.src_a + j) : (i32)(P.src_b + (j - P.na));
+}
+
+// The window's renames in final order, x = 0 .. RN-1: branch s(x), rank own(x) in
+// its branch's renames of the window, posl = the window-local x of each branch's
+// renames (A's first, then B's).  Natural head of x: the other branch's next
+// rename, the (x - own(x))-th of that branch in the window if there is one.
+// Flags -> candidate slots in M order; thread 0 writes where the boundary renames
+// (after the other branch's last rename of the window) start.
+// SymCls(x) -> (symbol, newName class) of rename x.
+template <int NT, typename SideOwn, typename SymCls>
+__device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mbase, int RN, int cntA,
+                                                 int cntB, const u16* posl, u64* cb, SideOwn side_own,
+                                                 SymCls sym_cls) {
+  constexpr int NW = NT / WAVE;
+  const int t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
+  const int nrc = (RN + WAVE - 1) / WAVE;
+  for (int c = wv; c < nrc; c += NW) {
+    const int x = c * WAVE + lane;
+    bool f = false;
+    if (x < RN) {
+      int s, own;
+      side_own(x, &s, &own);
+      const int k = x - own;
+      if (k < (s ? cntA : cntB)) {
+        const int h = posl[(s ? 0 : cntA) + k];
+        const uint2 me = sym_cls(x), hd = sym_cls(h);
+        f = me.x == hd.x && me.y != hd.y;
+      }
+    }
+    const u64 b = __ballot(f);
+    if (lane == 0) cb[c] = b;
+  }
+  if (t == 0) {
+    // boundary renames: those after the other branch's last rename of the window
+    u32 bnd = 0;
+    if (RN) {
+      int s, own;
+      side_own(RN - 1, &s, &own);
+      const int cnt_o = s ? cntA : cntB;
+      const u32 bx = cnt_o ? (u32)posl[(s ? 0 : cntA) + cnt_o - 1] + 1u : 0u;
+      bnd = bx | ((u32)s << 31);
+    }
+    P.wbnd[w] = bnd;
+  }
+  __syncthreads();
+  const u64 nall = (u64)(P.na + P.nb);
+  for (int c = wv; c < nrc; c += NW) {
+    const u64 b = cb[c];
+    if (!b) continue;
+    u32 before = lane < c ? (u32)__popcll(cb[lane]) : 0u;  // c < NCHUNK <= WAVE
+    before = wave_incl_sum(before);
+    before = __builtin_amdgcn_readlane(before, WAVE - 1);
+    if ((b >> lane) & 1ull) {
+      const u64 slot = Mbase + before + (u32)__popcll(b & lanemask_lt());
+      if (slot < nall) P.cslot[slot] = (u32)(Mbase + (u64)(c * WAVE + lane));
+    }
+  }
+  if (t == 0) {
+    u32 tot = 0;
+    for (int c = 0; c < nrc; ++c) tot += (u32)__popcll(cb[c]);
+    P.wcand[w] = tot;
   }
 }
 
 // ---------------------------------------------------------------------------
 // presorted windows (timestamps non-decreasing in each branch log)
 
+#ifndef WF_NT
 #define WF_NT 512
+#endif
 #define WF_WAVES (WF_NT / WAVE)
 #define WF_ITEMS (WIN_CAP / WF_NT)
 
@@ -142,17 +186,17 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   __shared__ __attribute__((aligned(16))) u64 sts[WIN_CAP];  // element space: timestamps; later slot-space rank keys
   __shared__ u16 sord[WIN_CAP];       // S order (merge), later the final order
   __shared__ u16 fin[WIN_CAP];        // slot -> element, later rename ranks
-  __shared__ u16 sl[WIN_CAP];         // element -> slot, later rank -> slot
+  __shared__ u16 sl[WIN_CAP];         // element -> slot, later rank -> slot, later posl
   __shared__ u8 skind[WIN_CAP];
-  __shared__ u8 srank[WIN_CAP];
-  __shared__ u64 gbits[NCHUNK];       // group-start bits over slots
+  __shared__ u8 skS[WIN_CAP];         // kinds in S order
+  __shared__ u64 gbits[NCHUNK];       // group-start bits over slots, later candidate ballots
   __shared__ u16 ccnt[NCHUNK][SMX_N_KINDS];
   __shared__ u16 rc[NCHUNK][2];
   __shared__ u32 kbase[SMX_N_KINDS + 1];
   __shared__ u32 wck[SMX_N_KINDS];
   __shared__ u64 base[SMX_N_KINDS + 1];
   __shared__ u32 woffk[SMX_N_KINDS + 2];  // this window's offsets: kinds, renames of A, of B
-  rkey_t* pkey = (rkey_t*)sts;        // slot space: rank keys (after step 4)
+  __shared__ u32 wtot[2];                 // the window's renames of A, of B
   u16* rown = fin;                    // rename rank within its branch (after step 5)
 
   const int t = threadIdx.x;
@@ -179,15 +223,12 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     }
     return;
   }
-  if (sz == 0) return;
   const i64 bpos = P.na + b0 - na;  // op index of B element e is bpos + e
   const i64 bld = bpos + P.bgap;    // ... stored at field index bld + e
   WSTAMP(0);
 
-  // 1. load the sort keys (kind, timestamp, top of the id) to LDS.  The payload
-  //    (sym, v0, v1) is loaded after the rank phase, so its HBM latency overlaps
-  //    the later LDS phases and it holds no registers across the rank loop.
-  u64 hi_r[WF_ITEMS];
+  // 1. load the sort keys (kind, timestamp, top of the id) and the payload
+  u32 hi_r[WF_ITEMS];  // the top 32 bits of oid_hi: the rank key (only they are loaded)
   u32 sym_r[WF_ITEMS];
   i32 v0_r[WF_ITEMS], v1_r[WF_ITEMS];
   u32 k_r[WF_ITEMS];
@@ -195,44 +236,36 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   // all loads are issued unconditionally (clamped to a valid op) so that the
   // loads of a lane are in flight together; the guards apply to the LDS stores only
   u64 ts_r[WF_ITEMS];
-  auto op_index = [&](int e) -> i64 {
+  auto op_index = [&](int e) -> i64 {  // (an empty window still writes its exports)
     const int ec = e < sz ? e : 0;
-    return ec < na ? a0 + ec : bld + ec;
+    return sz == 0 ? 0 : (ec < na ? a0 + ec : bld + ec);
   };
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const i64 j = op_index(t + WF_NT * i);
     k_r[i] = P.kind[j];
     ts_r[i] = P.kts[j];
-    hi_r[i] = P.khi[j];
-#if !SMX_LATE_PAYLOAD
+    hi_r[i] = reinterpret_cast<const u32*>(P.khi)[2 * j + 1];
     sym_r[i] = P.sym[j];
     v0_r[i] = P.v0[j];
     v1_r[i] = P.v1[j];
-#endif
   }
-  auto load_payload = [&]() {
-    if (!SMX_LATE_PAYLOAD) return;
-#pragma unroll
-    for (int i = 0; i < WF_ITEMS; ++i) {
-      // opaque element index: the compiler must not keep the key loads' 64-bit
-      // addresses alive (in registers or scratch) across the LDS phases
-      int e = t + WF_NT * i;
-      asm volatile("" : "+v"(e));
-      const i64 j = op_index(e);
-      sym_r[i] = P.sym[j];
-      v0_r[i] = P.v0[j];
-      v1_r[i] = P.v1[j];
-    }
-  };
+  u32 none_mv = 0;  // moves with a None value (prefix fix-up)
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
     if (e < sz) {
-      bad |= k_r[i] >= SMX_N_KINDS;
-      k_r[i] = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
+      bad |= k_r[i] >= SMX_N_KINDS || sym_r[i] >= (u64)P.n_sym;
+      const u32 k = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
       sts[e] = ts_r[i];
-      skind[e] = (u8)k_r[i];
+      skind[e] = (u8)k;
+      // the payload's first word: sym | the move's has-value bits (msym)
+      if (k == KMOVE) {
+        sym_r[i] = (sym_r[i] & SYM_MASK) | (v0_r[i] >= 0 ? MS_HAS_A : 0u) | (v1_r[i] >= 0 ? MS_HAS_F : 0u);
+        none_mv += v0_r[i] < 0 || v1_r[i] < 0;
+      } else {
+        sym_r[i] &= SYM_MASK;
+      }
     }
   }
   // kinds of the <= 255 ops between each branch's chunk start and the window start
@@ -262,32 +295,26 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   }
   __syncthreads();
   WSTAMP(1);
-  // window offsets: the partial-chunk kinds; presorted-layout check: every adjacent
-  // pair of each branch log is non-decreasing (the pair straddling a window start
-  // is checked here too); moves with a None value are counted for the prefix fix-up
+  if (P.ablate & 16) {  // diagnostics: load only (keeps every load live)
+    u32 x = 0;
+#pragma unroll
+    for (int i = 0; i < WF_ITEMS; ++i) x += sym_r[i] + (u32)v0_r[i] + (u32)v1_r[i] + (u32)hi_r[i];
+    if (x == 0x9e3779b9u) P.meta->dup_key = 1;
+    return;
+  }
+  // window offsets: the partial-chunk kinds
   if (kpart != 0xffffffffu) {
     const u32 k = kpart < SMX_N_KINDS ? kpart : SMX_N_KINDS - 1;
     atomicAdd(&woffk[k], 1u);
     if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + (t >= CH)], 1u);
   }
-  if (P.ablate & 8) {  // load + write only
-    load_payload();
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < WF_ITEMS; ++i) {
-      const int e = t + WF_NT * i;
-      if (e >= sz) continue;
-      const u32 src = (u32)(e < na ? a0 + e : bpos + e);
-      win_emit(P, base, w, k_r[i], (u32)e, 0, src, sym_r[i], v0_r[i], v1_r[i], e >= na, 0);
-    }
-    return;
-  }
 
-  // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties:
-  //    merge path, WF_ITEMS outputs per lane.  (Per-element rank searches, four
-  //    interleaved binary searches per lane, measured 2-3x slower: LDS-bound.)
-  //    Shares its barrier with the layout check: a window that fails the check
-  //    discards the merge.
+  // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties
+  //    (compose.py:54): merge path, WF_ITEMS outputs per lane, with the kinds
+  //    copied into S order.  Presorted-layout check: every adjacent pair of each
+  //    branch log is non-decreasing (the pair straddling a window start is checked
+  //    here too); it shares the merge's barrier and a window that fails it discards
+  //    the merge.
   bool dec = false;
   if (t == 0) dec = (a0 > 0 && na > 0 && prev_a > ts_r[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
 #pragma unroll
@@ -308,14 +335,15 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     int ia = lo, ib = d0 - lo;
     for (int d = d0; d < d1; ++d) {
       const bool take_a = ia < na && (ib >= nb || sts[ia] <= sts[na + ib]);
-      sord[d] = (u16)(take_a ? ia++ : na + ib++);
+      const int e = take_a ? ia++ : na + ib++;
+      sord[d] = (u16)e;
+      skS[d] = skind[e];
     }
   }
   if (__syncthreads_or(dec)) {
     if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
     return;
   }
-  WSTAMP(20);
   WSTAMP(3);
 
   // 3. stable multisplit of S by rank (wave ballots); element, kind and rank stay in
@@ -327,9 +355,8 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   for (int j = 0; j < WF_ITEMS; ++j) {
     const int m = t + WF_NT * j;
     me[j] = m < sz ? sord[m] : 0;
+    mkr[j] = m < sz ? skS[m] : 0u;
   }
-#pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) mkr[j] = t + WF_NT * j < sz ? skind[me[j]] : 0u;
   const u64 ltm = lanemask_lt();
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {
@@ -359,7 +386,6 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     if (lane == SMX_N_KINDS - 1) kbase[SMX_N_KINDS] = inc;
   }
   __syncthreads();
-  WSTAMP(5);
   WSTAMP(6);
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {
@@ -389,78 +415,100 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   }
   __syncthreads();
   WSTAMP(8);
-  // slot-space rank keys: a prefix of oid_hi, then the slot (unique per window)
+  // slot-space rank keys: the top 32 bits of oid_hi; sl is reset to "no slot" for
+  // the rank phase's collision check
+  u32* pkey = (u32*)sts;
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
     if (e < sz) {
       const int p = sl[e];
-      pkey[p] = ((rkey_t)(hi_r[i] >> RK_PREFIX_SHIFT) << 11) | (rkey_t)p;
+      pkey[p] = hi_r[i];
+      sl[e] = 0xffffu;
     }
   }
   __syncthreads();
   WSTAMP(9);
 
-  // 5. order each group by (oid, side, index).  Counting rank on 32-bit keys (21-bit
-  //    oid prefix, slot), four per LDS read; slot order is (side, index) order inside
-  //    a group.  If two adjacent ranks share the prefix (about 1 window in 100 on
-  //    random ids; always for duplicate ids) the window is re-ranked exactly on the
-  //    full oid.
-#pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) {
-    const int p = t + WF_NT * j;
-    if (p >= sz) break;
-    int r = p;
+  // 5. order each group by (oid, side, index): counting rank over the group on the
+  //    32-bit keys, four per LDS read.  Two keys of a group that are equal (about one
+  //    window in 10^4 on random ids; every duplicate id) get the same rank and leave
+  //    a rank without a slot: such a window is re-ranked exactly on (oid_hi, oid_lo,
+  //    slot) -- slot order is (side, index) order inside a group.
+  auto group_of = [&](int p, int* gs_o, int* ge_o) {
     const int bit = p & 63;
     int wi = p >> 6;
     u64 word = gbits[wi] & (bit == 63 ? ~0ull : ((1ull << (bit + 1)) - 1));
     while (word == 0) word = gbits[--wi];
-    const int gs = wi * 64 + 63 - __clzll(word);
+    *gs_o = wi * 64 + 63 - __clzll(word);
     wi = p >> 6;
     word = bit == 63 ? 0ull : (gbits[wi] & ~((1ull << (bit + 1)) - 1));
     while (word == 0 && ++wi < nch) word = gbits[wi];
-    int ge = word ? wi * 64 + __ffsll((unsigned long long)word) - 1 : sz;
-    ge = ge < sz ? ge : sz;
+    const int ge = word ? wi * 64 + __ffsll((unsigned long long)word) - 1 : sz;
+    *ge_o = ge < sz ? ge : sz;
+  };
+  // the group bounds of a wave's 64 consecutive slots from one read of every
+  // group-start word (nch <= 32) and lane broadcasts: no dependent LDS chain
+  const u64 gw = lane < nch ? gbits[lane] : 0ull;
+  const u64 gnz = __ballot(gw != 0);
+  auto bcast64 = [](u64 v, int l) -> u64 {
+    return (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, l) |
+           ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), l) << 32);
+  };
+  const u64 le_mask = lanemask_lt() | (1ull << lane);
+#pragma unroll
+  for (int j = 0; j < WF_ITEMS; ++j) {
+    const int wi = __builtin_amdgcn_readfirstlane((WF_NT * j) / WAVE + wv);  // this wave's slot chunk
+    if (wi >= nch) break;  // wave-uniform
+    const int p = wi * WAVE + lane;
+    const u64 W = bcast64(gw, wi);
+    int gs, ge;
+    {
+      const u64 below = W & le_mask;
+      if (below) {
+        gs = wi * WAVE + 63 - __clzll(below);
+      } else {  // the group began in an earlier chunk (slot 0 always starts one)
+        const u64 prev = gnz & ((1ull << wi) - 1);
+        const int wp = prev ? 63 - __clzll(prev) : 0;
+        gs = wp * WAVE + 63 - __clzll(bcast64(gw, wp) | 1ull);
+      }
+      const u64 above = W & ~le_mask;
+      if (above) {
+        ge = wi * WAVE + __ffsll((unsigned long long)above) - 1;
+      } else {
+        const u64 nxt = wi + 1 < WAVE ? gnz & ~((2ull << wi) - 1) : 0ull;
+        const int wn = nxt ? __ffsll((unsigned long long)nxt) - 1 : 0;
+        ge = nxt ? wn * WAVE + __ffsll((unsigned long long)bcast64(gw, wn)) - 1 : sz;
+      }
+      ge = ge < sz ? ge : sz;
+    }
+    if (p >= sz) continue;
+    int r = p;
     if (ge - gs > 1 && !(P.ablate & 2)) {
-      const rkey_t kp = pkey[p];
-      const rkey16_t* pv = reinterpret_cast<const rkey16_t*>(pkey);
-      constexpr int K = RK_PER16;
-      const int q0 = gs & ~(K - 1);
+      const u32 kp = pkey[p];
+      const uint4* pv = reinterpret_cast<const uint4*>(pkey);
+      const int q0 = gs & ~3;
       int c = 0;
       int q = q0;
-      // RK_NRD x 16 bytes of keys per step: independent LDS reads in flight
-      constexpr int NR = RK_NRD;
-      for (; q + NR * K <= ge; q += NR * K) {
-        rkey16_t x[NR];
-#pragma unroll
-        for (int u = 0; u < NR; ++u) x[u] = pv[q / K + u];
-#pragma unroll
-        for (int u = 0; u < NR; ++u) c += rk_count(x[u], kp);
+      for (; q + 8 <= ge; q += 8) {  // 2 x 16 bytes of keys per step in flight
+        const uint4 x0 = pv[q / 4], x1 = pv[q / 4 + 1];
+        c += rk4(x0, kp) + rk4(x1, kp);
       }
 #pragma unroll
-      for (int u = 0; u < NR; ++u) {  // fewer left: up to NR more reads, masked
-        const int qq = q + K * u;
-        if (qq < ge) c += rk_count(pv[qq / K], kp, ge - qq);
+      for (int u = 0; u < 2; ++u) {  // fewer left: up to 2 more reads, masked
+        const int qq = q + 4 * u;
+        if (qq < ge) c += rk4(pv[qq / 4], kp, ge - qq);
       }
-      if (q0 < gs) c -= rk_count(pv[q0 / K], kp, gs - q0);  // slots before the group
+      if (q0 < gs) c -= rk4(pv[q0 / 4], kp, gs - q0);  // slots before the group
       r = gs + c;
     }
     sord[r] = fin[p];
     sl[r] = (u16)p;  // sl now maps rank -> slot
   }
-  load_payload();
   __syncthreads();
   WSTAMP(10);
-  // Ranks are exact unless two elements of a group share the key prefix: then
-  // they sit at adjacent ranks in slot order.  Such runs (rare on random ids;
-  // every duplicate id) are re-sorted on the full oid, stably.
-  auto run_next = [&](int r) -> bool {  // rank r + 1 continues r's prefix run
-    const int r1 = r + 1;
-    if (r1 >= sz || ((gbits[r1 >> 6] >> (r1 & 63)) & 1ull)) return false;  // next group
-    return (pkey[sl[r]] >> 11) == (pkey[sl[r1]] >> 11);
-  };
   // 6. renames: rank among the window's renames of the same branch (final order).
-  //    Computed in the tie-detection phase; redone after a (rare) tie fix.
+  //    Computed in the collision-check phase; redone after a (rare) exact re-rank.
   const int R0 = kbase[KREN], RN = wck[KREN];
   const int nrc = (RN + WAVE - 1) / WAVE;
   auto rename_ranks = [&]() {
@@ -480,35 +528,33 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   };
   bool tie = false;
 #pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) {  // detection: prefixes of adjacent ranks (any group)
+  for (int j = 0; j < WF_ITEMS; ++j) {
     const int r = t + WF_NT * j;
-    if (r + 1 < sz) tie |= (pkey[sl[r]] >> 11) == (pkey[sl[r + 1]] >> 11);
+    if (r < sz) tie |= sl[r] == 0xffffu;
   }
   rename_ranks();
   const bool any_tie = __syncthreads_or(tie);
   WSTAMP(21);
   if (any_tie) {
-    for (int r0 = t; r0 + 1 < sz; r0 += WF_NT) {
-      if (!run_next(r0) || (r0 > 0 && run_next(r0 - 1))) continue;  // not a run start
-      int r1 = r0 + 1;
-      while (run_next(r1)) ++r1;
-      // insertion sort of sord[r0..r1] by (oid_hi, oid_lo); equal ids keep slot order
-      for (int x = r0 + 1; x <= r1; ++x) {
-        const int ex = sord[x];
-        const i64 jx = ex < na ? a0 + ex : bld + ex;
-        const u64 hx = P.khi[jx], lx = P.klo[jx];
-        int y = x - 1;
-        while (y >= r0) {
-          const int ey = sord[y];
-          const i64 jy = ey < na ? a0 + ey : bld + ey;
-          const u64 hy = P.khi[jy], ly = P.klo[jy];
-          if (hy < hx || (hy == hx && ly <= lx)) break;
-          sord[y + 1] = (u16)ey;
-          --y;
-        }
-        sord[y + 1] = (u16)ex;
+    // exact ranks from the full ids (global memory; rare)
+    for (int p = t; p < sz; p += WF_NT) {
+      int gs, ge;
+      group_of(p, &gs, &ge);
+      const int ex = fin[p];
+      const i64 jx = ex < na ? a0 + ex : bld + ex;
+      const u64 hx = P.khi[jx], lx = P.klo[jx];
+      int c = 0;
+      for (int q = gs; q < ge; ++q) {
+        if (q == p) continue;
+        const int ey = fin[q];
+        const i64 jy = ey < na ? a0 + ey : bld + ey;
+        const u64 hy = P.khi[jy], ly = P.klo[jy];
+        c += hy < hx || (hy == hx && (ly < lx || (ly == lx && q < p)));
       }
+      sl[gs + c] = (u16)p;
     }
+    __syncthreads();
+    for (int r = t; r < sz; r += WF_NT) sord[r] = fin[sl[r]];
     __syncthreads();
     rename_ranks();
     __syncthreads();
@@ -522,28 +568,21 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       rc[lane][0] = (u16)(i0 - x0);
       rc[lane][1] = (u16)(i1 - x1);
     }
+    if (lane == WAVE - 1) {
+      wtot[0] = i0;
+      wtot[1] = i1;
+    }
   }
+  if (none_mv) atomicAdd((unsigned long long*)&P.meta->n_move_none, (unsigned long long)none_mv);
   __syncthreads();
   WSTAMP(12);
 
-  // 7. write T-ordered records in final order (consecutive lanes -> consecutive T
-  //    inside each kind: coalesced).  The register payload is staged through the
-  //    now-free timestamp buffer in two rounds (sym + v0, then v1).
+  // 7. payload by element, round 1: sym (| the move's has-value bits) and v0; the
+  //    position of each rename in its branch's list (posl)
   if (P.ablate & 4) return;
-  {
-    // payload checks: symbols in range; moves with a None value (prefix fix-up)
-    u32 none_mv = 0;
-#pragma unroll
-    for (int i = 0; i < WF_ITEMS; ++i) {
-      if (t + WF_NT * i >= sz) continue;
-      bad |= sym_r[i] >= (u64)P.n_sym;
-      none_mv += (skind[t + WF_NT * i] == KMOVE && (v0_r[i] < 0 || v1_r[i] < 0));
-    }
-    if (bad) P.meta->bad_sym = 1;
-    if (none_mv) atomicAdd((unsigned long long*)&P.meta->n_move_none, (unsigned long long)none_mv);
-  }
-  u32* st_a = (u32*)sts;             // [WIN_CAP] sym
+  u32* st_a = (u32*)sts;             // [WIN_CAP] sym | flags
   i32* st_b = (i32*)sts + WIN_CAP;   // [WIN_CAP] v0, then v1
+  u16* posl = sl;
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
@@ -552,49 +591,70 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       st_b[e] = v0_r[i];
     }
   }
+  const int cntA = wtot[0], cntB = wtot[1];
+  for (int x = t; x < RN; x += WF_NT) {
+    const int e = sord[R0 + x];
+    const int s = e >= na;
+    posl[(s ? cntA : 0) + rc[x >> 6][s] + rown[x]] = (u16)x;
+  }
+  if (t == 0) {
+    P.wren[2 * w] = woffk[KREN];
+    P.wren[2 * w + 1] = woffk[CNT_REN_A];
+  }
   __syncthreads();
   WSTAMP(13);
-  const u64 wofs_ra = woffk[SMX_N_KINDS], wofs_rb = woffk[SMX_N_KINDS + 1];
+  // 8. natural-head DivergentRename flags -> candidate slots; window exports
+  win_rename_flags<WF_NT>(
+      P, w, woffk[KREN], RN, cntA, cntB, posl, gbits,
+      [&](int x, int* s, int* own) {
+        const int e = sord[R0 + x];
+        *s = e >= na;
+        *own = rc[x >> 6][*s] + rown[x];
+      },
+      [&](int x) -> uint2 {
+        const int e = sord[R0 + x];
+        return make_uint2(st_a[e] & SYM_MASK, (u32)st_b[e]);
+      });
+  WSTAMP(14);
+
+  // 9. T-ordered records in final order (consecutive lanes -> consecutive T inside
+  //    each kind: coalesced)
   const u64 nall = (u64)(P.na + P.nb);
+  const u64 nmv = base[KREN];
   for (int x = t; x < sz; x += WF_NT) {
     const int e = sord[x];
     const u32 k = skind[e];
     const u64 T = base[k] + woffk[k] + (u32)(x - kbase[k]);
     if (T >= nall) continue;  // only a failed (discarded) presorted plan can trip this
-    const u32 s = st_a[e];
-    P.order[T] = (i32)(e < na ? a0 + e : bpos + e);
-    P.symT[T] = s;
+    const i64 j = e < na ? a0 + e : bpos + e;
+    const u32 sa = st_a[e];
     if (k == KMOVE) {
-      P.mvA[T] = st_b[e];
-    } else if (k == KREN) {
-      const int side = e >= na;
-      const int xr = x - R0;
-      const u32 own = (u32)((side ? wofs_rb : wofs_ra) + rc[xr / WAVE][side] + rown[xr]);
-      const u64 m = T - base[KREN];
-      P.Msym[m] = s;
-      P.Mcls[m] = st_b[e];
-      P.Mside[m] = (u8)side;
-      P.Mown[m] = own;
-      if (own < (u64)(side ? P.nb : P.na)) (side ? P.RB : P.RA)[own] = (u32)m;
+      P.out_order[T] = win_gsrc(P, j);
+      P.out_addr[T] = st_b[e];
+      P.out_ctx[T] = -1;
+      P.msym[T] = sa;
+    } else {
+      P.tsrc[T - nmv] = (i32)j;
+      P.tsym[T - nmv] = sa & SYM_MASK;
     }
   }
   __syncthreads();
-  WSTAMP(14);
+  WSTAMP(15);
+  // round 2: v1 -> the move's newFile, the rename's chain value
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
     if (e < sz) st_b[e] = v1_r[i];
   }
   __syncthreads();
-  WSTAMP(15);
   for (int x = t; x < sz; x += WF_NT) {
     const int e = sord[x];
     const u32 k = skind[e];
     if (k != KMOVE && k != KREN) continue;
     const u64 T = base[k] + woffk[k] + (u32)(x - kbase[k]);
     if (T >= nall) continue;
-    if (k == KMOVE) P.mvF[T] = st_b[e];
-    else P.Mstr[T - base[KREN]] = st_b[e];
+    if (k == KMOVE) P.out_file[T] = st_b[e];
+    else P.Rstr[T - nmv] = st_b[e];
   }
   if (DBG) {
     __syncthreads();
@@ -621,7 +681,7 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   __shared__ u64 shi[WIN_CAP];
   __shared__ u64 slo[WIN_CAP];
   __shared__ u32 ssrc[WIN_CAP];
-  __shared__ u16 sord[WIN_CAP];
+  __shared__ u16 sord[WIN_CAP];       // merge order, later posl
   __shared__ u16 fin[WIN_CAP];
   __shared__ u16 rown[WIN_CAP];
   __shared__ u8 skind[WIN_CAP];
@@ -631,6 +691,8 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   __shared__ u32 kbase[SMX_N_KINDS + 1];
   __shared__ u32 wck[SMX_N_KINDS];
   __shared__ u64 base[SMX_N_KINDS + 1];
+  __shared__ u64 cb[NCHUNK];
+  __shared__ u32 wtot[2];
 
   const int t = threadIdx.x;
   const int lane = t & (WAVE - 1);
@@ -640,7 +702,6 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   const int na = (int)(P.bnd[2 * w + 2] - a0);
   const int nb = (int)(P.bnd[2 * w + 3] - b0);
   const int sz = na + nb;
-  if (sz == 0) return;
 
   bool bad = false;
   for (int e = t; e < sz; e += WG_NT) {
@@ -659,7 +720,7 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
   __syncthreads();
 
-  {
+  if (sz > 0) {
     const int d0 = t * WG_ITEMS < sz ? t * WG_ITEMS : sz;
     const int d1 = d0 + WG_ITEMS < sz ? d0 + WG_ITEMS : sz;
     int lo = d0 - nb > 0 ? d0 - nb : 0, hi = d0 < na ? d0 : na;
@@ -742,19 +803,56 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
       rc[lane][0] = (u16)(i0 - x0);
       rc[lane][1] = (u16)(i1 - x1);
     }
+    if (lane == WAVE - 1) {
+      wtot[0] = i0;
+      wtot[1] = i1;
+    }
   }
   __syncthreads();
+  const int cntA = wtot[0], cntB = wtot[1];
+  u16* posl = sord;
+  for (int x = t; x < RN; x += WG_NT) {
+    const int e = fin[R0 + x];
+    const int s = e >= na;
+    posl[(s ? cntA : 0) + rc[x >> 6][s] + rown[x]] = (u16)x;
+  }
+  if (t == 0) {
+    P.wren[2 * w] = P.woff[(i64)KREN * P.W + w];
+    P.wren[2 * w + 1] = P.woff[(i64)CNT_REN_A * P.W + w];
+  }
+  __syncthreads();
+  win_rename_flags<WG_NT>(
+      P, w, P.woff[(i64)KREN * P.W + w], RN, cntA, cntB, posl, cb,
+      [&](int x, int* s, int* own) {
+        const int e = fin[R0 + x];
+        *s = e >= na;
+        *own = rc[x >> 6][*s] + rown[x];
+      },
+      [&](int x) -> uint2 {
+        const u32 src = ssrc[fin[R0 + x]];
+        return make_uint2(P.sym[src], (u32)P.v0[src]);
+      });
 
+  const u64 nall = (u64)(P.na + P.nb);
+  const u64 nmv = base[KREN];
   for (int x = t; x < sz; x += WG_NT) {
     const int e = fin[x];
     const u32 k = skind[e];
     const u32 src = ssrc[e];
-    const int side = e >= na;
-    u32 own = 0;
-    if (k == KREN) {
-      const int xr = x - R0;
-      own = P.woff[(i64)(CNT_REN_A + side) * P.W + w] + rc[xr / WAVE][side] + rown[xr];
+    const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (u32)(x - kbase[k]);
+    if (T >= nall) continue;
+    const u32 s = P.sym[src];
+    if (k == KMOVE) {
+      const i32 a = P.v0[src], f = P.v1[src];
+      P.out_order[T] = win_gsrc(P, src);
+      P.out_addr[T] = a;
+      P.out_file[T] = f;
+      P.out_ctx[T] = -1;
+      P.msym[T] = (s & SYM_MASK) | (a >= 0 ? MS_HAS_A : 0u) | (f >= 0 ? MS_HAS_F : 0u);
+    } else {
+      P.tsrc[T - nmv] = (i32)src;
+      P.tsym[T - nmv] = s;
+      if (k == KREN) P.Rstr[T - nmv] = P.v1[src];
     }
-    win_emit(P, base, w, k, (u32)x, kbase[k], src, P.sym[src], P.v0[src], P.v1[src], side, own);
   }
 }

@@ -26,6 +26,8 @@ Key encodings (all exact; chosen once per call so every op uses the same one):
 """
 from __future__ import annotations
 
+from collections import OrderedDict
+
 import re
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Sequence
@@ -67,17 +69,26 @@ class _Tag:
         self.name = name
 
 
-_LIST, _DICT, _SET, _TUPLE = _Tag("list"), _Tag("dict"), _Tag("set"), _Tag("tuple")
+_LIST, _DICT, _TUPLE = _Tag("list"), _Tag("dict"), _Tag("tuple")
 
 
 def _freeze(v: Any):
-    """Hashable stand-in with the same ``==`` behaviour as ``v``."""
+    """Hashable stand-in with the same ``==`` behaviour as ``v``.
+
+    ``bytearray`` compares equal to the ``bytes`` of the same content and ``set`` to
+    the ``frozenset`` of the same elements, so they freeze to exactly those.  An
+    ``OrderedDict`` compares order-sensitively with another one but not with a
+    ``dict``, which no single key can express: it is rejected."""
     if isinstance(v, list):
         return (_LIST, tuple(_freeze(x) for x in v))
+    if isinstance(v, OrderedDict):
+        raise TypeError("OrderedDict")
     if isinstance(v, dict):
         return (_DICT, frozenset((k, _freeze(x)) for k, x in v.items()))
-    if isinstance(v, (set, bytearray)):
-        return (_SET, frozenset(v))
+    if isinstance(v, bytearray):
+        return bytes(v)
+    if isinstance(v, set):
+        return frozenset(v)
     if isinstance(v, tuple):
         try:
             hash(v)

@@ -1,7 +1,7 @@
 """A/B timing of the compose stages for one library build (SMX_LIB=...):
 median over rounds of per-stage ms per merge (all calls of a stage in one merge summed,
 e.g. failed presorted attempts before the generic plan) on the c3 workload (or
-argv[1] ops of config argv[2])."""
+argv[1] ops of config argv[2], argv[3] symbols)."""
 import os
 import sys
 
@@ -16,7 +16,10 @@ def main():
     from semantic_merge_amd import _lib, synth
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
     cfg = sys.argv[2] if len(sys.argv) > 2 else "c3"
-    spec = synth.LiftSpec(**{**synth.CONFIGS[cfg].__dict__, "n_total": n})
+    kw = {"n_total": n}
+    if len(sys.argv) > 3:
+        kw["n_sym"] = int(sys.argv[3])
+    spec = synth.LiftSpec(**{**synth.CONFIGS[cfg].__dict__, **kw})
     soa = synth.lift_soa(synth.lift_logs(spec))
     dc = _lib.DeviceCompose(soa)
     lib = _lib.lib()

@@ -1,6 +1,6 @@
 """Window-kernel ablation: time k_window_f variants in ONE process, interleaved rounds
 (cdna_hip_programming.md §5.4 rule 24).  SMX_ABLATE bits: 1 skip layout check,
-2 skip group ranking loop, 4 skip writes, 8 load+write only.  Results of ablated
+2 skip group ranking loop, 4 skip the output phases, 16 load only.  Results of ablated
 runs are invalid by design; only the window stage time is read."""
 import os
 import sys
@@ -20,8 +20,8 @@ def main():
     dc = _lib.DeviceCompose(soa)
     lib = _lib.lib()
     variants = [("base", {}), ("nocheck", {"SMX_ABLATE": "1"}), ("norank", {"SMX_ABLATE": "2"}),
-                ("nowrite", {"SMX_ABLATE": "4"}), ("loadwrite", {"SMX_ABLATE": "8"}),
-                ("tgt512", {"SMX_WIN_TGT": "512"}), ("tgt1536", {"SMX_WIN_TGT": "1536"}),
+                ("nowrite", {"SMX_ABLATE": "4"}), ("loadonly", {"SMX_ABLATE": "16"}),
+                ("tgt1280", {"SMX_WIN_TGT": "1280"}), ("tgt1536", {"SMX_WIN_TGT": "1536"}),
                 ("tgt1792", {"SMX_WIN_TGT": "1792"})]
     res = {k: [] for k, _ in variants}
     for rnd in range(4):

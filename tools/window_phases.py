@@ -10,10 +10,11 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 NST = 24
-NAMES = {0: "start", 1: "load", 2: "woff", 20: "check", 3: "merge", 4: "msplit", 5: "ccnt-scan",
-         6: "kbase", 7: "scatter", 8: "gbits", 9: "keys", 10: "rank", 21: "tiechk",
-         11: "renrank", 12: "rc-scan", 13: "stage1", 14: "write1", 15: "stage2", 16: "write2"}
-ORDER = [0, 1, 2, 20, 3, 4, 5, 6, 7, 8, 9, 10, 21, 11, 12, 13, 14, 15, 16]
+NAMES = {0: "start", 1: "load", 3: "check+merge", 4: "msplit", 6: "ccnt-scan",
+         7: "scatter", 8: "gbits", 9: "keys", 10: "rank", 21: "tiechk+renrank",
+         11: "tiefix", 12: "rc-scan", 13: "stage1+posl", 14: "flags+cand", 15: "write1",
+         16: "stage2+write2"}
+ORDER = [0, 1, 3, 4, 6, 7, 8, 9, 10, 21, 11, 12, 13, 14, 15, 16]
 
 
 def main():
