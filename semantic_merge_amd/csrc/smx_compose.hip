@@ -897,22 +897,6 @@ static WalkArgs walk_args(const Ctx& C, const smx_shard* sh) {
   return Wk;
 }
 
-__global__ void k_walk_init(ComposeMeta* meta) {
-  meta->n_cand = 0;
-  meta->n_conf = 0;
-  meta->n_conf_loc = 0;
-  meta->n_skip = 0;
-  meta->q_in = 0;
-  meta->nconf_in = 0;
-  meta->out_open = 0;
-  meta->out_ahead = 0;
-  meta->out_d = 0;
-  meta->halo_overflow = 0;
-  meta->nskip_in = 0;
-}
-
-__global__ void k_walk_done(ComposeMeta* meta) { meta->n_conf = meta->nconf_in + meta->n_conf_loc; }
-
 // DivergentRename walk (smx_walk.h): conflicts, skip bits, sorted skip list.
 // Every size is read on the device from meta: no host sync.
 static int launch_walk(const Ctx& C, const smx_shard* sh) {
@@ -923,11 +907,10 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
   u32* skiplist = C.ws<u32>(B_SKIPLIST);
   u32* part = C.ws<u32>(B_PART);
   HIP_TRY(hipMemsetAsync(skipbits, 0, (size_t)(SMX_CEIL_DIV(n, (i64)64) + 1) * 8, st));
-  hipLaunchKernelGGL(k_walk_init, dim3(1), dim3(1), 0, st, meta);
   const WalkArgs Wk = walk_args(C, sh);
   u32* cslot = C.ws<u32>(B_CSLOT);
   u32* wcand = C.ws<u32>(B_WCAND);
-  u32* wcandB = C.ws<u32>(B_WCANDB);
+  u32* wtot = C.ws<u32>(B_WCANDB);
   u32* wcoff = C.ws<u32>(B_WCOFF);
   u32* cand = C.ws<u32>(B_CAND);
   u32* q = C.ws<u32>(B_Q);
@@ -938,23 +921,22 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
   // u64 counters of meta: the scans write their u32 totals into the low word
   // (little endian) of the zeroed fields
   u32* nconf32 = (u32*)&meta->n_conf_loc;
+  u32* ncand32 = (u32*)&meta->n_cand;
   const u64* ncand_dev = &meta->n_cand;
   const i64 Wmax = max_windows(n);
   const int gsmall = 256;  // grid for loops over the (few) candidates
+  hipLaunchKernelGGL(k_boundary, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, meta, cslot, wcand, wtot);
   if (sh && sh->in_d > 0)
     hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d, meta,
                        C.out->conflicts, (u64)C.out->conflict_cap, skiplist, skipbits);
-  hipLaunchKernelGGL(k_boundary, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, cslot, wcand, wcandB);
-  hipLaunchKernelGGL(k_cand_offsets, dim3(1), dim3(FO_NT), 0, st, Wk, wcand, wcandB, wcoff, &meta->n_cand);
-  hipLaunchKernelGGL(k_cand_compact, dim3(SMX_CEIL_DIV(Wmax, (i64)NWAVES)), dim3(BLOCK), 0, st, Wk, cslot, wcoff,
-                     ncand_dev, cand);
+  HIP_TRY((scan_excl<OpSum, u32, u32>(wtot, wcoff, Wmax, &meta->n_win, part, ncand32, st)));
+  hipLaunchKernelGGL(k_cand_compact, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, cslot, wcoff, ncand_dev, cand);
   hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
-  HIP_TRY((scan_excl<OpMax, u32, u32>(q, pm, 0, ncand_dev, part, (u32*)nullptr, st)));
+  hipLaunchKernelGGL(k_scan1<OpMax>, dim3(1), dim3(S1_NT), 0, st, q, pm, ncand_dev, (u64)n, (u32*)nullptr);
   hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, q, pm, nconf, meta, nreal);
-  HIP_TRY((scan_excl<OpSum, u32, u32>(nreal, coff, 0, ncand_dev, part, nconf32, st)));
+  hipLaunchKernelGGL(k_scan1<OpSum>, dim3(1), dim3(S1_NT), 0, st, nreal, coff, ncand_dev, (u64)n, nconf32);
   hipLaunchKernelGGL(k_replay_write, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, nreal, coff, meta,
                      C.out->conflicts, (u64)C.out->conflict_cap, skiplist, skipbits);
-  hipLaunchKernelGGL(k_walk_done, dim3(1), dim3(1), 0, st, meta);
   HIP_TRY(hipGetLastError());
   return SMX_OK;
 }

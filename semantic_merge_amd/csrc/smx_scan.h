@@ -9,8 +9,9 @@
 #define SCAN_ITEMS 8
 #define SCAN_TILE (BLOCK * SCAN_ITEMS)
 
+// n_dev: the length, held on the device, at most n_host (the arrays' capacity)
 __device__ __forceinline__ i64 scan_len(const u64* n_dev, i64 n_host) {
-  return n_dev ? (i64)(*n_dev) : n_host;
+  return n_dev ? (i64)min(*n_dev, (u64)n_host) : n_host;
 }
 
 template <typename Op, typename TI, typename TO>

@@ -83,93 +83,61 @@ __device__ __forceinline__ bool tb_record(const TbArgs& A, u64 r, u32* sym, u32*
 
 // The TB_ITEMS records of a lane (r = base + it * TB_NT + lane), loads issued
 // together: a tile is all moves, all renames, or (one tile) mixed.
-// VB: also OR (value + 1) of the tile's values into vb (addr, file, name) for the
-// packed final-state table widths (k_tb_scatter only).
-template <bool VB = false>
 __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[TB_ITEMS], u32 (&fl)[TB_ITEMS],
-                                         bool (&ok)[TB_ITEMS], u32* vb = nullptr) {
+                                         bool (&ok)[TB_ITEMS]) {
   const u64 nrec = A.nMv + A.nR;
   const u64 end = base + (u64)TB_TILE;
   if (end <= A.nMv) {
     u32 x[TB_ITEMS];
-    i32 a[TB_ITEMS], f[TB_ITEMS];
 #pragma unroll
-    for (int it = 0; it < TB_ITEMS; ++it) {
-      const u64 r = base + (u64)it * TB_NT + threadIdx.x;
-      x[it] = A.msym[r];
-      if (VB) {
-        a[it] = A.mv_addr[r];
-        f[it] = A.mv_file[r];
-      }
-    }
+    for (int it = 0; it < TB_ITEMS; ++it) x[it] = A.msym[base + (u64)it * TB_NT + threadIdx.x];
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
       ok[it] = (x[it] & (MS_HAS_A | MS_HAS_F)) != 0;
       fl[it] = (x[it] & MS_HAS_A ? REC_HAS_A : 0u) | (x[it] & MS_HAS_F ? REC_HAS_F : 0u);
       sym[it] = min(x[it] & SYM_MASK, A.smax);
-      if (VB) {
-        vb[0] |= (u32)(a[it] + 1);
-        vb[1] |= (u32)(f[it] + 1);
-      }
     }
   } else if (base >= A.nMv && end <= nrec) {
     u32 s[TB_ITEMS];
-    i32 c[TB_ITEMS];
     const u64 m0 = base - A.nMv;
-    // the tile's 16384 skip bits: 256 words, lanes of a wave step share one
+#pragma unroll
+    for (int it = 0; it < TB_ITEMS; ++it) s[it] = A.tsym[m0 + (u64)it * TB_NT + threadIdx.x];
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
-      const u64 m = m0 + (u64)it * TB_NT + threadIdx.x;
-      s[it] = A.tsym[m];
-      if (VB) c[it] = A.Rstr[m];
-    }
-#pragma unroll
-    for (int it = 0; it < TB_ITEMS; ++it) {
-      const u64 m = m0 + (u64)it * TB_NT + threadIdx.x;
-      ok[it] = !tb_skipped(A, m);
+      ok[it] = !tb_skipped(A, m0 + (u64)it * TB_NT + threadIdx.x);
       fl[it] = 0;
       sym[it] = min(s[it], A.smax);
-      if (VB) vb[2] |= (u32)(c[it] + 1);
     }
   } else {
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
       const u64 r = base + (u64)it * TB_NT + threadIdx.x;
       ok[it] = r < nrec && tb_record(A, r, &sym[it], &fl[it]);
-      if (VB && r < A.nMv) {
-        vb[0] |= (u32)(A.mv_addr[r] + 1);
-        vb[1] |= (u32)(A.mv_file[r] + 1);
-      } else if (VB && r < nrec) {
-        vb[2] |= (u32)(A.Rstr[r - A.nMv] + 1);
-      }
     }
   }
 }
 
 // Tile-local bucket sort: the tile's records are counting-sorted by bucket in
 // LDS and written back to the tile's own range; lst[tile][b] = start of bucket b
-// in the tile, lst[tile][nbk] = the tile's record count.  Also ORs the value
-// widths of the packed final-state table (smx_common.h FinPack) into meta->vbits.
+// in the tile, lst[tile][nbk] = the tile's record count.  (The value widths of the
+// packed final-state table, smx_common.h FinPack, come from the window kernels.)
 __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict__ lst, u32* __restrict__ rec) {
   __shared__ u32 stage[TB_TILE];        // TB_TILE * 4 bytes
   __shared__ u32 lstart[TB_MAXBK];      // local bucket starts (then cursors)
   __shared__ u32 wsum[TB_NW + 1];
-  __shared__ u32 vb[3];
   const TbArgs A = tb_load(A0);
   const u64 nrec = A.nMv + A.nR;
   const u64 base = (u64)blockIdx.x * TB_TILE;
   if (base >= nrec) return;
   const u32 nbk = A.nbk;
   for (u32 i = threadIdx.x; i < nbk; i += TB_NT) lstart[i] = 0;
-  if (threadIdx.x < 3) vb[threadIdx.x] = 0;
   __syncthreads();
   u32 q[TB_ITEMS];
   u32 bk[TB_ITEMS];
   {
     u32 s[TB_ITEMS], fl[TB_ITEMS];
     bool ok[TB_ITEMS];
-    u32 v3[3] = {0u, 0u, 0u};
-    tb_items<true>(A, base, s, fl, ok, v3);
+    tb_items(A, base, s, fl, ok);
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
       const u32 loc = (u32)(it * TB_NT) + threadIdx.x;
@@ -180,12 +148,6 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
         q[it] = loc | ((s[it] - b * A.width) << 14) | fl[it];
         atomicAdd(&lstart[b], 1u);
       }
-    }
-    u32 oa = wave_or_to_last(v3[0]), of = wave_or_to_last(v3[1]), oc = wave_or_to_last(v3[2]);
-    if ((threadIdx.x & (WAVE - 1)) == WAVE - 1) {
-      if (oa) atomicOr(&vb[0], oa);
-      if (of) atomicOr(&vb[1], of);
-      if (oc) atomicOr(&vb[2], oc);
     }
   }
   __syncthreads();
@@ -214,12 +176,6 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
       wsum[TB_NW] = tot;
       lt[nbk] = tot;
     }
-  }
-  if (threadIdx.x < 3 && vb[threadIdx.x]) {
-    u32* g = const_cast<ComposeMeta*>(A.meta)->vbits;
-    const u32 mine = vb[threadIdx.x];
-    const u32 cur = __hip_atomic_load(&g[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((cur | mine) != cur) atomicOr(&g[threadIdx.x], mine);
   }
   __syncthreads();
   const u32 total = wsum[TB_NW];

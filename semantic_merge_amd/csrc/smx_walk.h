@@ -218,14 +218,32 @@ __device__ u32 replay_region(const WalkArgs& W, u32 p, ReplayState& st, u32* nco
 
 // Renames after the other branch's last rename of their window: their natural
 // head is that branch's first rename after the window.  Flagged ones follow the
-// window's in-window candidates in its slots (wcandB[w] of them).  Re-running it
-// (sharded walk rounds) rewrites the same slots.
-__global__ void __launch_bounds__(BLOCK) k_boundary(WalkArgs W0, u32* __restrict__ cslot,
-                                                    const u32* __restrict__ wcand, u32* __restrict__ wcandB) {
+// window's in-window candidates in its slots; wtot[w] = all of the window's
+// candidates.  Re-running it (sharded walk rounds) rewrites the same slots.  Block
+// 0 also resets the walk's counters in meta.
+__global__ void __launch_bounds__(BLOCK) k_boundary(WalkArgs W0, ComposeMeta* meta, u32* __restrict__ cslot,
+                                                    const u32* __restrict__ wcand, u32* __restrict__ wtot) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    meta->n_cand = 0;
+    meta->n_conf = 0;
+    meta->n_conf_loc = 0;
+    meta->n_skip = 0;
+    meta->q_in = 0;
+    meta->nconf_in = 0;
+    meta->out_open = 0;
+    meta->out_ahead = 0;
+    meta->out_d = 0;
+    meta->halo_overflow = 0;
+    meta->nskip_in = 0;
+  }
   const WalkArgs W = walk_load(W0);
-  if (W.fail) return;
   for (u64 w = (u64)blockIdx.x * BLOCK + threadIdx.x; w < W.Wn; w += (u64)gridDim.x * BLOCK) {
+    if (W.fail) {  // a failed plan: no candidates (the scan below still runs)
+      wtot[w] = 0;
+      continue;
+    }
     const u64 Mb = W.wren[2 * w], Me = w + 1 < W.Wn ? (u64)W.wren[2 * (w + 1)] : W.nR;
+    const u32 c0 = wcand[w];
     u32 cnt = 0;
     if (Me > Mb) {
       const u32 wb = W.wbnd[w];
@@ -233,58 +251,59 @@ __global__ void __launch_bounds__(BLOCK) k_boundary(WalkArgs W0, u32* __restrict
       const u32 hc = walk_next(W, o, Me);
       if (hc != CUR_NONE) {
         const WalkHead hd = walk_at(W, o, hc);
-        u32* out = cslot + Mb + wcand[w];
+        u32* out = cslot + Mb + c0;
         for (u64 m = Mb + (wb & 0x7fffffffu); m < Me; ++m)
           if (W.tsym[m] == hd.sym && walk_cls_of_src(W, W.tsrc[m]) != hd.cls) out[cnt++] = (u32)m;
       }
     }
-    wcandB[w] = cnt;
+    wtot[w] = c0 + cnt;
   }
 }
 
-// Exclusive scan of the per-window candidate counts (one block) and the total
-// into meta->n_cand.
-#define FO_NT 1024
-__global__ void __launch_bounds__(FO_NT) k_cand_offsets(WalkArgs W0, const u32* __restrict__ wcand,
-                                                        const u32* __restrict__ wcandB, u32* __restrict__ woff,
-                                                        u64* total) {
-  const WalkArgs W = walk_load(W0);
-  if (W.fail) return;
-  const u64 nw = W.Wn;
-  __shared__ u32 s[FO_NT / WAVE + 1];
-  u32 carry = 0;
-  for (u64 r0 = 0; r0 < nw; r0 += FO_NT * 16) {
-    const u64 b = r0 + threadIdx.x * 16;
-    u32 v[16];
-    u32 acc = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      v[j] = b + j < nw ? wcand[b + j] + wcandB[b + j] : 0u;
-      acc += v[j];
-    }
-    u32 tot;
-    u32 run = carry + block_excl_scan<OpSum, u32, FO_NT / WAVE>(acc, s, &tot);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (b + j < nw) woff[b + j] = run;
-      run += v[j];
-    }
-    carry += tot;
-  }
-  if (threadIdx.x == 0) *total = carry;
-}
-
-// One wave per window: its candidate slots -> cand[] at the window's offset.
+// One thread per window: its candidate slots -> cand[] at the window's offset
+// (woff = exclusive scan of wtot; the total is meta->n_cand).
 __global__ void __launch_bounds__(BLOCK) k_cand_compact(WalkArgs W0, const u32* __restrict__ cslot,
                                                         const u32* __restrict__ woff, const u64* __restrict__ total,
                                                         u32* __restrict__ out) {
   const WalkArgs W = walk_load(W0);
-  const u64 w = (u64)blockIdx.x * NWAVES + threadIdx.x / WAVE;
-  if (W.fail || w >= W.Wn) return;
-  const u32 o = woff[w];
-  const u32 e = w + 1 < W.Wn ? woff[w + 1] : (u32)*total;
-  const u64 Mb = W.wren[2 * w];
-  for (u32 i = threadIdx.x & (WAVE - 1); o + i < e; i += WAVE) out[o + i] = cslot[Mb + i];
+  if (W.fail) return;
+  for (u64 w = (u64)blockIdx.x * BLOCK + threadIdx.x; w < W.Wn; w += (u64)gridDim.x * BLOCK) {
+    const u32 o = woff[w];
+    const u32 e = w + 1 < W.Wn ? woff[w + 1] : (u32)*total;
+    const u64 Mb = W.wren[2 * w];
+    for (u32 i = 0; o + i < e; ++i) out[o + i] = cslot[Mb + i];
+  }
+}
+
+// Single-block exclusive scan (sum or max) of n = *n_dev values; *total_lo (low
+// word of a zeroed u64) = the total.  For the candidate arrays, which are short on
+// real logs (one block, no extra launches); long ones loop.
+#define S1_NT 1024
+template <typename Op>
+__global__ void __launch_bounds__(S1_NT) k_scan1(const u32* __restrict__ in, u32* __restrict__ out,
+                                                 const u64* n_dev, u64 cap, u32* total_lo) {
+  __shared__ u32 s[S1_NT / WAVE + 1];
+  const u64 n = min(*n_dev, cap);  // cap: the arrays' capacity
+  u32 carry = Op::template identity<u32>();
+  for (u64 r0 = 0; r0 < n; r0 += S1_NT * 8) {
+    const u64 b = r0 + threadIdx.x * 8;
+    u32 v[8];
+    u32 acc = Op::template identity<u32>();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = b + j < n ? in[b + j] : Op::template identity<u32>();
+      acc = Op::apply(acc, v[j]);
+    }
+    u32 tot;
+    u32 run = Op::apply(carry, block_excl_scan<Op, u32, S1_NT / WAVE>(acc, s, &tot));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (b + j < n) out[b + j] = run;
+      run = Op::apply(run, v[j]);
+    }
+    carry = Op::apply(carry, tot);
+  }
+  if (total_lo && threadIdx.x == 0) *total_lo = carry;
 }
 
 // Incoming open region (sharded merge): the previous shards' walk ended with
@@ -369,6 +388,7 @@ __global__ void k_replay_write(WalkArgs W0, const u32* __restrict__ cand, const 
                                const u32* __restrict__ coff, ComposeMeta* meta, i32* __restrict__ pairs,
                                u64 pair_cap, u32* __restrict__ skiplist, u64* __restrict__ skipbits) {
   const WalkArgs W = walk_load(W0);
+  if (blockIdx.x == 0 && threadIdx.x == 0) meta->n_conf = meta->nconf_in + meta->n_conf_loc;
   if (W.fail) return;
   const u64 nc = meta->n_cand;
   const u64 off0 = meta->nconf_in, soff0 = meta->nskip_in;

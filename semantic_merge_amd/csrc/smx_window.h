@@ -96,6 +96,17 @@ struct WinArgs {
   u64* dbg;         // diagnostics only: phase timestamps (k_window_f<true>)
 };
 
+// OR of the per-wave value widths into meta->vbits (k_tb_reduce packs the final-state
+// table with them); an atomic only when it adds bits.
+__device__ __forceinline__ void win_publish_widths(ComposeMeta* meta, const u32* vbw, int nw) {
+  for (int q = 0; q < 3; ++q) {
+    u32 m = 0;
+    for (int w = 0; w < nw; ++w) m |= vbw[w * 3 + q];
+    const u32 cur = __hip_atomic_load(&meta->vbits[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cur | m) != cur) atomicOr(&meta->vbits[q], m);
+  }
+}
+
 __device__ __forceinline__ i32 win_gsrc(const WinArgs& P, i64 j) {
   return j < P.na ? (i32)(P.src_a + j) : (i32)(P.src_b + (j - P.na));
 }
@@ -197,6 +208,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   __shared__ u64 base[SMX_N_KINDS + 1];
   __shared__ u32 woffk[SMX_N_KINDS + 2];  // this window's offsets: kinds, renames of A, of B
   __shared__ u32 wtot[2];                 // the window's renames of A, of B
+  __shared__ u32 vbw[WF_WAVES][3];        // per wave: value widths (addr, file, name)
   u16* rown = fin;                    // rename rank within its branch (after step 5)
 
   const int t = threadIdx.x;
@@ -251,6 +263,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     v1_r[i] = P.v1[j];
   }
   u32 none_mv = 0;  // moves with a None value (prefix fix-up)
+  u32 vb_a = 0, vb_f = 0, vb_c = 0;  // OR of (value + 1): widths of the packed final-state table
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
@@ -263,10 +276,21 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       if (k == KMOVE) {
         sym_r[i] = (sym_r[i] & SYM_MASK) | (v0_r[i] >= 0 ? MS_HAS_A : 0u) | (v1_r[i] >= 0 ? MS_HAS_F : 0u);
         none_mv += v0_r[i] < 0 || v1_r[i] < 0;
+        vb_a |= (u32)(v0_r[i] + 1);
+        vb_f |= (u32)(v1_r[i] + 1);
       } else {
         sym_r[i] &= SYM_MASK;
+        if (k == KREN) vb_c |= (u32)(v1_r[i] + 1);
       }
     }
+  }
+  vb_a = wave_or_to_last(vb_a);
+  vb_f = wave_or_to_last(vb_f);
+  vb_c = wave_or_to_last(vb_c);
+  if (lane == WAVE - 1) {
+    vbw[wv][0] = vb_a;
+    vbw[wv][1] = vb_f;
+    vbw[wv][2] = vb_c;
   }
   // kinds of the <= 255 ops between each branch's chunk start and the window start
   // (window offsets below); lanes 0..255 branch A, 256..511 branch B
@@ -316,7 +340,10 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   //    here too); it shares the merge's barrier and a window that fails it discards
   //    the merge.
   bool dec = false;
-  if (t == 0) dec = (a0 > 0 && na > 0 && prev_a > ts_r[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
+  if (t == 0) {
+    dec = (a0 > 0 && na > 0 && prev_a > ts_r[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
+    win_publish_widths(P.meta, &vbw[0][0], WF_WAVES);
+  }
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
@@ -693,6 +720,7 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   __shared__ u64 base[SMX_N_KINDS + 1];
   __shared__ u64 cb[NCHUNK];
   __shared__ u32 wtot[2];
+  __shared__ u32 vbw[WG_NT / WAVE][3];
 
   const int t = threadIdx.x;
   const int lane = t & (WAVE - 1);
@@ -704,6 +732,7 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   const int sz = na + nb;
 
   bool bad = false;
+  u32 vb_a = 0, vb_f = 0, vb_c = 0;
   for (int e = t; e < sz; e += WG_NT) {
     const i64 j = e < na ? a0 + e : P.na + b0 + (e - na);
     const u32 src = P.perm[j];
@@ -714,12 +743,27 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
     const u32 k = P.kind[src];
     bad |= (k >= SMX_N_KINDS) || (P.sym[src] >= (u64)P.n_sym);
     skind[e] = (u8)(k < SMX_N_KINDS ? k : SMX_N_KINDS - 1);
+    if (k == KMOVE) {
+      vb_a |= (u32)(P.v0[src] + 1);
+      vb_f |= (u32)(P.v1[src] + 1);
+    } else if (k == KREN) {
+      vb_c |= (u32)(P.v1[src] + 1);
+    }
+  }
+  vb_a = wave_or_to_last(vb_a);
+  vb_f = wave_or_to_last(vb_f);
+  vb_c = wave_or_to_last(vb_c);
+  if (lane == WAVE - 1) {
+    vbw[wv][0] = vb_a;
+    vbw[wv][1] = vb_f;
+    vbw[wv][2] = vb_c;
   }
   if (bad) P.meta->bad_sym = 1;
   for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WG_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
   __syncthreads();
 
+  if (t == 0) win_publish_widths(P.meta, &vbw[0][0], WG_NT / WAVE);
   if (sz > 0) {
     const int d0 = t * WG_ITEMS < sz ? t * WG_ITEMS : sz;
     const int d1 = d0 + WG_ITEMS < sz ? d0 + WG_ITEMS : sz;

@@ -1,4 +1,3 @@
 set -o pipefail
-O=gpurun_out/r02i; mkdir -p $O
+O=gpurun_out/r02k; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1; tail -2 $O/tests.log
-for r in 1 2; do timeout -k 10 200 python -u tools/stage_ab.py 2>/dev/null; done
