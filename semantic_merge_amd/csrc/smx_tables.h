@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
 
 #define TBR_NT 1024
 #ifndef TBR_TK
-#define TBR_TK 8
+#define TBR_TK 16
 #endif
 // TBR_TK: tiles per wave step in k_tb_reduce
 
