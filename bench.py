@@ -1,24 +1,42 @@
 """Benchmark: op-log compose+conflict throughput on device-resident synthetic logs.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--n-ops N]
+                    [--weak | --independent] [--no-pmc] [--no-cpu-baseline] [--no-e2e]
 
 One step = one composition (semmerge/compose.py:11-114 restated on the GPU) of
-SURVEY §8(d) config 3: 100M lift-shaped ops (50M per branch) per GPU, 1M symbols,
-seed 11.  Inputs are resident in HBM before timing.  N = 1: one smx_compose call.
-N > 1 (torchrun, one process per GPU): ONE merge of N x 100M ops sharded by
-timestamp key range (semantic_merge_amd/shard.py): each rank starts from its
-index slices of both branch logs, and a step is the whole sharded composition --
-the RCCL all-to-all that moves ops to their key-range shard, the per-shard
-kernels, the walk hand-off and the MAX all-reduce of the chain tables (weak
-scaling: 100M ops per GPU).  --independent runs N unrelated merges instead.  The
-time is the max over ranks; rank 0 prints one JSON line.
+SURVEY §8(d) config 3: 100M lift-shaped ops (50M per branch), 1M symbols, seed 11.
+Inputs are resident in HBM before timing.  N = 1: one smx_compose call per step.
+N > 1 (torchrun, one process per GPU): by default ONE merge of the same 100M ops
+split over the N ranks (strong scaling, BASELINE config 3 "100M ops across 8 GPUs"),
+sharded by timestamp key range (semantic_merge_amd/shard.py); a step is the whole
+sharded composition -- the packed all-to-all that moves ops to their key-range
+shard, the per-shard kernels, the walk hand-off and the MAX all-reduce of the chain
+tables.  --weak: N x 100M ops (100M per GPU); --independent: N unrelated merges.
+The time is the max over ranks; rank 0 prints one JSON line.
+
+Rank 0 at N = 1 also reports, after the timed steps (never inside them):
+  roofline.traffic / pipeline_traffic  HBM bytes per launch from rocprofv3 --pmc
+        FETCH_SIZE and WRITE_SIZE passes over this same workload (child processes,
+        one counter per pass; FETCH_SIZE x2 for gfx950's streaming reads, WRITE_SIZE
+        x1, MI355X_MICROARCH.md "HBM"), null when rocprofv3 is unavailable
+  cpu_baseline   the C port of the reference loop (oracle/compose_ref.c) on 1 thread,
+        plus legs: the same on every host thread at once (independent samples),
+        the pure-Python restatement (oracle/compose_ref.py) on 1 core, and the
+        reference's own compose_oplogs as measured in the build container
+  end_to_end     the drop-in compose_oplogs on a config-2-shaped log of Op objects:
+        native marshal, device compose, native materialise
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -30,10 +48,141 @@ METRIC = "op-log compose+conflict throughput (ops/s), 100M-op logs, 1/2/4/8 GPUs
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 PIPE_BYTES_PER_OP = 53         # 37 B in + 16 B out per op (+8 B per conflict)
 WINDOW_BYTES_PER_OP = 41       # k_window: 37 B of input read once + 4 B T-order index written
+REF_PY_OPS_S = 47_600          # SURVEY §3.4 / BASELINE.md: reference compose_oplogs, 1 core, 1M ops
+FETCH_FACTOR, WRITE_FACTOR = 2.0, 1.0   # gfx950 FETCH_SIZE reads 1/2 of streamed bytes (guide)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def pmc_traffic(args) -> dict:
+    """HBM bytes per launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a
+    child run of this benchmark (2 timed + 1 warm-up merges)."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return {"status": "rocprofv3 not found"}
+    out = {}
+    per = {}   # kernel -> counter -> [values per dispatch]
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="smx_pmc_", dir="/tmp")
+        cmd = [exe, "--pmc", counter, "--kernel-include-regex", "k_", "-d", d, "-o", "p",
+               "--output-format", "csv", "--", sys.executable, os.path.join(REPO, "bench.py"),
+               "--steps", "2", "--warmup", "1", "--config", args.config, "--no-cpu-baseline",
+               "--no-pmc", "--no-e2e"]
+        if args.n_ops:
+            cmd += ["--n-ops", str(args.n_ops)]
+        if args.n_sym:
+            cmd += ["--n-sym", str(args.n_sym)]
+        env = dict(os.environ, TMPDIR="/tmp")
+        try:
+            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, timeout=240)
+        except subprocess.TimeoutExpired:
+            return {"status": f"{counter} pass timed out"}
+        if r.returncode != 0:
+            return {"status": f"{counter} pass failed rc={r.returncode}: "
+                              + r.stderr.decode(errors="replace")[-200:]}
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        for f in files:
+            for row in csv.DictReader(open(f)):
+                name = row["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+                per.setdefault(name, {}).setdefault(row["Counter_Name"], []).append(
+                    float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+    merges = 3  # warm-up + 2 timed steps in the child
+
+    def kbytes(vals, factor):
+        return sum(vals) * 1024.0 * factor
+
+    win = [k for k in per if k.startswith("k_window_f") or k.startswith("k_window_g")]
+    if win:
+        k = win[0]
+        f, w = per[k].get("FETCH_SIZE", []), per[k].get("WRITE_SIZE", [])
+        out["kernel"] = k
+        out["traffic"] = round((kbytes(f, FETCH_FACTOR) + kbytes(w, WRITE_FACTOR)) / max(len(f), 1))
+    tot = 0.0
+    kern = {}
+    for k, cs in per.items():
+        b = (kbytes(cs.get("FETCH_SIZE", []), FETCH_FACTOR)
+             + kbytes(cs.get("WRITE_SIZE", []), WRITE_FACTOR)) / merges
+        kern[k] = round(b)
+        tot += b
+    out["pipeline_traffic"] = round(tot)
+    out["per_kernel"] = dict(sorted(kern.items(), key=lambda x: -x[1])[:12])
+    out["status"] = "ok"
+    return out
+
+
+def cpu_baseline(soa, args) -> dict:
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import compose_ref, oracle  # test infrastructure: the checker, timed here
+    from semantic_merge_amd.marshal import SoA
+
+    def sample(half):
+        half = min(half, soa.n_a, soa.n_b)
+        idx = np.concatenate([np.arange(half), soa.n_a + np.arange(half)])
+        return SoA(half, half, soa.kind[idx], soa.ts[idx], soa.oid_hi[idx], soa.oid_lo[idx],
+                   soa.sym[idx], soa.v0[idx], soa.v1[idx], soa.n_sym)
+
+    s1 = sample(args.cpu_sample // 2)
+    t0 = time.perf_counter()
+    oracle.compose(s1)
+    dt = time.perf_counter() - t0
+    res = {"value": round(s1.n / dt, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+           "sample": f"first {s1.n_a:,} ops of each branch of the same workload ({s1.n:,} ops) "
+                     f"through oracle/compose_ref.c, 1 thread, {dt:.1f}s"}
+    legs = {}
+    # every host thread at once: independent merges (ctypes releases the GIL)
+    threads = min(16, os.cpu_count() or 1)
+    sN = sample(args.cpu_sample // 8)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda _: oracle.compose(sN), range(threads)))
+    dtN = time.perf_counter() - t0
+    legs["c_port_all_threads"] = {"value": round(threads * sN.n / dtN, 1), "cores": threads,
+                                  "sample": f"{threads} independent {sN.n:,}-op merges, {dtN:.1f}s"}
+    sp = sample(200_000)
+    t0 = time.perf_counter()
+    compose_ref.compose(sp)
+    dtp = time.perf_counter() - t0
+    legs["python_restatement_1core"] = {"value": round(sp.n / dtp, 1), "cores": 1,
+                                        "sample": f"{sp.n:,} ops through oracle/compose_ref.py, {dtp:.1f}s"}
+    legs["reference_python_build_container"] = {
+        "value": REF_PY_OPS_S, "cores": 1,
+        "sample": "reference semmerge compose_oplogs on 1M config-2 ops, measured in the build "
+                  "container (Xeon), not on this host (SURVEY.md §3.4, BASELINE.md)"}
+    res["legs"] = legs
+    return res
+
+
+def end_to_end(n_ops: int) -> dict:
+    """The drop-in compose_oplogs on Op objects (config-2 shape), split into its legs."""
+    from semantic_merge_amd import synth
+    from semantic_merge_amd._lib import compose_soa
+    from semantic_merge_amd.marshal import marshal_native
+    from semantic_merge_amd.materialize import materialize_conflicts, materialize_ops_native
+    from semantic_merge_amd.oplog import ops_from_dicts
+
+    logs = synth.lift_logs(synth.LiftSpec(n_ops, max(n_ops // 100, 1), 7))
+    A, B = synth.lift_op_dicts(logs)
+    oa, ob = ops_from_dicts(A), ops_from_dicts(B)
+    compose_soa(marshal_native(oa[:100], ob[:100]))  # warm the device path
+    t = [time.perf_counter()]
+    soa = marshal_native(oa, ob)
+    t.append(time.perf_counter())
+    order, addr, file, ctx, pairs = compose_soa(soa)
+    t.append(time.perf_counter())
+    ops = oa + ob
+    out = materialize_ops_native(ops, soa.kind, soa.strings, order, addr, file, ctx)
+    materialize_conflicts(ops, pairs)
+    t.append(time.perf_counter())
+    tot = t[3] - t[0]
+    return {"n_ops": n_ops, "composed": len(out), "ops_per_s": round(n_ops / tot, 1),
+            "marshal_s": round(t[1] - t[0], 4), "device_s": round(t[2] - t[1], 4),
+            "materialize_s": round(t[3] - t[2], 4), "total_s": round(tot, 4),
+            "note": "compose_oplogs drop-in on Op objects; device_s includes host<->device copies"}
 
 
 def main() -> None:
@@ -45,9 +194,13 @@ def main() -> None:
     ap.add_argument("--n-ops", type=int, default=0, help="override the config's op count")
     ap.add_argument("--n-sym", type=int, default=0, help="override the config's symbol count")
     ap.add_argument("--cpu-sample", type=int, default=40_000_000,
-                    help="ops in the CPU-baseline sample (rank 0, N=1 only)")
+                    help="ops in the 1-thread CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the drop-in end-to-end leg")
+    ap.add_argument("--e2e-ops", type=int, default=100_000)
     ap.add_argument("--verify", action="store_true", help="check GPU == oracle (slow, N = 1)")
+    ap.add_argument("--weak", action="store_true", help="N > 1: N x the config's ops (weak scaling)")
     ap.add_argument("--independent", action="store_true",
                     help="N > 1: independent merges per rank instead of one sharded merge")
     args = ap.parse_args()
@@ -79,11 +232,14 @@ def main() -> None:
     if args.n_sym:
         spec = synth.LiftSpec(**{**spec.__dict__, "n_sym": args.n_sym})
     sharded = world > 1 and not args.independent
+    strong = sharded and not args.weak
+    n_job = spec.n_total if strong else world * spec.n_total   # ops of the whole job per step
     t0 = time.time()
     sc = dc = None
     if sharded:
         from semantic_merge_amd import shard
-        soa, na_g, nb_g = synth.lift_slice_soa(spec, rank, world)
+        rank_spec = synth.LiftSpec(**{**spec.__dict__, "n_total": spec.n_total // world}) if strong else spec
+        soa, na_g, nb_g = synth.lift_slice_soa(rank_spec, rank, world)
         sl_a, sl_b, _, _ = shard.slices_from_soa(soa, 0, 1, dev)
         log(f"[rank {rank}] generated slice of {soa.n:,} ops in {time.time() - t0:.1f}s")
         sc = shard.ShardedCompose(sl_a, sl_b, na_g, nb_g, soa.n_sym, shard.Comm(), dev)
@@ -118,11 +274,12 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     lib.smx_set_profiling(0)
+    plan = _lib.DeviceCompose.last_plan()
     stages = _lib.stage_times()
     if sharded:
         fin = sc.sum_final
         nconf = int(fin[:, shard.S_NCONF].sum())
-        k = world * soa.n - int(fin[:, shard.S_NSKIP].sum())
+        k = int(fin[:, 0:18].sum()) - int(fin[:, shard.S_NSKIP].sum())
     else:
         k, nconf = (int(x) for x in dc.counts.cpu().tolist())
     elapsed = max_over_ranks(elapsed, dev)
@@ -143,34 +300,28 @@ def main() -> None:
 
     n = soa.n
     ms_step = elapsed / args.steps * 1e3
-    value = job_throughput(n, world, args.steps, elapsed)
+    value = job_throughput(n_job, 1, args.steps, elapsed)
     win_ms, win_calls = stages.get("window", (0.0, 0))
     win_avg = win_ms / max(win_calls, 1)
     achieved = WINDOW_BYTES_PER_OP * n / (win_avg * 1e-3) / 1e9 if win_avg > 0 else None
-    traffic = None
-    prof = os.path.join(REPO, "profiles", "pmc_window.json")
-    if os.path.exists(prof) and args.config == "c3":  # measured on the config-3 window kernel
-        rec = json.load(open(prof))
-        if rec.get("n_ops") == n:
-            traffic = rec.get("hbm_bytes_per_launch")
-    pipe_gbs = (PIPE_BYTES_PER_OP * n + 8 * nconf) / (ms_step * 1e-3) / 1e9
+    pipe_gbs = (PIPE_BYTES_PER_OP * n_job + 8 * nconf) / (ms_step * 1e-3) / 1e9
 
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        from oracle import oracle
-        from semantic_merge_amd.marshal import SoA
-        half = min(args.cpu_sample // 2, soa.n_a, soa.n_b)
-        idx = np.concatenate([np.arange(half), soa.n_a + np.arange(half)])
-        sample = SoA(half, half, soa.kind[idx], soa.ts[idx], soa.oid_hi[idx], soa.oid_lo[idx],
-                     soa.sym[idx], soa.v0[idx], soa.v1[idx], soa.n_sym)
-        t0 = time.perf_counter()
-        oracle.compose(sample)
-        dt = time.perf_counter() - t0
-        cpu = {"value": round(2 * half / dt, 1), "unit": "ops/s", "cores": 1, "kind": "port",
-               "sample": f"first {half:,} ops of each branch of the same workload "
-                         f"({2 * half:,} ops) through oracle/compose_ref.c, 1 thread, "
-                         f"{dt:.1f}s"}
+    solo = world == 1
+    pmc = pmc_traffic(args) if solo and not args.no_pmc else None
+    cpu = cpu_baseline(soa, args) if solo and not args.no_cpu_baseline else None
+    e2e = None
+    if solo and not args.no_e2e:
+        try:
+            e2e = end_to_end(args.e2e_ops)
+        except Exception as exc:  # reported, never fatal for the headline
+            e2e = {"status": f"failed: {exc}"}
 
+    if strong:
+        par = f"key-range shards x{world}, strong scaling (packed RCCL all-to-all + all-gathers + MAX all-reduce)"
+    elif sharded:
+        par = f"key-range shards x{world}, weak scaling (packed RCCL all-to-all + all-gathers + MAX all-reduce)"
+    else:
+        par = f"independent merges x{world}" if world > 1 else "single GPU"
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -180,33 +331,31 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (lift-shaped op logs generated from a seed, SURVEY §8(d))",
         "config": {
-            "workload": (f"{args.config}: one merge of {world * n:,} ops ({n:,} per GPU, "
-                         f"{soa.n_a:,} per branch per GPU), {soa.n_sym:,} symbols, "
-                         f"{spec.ops_per_ms} ops/ms, seed {spec.seed}"
+            "workload": (f"{args.config}: one merge of {n_job:,} ops ({n:,} per GPU), "
+                         f"{soa.n_sym:,} symbols, {spec.ops_per_ms} ops/ms, seed {spec.seed}"
                          + (", sharded by timestamp key range" if sharded else "")
                          + (f", {world} independent merges" if world > 1 and not sharded else "")),
             "n_ops_per_gpu": n,
-            "n_ops_total": world * n,
+            "n_ops_total": n_job,
             "n_sym": soa.n_sym,
             "composed_ops": k,
             "conflicts": nconf,
-            "parallelism": (f"key-range shards x{world} (RCCL all-to-all + all-gathers + "
-                            f"MAX all-reduce)" if sharded else
-                            (f"independent merges x{world}" if world > 1 else "single GPU")),
+            "plan": plan,
+            "parallelism": par,
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_window",
+            "kernel": "k_window_f",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": traffic,
+            "traffic": pmc.get("traffic") if pmc else None,
             "bytes_per_op": WINDOW_BYTES_PER_OP,
             "avg_launch_ms": round(win_avg, 4),
         },
@@ -216,10 +365,13 @@ def main() -> None:
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),
+            "pipeline_traffic": pmc.get("pipeline_traffic") if pmc else None,
         },
+        "pmc": pmc,
         "stages_ms_per_step": {k2: round(v[0] / max(v[1], 1), 4) for k2, v in stages.items()
                                if v[1]},
         "cpu_baseline": cpu,
+        "end_to_end": e2e,
     }
     print(json.dumps(out), flush=True)
     if dist:

@@ -13,8 +13,8 @@
  * owned by the caller; the library never allocates: temporary space comes from a
  * caller-provided workspace sized by the *_workspace_bytes queries.  Calls are
  * stream-ordered on `stream` (a hipStream_t passed as void*; NULL = the null
- * stream).  smx_compose performs one internal stream synchronisation to choose its
- * sort strategy; read device-side counts only after synchronising the stream.
+ * stream).  smx_compose performs one stream synchronisation (in smx_compose_finish)
+ * to check its plan; read device-side counts only after synchronising the stream.
  *
  * Return value: 0 on success, a negative SMX_E* code otherwise; the message is
  * available from smx_last_error() (thread-local).  Nothing aborts the process.
@@ -95,9 +95,29 @@ typedef struct smx_compose_out {
 /* Workspace needed by smx_compose for these sizes. */
 int smx_compose_workspace_bytes(int64_t n_a, int64_t n_b, int64_t n_sym, size_t* bytes);
 
-/* Compose one merge on the GPU (see the header comment for semantics). */
+/* Compose one merge on the GPU (see the header comment for semantics).
+ * = smx_compose_async followed by smx_compose_finish. */
 int smx_compose(const smx_ops* ops, const smx_compose_out* out, void* workspace,
                 size_t workspace_bytes, void* stream);
+
+/* The same composition in two halves.  smx_compose_async enqueues the plan for
+ * timestamp-ordered branch logs (what lift.ts emits) and every later stage with no
+ * host synchronisation, so it can be captured in a hipGraph; after the stream has
+ * run it, counts[0] >= 0 means the results are complete, -2 that the logs need
+ * another plan and -3 that moves with a None newAddress/newFile still need their
+ * prefix fix-up: smx_compose_finish (one stream synchronisation) then completes
+ * them.  smx_compose_finish on complete results only checks them. */
+int smx_compose_async(const smx_ops* ops, const smx_compose_out* out, void* workspace,
+                      size_t workspace_bytes, void* stream);
+int smx_compose_finish(const smx_ops* ops, const smx_compose_out* out, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* The order plan the last composition on this thread ran (bench reporting). */
+#define SMX_PLAN_PRESORTED 0 /* timestamp-ordered logs: presorted windows */
+#define SMX_PLAN_SEGMENTED 1 /* ordered logs with long equal-timestamp groups */
+#define SMX_PLAN_RADIX 2     /* unordered logs: radix sort on (ts, oid_hi) */
+#define SMX_PLAN_RADIX_LO 3  /* ... and oid_lo (duplicate (ts, oid_hi) pairs) */
+int smx_last_plan(void);
 
 /*
  * Sharded single merge: one process per GPU, shard r of G.

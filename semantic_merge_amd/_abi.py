@@ -64,6 +64,7 @@ class SmxShard(C.Structure):
 
 
 SHARD_ORDER, SHARD_WALK, SHARD_TABLES, SHARD_EMIT = 0, 1, 2, 3
+PLAN_NAMES = ("presorted", "segmented", "radix", "radix+oid_lo")  # smx_last_plan()
 SHARD_SUMMARY = 32
 
 
@@ -95,6 +96,9 @@ class SmxRgaOut(C.Structure):
 EXPORTS = (
     "smx_compose_workspace_bytes",
     "smx_compose",
+    "smx_compose_async",
+    "smx_compose_finish",
+    "smx_last_plan",
     "smx_shard_step",
     "smx_set_profiling",
     "smx_stage_times",
@@ -115,6 +119,11 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.smx_compose.argtypes = [C.POINTER(SmxOps), C.POINTER(SmxComposeOut), C.c_void_p,
                                 C.c_size_t, C.c_void_p]
     lib.smx_compose.restype = C.c_int
+    for f in ("smx_compose_async", "smx_compose_finish"):
+        getattr(lib, f).argtypes = lib.smx_compose.argtypes
+        getattr(lib, f).restype = C.c_int
+    lib.smx_last_plan.argtypes = []
+    lib.smx_last_plan.restype = C.c_int
     lib.smx_shard_step.argtypes = [C.POINTER(SmxOps), C.POINTER(SmxShard), C.POINTER(SmxComposeOut),
                                    C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]
     lib.smx_shard_step.restype = C.c_int

@@ -92,11 +92,25 @@ class DeviceCompose:
                                        _ptr(self.ctx), _ptr(self.conf), self.cap,
                                        _ptr(self.counts))
 
-    def run(self, stream=None) -> None:
-        """Enqueue one composition on `stream` (default: torch's current stream)."""
+    def _args(self, stream):
         s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
-        check(lib().smx_compose(C.byref(self._ops), C.byref(self._out), _ptr(self.ws),
-                                self.ws_bytes, s.cuda_stream))
+        return (C.byref(self._ops), C.byref(self._out), _ptr(self.ws), self.ws_bytes, s.cuda_stream)
+
+    def run(self, stream=None) -> None:
+        """One composition on `stream` (default: torch's current stream)."""
+        check(lib().smx_compose(*self._args(stream)))
+
+    def run_async(self, stream=None) -> None:
+        """Enqueue the host-sync-free part (smx_compose_async; capturable in a graph)."""
+        check(lib().smx_compose_async(*self._args(stream)))
+
+    def finish(self, stream=None) -> None:
+        """Complete what run_async left (smx_compose_finish: one stream sync)."""
+        check(lib().smx_compose_finish(*self._args(stream)))
+
+    @staticmethod
+    def last_plan() -> str:
+        return _abi.PLAN_NAMES[lib().smx_last_plan()]
 
     def results(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
         self.torch.cuda.synchronize(self.device)

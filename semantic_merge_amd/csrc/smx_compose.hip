@@ -581,6 +581,7 @@ struct EmitArgs {
   i32* out_file;
   i32* out_ctx;
   i64* counts;
+  int status_none;  // report pending None-value moves (single merge) in counts[0]
 };
 
 #ifndef SMX_EMIT_NT
@@ -625,8 +626,10 @@ struct EmitArgs {
 __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
   const ComposeMeta* M = E.meta;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const bool bad = M->bad_sym != 0;  // invalid input (sym >= n_sym or kind >= 18)
-    E.counts[0] = bad ? -1 : (i64)(E.n - M->n_skip);
+    // -1 invalid input (sym >= n_sym or kind >= 18); -2 the plan failed, -3 moves
+    // with a None value still need their prefix fix-up (smx_compose_finish)
+    const bool bad = M->bad_sym != 0;
+    E.counts[0] = bad ? -1 : M->f_fail ? -2 : (M->n_move_none && E.status_none) ? -3 : (i64)(E.n - M->n_skip);
     E.counts[1] = bad ? -1 : (i64)M->n_conf;
   }
   if (M->f_fail | M->bad_sym) return;
@@ -995,13 +998,13 @@ static int launch_tables(const Ctx& C, u64* part_tab, u32 tag, bool* bucketed) {
   return SMX_OK;
 }
 
-static int launch_emit(const Ctx& C, bool packable) {
+static int launch_emit(const Ctx& C, bool packable, const smx_shard* sh) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   const i64 n = C.n;
   EmitArgs E{C.ws<i32>(B_TSRC), C.ws<u32>(B_TSYM), C.ws<u64>(B_SKIPBITS), C.ws<u32>(B_SKIPLIST),
              C.ws<int4>(B_FIN), meta, (u64)n, (u32)(C.n_sym - 1), packable ? 1 : 0, (u64)C.na, C.src_a,
-             C.src_b, C.out->order, C.out->addr, C.out->file, C.out->ctx, C.out->counts};
+             C.src_b, C.out->order, C.out->addr, C.out->file, C.out->ctx, C.out->counts, sh ? 0 : 1};
   const i64 ewaves = SMX_CEIL_DIV(n, (i64)EMIT_WT);
   hipLaunchKernelGGL(k_emit, dim3(SMX_CEIL_DIV(ewaves, (i64)NWAVES)), dim3(BLOCK), 0, st, E);
   HIP_TRY(hipGetLastError());
@@ -1019,7 +1022,7 @@ static int launch_tail(const Ctx& C) {
   if ((rc = launch_tables(C, nullptr, 0, &bucketed))) return rc;
   C.tm->end(ST_TABLES);
   C.tm->begin(ST_EMIT);
-  if ((rc = launch_emit(C, bucketed))) return rc;
+  if ((rc = launch_emit(C, bucketed, nullptr))) return rc;
   C.tm->end(ST_EMIT);
   return SMX_OK;
 }
@@ -1416,12 +1419,16 @@ static int profiling_on() {
 // is a no-op if the window kernel flags the plan as failed; a window that overflows
 // LDS (dense timestamp ties) retries with smaller windows; a log that is not
 // timestamp-ordered goes to the generic plan when allowed.  hm: the meta after it.
-static int run_order(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm) {
-  i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
-  int rc = run_presorted(C, tgt);
-  if (rc) return rc;
-  if (tail && (rc = launch_tail(C))) return rc;
-  if ((rc = read_meta(C, hm))) return rc;
+// The plan the last compose on this thread used (smx_last_plan).
+static thread_local int g_plan = SMX_PLAN_PRESORTED;
+
+// After a presorted attempt with target window size tgt (hm: the meta it left):
+// a window that overflows LDS (dense timestamp ties) retries with smaller windows;
+// a log that is not timestamp-ordered goes to the generic plan when allowed.  The
+// tail (walk, tables, emit) is launched behind each plan when `tail`.
+static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm, i64 tgt) {
+  int rc;
+  g_plan = SMX_PLAN_PRESORTED;
   while (hm->f_fail == 2 && !hm->bad_sym && tgt > WIN_TGT_MIN) {  // dense groups: smaller windows
     tgt = (tgt / 2) / CH * CH;
     if ((rc = run_presorted(C, tgt))) return rc;
@@ -1432,16 +1439,38 @@ static int run_order(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* h
     if (C.ops->b_gap != 0)
       return set_err(SMX_E_ARG, "branch logs not timestamp-ordered: the generic plan needs b_gap = 0");
     bool fallback = true;
+    g_plan = SMX_PLAN_SEGMENTED;
     if (!(hm->f_fail & 1) && (rc = run_generic(C, GEN_SEG, &fallback))) return rc;  // ordered, long groups
     if (fallback) {
+      g_plan = SMX_PLAN_RADIX;
       if ((rc = run_generic(C, GEN_RADIX, &fallback))) return rc;
       if ((rc = read_meta(C, hm))) return rc;
-      if (hm->dup_key && (rc = run_generic(C, GEN_RADIX_LO, &fallback))) return rc;
+      if (hm->dup_key) {
+        g_plan = SMX_PLAN_RADIX_LO;
+        if ((rc = run_generic(C, GEN_RADIX_LO, &fallback))) return rc;
+      }
     }
     if (tail && (rc = launch_tail(C))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
   }
   return SMX_OK;
+}
+
+// T order of the merge (plan + window kernels): the presorted plan first, with the
+// tail launched behind it when `tail` -- every tail kernel is a no-op if the window
+// kernel flags the plan as failed -- then the fallbacks.  hm: the meta after it.
+static int run_order(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm) {
+  const i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
+  int rc = run_presorted(C, tgt);
+  if (rc) return rc;
+  if (tail && (rc = launch_tail(C))) return rc;
+  if ((rc = read_meta(C, hm))) return rc;
+  return order_fallbacks(C, allow_generic, tail, hm, tgt);
+}
+
+__global__ void k_counts(const ComposeMeta* meta, u64 n, i64* counts) {
+  counts[0] = (i64)(n - meta->n_skip);
+  counts[1] = (i64)meta->n_conf;
 }
 
 // Moves whose newAddress or newFile is None see the symbol's inclusive prefix of
@@ -1466,29 +1495,52 @@ static int run_mvprefix(const Ctx& C, const ComposeMeta& hm, const u64* mvpre) {
   return SMX_OK;
 }
 
-static int compose_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
-                        hipStream_t st) {
+// smx_compose_async: the presorted plan and its tail, enqueued without a host
+// sync (hipGraph-capturable).  counts[0] < -1 afterwards asks for
+// smx_compose_finish: -2 the plan failed, -3 moves with a None value need their
+// prefix fix-up.
+static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
+                              hipStream_t st) {
   Layout L{};
   int rc = check_args(ops, out, ws, ws_bytes, &L);
   if (rc) return rc;
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
+  g_plan = SMX_PLAN_PRESORTED;
   if (n == 0) {
     HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
     return SMX_OK;
   }
   StageTimer tm(st, profiling_on() != 0);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
-  if (env_int("SMX_ABLATE", 0)) {  // diagnostics: timing of the window stage only
-    if ((rc = run_presorted(C, env_int("SMX_WIN_TGT", WIN_TGT)))) return rc;
-    tm.flush();
-    return SMX_OK;
-  }
+  if ((rc = run_presorted(C, env_int("SMX_WIN_TGT", WIN_TGT)))) return rc;
+  if (!env_int("SMX_ABLATE", 0) && (rc = launch_tail(C))) return rc;  // SMX_ABLATE: window stage only
+  tm.flush();
+  return SMX_OK;
+}
+
+// smx_compose_finish: one host sync; runs whatever the asynchronous part left
+// (the fallback plans, the None-value move prefix) and the final counts.
+static int compose_finish_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
+                               hipStream_t st) {
+  Layout L{};
+  int rc = check_args(ops, out, ws, ws_bytes, &L);
+  if (rc) return rc;
+  const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
+  if (n == 0 || env_int("SMX_ABLATE", 0)) return SMX_OK;
+  StageTimer tm(st, profiling_on() != 0);
+  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
   ComposeMeta hm;
-  if ((rc = run_order(C, true, true, &hm))) return rc;
+  if ((rc = read_meta(C, &hm))) return rc;
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
-  tm.begin(ST_MVPREFIX);
-  if ((rc = run_mvprefix(C, hm, nullptr))) return rc;
-  tm.end(ST_MVPREFIX);
+  if (hm.f_fail && (rc = order_fallbacks(C, true, true, &hm, env_int("SMX_WIN_TGT", WIN_TGT)))) return rc;
+  if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
+  if (hm.n_move_none && hm.kcnt[KMOVE]) {
+    tm.begin(ST_MVPREFIX);
+    if ((rc = run_mvprefix(C, hm, nullptr))) return rc;
+    hipLaunchKernelGGL(k_counts, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), (u64)n, out->counts);
+    HIP_TRY(hipGetLastError());
+    tm.end(ST_MVPREFIX);
+  }
   tm.flush();
   return SMX_OK;
 }
@@ -1598,7 +1650,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       tm.begin(ST_EMIT);
       hipLaunchKernelGGL(k_fin_from_tab, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, sh->fin_tab, sh->glob, n_sym,
                          C.ws<ComposeMeta>(B_META), C.ws<int4>(B_FIN));
-      if ((rc = launch_emit(C, true))) return rc;
+      if ((rc = launch_emit(C, true, sh))) return rc;
       tm.end(ST_EMIT);
       ComposeMeta hm;
       if ((rc = read_meta(C, &hm))) return rc;
@@ -1624,15 +1676,33 @@ extern "C" int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const 
   }
 }
 
-extern "C" int smx_compose(const smx_ops* ops, const smx_compose_out* out, void* workspace,
-                           size_t workspace_bytes, void* stream) {
+extern "C" int smx_compose_async(const smx_ops* ops, const smx_compose_out* out, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
   if (!ops) return set_err(SMX_E_ARG, "null ops");
   try {
-    return compose_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream);
+    return compose_async_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream);
   } catch (const std::exception& e) {
     return set_err(SMX_E_HIP, e.what());
   }
 }
+
+extern "C" int smx_compose_finish(const smx_ops* ops, const smx_compose_out* out, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  if (!ops) return set_err(SMX_E_ARG, "null ops");
+  try {
+    return compose_finish_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream);
+  } catch (const std::exception& e) {
+    return set_err(SMX_E_HIP, e.what());
+  }
+}
+
+extern "C" int smx_compose(const smx_ops* ops, const smx_compose_out* out, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  const int rc = smx_compose_async(ops, out, workspace, workspace_bytes, stream);
+  return rc ? rc : smx_compose_finish(ops, out, workspace, workspace_bytes, stream);
+}
+
+extern "C" int smx_last_plan(void) { return g_plan; }
 
 extern "C" int smx_set_profiling(int enabled) {
   std::lock_guard<std::mutex> g(g_prof_mu);

@@ -152,18 +152,22 @@ def test_shard_tiny_with_empty_shards():
 
 def test_bench_two_ranks_sharded():
     """bench.py's N > 1 path (one sharded merge, torchrun) end to end, 2 ranks on this
-    GPU over gloo: one JSON line with the whole-job rate."""
+    GPU over gloo: one JSON line with the whole-job rate; strong scaling by default
+    (the config's ops split over the ranks), weak with --weak."""
     import json
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, SMX_BENCH_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--n-ops", "2000000", "--n-sym", "20000"]
-    r = subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-2000:]
-    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
-    out = json.loads(line)
-    assert out["n_gpus"] == 2 and out["config"]["n_ops_total"] == 4_000_000
-    assert out["value"] > 0 and "key-range shards" in out["config"]["parallelism"]
+    for extra, total, scaling in (([], 2_000_000, "strong"), (["--weak"], 4_000_000, "weak")):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+               "--gpus", "2", "--steps", "2", "--warmup", "1", "--n-ops", "2000000", "--n-sym",
+               "20000"] + extra
+        r = subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+        out = json.loads(line)
+        assert out["n_gpus"] == 2 and out["config"]["n_ops_total"] == total
+        assert out["scaling"] == scaling
+        assert out["value"] > 0 and "key-range shards" in out["config"]["parallelism"]
