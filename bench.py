@@ -241,8 +241,9 @@ def main() -> None:
         rank_spec = synth.LiftSpec(**{**spec.__dict__, "n_total": spec.n_total // world}) if strong else spec
         soa, na_g, nb_g = synth.lift_slice_soa(rank_spec, rank, world)
         sl_a, sl_b, _, _ = shard.slices_from_soa(soa, 0, 1, dev)
+        sl_a.start = sl_b.start = rank * soa.n_a          # this rank's index slice of each branch
         log(f"[rank {rank}] generated slice of {soa.n:,} ops in {time.time() - t0:.1f}s")
-        sc = shard.ShardedCompose(sl_a, sl_b, na_g, nb_g, soa.n_sym, shard.Comm(), dev)
+        sc = shard.ShardedCompose(sl_a, sl_b, na_g, nb_g, soa.n_sym, shard.Comm(), dev, mode="range")
         del sl_a, sl_b
         run = sc.run
         log(f"[rank {rank}] resident on {dev}; shard buffers with headroom {sc.hd:,}")
@@ -277,9 +278,7 @@ def main() -> None:
     plan = _lib.DeviceCompose.last_plan()
     stages = _lib.stage_times()
     if sharded:
-        fin = sc.sum_final
-        nconf = int(fin[:, shard.S_NCONF].sum())
-        k = int(fin[:, 0:18].sum()) - int(fin[:, shard.S_NSKIP].sum())
+        k, nconf = sc.totals()
     else:
         k, nconf = (int(x) for x in dc.counts.cpu().tolist())
     elapsed = max_over_ranks(elapsed, dev)

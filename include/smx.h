@@ -132,7 +132,13 @@ int smx_last_plan(void);
  * The host drives four steps on the same workspace, exchanging the small
  * per-shard summaries (and the partial tables) between them with collectives:
  *   SMX_SHARD_ORDER   plan + window kernels; writes summary[0..21] and the
- *                     first halo_cap renames of each branch (export_*)
+ *                     first halo_cap renames of each branch (export_*).  With
+ *                     src_map == NULL it is asynchronous (no host sync): the
+ *                     presorted plan only; a failure shows in summary[21]
+ *                     (bit 0 not ordered, bit 1 invalid input, bit 2 a window
+ *                     overflowed on dense timestamp ties) and is repaired by
+ *   SMX_SHARD_ORDER_FIX  the plan fallbacks (smaller windows; with b_gap = 0 the
+ *                     generic plan); rewrites summary[0..21] and the exports
  *   SMX_SHARD_WALK    DivergentRename walk with the halo (the next shards'
  *                     exports) and an incoming open region (in_ahead, in_d);
  *                     may be re-run when the incoming region changes;
@@ -142,7 +148,9 @@ int smx_last_plan(void);
  *   SMX_SHARD_EMIT    composed output from the reduced tables (fin_tab) and
  *                     the global value widths (glob[0..2]); mv_prefix (or NULL
  *                     when no move has a None value) = [2][n_sym] last non-None
- *                     move values of the lower shards
+ *                     move values of the lower shards.  With summary_host set
+ *                     (this shard's summary as the host last gathered it) the
+ *                     step needs no host sync.
  * Source indices in order[] and conflicts are global: local A op j is
  * src_a + j, local B op j is src_b + j.  summary (int64):
  *   [0..17] ops per kind  [18..19] renames of A, B  [20] moves with a None value
@@ -155,6 +163,7 @@ int smx_last_plan(void);
 #define SMX_SHARD_WALK 1
 #define SMX_SHARD_TABLES 2
 #define SMX_SHARD_EMIT 3
+#define SMX_SHARD_ORDER_FIX 4
 #define SMX_SHARD_SUMMARY 32
 
 typedef struct smx_shard {
@@ -181,6 +190,16 @@ typedef struct smx_shard {
   const uint64_t* fin_tab;   /* [3][n_sym], MAX-reduced part_tab */
   const int64_t* glob;       /* [3] value bit widths, MAX over shards */
   const uint64_t* mv_prefix; /* [2][n_sym] or NULL */
+  /* Device-held alternatives, so a step needs no host round trip (NULL: the host
+   * fields above are used). */
+  const int64_t* halo_dev;     /* [4] halo_n[0], halo_n[1], halo_more[0], halo_more[1] */
+  const int64_t* in_state_dev; /* [2] in_ahead, in_d */
+  /* A shard built by a sample-sort exchange (branch logs in any order; b_gap = 0):
+   * the global source index of each local op j, [n_a + n_b]; replaces src_a/src_b
+   * and lets the ORDER step use the generic (sorting) plan.  NULL otherwise. */
+  const int32_t* src_map;
+  /* host memory: this shard's summary [SMX_SHARD_SUMMARY] after WALK, or NULL */
+  const int64_t* summary_host;
 } smx_shard;
 
 int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const smx_compose_out* out,

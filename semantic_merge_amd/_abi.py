@@ -60,10 +60,15 @@ class SmxShard(C.Structure):
         ("fin_tab", C.c_void_p),
         ("glob", C.c_void_p),
         ("mv_prefix", C.c_void_p),
+        ("halo_dev", C.c_void_p),
+        ("in_state_dev", C.c_void_p),
+        ("src_map", C.c_void_p),
+        ("summary_host", C.c_void_p),
     ]
 
 
 SHARD_ORDER, SHARD_WALK, SHARD_TABLES, SHARD_EMIT = 0, 1, 2, 3
+SHARD_ORDER_FIX = 4
 PLAN_NAMES = ("presorted", "segmented", "radix", "radix+oid_lo")  # smx_last_plan()
 SHARD_SUMMARY = 32
 

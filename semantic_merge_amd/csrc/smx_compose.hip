@@ -576,6 +576,7 @@ struct EmitArgs {
   int allow_pack;  // the final-state table came from k_tb_reduce (packs when widths fit)
   u64 na_loc;      // local op j -> global j < na_loc ? src_a + j : src_b + j - na_loc
   i64 src_a, src_b;
+  const i32* src_map;  // or, for a sample-sorted shard, src_map[j]
   i32* out_order;
   i32* out_addr;
   i32* out_file;
@@ -639,6 +640,7 @@ __global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
   const u64 nR = min(M->kcnt[KREN], nP);
   const u64 nout = E.n - nskip, nRk = nR - nskip;
   auto gsrc = [&](i32 j) -> i32 {
+    if (E.src_map) return E.src_map[j];
     return (u64)j < E.na_loc ? (i32)(E.src_a + j) : (i32)(E.src_b + ((i64)j - (i64)E.na_loc));
   };
   const FinPack FP = fin_pack_of(M->vbits, E.allow_pack != 0);
@@ -834,6 +836,7 @@ struct Ctx {
   i64 na, nb, n, n_sym;
   i64 src_a, src_b;  // global source index of local op j (see WinArgs)
   StageTimer* tm;
+  const i32* src_map = nullptr;
   template <typename T>
   T* ws(int b) const { return (T*)(base + L.off[b]); }
 };
@@ -859,6 +862,7 @@ static WinArgs win_args(const Ctx& C) {
   P.n_sym = C.n_sym;
   P.src_a = C.src_a;
   P.src_b = C.src_b;
+  P.src_map = C.src_map;
   P.bnd = C.ws<i64>(B_BND);
   P.woff = C.ws<u32>(B_WOFF);
   P.meta = C.ws<ComposeMeta>(B_META);
@@ -890,6 +894,8 @@ static WalkArgs walk_args(const Ctx& C, const smx_shard* sh) {
   Wk.bgap = C.ops->b_gap;
   Wk.src_a = C.src_a;
   Wk.src_b = C.src_b;
+  Wk.src_map = C.src_map;
+  Wk.halo_dev = sh ? sh->halo_dev : nullptr;
   for (int b = 0; b < 2; ++b) {
     Wk.halo_sym[b] = sh ? sh->halo_sym[b] : nullptr;
     Wk.halo_cls[b] = sh ? sh->halo_cls[b] : nullptr;
@@ -929,9 +935,10 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
   const i64 Wmax = max_windows(n);
   const int gsmall = 256;  // grid for loops over the (few) candidates
   hipLaunchKernelGGL(k_boundary, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, meta, cslot, wcand, wtot);
-  if (sh && sh->in_d > 0)
-    hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d, meta,
-                       C.out->conflicts, (u64)C.out->conflict_cap, skiplist, skipbits);
+  if (sh && (sh->in_d > 0 || sh->in_state_dev))
+    hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d,
+                       (const i64*)sh->in_state_dev, meta, C.out->conflicts, (u64)C.out->conflict_cap, skiplist,
+                       skipbits);
   HIP_TRY((scan_excl<OpSum, u32, u32>(wtot, wcoff, Wmax, &meta->n_win, part, ncand32, st)));
   hipLaunchKernelGGL(k_cand_compact, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, cslot, wcoff, ncand_dev, cand);
   hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
@@ -1004,7 +1011,7 @@ static int launch_emit(const Ctx& C, bool packable, const smx_shard* sh) {
   const i64 n = C.n;
   EmitArgs E{C.ws<i32>(B_TSRC), C.ws<u32>(B_TSYM), C.ws<u64>(B_SKIPBITS), C.ws<u32>(B_SKIPLIST),
              C.ws<int4>(B_FIN), meta, (u64)n, (u32)(C.n_sym - 1), packable ? 1 : 0, (u64)C.na, C.src_a,
-             C.src_b, C.out->order, C.out->addr, C.out->file, C.out->ctx, C.out->counts, sh ? 0 : 1};
+             C.src_b, C.src_map, C.out->order, C.out->addr, C.out->file, C.out->ctx, C.out->counts, sh ? 0 : 1};
   const i64 ewaves = SMX_CEIL_DIV(n, (i64)EMIT_WT);
   hipLaunchKernelGGL(k_emit, dim3(SMX_CEIL_DIV(ewaves, (i64)NWAVES)), dim3(BLOCK), 0, st, E);
   HIP_TRY(hipGetLastError());
@@ -1554,7 +1561,19 @@ __global__ void k_shard_summary(const ComposeMeta* meta, i64* summary) {
   summary[18] = (i64)meta->n_ren_side[0];
   summary[19] = (i64)meta->n_ren_side[1];
   summary[20] = (i64)meta->n_move_none;
-  summary[21] = (i64)((meta->f_fail ? 1 : 0) | (meta->bad_sym ? 2 : 0));
+  summary[21] = (i64)((meta->f_fail & 1 ? 1 : 0) | (meta->bad_sym ? 2 : 0) | (meta->f_fail & 2 ? 4 : 0));
+}
+
+// An empty shard hands the incoming open region (device- or host-held) straight on.
+__global__ void k_pass_region(const i64* in_dev, i64 in_ahead, i64 in_d, i64* summary) {
+  if (in_dev) {
+    in_ahead = in_dev[0];
+    in_d = in_dev[1];
+  }
+  summary[22] = in_d > 0 ? 1 : 0;
+  summary[23] = in_d > 0 ? in_ahead : 0;
+  summary[24] = in_d > 0 ? in_d : 0;
+  summary[25] = summary[26] = summary[27] = 0;
 }
 
 __global__ void k_shard_walk_sum(const ComposeMeta* meta, i64* summary) {
@@ -1595,32 +1614,51 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
   StageTimer tm(st, profiling_on() != 0);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, sh->src_a, sh->src_b, &tm};
+  C.src_map = sh->src_map;
+  if (sh->src_map && ops->b_gap != 0) return set_err(SMX_E_ARG, "src_map needs b_gap = 0");
   if (n == 0) {  // an empty shard: neutral summaries and outputs
     if (step == SMX_SHARD_ORDER) HIP_TRY(hipMemsetAsync(sh->summary, 0, SMX_SHARD_SUMMARY * 8, st));
     if (step == SMX_SHARD_WALK) {
       // the open region passes through unchanged (or none comes in): always rewrite
       // the outgoing state, a previous round may have left another one
-      const i64 pass[6] = {sh->in_d > 0 ? 1 : 0, sh->in_d > 0 ? sh->in_ahead : 0, sh->in_d > 0 ? sh->in_d : 0,
-                           0, 0, 0};
-      HIP_TRY(hipMemcpyAsync(sh->summary + 22, pass, sizeof(pass), hipMemcpyHostToDevice, st));
-      HIP_TRY(hipStreamSynchronize(st));
+      hipLaunchKernelGGL(k_pass_region, dim3(1), dim3(1), 0, st, (const i64*)sh->in_state_dev,
+                         (i64)sh->in_ahead, (i64)sh->in_d, sh->summary);
+      HIP_TRY(hipGetLastError());
     }
     if (step == SMX_SHARD_TABLES && sh->part_tab)
       HIP_TRY(hipMemsetAsync(sh->part_tab, 0, (size_t)3 * n_sym * 8, st));
     if (step == SMX_SHARD_EMIT) HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
     return SMX_OK;
   }
+  auto order_outputs = [&]() -> int {
+    hipLaunchKernelGGL(k_shard_summary, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary);
+    if (sh->halo_cap > 0)
+      hipLaunchKernelGGL(k_halo_export, dim3(1), dim3(EX_NT), 0, st, walk_args(C, nullptr), sh->export_sym,
+                         sh->export_cls, sh->export_src, (u64)sh->halo_cap);
+    HIP_TRY(hipGetLastError());
+    return SMX_OK;
+  };
   switch (step) {
-    case SMX_SHARD_ORDER: {
+    case SMX_SHARD_ORDER:
+    case SMX_SHARD_ORDER_FIX: {
       if (sh->halo_cap < 0 || (sh->halo_cap > 0 && (!sh->export_sym || !sh->export_cls || !sh->export_src)))
         return set_err(SMX_E_ARG, "bad export buffers");
+      const i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
+      if (step == SMX_SHARD_ORDER && !sh->src_map) {  // asynchronous: failures show in summary[21]
+        g_plan = SMX_PLAN_PRESORTED;
+        if ((rc = run_presorted(C, tgt))) return rc;
+        return order_outputs();
+      }
       ComposeMeta hm;
-      if ((rc = run_order(C, false, false, &hm))) return rc;  // times its own plan / window stages
-      hipLaunchKernelGGL(k_shard_summary, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary);
-      if (sh->halo_cap > 0)
-        hipLaunchKernelGGL(k_halo_export, dim3(1), dim3(EX_NT), 0, st, walk_args(C, nullptr), sh->export_sym,
-                           sh->export_cls, sh->export_src, (u64)sh->halo_cap);
-      HIP_TRY(hipGetLastError());
+      if (step == SMX_SHARD_ORDER) {
+        // a sample-sorted shard's branch logs are in any order: the generic plan
+        if ((rc = run_order(C, true, false, &hm))) return rc;  // times its own stages
+      } else {
+        if ((rc = read_meta(C, &hm))) return rc;
+        // a compacted shard (b_gap = 0) may take the generic plan
+        if (hm.f_fail && (rc = order_fallbacks(C, ops->b_gap == 0, false, &hm, tgt))) return rc;
+      }
+      if ((rc = order_outputs())) return rc;
       if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
       if (hm.f_fail)
         return set_err(SMX_E_ARG, "sharded merge needs timestamp-ordered branch logs in every shard");
@@ -1653,7 +1691,12 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       if ((rc = launch_emit(C, true, sh))) return rc;
       tm.end(ST_EMIT);
       ComposeMeta hm;
-      if ((rc = read_meta(C, &hm))) return rc;
+      if (sh->summary_host) {  // what the move prefix needs, as the host gathered it
+        hm.kcnt[KMOVE] = (u64)sh->summary_host[KMOVE];
+        hm.n_move_none = (u64)sh->summary_host[20];
+      } else if ((rc = read_meta(C, &hm))) {
+        return rc;
+      }
       tm.begin(ST_MVPREFIX);
       if ((rc = run_mvprefix(C, hm, sh->mv_prefix))) return rc;
       tm.end(ST_MVPREFIX);

@@ -47,10 +47,13 @@ struct WalkArgs {
   const i32* halo_src[2];
   u64 halo_n[2];
   int halo_more[2];
+  const i64* halo_dev;  // device-held halo_n / halo_more (smx_shard.halo_dev), or null
   i64 src_a, src_b;
+  const i32* src_map;   // sample-sorted shard: global source of local op j, or null
 };
 
 __device__ __forceinline__ i32 walk_gsrc(const WalkArgs& W, i32 j) {
+  if (W.src_map) return W.src_map[j];
   return (u64)j < W.na_cap ? (i32)(W.src_a + j) : (i32)(W.src_b + ((i64)j - (i64)W.na_cap));
 }
 
@@ -63,6 +66,12 @@ __device__ __forceinline__ WalkArgs walk_load(WalkArgs W) {
   W.nRB = min(m->n_ren_side[1], W.nb_cap);
   W.nR = W.nRA + W.nRB;
   W.Wn = m->n_win;
+  if (W.halo_dev) {
+    for (int b = 0; b < 2; ++b) {
+      W.halo_n[b] = W.halo_sym[b] ? (u64)max(W.halo_dev[b], (i64)0) : 0;
+      W.halo_more[b] = W.halo_dev[2 + b] != 0;
+    }
+  }
   return W;
 }
 
@@ -309,9 +318,14 @@ __global__ void __launch_bounds__(S1_NT) k_scan1(const u32* __restrict__ in, u32
 // Incoming open region (sharded merge): the previous shards' walk ended with
 // state (ahead, d > 0); continue it from position 0.  Its conflicts come first in
 // this shard's list; candidates before its end are covered.
-__global__ void k_replay_in(WalkArgs W0, int in_ahead, u32 in_d, ComposeMeta* meta, i32* __restrict__ pairs,
-                            u64 pair_cap, u32* __restrict__ skiplist, u64* __restrict__ skipbits) {
+__global__ void k_replay_in(WalkArgs W0, int in_ahead, u32 in_d, const i64* in_dev, ComposeMeta* meta,
+                            i32* __restrict__ pairs, u64 pair_cap, u32* __restrict__ skiplist,
+                            u64* __restrict__ skipbits) {
   const WalkArgs W = walk_load(W0);
+  if (in_dev) {  // device-held incoming state
+    in_ahead = (int)in_dev[0];
+    in_d = in_dev[1] > 0 ? (u32)in_dev[1] : 0u;
+  }
   if (W.fail || in_d == 0 || threadIdx.x != 0 || blockIdx.x != 0) return;
   ReplayState st = replay_fresh();
   st.ahead = in_ahead;

@@ -74,6 +74,7 @@ struct WinArgs {
   i64 W;
   i64 n_sym;
   i64 src_a, src_b; // global source index of local op j (sharded merge; 0 / na otherwise)
+  const i32* src_map;  // sample-sorted shard: global source of local op j, or null
   int ablate;       // diagnostics only (SMX_ABLATE): skip phases, results invalid
   const i64* bnd;
   const u32* woff;  // [NCNT][W] exclusive offsets over windows (generic plan)
@@ -108,6 +109,7 @@ __device__ __forceinline__ void win_publish_widths(ComposeMeta* meta, const u32*
 }
 
 __device__ __forceinline__ i32 win_gsrc(const WinArgs& P, i64 j) {
+  if (P.src_map) return P.src_map[j];
   return j < P.na ? (i32)(P.src_a + j) : (i32)(P.src_b + (j - P.na));
 }
 

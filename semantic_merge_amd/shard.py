@@ -2,23 +2,30 @@
 
 The reference composes two branch logs in one sequential loop (semmerge/compose.py:11-114).
 Its output order T is (precedence, timestamp, id, side, index): kind-major, so a shard that
-owns every op of both branches whose timestamp falls in a key range [tau_r, tau_{r+1}) owns,
-for each kind, one contiguous piece of T, and the pieces of the shards follow each other in
-shard order.  One process per GPU; the steps of one merge are
+owns every op of both branches whose key falls in a key range owns, for each kind, one
+contiguous piece of T, and the pieces of the shards follow each other in shard order.  One
+process per GPU; the steps of one merge and the collectives each one uses:
 
 1. exchange   each rank starts with an index slice of each branch log (how the logs are
-              loaded); one all-to-all (RCCL over xGMI) moves every op to the rank owning its
-              timestamp.  Lift-shaped logs are timestamp-ordered, so only the ops near the
-              slice edges move.
-2. order      smx_shard_step(ORDER): the single-GPU plan + window kernels on the shard.
-3. walk       the DivergentRename walk (compose.py:60-70, 88-98) runs per shard; the natural
-              head of a rename near a shard's end can be a rename of a later shard, so each
-              shard gets a halo (the next renames of each branch, all-gathered), and a region
-              still open at a shard's end is handed to the next shard (re-run on the rare
-              shards whose incoming region changed).
-4. tables     per-symbol last writers (compose.py:27-28, 71-82, 99-110): each shard's
-              partial tables tagged (shard + 1) << 32, one MAX all-reduce keeps the last
-              writer over shards.
+              loaded).  Timestamp-ordered logs (lift.ts emits them) are split by timestamp
+              range: one all_gather of 8 words per rank, splitters and per-destination
+              counts on the device, one all_gather of the counts (the one host sync: the
+              all-to-all needs its split sizes), then ONE all_to_all_single of packed 37-B
+              op records; only the ops near the slice edges move.  Logs in any order take
+              a sample sort instead: an all_gather of key samples, splitters on the full
+              T key, one all_gather of counts, one all_to_all_single of 41-B records
+              (with the op's global index).
+2. order      smx_shard_step(ORDER): the single-GPU plan + window kernels on the shard
+              (asynchronous on the presorted plan), then one all_gather of the summary
+              and the halo exports; the halo is assembled on the device.
+3. walk       the DivergentRename walk (compose.py:60-70, 88-98) with the halo (the next
+              renames of each branch on the following shards) and the incoming open
+              region held on the device; one all_gather of the summaries and one host
+              read per round; a shard whose incoming region changed re-runs (rare).
+4. tables     per-symbol last writers (compose.py:27-28, 71-82, 99-110): partial tables
+              tagged (shard + 1) << 32, with the value widths appended, in ONE MAX
+              all_reduce.  Moves with a None value add an all_gather of the move tables
+              (the lower shards' prefix).
 5. emit       composed output per shard; order[] and conflicts hold global source indices.
 
 Collectives run on device tensors over RCCL ("nccl"); on "gloo" (the CPU tests and
@@ -39,6 +46,12 @@ FIELDS = ("kind", "ts", "hi", "lo", "sym", "v0", "v1")
 S_KINDS, S_REN, S_MVNONE, S_FAIL = 0, 18, 20, 21
 S_OPEN, S_AHEAD, S_D, S_NCONF, S_NSKIP, S_OVER, S_WIDTH = 22, 23, 24, 25, 26, 27, 28
 N_KINDS = 18
+SUM = _abi.SHARD_SUMMARY
+I64_MIN = -(2 ** 63)
+
+# packed exchange record: ts, hi, lo (8 B each), sym, v0, v1 (4 B), kind (1 B) = 37 B;
+# the sample-sort exchange appends the op's global source index (4 B) = 41 B
+REC_FIELDS = ("ts", "hi", "lo", "sym", "v0", "v1", "kind")
 
 
 class Comm:
@@ -71,9 +84,10 @@ class Comm:
             t.copy_(x)
 
     def all_to_all(self, t, in_splits: Sequence[int], out_splits: Sequence[int]):
+        """Rows of t (dim 0) to the ranks: in_splits rows to each, out_splits from each."""
         import torch
         x = self._host(t.contiguous())
-        out = torch.empty(int(sum(out_splits)), dtype=x.dtype, device=x.device)
+        out = torch.empty((int(sum(out_splits)),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
         self.dist.all_to_all_single(out, x, list(map(int, out_splits)), list(map(int, in_splits)),
                                     group=self.group)
         return out.to(t.device)
@@ -116,25 +130,76 @@ def slices_from_soa(soa, rank: int, world: int, device) -> Tuple[BranchSlice, Br
 
 def _u64_key(t):
     """int64 tensor holding u64 payloads -> order-preserving signed image."""
-    return t ^ (-(2 ** 63))
+    return t ^ I64_MIN
+
+
+def pack_records(cols: dict, gidx=None):
+    """Field tensors of m ops -> uint8 [m, 37] (or [m, 41] with gidx) packed records."""
+    import torch
+    m = int(cols["kind"].numel())
+    parts = [cols[f].contiguous().view(torch.uint8).reshape(m, cols[f].element_size()) for f in REC_FIELDS]
+    if gidx is not None:
+        parts.append(gidx.contiguous().view(torch.uint8).reshape(m, 4))
+    return torch.cat(parts, dim=1)
+
+
+def unpack_records(rec, dtypes: dict, with_gidx: bool = False):
+    """uint8 [m, R] records -> (dict of field tensors, gidx int32 or None)."""
+    import torch
+    m = int(rec.shape[0])
+
+    def col(o, w, dt):  # a fresh aligned copy of the byte columns [o, o + w)
+        t = torch.empty((m, w), dtype=torch.uint8, device=rec.device)
+        t.copy_(rec[:, o:o + w])
+        return t.view(dt).reshape(-1)
+
+    out, o = {}, 0
+    for f in REC_FIELDS:
+        w = torch.empty(0, dtype=dtypes[f]).element_size()
+        out[f] = col(o, w, dtypes[f])
+        o += w
+    g = col(o, 4, torch.int32) if with_gidx else None
+    return out, g
+
+
+def lex_dest(keys: Sequence, splitters):
+    """Shard of each op: the number of splitters (rows of `splitters`, [k, len(keys)])
+    at or below the op's key tuple, compared lexicographically."""
+    import torch
+    n = int(keys[0].numel())
+    k = int(splitters.shape[0])
+    gt = torch.zeros((n, k), dtype=torch.bool, device=keys[0].device)
+    eq = torch.ones((n, k), dtype=torch.bool, device=keys[0].device)
+    for i, key in enumerate(keys):
+        col = key.view(n, 1)
+        s = splitters[:, i].view(1, k)
+        gt |= eq & (col > s)
+        eq &= col == s
+    return (gt | eq).sum(dim=1)
 
 
 class ShardedCompose:
     """One rank's part of a sharded merge.  `a`, `b`: this rank's index slices of the
-    global branch logs (timestamp-ordered), na_glob / nb_glob the global branch sizes.
+    global branch logs, na_glob / nb_glob the global branch sizes.
 
-    The slices are copied once into field buffers with `headroom` free entries on both
-    sides of each branch range; the exchange writes the ops arriving from the
-    neighbouring shards into the headroom, so the ops that stay (nearly all of them on
-    lift-shaped logs) never move, and the shard is handed to the kernels in place:
-    A' at [a_lo, a_hi) and B' at [b_lo, b_hi) of every field buffer, B' after a gap
-    (smx_ops.b_gap)."""
+    mode "range" (timestamp-ordered logs): the slices are copied once into field buffers
+    with `headroom` free entries on both sides of each branch range; the exchange writes
+    the ops arriving from the neighbouring shards into the headroom, so the ops that stay
+    (nearly all of them) never move, and the shard is handed to the kernels in place: A'
+    at [a_lo, a_hi) and B' at [b_lo, b_hi) of every field buffer, B' after a gap
+    (smx_ops.b_gap).  mode "sample" (logs in any order): a sample-sort exchange into
+    contiguous shard buffers, with a global source map (smx_shard.src_map) and the
+    generic sorting plan.  "auto" picks range when every slice is ordered."""
 
     def __init__(self, a: BranchSlice, b: BranchSlice, na_glob: int, nb_glob: int, n_sym: int,
                  comm: Comm, device, halo_cap: int = 4096, headroom: Optional[int] = None,
-                 restore: bool = True) -> None:
+                 restore: bool = True, mode: str = "auto", oversample: int = 64) -> None:
         import torch
+        if mode not in ("auto", "range", "sample"):
+            raise ValueError(f"mode {mode!r}")
         self.torch = torch
+        self.mode = mode
+        self.oversample = oversample
         self.na_glob, self.nb_glob = na_glob, nb_glob
         self.n_sym = n_sym
         self.comm = comm
@@ -144,17 +209,27 @@ class ShardedCompose:
         self.restore = restore
         self.na_s, self.nb_s = a.n, b.n
         self.a_start, self.b_start = a.start, b.start
+        self.dtypes = {f: getattr(a, f).dtype for f in FIELDS}
         hd = headroom if headroom is not None else max(1 << 16, (a.n + b.n) // 32)
         self._alloc(hd, a, b)
         self._ws = None
         self._ws_bytes = 0
         self._outn = -1
-        self.summary = torch.zeros(_abi.SHARD_SUMMARY, dtype=torch.int64, device=self.dev)
-        self.xsym = torch.zeros(2 * self.H, dtype=torch.int32, device=self.dev)
-        self.xcls = torch.zeros(2 * self.H, dtype=torch.int32, device=self.dev)
-        self.xsrc = torch.zeros(2 * self.H, dtype=torch.int32, device=self.dev)
-        self.part = torch.zeros(3 * max(n_sym, 1), dtype=torch.int64, device=self.dev)
-        self.glob = torch.zeros(3, dtype=torch.int64, device=self.dev)
+        self._saved = []
+        self.sbuf, self.src_map = None, None
+        dv = self.dev
+        self.summary = torch.zeros(SUM, dtype=torch.int64, device=dv)
+        H2 = 2 * max(self.H, 1)
+        self.xport = torch.zeros((3, H2), dtype=torch.int32, device=dv)     # sym, cls, src exports
+        self.halo = torch.zeros((2, 3, max(self.H, 1)), dtype=torch.int32, device=dv)
+        self.halo_dev = torch.zeros(4, dtype=torch.int64, device=dv)
+        self.in_state = (0, 0)
+        self.in_dev = torch.zeros(2, dtype=torch.int64, device=dv)
+        # partial tables [3][n_sym] then the 3 value widths: one MAX all_reduce for both
+        self.part = torch.zeros(3 * max(n_sym, 1) + 3, dtype=torch.int64, device=dv)
+        self.glob = self.part[3 * max(n_sym, 1):]
+        self.n_xchg = 0      # ops this rank received from other ranks in the last exchange
+        self.order_fixes = 0  # ORDER_FIX runs (dense timestamp ties) on this rank
 
     def _alloc(self, hd: int, a, b) -> None:
         """Field buffers [hd | A slice | 2 hd | B slice | hd]; a, b: BranchSlices or the
@@ -179,44 +254,65 @@ class ShardedCompose:
         return self.buf[f][self._oa: self._oa + self.na_s] if br == 0 else \
             self.buf[f][self._ob: self._ob + self.nb_s]
 
-    def _splitters(self) -> np.ndarray:
-        """tau[1..world-1]: shard r owns timestamps in [tau[r], tau[r+1])."""
+    def _range_counts(self):
+        """Device: timestamp splitters from one all_gather of each slice's first / last
+        keys, this rank's op counts per (branch, destination) and the ordered flag:
+        int64 [2 * world + 1]."""
         torch = self.torch
-        info = torch.zeros(6, dtype=torch.int64, device=self.dev)
+        dv, W = self.dev, self.world
+        info = torch.zeros(7, dtype=torch.int64, device=dv)
         info[0], info[1] = self.na_s, self.nb_s
-        ta, tb = self._orig(0, "ts"), self._orig(1, "ts")
-        if self.na_s:
-            info[2], info[3] = _u64_key(ta[0]), _u64_key(ta[-1])
-        if self.nb_s:
-            info[4], info[5] = _u64_key(tb[0]), _u64_key(tb[-1])
-        g = self.comm.all_gather(info).cpu().numpy()
-        for side, (ni, fi, li) in enumerate(((0, 2, 3), (1, 4, 5))):
-            nz = g[g[:, ni] > 0]
-            if len(nz) > 1 and np.any(nz[1:, fi] < nz[:-1, li]):
-                raise ValueError("sharded merge needs timestamp-ordered branch logs "
-                                 f"(branch {'AB'[side]} decreases across rank slices)")
-        tau = np.empty(self.world, dtype=np.int64)
-        tau[0] = np.iinfo(np.int64).min
-        for r in range(1, self.world):
-            cand = g[r, 2] if g[r, 0] else (g[r, 4] if g[r, 1] else tau[r - 1])
-            tau[r] = max(tau[r - 1], cand)
-        return tau
-
-    def exchange(self) -> None:
-        """The all-to-all: every op to the shard owning its timestamp (collective)."""
-        torch = self.torch
-        r, W = self.rank, self.world
-        tau = torch.from_numpy(self._splitters()[1:]).to(self.dev)
+        ok = torch.ones((), dtype=torch.bool, device=dv)
+        for br, n in ((0, self.na_s), (1, self.nb_s)):
+            if n:
+                k = _u64_key(self._orig(br, "ts"))
+                info[2 + 2 * br], info[3 + 2 * br] = k[0], k[-1]
+                if n > 1 and self.mode == "auto":  # "range": the ORDER plan checks the order itself
+                    ok &= (k[1:] >= k[:-1]).all()
+        info[6] = ok.to(torch.int64)
+        g = self.comm.all_gather(info)                                     # [W, 7]
+        ordered = g[:, 6].min() == 1
+        for br in range(2):                 # slices of a branch must follow each other
+            nz = g[:, br] > 0
+            first, last = g[:, 2 + 2 * br], g[:, 3 + 2 * br]
+            lmax = torch.cummax(torch.where(nz, last, torch.full_like(last, I64_MIN)), 0).values
+            prev = torch.cat([torch.full((1,), I64_MIN, dtype=torch.int64, device=dv), lmax[:-1]])
+            ordered &= (~nz | (first >= prev)).all()
+        cand = torch.where(g[:, 0] > 0, g[:, 2], torch.where(g[:, 1] > 0, g[:, 4],
+                                                              torch.full_like(g[:, 2], I64_MIN)))
+        cand[0] = I64_MIN
+        tau = torch.cummax(cand, 0).values                                 # shard r owns [tau_r, tau_r+1)
         counts = []
         for br, n in ((0, self.na_s), (1, self.nb_s)):
             if n:
-                cut = torch.searchsorted(_u64_key(self._orig(br, "ts")).contiguous(), tau, right=False)
-                edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.dev), cut,
-                                   torch.full((1,), n, dtype=torch.int64, device=self.dev)])
+                cut = torch.searchsorted(_u64_key(self._orig(br, "ts")).contiguous(), tau[1:].contiguous())
+                edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=dv), cut,
+                                   torch.full((1,), n, dtype=torch.int64, device=dv)])
                 counts.append(edges[1:] - edges[:-1])
             else:
-                counts.append(torch.zeros(W, dtype=torch.int64, device=self.dev))
-        allc = self.comm.all_gather(torch.stack(counts)).cpu().numpy()  # [src, branch, dest]
+                counts.append(torch.zeros(W, dtype=torch.int64, device=dv))
+        return torch.cat(counts + [ordered.view(1).to(torch.int64)])
+
+    def exchange(self) -> None:
+        """Every op to the shard owning its key (collective)."""
+        self._saved = []
+        W = self.world
+        if self.mode != "sample":
+            allc = self.comm.all_gather(self._range_counts()).cpu().numpy()  # the host sync
+            if allc[:, 2 * W].min() == 1:
+                self.exchange_mode = "range"
+                self._exchange_range(allc[:, :2 * W].reshape(W, 2, W))
+                return
+            if self.mode == "range":
+                raise ValueError("sharded merge (mode 'range') needs timestamp-ordered branch logs "
+                                 "(a slice is unordered or a branch decreases across rank slices)")
+        self.exchange_mode = "sample"
+        self._exchange_sample()
+
+    def _exchange_range(self, allc: np.ndarray) -> None:
+        """allc[src, branch, dest]: op counts of the key-range split."""
+        torch = self.torch
+        r, W = self.rank, self.world
         send, recv = allc[r], allc[:, :, r]                              # [br, dest], [src, br]
         lo_s, hi_s = send[:, :r].sum(axis=1), send[:, r + 1:].sum(axis=1)
         lo_r, hi_r = recv[:r].sum(axis=0), recv[r + 1:].sum(axis=0)
@@ -226,48 +322,140 @@ class ShardedCompose:
         first = [int(allc[:, br, :r].sum()) for br in range(2)]
         self.src_a = first[0]
         self.src_b = self.na_glob + first[1]
-        # ranges of the shard in the buffers
         n0 = (self.na_s, self.nb_s)
         base = (self._oa, self._ob)
         self.rng = [(base[br] + int(lo_s[br] - lo_r[br]), base[br] + n0[br] - int(hi_s[br] - hi_r[br]))
                     for br in range(2)]
         in_splits = [0 if d == r else int(send[0, d] + send[1, d]) for d in range(W)]
         out_splits = [0 if q == r else int(recv[q, 0] + recv[q, 1]) for q in range(W)]
-        self._saved = []
+        self.n_xchg = int(sum(out_splits))
         moving = int(allc.sum()) - sum(int(allc[q, :, q].sum()) for q in range(W))
         if moving:  # the same decision on every rank: the all-to-all is collective
             soff = [np.concatenate([[0], np.cumsum(send[br])]) for br in range(2)]
+            cols = {}
+            for f in REC_FIELDS:
+                pieces = [self._orig(br, f)[soff[br][d]: soff[br][d + 1]]
+                          for d in range(W) if d != r for br in range(2)]
+                cols[f] = torch.cat(pieces) if pieces else self.buf[f][:0]
+            got = self.comm.all_to_all(pack_records(cols), in_splits, out_splits)
+            f_in, _ = unpack_records(got, self.dtypes)
             roff = np.concatenate([[0], np.cumsum(out_splits)])
-            # received pieces of each branch from the lower / higher shards, in shard order
-            idx = {}
             for br in range(2):
-                for part, qs in (("lo", range(r)), ("hi", range(r + 1, W))):
+                for part, qs, dst0 in (("lo", range(r), self.rng[br][0]),
+                                       ("hi", range(r + 1, W), base[br] + n0[br] - int(hi_s[br]))):
                     ii = [np.arange(roff[q] + (recv[q, 0] if br else 0),
                                     roff[q] + (recv[q, 0] if br else 0) + recv[q, br]) for q in qs]
                     ii = np.concatenate(ii) if ii else np.zeros(0, np.int64)
-                    idx[br, part] = torch.from_numpy(ii.astype(np.int64)).to(self.dev)
-            for f in FIELDS:
-                pieces = []
-                for d in range(W):
-                    if d == r:
+                    if len(ii) == 0:
                         continue
-                    for br in range(2):
-                        o = self._orig(br, f)
-                        pieces.append(o[soff[br][d]: soff[br][d + 1]])
-                sendbuf = torch.cat(pieces) if pieces else self.buf[f][:0]
-                got = self.comm.all_to_all(sendbuf, in_splits, out_splits)
-                for br in range(2):
-                    lo, hi = self.rng[br]
-                    o0 = base[br]
-                    for part, dst0 in (("lo", lo), ("hi", o0 + n0[br] - int(hi_s[br]))):
-                        ix = idx[br, part]
-                        if ix.numel() == 0:
-                            continue
+                    ix = torch.from_numpy(ii.astype(np.int64)).to(self.dev)
+                    for f in FIELDS:
                         if self.restore:  # originals under the arriving ops, put back after the step
-                            self._saved.append((f, dst0, self.buf[f][dst0: dst0 + ix.numel()].clone()))
-                        self.buf[f][dst0: dst0 + ix.numel()] = got[ix]
+                            self._saved.append((f, dst0, self.buf[f][dst0: dst0 + len(ii)].clone()))
+                        self.buf[f][dst0: dst0 + len(ii)] = f_in[f][ix]
         self.n_a = self.rng[0][1] - self.rng[0][0]
         self.n_b = self.rng[1][1] - self.rng[1][0]
+        self._fields = self.buf
+        self._map_on = False
+        self._bind()
+
+    def _keys(self):
+        """Full T keys of this rank's ops, A slice then B slice: kind (precedence rank),
+        ts, oid hi, oid lo (u64 as ordered int64) and the global source index (side,
+        then index within the branch)."""
+        torch = self.torch
+        cat = torch.cat
+        kind = cat([self._orig(0, "kind"), self._orig(1, "kind")]).to(torch.int64)
+        ts = _u64_key(cat([self._orig(0, "ts"), self._orig(1, "ts")]))
+        hi = _u64_key(cat([self._orig(0, "hi"), self._orig(1, "hi")]))
+        lo = _u64_key(cat([self._orig(0, "lo"), self._orig(1, "lo")]))
+        gidx = cat([torch.arange(self.a_start, self.a_start + self.na_s, device=self.dev),
+                    torch.arange(self.na_glob + self.b_start, self.na_glob + self.b_start + self.nb_s,
+                                 device=self.dev)])
+        return [kind, ts, hi, lo, gidx]
+
+    def _exchange_sample(self) -> None:
+        """Sample sort on the full T key: all_gather of samples, splitters (device), one
+        all_gather of the counts (host sync), one all_to_all of 41-B records."""
+        torch = self.torch
+        r, W, dv = self.rank, self.world, self.dev
+        keys = self._keys()
+        n = self.na_s + self.nb_s
+        S = self.oversample * W
+        samp = torch.ones((S, 6), dtype=torch.int64, device=dv)         # col 0: 0 = valid
+        k = min(n, S)
+        if k:
+            pos = torch.arange(k, device=dv) * n // k                    # evenly spaced
+            samp[:k, 0] = 0
+            for i, key in enumerate(keys):
+                samp[:k, 1 + i] = key[pos]
+        allS = self.comm.all_gather(samp).reshape(W * S, 6)
+        order = torch.arange(W * S, device=dv)
+        for c in range(5, -1, -1):                                        # lexsort, last key first
+            order = order[torch.sort(allS[order, c], stable=True).indices]
+        srt = allS[order]
+        nvalid = (allS[:, 0] == 0).sum()
+        at = (torch.arange(1, W, device=dv) * nvalid // W).clamp(max=W * S - 1)
+        split = srt[at, 1:]                                               # [W-1, 5]
+        if n:
+            dest = lex_dest(keys, split) if W > 1 else torch.zeros(n, dtype=torch.int64, device=dv)
+            side = torch.cat([torch.zeros(self.na_s, dtype=torch.int64, device=dv),
+                              torch.ones(self.nb_s, dtype=torch.int64, device=dv)])
+            key2 = dest * 2 + side
+            perm = torch.sort(key2, stable=True).indices
+            cnt = torch.bincount(key2, minlength=2 * W)
+        else:
+            perm = torch.zeros(0, dtype=torch.int64, device=dv)
+            cnt = torch.zeros(2 * W, dtype=torch.int64, device=dv)
+        allc = self.comm.all_gather(cnt).cpu().numpy().reshape(W, W, 2)   # [src, dest, side]: host sync
+        cols = {f: torch.cat([self._orig(0, f), self._orig(1, f)])[perm] for f in REC_FIELDS}
+        rec = pack_records(cols, keys[4].to(torch.int32)[perm])
+        in_splits = [int(allc[r, d].sum()) for d in range(W)]
+        out_splits = [int(allc[q, r].sum()) for q in range(W)]
+        self.n_xchg = int(sum(out_splits)) - int(allc[r, r].sum())
+        got = self.comm.all_to_all(rec, in_splits, out_splits)
+        f_in, g_in = unpack_records(got, self.dtypes, with_gidx=True)
+        roff = np.concatenate([[0], np.cumsum(out_splits)])
+        # A' then B': each source's A records then its B records, sources in rank order
+        # (= global index order within each branch)
+        ia = [np.arange(roff[q], roff[q] + allc[q, r, 0]) for q in range(W)]
+        ib = [np.arange(roff[q] + allc[q, r, 0], roff[q + 1]) for q in range(W)]
+        ii = np.concatenate(ia + ib).astype(np.int64)
+        ix = torch.from_numpy(ii).to(dv)
+        self.n_a = int(allc[:, r, 0].sum())
+        self.n_b = int(allc[:, r, 1].sum())
+        n_loc = self.n_a + self.n_b
+        self._sbuf(n_loc)
+        for f in FIELDS:
+            self.sbuf[f][:n_loc] = f_in[f][ix]
+        self.src_map[:n_loc] = g_in[ix]
+        self.rng = [(0, self.n_a), (self.n_a, n_loc)]
+        self.src_a, self.src_b = 0, self.na_glob
+        self._fields = self.sbuf
+        self._map_on = True
+        self._bind()
+
+    def _sbuf(self, n_loc: int) -> None:
+        torch = self.torch
+        if self.sbuf is None or self.sbuf["kind"].numel() < max(n_loc, 1):
+            cap = max(n_loc + n_loc // 16, 1)
+            self.sbuf = {f: torch.zeros(cap, dtype=self.dtypes[f], device=self.dev) for f in FIELDS}
+            self.src_map = torch.zeros(cap, dtype=torch.int32, device=self.dev)
+
+    def _compact(self) -> None:
+        """A range shard as one contiguous [A' | B'] (b_gap = 0), so that ORDER_FIX may
+        take the generic plan; sources stay src_a + j / src_b + j."""
+        if self._fields is self.sbuf:
+            return
+        n_loc = self.n_a + self.n_b
+        self._sbuf(n_loc)
+        (a_lo, a_hi), (b_lo, b_hi) = self.rng
+        for f in FIELDS:
+            self.sbuf[f][:self.n_a] = self.buf[f][a_lo:a_hi]
+            self.sbuf[f][self.n_a:n_loc] = self.buf[f][b_lo:b_hi]
+        self.rng = [(0, self.n_a), (self.n_a, n_loc)]
+        self._fields = self.sbuf
+        self._map_on = False
         self._bind()
 
     def _restore(self) -> None:
@@ -297,7 +485,8 @@ class ShardedCompose:
             self._ws_bytes = ws.value
         a_lo = self.rng[0][0]
         gap = self.rng[1][0] - self.rng[0][1]
-        fp = {f: self.buf[f].data_ptr() + a_lo * self.buf[f].element_size() for f in FIELDS}
+        fb = self._fields
+        fp = {f: fb[f].data_ptr() + a_lo * fb[f].element_size() for f in FIELDS}
         self._ops = _abi.SmxOps(self.n_a, self.n_b, self.n_sym, fp["kind"], fp["ts"], fp["hi"],
                                 fp["lo"], fp["sym"], fp["v0"], fp["v1"], gap)
         self._out = _abi.SmxComposeOut(_ptr(self.order), _ptr(self.addr), _ptr(self.file),
@@ -308,10 +497,16 @@ class ShardedCompose:
         sh.src_a, sh.src_b = self.src_a, self.src_b
         sh.summary = _ptr(self.summary)
         sh.halo_cap = self.H
-        sh.export_sym, sh.export_cls, sh.export_src = _ptr(self.xsym), _ptr(self.xcls), _ptr(self.xsrc)
+        sh.export_sym, sh.export_cls, sh.export_src = (_ptr(self.xport[i]) for i in range(3))
         sh.part_tab = _ptr(self.part)
         sh.fin_tab = _ptr(self.part)
         sh.glob = _ptr(self.glob)
+        if self.H > 0:
+            for b in range(2):
+                sh.halo_sym[b], sh.halo_cls[b], sh.halo_src[b] = (_ptr(self.halo[b, i]) for i in range(3))
+        sh.halo_dev = _ptr(self.halo_dev)
+        sh.in_state_dev = _ptr(self.in_dev)
+        sh.src_map = _ptr(self.src_map) if self._map_on else None
         self._sh = sh
 
     def _step(self, step: int) -> None:
@@ -325,83 +520,106 @@ class ShardedCompose:
         torch = self.torch
         self.exchange()
         self._step(_abi.SHARD_ORDER)
-        summ = self.comm.all_gather(self.summary).cpu().numpy()
-        xs = self.comm.all_gather(torch.stack([self.xsym, self.xcls, self.xsrc]))
-        self.sum_order = summ
-        self._set_halo(summ, xs)
-        self._walk()
+        self._order_exchange()
+        summ = self._walk()
+        if summ[:, S_FAIL].any():          # an asynchronous ORDER failed somewhere
+            if int(np.bitwise_or.reduce(summ[:, S_FAIL])) & 3:
+                self._fail(summ)
+            err = None
+            if summ[self.rank, S_FAIL]:     # dense timestamp ties: smaller windows, else generic
+                self.order_fixes += 1
+                try:
+                    self._compact()
+                    self._step(_abi.SHARD_ORDER_FIX)
+                except RuntimeError as e:   # reported by every rank below
+                    err = e
+            self._order_exchange()
+            summ = self._walk()
+            if summ[:, S_FAIL].any():
+                self._fail(summ, err)
+        self.sum_walk = summ
         self._step(_abi.SHARD_TABLES)
-        summ = self.comm.all_gather(self.summary).cpu().numpy()
-        self.glob.copy_(torch.from_numpy(summ[:, S_WIDTH:S_WIDTH + 3].max(axis=0)))
+        n3 = 3 * max(self.n_sym, 1)
+        self.part[n3:].copy_(self.summary[S_WIDTH:S_WIDTH + 3])
         mvpre = None
         if summ[:, S_MVNONE].sum() > 0:
             mv = self.comm.all_gather(self.part[: 2 * self.n_sym])      # [world, 2*n_sym]
-            lower = mv[: self.rank]
-            mvpre = lower.max(dim=0).values if self.rank > 0 else torch.zeros_like(mv[0])
+            mvpre = mv[: self.rank].max(dim=0).values if self.rank > 0 else torch.zeros_like(mv[0])
             mvpre = mvpre.contiguous()
         self._mvpre = mvpre
         self._sh.mv_prefix = _ptr(mvpre) if mvpre is not None else None
-        self.comm.all_reduce_max(self.part)
+        self.comm.all_reduce_max(self.part)        # last writers and value widths together
+        self._sum_host = np.ascontiguousarray(summ[self.rank], dtype=np.int64)
+        self._sh.summary_host = self._sum_host.ctypes.data
         self._step(_abi.SHARD_EMIT)
-        self.sum_final = self.comm.all_gather(self.summary).cpu().numpy()
         if self.restore:
             self._restore()
 
-    def _set_halo(self, summ: np.ndarray, xs) -> None:
-        """Halo of branch b: the renames of b on the following shards, first H of them."""
-        torch = self.torch
-        H, r, W = self.H, self.rank, self.world
-        self._halo = []
-        for b in range(2):
-            pieces, got = [], 0
-            rest = int(summ[r + 1:, S_REN + b].sum())
-            for q in range(r + 1, W):
-                if got >= H:
-                    break
-                k = min(int(summ[q, S_REN + b]), H, H - got)
-                if k:
-                    pieces.append(xs[q, :, b * H: b * H + k])
-                    got += k
-            if pieces:
-                h = torch.cat(pieces, dim=1).contiguous()
-            else:
-                h = torch.zeros((3, 1), dtype=torch.int32, device=self.dev)
-            self._halo.append(h)
-            self._sh.halo_n[b] = got
-            self._sh.halo_more[b] = 1 if rest > got else 0
-            self._sh.halo_sym[b] = _ptr(h[0]) if got else None
-            self._sh.halo_cls[b] = _ptr(h[1]) if got else None
-            self._sh.halo_src[b] = _ptr(h[2]) if got else None
+    def _fail(self, summ: np.ndarray, err=None):
+        f = int(np.bitwise_or.reduce(summ[:, S_FAIL]))
+        if f & 2:
+            raise ValueError("invalid input: sym[i] >= n_sym or kind[i] >= 18")
+        raise RuntimeError("sharded merge: the order plan failed on a shard"
+                           + (f" ({err})" if err else " (branch logs not timestamp-ordered)"))
 
-    def _walk(self) -> None:
-        """Walk with the incoming open region of the previous shards; a shard whose
-        incoming region changed re-runs, until no shard re-runs (at most world rounds:
-        a region hand-off moves one shard per round)."""
+    def _order_exchange(self) -> None:
+        """One all_gather of every shard's summary and halo exports; this shard's halo
+        (the first H renames of each branch on the following shards) assembled on the
+        device."""
+        torch = self.torch
+        H, r, W, dv = self.H, self.rank, self.world, self.dev
+        g = self.comm.all_gather(torch.cat([self.summary, self.xport.reshape(-1).view(torch.int64)]))
+        if H <= 0:
+            self.halo_dev.zero_()
+            return
+        summ = g[:, :SUM]
+        X = g[:, SUM:].contiguous().view(torch.int32).reshape(W, 3, 2 * H)
+        later = (torch.arange(W, device=dv) > r).to(torch.int64)
+        i = torch.arange(H, device=dv)
+        st = []
+        for b in range(2):
+            after = summ[:, S_REN + b] * later
+            c = after.clamp(max=H)
+            cum = torch.cumsum(c, 0)
+            got = cum[-1].clamp(max=H)
+            q = torch.searchsorted(cum, i, right=True).clamp(max=W - 1)
+            off = (i - (cum[q] - c[q])).clamp(min=0, max=H - 1)
+            self.halo[b].copy_(X[q, :, b * H + off].t())
+            st.append((got, (after.sum() > got).to(torch.int64)))
+        self.halo_dev.copy_(torch.stack([st[0][0], st[1][0], st[0][1], st[1][1]]))
+
+    def _walk(self) -> np.ndarray:
+        """Walk with the incoming open region of the previous shards (device-held); one
+        summary all_gather + host read per round; a shard whose incoming region changed
+        re-runs, until none does (a region hand-off moves one shard per round).  Every
+        rank sees every summary, so all take the same decisions without another
+        collective.  Returns the gathered summaries."""
         W, r = self.world, self.rank
-        used = (0, 0)
-        self._sh.in_ahead, self._sh.in_d = used
+        used = [(0, 0)] * W
+        self.in_dev.zero_()
         self._step(_abi.SHARD_WALK)
         for _ in range(W + 1):
             summ = self.comm.all_gather(self.summary).cpu().numpy()
-            if summ[:, S_OVER].any():
-                raise RuntimeError("sharded walk: a DivergentRename region crosses a shard "
-                                   "boundary deeper than the halo (raise halo_cap)")
-            want = (int(summ[r - 1, S_AHEAD]), int(summ[r - 1, S_D])) \
-                if r > 0 and summ[r - 1, S_OPEN] else (0, 0)
-            rerun = want != used
-            if rerun:
-                used = want
-                self._sh.in_ahead, self._sh.in_d = used
-                self._step(_abi.SHARD_WALK)
-            if not self._any(rerun):
+            if summ[:, S_FAIL].any():
                 break
-        self.sum_walk = summ
-        self.in_state = used
+            if summ[:, S_OVER].any():
+                raise AssertionError("sharded walk: a DivergentRename region crosses a shard "
+                                     "boundary deeper than the halo (raise halo_cap)")
+            want = [(int(summ[q - 1, S_AHEAD]), int(summ[q - 1, S_D]))
+                    if q > 0 and summ[q - 1, S_OPEN] else (0, 0) for q in range(W)]
+            if want == used:
+                break
+            if want[r] != used[r]:
+                self.in_dev.copy_(self.torch.tensor(want[r], dtype=self.torch.int64))
+                self._step(_abi.SHARD_WALK)
+            used = want
+        self.in_state = used[r]
+        return summ
 
-    def _any(self, flag: bool) -> bool:
-        t = self.torch.tensor([1 if flag else 0], dtype=self.torch.int64, device=self.dev)
-        self.comm.all_reduce_max(t)
-        return bool(t.item())
+    def totals(self) -> Tuple[int, int]:
+        """(composed ops, conflicts) of the whole merge after run() (collective)."""
+        g = self.comm.all_gather(self.counts).cpu().numpy()
+        return int(g[:, 0].sum()), int(g[:, 1].sum())
 
     # -- results ----------------------------------------------------------------------
     def results(self):
@@ -414,8 +632,8 @@ class ShardedCompose:
             raise RuntimeError("invalid input: sym >= n_sym or kind >= 18")
         if nc > self.cap:
             raise RuntimeError(f"{nc} conflicts exceed capacity {self.cap}")
-        kc = self.sum_order[self.rank, S_KINDS:S_KINDS + N_KINDS].astype(np.int64).copy()
-        kc[1] -= int(self.sum_final[self.rank, S_NSKIP])
+        kc = self.sum_walk[self.rank, S_KINDS:S_KINDS + N_KINDS].astype(np.int64).copy()
+        kc[1] -= int(self.sum_walk[self.rank, S_NSKIP])
         starts = np.concatenate([[0], np.cumsum(kc)])
         segs = [(kk, int(starts[kk]), int(kc[kk])) for kk in range(N_KINDS)]
         return (self.order[:k].cpu().numpy(), self.addr[:k].cpu().numpy(),

@@ -25,6 +25,13 @@ def _make(case):
     kind, n, n_sym, seed = case
     if kind == "chain":
         return _chain_soa(n, seed)
+    if kind == "c2s":  # config 2's shape, shuffled branch logs (any order)
+        spec = synth.LiftSpec(**{**synth.CONFIGS["c2s"].__dict__, "n_total": n, "n_sym": n_sym,
+                                 "seed": seed})
+        return synth.lift_soa(synth.lift_logs(spec))
+    if kind == "dense":  # long equal-timestamp groups: windows overflow, ORDER_FIX repairs
+        spec = synth.LiftSpec(n, n_sym, seed, ops_per_ms=4096)
+        return synth.lift_soa(synth.lift_logs(spec))
     if kind == "lift":
         spec = synth.LiftSpec(n, n_sym, seed, ops_per_ms=64)
     elif kind == "adv":  # rename-heavy, 30% of symbols renamed on both sides: many conflicts
@@ -68,7 +75,7 @@ def _chain_soa(n_ren, seed):
     return SoA(na, nb, kind, ts, hi, lo, sym, v0, v1, 5, ["a", "b"])
 
 
-def _worker(rank, world, port, case, halo, q):
+def _worker(rank, world, port, case, halo, q, mode="auto"):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -77,10 +84,15 @@ def _worker(rank, world, port, case, halo, q):
         from semantic_merge_amd import shard
         soa = _make(case)
         a, b, na, nb = shard.slices_from_soa(soa, rank, world, "cuda:0")
-        sc = shard.ShardedCompose(a, b, na, nb, soa.n_sym, shard.Comm(), "cuda:0", halo_cap=halo)
+        sc = shard.ShardedCompose(a, b, na, nb, soa.n_sym, shard.Comm(), "cuda:0", halo_cap=halo,
+                                  mode=mode)
         sc.run()
         res = sc.results()
-        q.put((rank, res, sc.in_state, int(sc.sum_walk[:, shard.S_OPEN].sum())))
+        first = (res, sc.totals())
+        sc.run()  # a second run on the same buffers (bench.py's steps) gives the same results
+        res2 = sc.results()
+        same = all(np.array_equal(x, y) for x, y in zip(first[0][:5], res2[:5]))
+        q.put((rank, res, sc.in_state, (sc.exchange_mode, same, first[1], sc.order_fixes)))
     except Exception as e:  # report to the parent instead of hanging the collective
         q.put((rank, repr(e), None, None))
         raise
@@ -88,11 +100,11 @@ def _worker(rank, world, port, case, halo, q):
         dist.destroy_process_group()
 
 
-def _run(case, world, halo=4096):
+def _run(case, world, halo=4096, mode="auto"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, halo, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, halo, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -106,16 +118,22 @@ def _run(case, world, halo=4096):
     return [got[r][0] for r in range(world)], got
 
 
-def _check(case, world, halo=4096):
+def _check(case, world, halo=4096, mode="auto", want_mode=None):
     from oracle import oracle
     from semantic_merge_amd import shard
-    parts, got = _run(case, world, halo)
+    parts, got = _run(case, world, halo, mode)
     glob = shard.assemble(parts)
     ref = oracle.compose(_make(case))
     names = ("order", "addr", "file", "ctx", "conflicts")
     for name, g, r in zip(names, glob, ref):
         assert g.shape == r.shape, f"{case} x{world}: {name} shape {g.shape} vs {r.shape}"
         assert np.array_equal(g, r), f"{case} x{world}: {name} differs"
+    for r in range(world):
+        emode, same, totals, _ = got[r][2]
+        assert same, f"rank {r}: a second run differs"
+        assert totals == (len(ref[0]), len(ref[4])), totals
+        if want_mode:
+            assert emode == want_mode, emode
     return got, ref
 
 
@@ -148,6 +166,23 @@ def test_shard_halo_too_short_fails_loudly():
 
 def test_shard_tiny_with_empty_shards():
     _check(("lift", 40, 5, 2), 3)
+
+
+def test_shard_sample_sort_shuffled_c2s():
+    """Branch logs in any order (config 2s's shape): the sample-sort exchange on the full
+    T key, the generic plan per shard, global sources through src_map."""
+    _check(("c2s", 300_000, 3_000, 7), 3, want_mode="sample")
+
+
+def test_shard_sample_sort_forced_on_ordered_logs():
+    _check(("adv", 80_000, 16, 3), 2, mode="sample", want_mode="sample")
+
+
+def test_shard_dense_ties_order_fix():
+    # 4096 ops per timestamp: presorted windows overflow on the first (asynchronous)
+    # ORDER; ORDER_FIX retries with smaller windows
+    got, _ = _check(("dense", 200_000, 2_000, 6), 2, want_mode="range")
+    assert any(got[r][2][3] for r in range(2)), "ORDER_FIX did not run"
 
 
 def test_bench_two_ranks_sharded():

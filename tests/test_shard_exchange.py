@@ -1,7 +1,9 @@
-"""Sharded merge, host side on CPU (gloo, 2-3 ranks): the key-range all-to-all puts every
-op on the shard owning its timestamp, in place (headroom), with the global source offsets
-the kernels need; the originals come back for the next step.  The compute steps need a
-GPU (tests/test_gpu_shard.py)."""
+"""Sharded merge, host side on CPU (gloo, 2-3 ranks): the key-range all-to-all (one
+all_to_all_single of packed records) puts every op on the shard owning its timestamp, in
+place (headroom), with the global source offsets the kernels need; the originals come
+back for the next step.  The sample-sort exchange (logs in any order) puts every op on
+the shard owning its full T key, with its global source index.  The compute steps need
+a GPU (tests/test_gpu_shard.py)."""
 import os
 import socket
 
@@ -36,6 +38,7 @@ def _worker(rank, world, port, args, q):
         sc = shard.ShardedCompose(a, b, na, nb, soa.n_sym, shard.Comm(), "cpu", halo_cap=64,
                                   headroom=headroom)
         sc.exchange()
+        assert sc.exchange_mode == "range"
         (a_lo, a_hi), (b_lo, b_hi) = sc.rng
         got = {f: (sc.buf[f][a_lo:a_hi].numpy().copy(), sc.buf[f][b_lo:b_hi].numpy().copy())
                for f in shard.FIELDS}
@@ -94,3 +97,140 @@ def test_exchange_key_ranges(world, n, opm, headroom):
     assert ea == na and eb == nb
     if headroom == 0:
         assert any(res[r][5] > 0 for r in range(world))  # the headroom grew
+
+
+def _spawn(target, world, args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        item = q.get(timeout=120)
+        res[item[0]] = item
+    for p in procs:
+        p.join(60)
+    errs = [res[r][1] for r in range(world) if isinstance(res[r][1], str)]
+    assert not errs, errs
+    return res
+
+
+def _shuffled(n, seed):
+    from semantic_merge_amd import synth
+    return synth.lift_soa(synth.lift_logs(synth.LiftSpec(n, 40, seed, ops_per_ms=3, shuffle=True)))
+
+
+def _sample_worker(rank, world, port, args, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from semantic_merge_amd import shard
+        n, seed, mode = args
+        soa = _shuffled(n, seed)
+        a, b, na, nb = shard.slices_from_soa(soa, rank, world, "cpu")
+        sc = shard.ShardedCompose(a, b, na, nb, soa.n_sym, shard.Comm(), "cpu", halo_cap=64,
+                                  mode=mode, oversample=32)
+        sc.exchange()
+        m = sc.n_a + sc.n_b
+        got = {f: sc.sbuf[f][:m].numpy().copy() for f in shard.FIELDS}
+        q.put((rank, sc.n_a, sc.exchange_mode, got, sc.src_map[:m].numpy().copy()))
+    except Exception as e:
+        q.put((rank, repr(e), None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,mode", [(2, 6_000, "sample"), (3, 9_001, "auto")])
+def test_exchange_sample_sort(world, n, mode):
+    """Unordered branch logs: every op lands exactly once on the shard owning its full T
+    key (kind, ts, oid, side, index), A' and B' in global index order, shards balanced."""
+    from semantic_merge_amd import shard
+    res = _spawn(_sample_worker, world, (n, 5, mode))
+    soa = _shuffled(n, 5)
+    cols = {"kind": soa.kind, "ts": soa.ts.view(np.int64), "hi": soa.oid_hi.view(np.int64),
+            "lo": soa.oid_lo.view(np.int64), "sym": soa.sym.view(np.int32), "v0": soa.v0, "v1": soa.v1}
+    seen = np.zeros(soa.n, np.int64)
+    prev_max = None
+    for r in range(world):
+        _, n_a, emode, got, smap = res[r]
+        assert emode == "sample"
+        seen[smap] += 1
+        for f in shard.FIELDS:
+            assert np.array_equal(got[f], cols[f][smap]), (r, f)
+        assert np.all(smap[:n_a] < soa.n_a) and np.all(smap[n_a:] >= soa.n_a)
+        assert np.all(np.diff(smap[:n_a]) > 0) and np.all(np.diff(smap[n_a:]) > 0)
+        assert len(smap) < 2.0 * soa.n / world                       # balanced by the samples
+        if len(smap):
+            keys = sorted(zip(soa.kind[smap].tolist(), soa.ts[smap].tolist(), soa.oid_hi[smap].tolist(),
+                              soa.oid_lo[smap].tolist(), smap.tolist()))
+            if prev_max is not None:
+                assert prev_max < keys[0]                             # key ranges in shard order
+            prev_max = keys[-1]
+    assert np.all(seen == 1)
+
+
+def test_packed_records_round_trip():
+    import torch
+    from semantic_merge_amd import shard
+    rng = np.random.default_rng(1)
+    m = 1000
+    cols = {"kind": torch.from_numpy(rng.integers(0, 18, m).astype(np.uint8)),
+            "ts": torch.from_numpy(rng.integers(-2**62, 2**62, m)),
+            "hi": torch.from_numpy(rng.integers(-2**62, 2**62, m)),
+            "lo": torch.from_numpy(rng.integers(-2**62, 2**62, m)),
+            "sym": torch.from_numpy(rng.integers(0, 2**30, m).astype(np.int32)),
+            "v0": torch.from_numpy(rng.integers(-1, 2**30, m).astype(np.int32)),
+            "v1": torch.from_numpy(rng.integers(-1, 2**30, m).astype(np.int32))}
+    gidx = torch.from_numpy(rng.integers(0, 2**31 - 1, m).astype(np.int32))
+    rec = shard.pack_records(cols, gidx)
+    assert rec.shape == (m, 41) and rec.dtype == torch.uint8
+    assert shard.pack_records(cols).shape == (m, 37)
+    back, g = shard.unpack_records(rec, {f: t.dtype for f, t in cols.items()}, with_gidx=True)
+    assert all(torch.equal(back[f], cols[f]) for f in cols) and torch.equal(g, gidx)
+    empty = shard.pack_records({f: t[:0] for f, t in cols.items()})
+    assert empty.shape == (0, 37)
+
+
+def _strong_worker(rank, world, port, args, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from semantic_merge_amd import shard, synth
+        n_total, = args
+        spec = synth.LiftSpec(n_total // world, 300, 9, ops_per_ms=7)    # bench.py's strong split
+        soa, na_g, nb_g = synth.lift_slice_soa(spec, rank, world)
+        a, b, _, _ = shard.slices_from_soa(soa, 0, 1, "cpu")
+        a.start = b.start = rank * soa.n_a
+        sc = shard.ShardedCompose(a, b, na_g, nb_g, soa.n_sym, shard.Comm(), "cpu", mode="range")
+        sc.exchange()
+        (a_lo, a_hi), (b_lo, b_hi) = sc.rng
+        ts = np.concatenate([sc.buf["ts"][a_lo:a_hi].numpy(), sc.buf["ts"][b_lo:b_hi].numpy()])
+        q.put((rank, sc.src_a, sc.src_b - na_g, a_hi - a_lo, b_hi - b_lo, ts.min() if len(ts) else None,
+               ts.max() if len(ts) else None, na_g, sc.n_xchg))
+    except Exception as e:
+        q.put((rank, repr(e)) + (None,) * 7)
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_strong_split_slices():
+    """bench.py --gpus N (strong scaling): each rank generates its own index slice of the
+    config's ops (synth.lift_slice_soa); the key-range exchange tiles both branches in
+    shard order, moving only the ops at the slice edges."""
+    world, n_total = 3, 60_000
+    res = _spawn(_strong_worker, world, (n_total,))
+    ea = eb = 0
+    for r in range(world):
+        _, sa, sb, la, lb, tmin, tmax, na_g, nx = res[r]
+        assert (sa, sb) == (ea, eb)
+        ea, eb = sa + la, sb + lb
+        assert nx < 64                            # ops_per_ms = 7: a few ops per edge move
+        if r + 1 < world and res[r + 1][5] is not None:
+            assert tmax < res[r + 1][5]
+    assert ea == na_g and eb == na_g and na_g == world * (n_total // world // 2)
