@@ -124,14 +124,102 @@ class DeviceCompose:
                 self.conf[: 2 * nc].cpu().numpy().reshape(nc, 2))
 
 
+def _al(x: int) -> int:
+    return (x + 255) & ~255
+
+
+class ComposeSession:
+    """Reusable buffers for a stream of merges of any size (the drop-in's path): one
+    pinned host staging area and one device area, grown on demand, never shrunk.  A
+    merge is one host-to-device copy of the packed SoA columns, smx_compose, and one
+    device-to-host copy of the outputs and counts -- no allocation after warm-up.
+    `last` holds the host / device split of the last merge in seconds."""
+
+    _IN = (("kind", 1), ("ts", 8), ("oid_hi", 8), ("oid_lo", 8), ("sym", 4), ("v0", 4), ("v1", 4))
+
+    def __init__(self, device: str = "cuda") -> None:
+        self.torch = _torch()
+        self.device = self.torch.device(device)
+        self.cap_n = self.cap_ws = -1
+        self.last = {}
+
+    def _ensure(self, n: int, ws_bytes: int) -> None:
+        torch = self.torch
+        if n > self.cap_n:
+            cap = max(n + n // 4, 1024)
+            in_b = sum(_al(cap * w) for _, w in self._IN)
+            out_b = 4 * _al(cap * 4) + _al(cap * 4) + 256     # 4 outputs, conflicts (2 * cap/2), counts
+            self.h_in = torch.empty(in_b, dtype=torch.uint8, pin_memory=True)
+            self.d_in = torch.empty(in_b, dtype=torch.uint8, device=self.device)
+            self.h_out = torch.empty(out_b, dtype=torch.uint8, pin_memory=True)
+            self.d_out = torch.empty(out_b, dtype=torch.uint8, device=self.device)
+            self.cap_n = cap
+        if ws_bytes > self.cap_ws:
+            self.ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=self.device)
+            self.cap_ws = ws_bytes
+
+    def compose(self, soa: SoA):
+        """(order, addr, file, ctx, conflict_pairs) of one merge, computed on the GPU."""
+        import time
+        t0 = time.perf_counter()
+        n = soa.n
+        if n == 0:
+            e = np.zeros(0, np.int32)
+            return e, e, e, e, np.zeros((0, 2), np.int32)
+        ws = C.c_size_t(0)
+        check(lib().smx_compose_workspace_bytes(soa.n_a, soa.n_b, soa.n_sym, C.byref(ws)))
+        self._ensure(n, ws.value)
+        hin = self.h_in.numpy()
+        off, ptrs = 0, {}
+        d0 = self.d_in.data_ptr()
+        for name, w in self._IN:   # pack the columns into the pinned staging area (laid out for n)
+            hin[off: off + n * w] = np.ascontiguousarray(getattr(soa, name)).view(np.uint8).reshape(-1)
+            ptrs[name] = d0 + off
+            off += _al(n * w)
+        t1 = time.perf_counter()
+        torch = self.torch
+        stream = torch.cuda.current_stream(self.device)
+        self.d_in[:off].copy_(self.h_in[:off], non_blocking=True)
+        ccap = max(min(soa.n_a, soa.n_b), 1)
+        o0 = self.d_out.data_ptr()
+        q = _al(n * 4)             # outputs laid out for n: one contiguous copy back
+        ops = _abi.SmxOps(soa.n_a, soa.n_b, soa.n_sym, ptrs["kind"], ptrs["ts"], ptrs["oid_hi"],
+                          ptrs["oid_lo"], ptrs["sym"], ptrs["v0"], ptrs["v1"])
+        cnt_off = 4 * q + _al(8 * ccap)
+        out = _abi.SmxComposeOut(o0, o0 + q, o0 + 2 * q, o0 + 3 * q, o0 + 4 * q, ccap, o0 + cnt_off)
+        check(lib().smx_compose(C.byref(ops), C.byref(out), self.ws.data_ptr(), ws.value, stream.cuda_stream))
+        self.h_out[:cnt_off + 16].copy_(self.d_out[:cnt_off + 16], non_blocking=True)
+        stream.synchronize()
+        t2 = time.perf_counter()
+        hout = self.h_out.numpy()
+        k, nc = (int(x) for x in hout[cnt_off: cnt_off + 16].view(np.int64))
+        if k < 0:
+            raise SmxError(-1, "invalid input: sym >= n_sym or kind >= 18")
+        if nc > ccap:
+            raise SmxError(-2, f"{nc} conflicts exceed capacity {ccap}")
+        res = tuple(hout[i * q: i * q + 4 * k].view(np.int32).copy() for i in range(4))
+        pairs = hout[4 * q: 4 * q + 8 * nc].view(np.int32).reshape(nc, 2).copy()
+        self.last = {"pack_s": t1 - t0, "device_s": t2 - t1, "unpack_s": time.perf_counter() - t2}
+        return res + (pairs,)
+
+
+_sessions = {}
+
+
+def session(device: str = "cuda") -> ComposeSession:
+    """The calling thread's ComposeSession on `device`."""
+    import threading
+    key = (threading.get_ident(), str(device))
+    s = _sessions.get(key)
+    if s is None:
+        s = _sessions[key] = ComposeSession(device)
+    return s
+
+
 def compose_soa(soa: SoA, device: str = "cuda"):
-    """(order, addr, file, ctx, conflict_pairs) of one merge, computed on the GPU."""
-    if soa.n == 0:
-        e = np.zeros(0, np.int32)
-        return e, e, e, e, np.zeros((0, 2), np.int32)
-    dc = DeviceCompose(soa, device)
-    dc.run()
-    return dc.results()
+    """(order, addr, file, ctx, conflict_pairs) of one merge, computed on the GPU
+    (through the thread's reusable ComposeSession)."""
+    return session(device).compose(soa)
 
 
 def stage_times():

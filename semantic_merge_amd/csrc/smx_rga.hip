@@ -10,9 +10,9 @@
 //    delete tombstones every present element of that value (crdt.py:33-43).
 //  * materialize = live elements in (key, index) order (crdt.py:45-46).
 // Pipeline: stable LSD radix partition of 40-byte event records by list id (LDS-staged,
-// coalesced) -> list bounds -> one block per list, in LDS: order by (value, index), one
-// sequential replay per value group, survivors ranked by (anchor, t, author, opid,
-// index) -> survivor-count scan -> compaction.
+// coalesced) -> list bounds -> one wave per list (k_rga_wave, in LDS): value groups by
+// hashing, one sequential replay per group, survivors ordered by (anchor, t, author,
+// opid, index) -> survivor-count scan -> compaction.
 #include <string>
 
 #include "smx_scan.h"
@@ -29,13 +29,7 @@
 //   w2 = opid_hi, w3 = opid_lo                              -> (w0..w3) is the crdt.py:48-57 key order
 //   w4 = value << 32 | op << 30 | event index              (index = creation order, the tie-break)
 #define RGA_REC 5
-#ifndef RGA_ABL
-#define RGA_ABL 0  // timing ablations of k_rga_list<256> (wrong results, in bounds): bit0 no
-                   // replay, bit1 no survivor sort
-#endif
 #define RGA_IDX_MASK 0x3fffffffu
-#define RGA_SMALL 256   // lists up to this many events: k_rga_list<RGA_SMALL, 256>, one block per list
-#define RGA_MID 1536    // ... up to this: k_rga_list<RGA_MID, 512> over the deferred lists; longer: k_rga_big
 
 // Grouping the events by list: a stable LSD radix partition of whole records on the
 // list id, 8 bits per pass (one pass up to 256 lists, two up to 65536, ...).  The first
@@ -43,11 +37,11 @@
 // in digit order and writes each digit's run of records contiguously, so every byte
 // moves in full cache lines.  Stable: each list's events stay in stream order.
 #ifndef RR_NT
-#define RR_NT 1024                        // scatter workgroup
+#define RR_NT 512                         // scatter workgroup (persistent, one per CU)
 #endif
 #define RR_NW (RR_NT / WAVE)
 #ifndef RREC_ITEMS
-#define RREC_ITEMS 3
+#define RREC_ITEMS 6
 #endif
 #define RREC_TILE (RR_NT * RREC_ITEMS)    // 3072 records (120 KB) per block and pass
 #define RREC_SEG (RREC_TILE / RR_NW)      // contiguous records per wave
@@ -79,112 +73,198 @@ __global__ void __launch_bounds__(BLOCK) k_rrec_hist(smx_rga_ops o, const u32* _
   hist[(i64)blockIdx.x * RGA_NDIG + threadIdx.x] = h[threadIdx.x];
 }
 
-// One tile per block: wave multisplit of the tile's records by digit (ranks and
-// per-wave digit counts), block scan of the digit totals, records staged in LDS in
-// digit order, then every digit's run written contiguously (RREC_TILE / 256 records
-// per run on average: whole cache lines).  Pass 2+ reads the previous pass's records
-// word by word (consecutive lanes, consecutive words) into their staged slots.
+// This thread's share of one tile, loaded into registers: pass 1 the input columns of
+// its RREC_ITEMS events, pass 2+ their list ids and RREC_ITEMS * 5 consecutive record
+// words of the previous pass (consecutive lanes, consecutive words).
+template <bool FIRST>
+struct RTile;
+template <>
+struct RTile<true> {
+  u32 list[RREC_ITEMS], value[RREC_ITEMS], anchor[RREC_ITEMS], author[RREC_ITEMS];
+  u32 op[RREC_ITEMS];
+  i64 t[RREC_ITEMS];
+  u64 hi[RREC_ITEMS], lo[RREC_ITEMS];
+};
+#define RREC_V4 ((RREC_TILE * RGA_REC * 8 / 16 + RR_NT - 1) / RR_NT)  // 16-byte loads per thread
+typedef u32 v4u32 __attribute__((ext_vector_type(4)));
+template <>
+struct RTile<false> {
+  u32 key[RREC_ITEMS];
+  v4u32 w[RREC_V4];
+};
+
+__device__ __forceinline__ i64 rrec_event(i64 base, u32 w, int it, u32 lane) {
+  return base + (i64)w * RREC_SEG + it * WAVE + lane;
+}
+
+template <bool FIRST>
+__device__ __forceinline__ void rrec_load(RTile<FIRST>& T, const smx_rga_ops& o, const u32* __restrict__ kin,
+                                          const u64* __restrict__ rin, i64 base, u32 t, u32 w, u32 lane) {
+  const i64 n = o.n_ops;
+  if constexpr (FIRST) {
+#pragma unroll
+    for (int it = 0; it < RREC_ITEMS; ++it) {
+      const i64 i = rrec_event(base, w, it, lane);
+      const bool v = i < n;
+      T.list[it] = v ? o.list[i] : 0u;
+      T.op[it] = v ? o.op[i] : 0u;
+      T.value[it] = v ? o.value[i] : 0u;
+      T.anchor[it] = v ? o.anchor[i] : 0u;
+      T.t[it] = v ? o.t[i] : 0;
+      T.author[it] = v ? o.author[i] : 0u;
+      T.hi[it] = v ? o.opid_hi[i] : 0ull;
+      T.lo[it] = v ? o.opid_lo[i] : 0ull;
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < RREC_ITEMS; ++it) {
+      const i64 i = rrec_event(base, w, it, lane);
+      T.key[it] = i < n ? kin[i] : 0u;
+    }
+    // 16-byte chunks of the tile's words; an odd last word of the whole stream reads
+    // 8 bytes of the buffer's (256-byte) padding with it
+    const i64 cnt = n - base < RREC_TILE ? n - base : RREC_TILE;
+    const i64 nv = (cnt * RGA_REC + 1) / 2;
+    const v4u32* q = reinterpret_cast<const v4u32*>(rin + (u64)base * RGA_REC);
+#pragma unroll
+    for (int i = 0; i < RREC_V4; ++i) {
+      const i64 x = (i64)t + (i64)i * RR_NT;
+      T.w[i] = x < nv ? __builtin_nontemporal_load(&q[x]) : v4u32{0, 0, 0, 0};
+    }
+  }
+}
+
+// A persistent workgroup per CU walks the tiles; per tile: wave multisplit of the
+// records by digit (ranks and per-wave digit counts), block scan of the digit totals,
+// records staged in LDS in digit order, then every digit's run written contiguously
+// (RREC_TILE / 256 records per run on average: whole cache lines).  The next tile's
+// loads are issued before the current tile's runs are written, so the two overlap.
 template <bool FIRST>
 __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32* __restrict__ kin,
                                                         const u64* __restrict__ rin, u32* __restrict__ kout,
                                                         u64* __restrict__ rout, int shift,
-                                                        const u32* __restrict__ offs) {
+                                                        const u32* __restrict__ offs, i32* __restrict__ err,
+                                                        u32 ntiles) {
   __shared__ u64 srec[RREC_TILE * RGA_REC];  // 120 KB
   __shared__ u32 skey[RREC_TILE];
   __shared__ u16 spos[RREC_TILE];            // tile record -> staged slot (pass 2+)
   __shared__ u16 wc[RR_NW][RGA_NDIG];        // per-wave digit counts, then offsets
   __shared__ u32 lstart[RGA_NDIG];
   __shared__ u32 gofs[RGA_NDIG];
-  const int t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
-  const i64 n = o.n_ops, base = (i64)blockIdx.x * RREC_TILE;
-  const u32 cnt = (u32)(n - base < RREC_TILE ? n - base : RREC_TILE);
-  i32 dummy = 0;
-  for (int x = t; x < RR_NW * RGA_NDIG; x += RR_NT) (&wc[0][0])[x] = 0;
-  if (t < RGA_NDIG) gofs[t] = offs[(i64)blockIdx.x * RGA_NDIG + t];
-  __syncthreads();
+  const u32 t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
+  const i64 n = o.n_ops;
   const u64 lt = lanemask_lt();
-  u32 key[RREC_ITEMS], dr[RREC_ITEMS];
-#pragma unroll
-  for (int it = 0; it < RREC_ITEMS; ++it) {
-    const i64 i = base + (i64)w * RREC_SEG + it * WAVE + lane;
-    const bool valid = i < n;
-    key[it] = valid ? (FIRST ? rga_list_of(o, i, &dummy) : kin[i]) : 0u;
-    const u32 d = (key[it] >> shift) & 255u;
-    const u64 peers = wave_peers<8>(d, valid);
-    const u32 before = wc[w][d];
-    dr[it] = d | ((before + (u32)__popcll(peers & lt)) << 8);
-    if (valid && (peers >> lane) == 1ull) wc[w][d] = (u16)(before + (u32)__popcll(peers));
-  }
-  __syncthreads();
-  if (t < RGA_NDIG) {
-    u32 tot = 0;
-#pragma unroll
-    for (int q = 0; q < RR_NW; ++q) tot += wc[q][t];
-    lstart[t] = tot;
-  }
-  __syncthreads();
-  if (t < WAVE) {  // exclusive scan of the 256 digit totals, 4 per lane
-    u32 x[4], sum = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      x[j] = lstart[4 * t + j];
-      sum += x[j];
-    }
-    u32 run = wave_incl_sum(sum) - sum;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lstart[4 * t + j] = run;
-      run += x[j];
-    }
-  }
-  __syncthreads();
-  if (t < RGA_NDIG) {
-    u32 acc = lstart[t];
-#pragma unroll
-    for (int q = 0; q < RR_NW; ++q) {
-      const u32 c = wc[q][t];
-      wc[q][t] = (u16)acc;
-      acc += c;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int it = 0; it < RREC_ITEMS; ++it) {
-    const u32 li = (u32)(w * RREC_SEG + it * WAVE + lane);
-    const i64 i = base + li;
-    if (i >= n) continue;
-    const u32 d = dr[it] & 255u, p = wc[w][d] + (dr[it] >> 8);
-    skey[p] = key[it];
-    if (FIRST) {
-      u64* r = &srec[p * RGA_REC];
-      const u64 tt = (u64)o.t[i] ^ 0x8000000000000000ull;
-      r[0] = ((u64)o.anchor[i] << 32) | (tt >> 32);
-      r[1] = (tt << 32) | o.author[i];
-      r[2] = o.opid_hi[i];
-      r[3] = o.opid_lo[i];
-      const u32 op = o.op[i] > 2 ? 0u : o.op[i];
-      r[4] = ((u64)o.value[i] << 32) | (op << 30) | (u32)i;
-    } else {
-      spos[li] = (u16)p;
-    }
-  }
-  if (!FIRST) {
+  RTile<FIRST> T;
+  u32 tile = blockIdx.x;
+  if (tile < ntiles) rrec_load<FIRST>(T, o, kin, rin, (i64)tile * RREC_TILE, t, w, lane);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const i64 base = (i64)tile * RREC_TILE;
+    const u32 cnt = (u32)(n - base < RREC_TILE ? n - base : RREC_TILE);
+    for (int x = t; x < RR_NW * RGA_NDIG; x += RR_NT) (&wc[0][0])[x] = 0;
+    if (t < RGA_NDIG) gofs[t] = offs[(i64)tile * RGA_NDIG + t];
     __syncthreads();
-    const u64* q = rin + (u64)base * RGA_REC;
-    for (u32 x = t; x < cnt * RGA_REC; x += RR_NT) {
-      const u32 r = x / RGA_REC, k = x - r * RGA_REC;
-      srec[spos[r] * RGA_REC + k] = __builtin_nontemporal_load(&q[x]);
+    u32 key[RREC_ITEMS], dr[RREC_ITEMS];
+#pragma unroll
+    for (int it = 0; it < RREC_ITEMS; ++it) {
+      const bool valid = rrec_event(base, w, it, lane) < n;
+      if constexpr (FIRST) {
+        key[it] = T.list[it];
+        if (valid && (key[it] >= (u64)o.n_lists || T.op[it] > 2)) {
+          *err = 1;
+          key[it] = 0;
+        }
+      } else {
+        key[it] = T.key[it];
+      }
+      const u32 d = (key[it] >> shift) & 255u;
+      const u64 peers = wave_peers<8>(d, valid);
+      const u32 before = wc[w][d];
+      dr[it] = d | ((before + (u32)__popcll(peers & lt)) << 8);
+      if (valid && (peers >> lane) == 1ull) wc[w][d] = (u16)(before + (u32)__popcll(peers));
     }
-  }
-  __syncthreads();
-  for (u32 p = t; p < cnt; p += RR_NT) {
-    const u32 d = (skey[p] >> shift) & 255u;
-    kout[gofs[d] + p - lstart[d]] = skey[p];
-  }
-  for (u32 x = t; x < cnt * RGA_REC; x += RR_NT) {  // word-wise: consecutive lanes, consecutive words
-    const u32 p = x / RGA_REC, k = x - p * RGA_REC;
-    const u32 d = (skey[p] >> shift) & 255u;
-    rout[(u64)(gofs[d] + p - lstart[d]) * RGA_REC + k] = srec[x];
+    __syncthreads();
+    if (t < RGA_NDIG) {
+      u32 tot = 0;
+#pragma unroll
+      for (int q = 0; q < RR_NW; ++q) tot += wc[q][t];
+      lstart[t] = tot;
+    }
+    __syncthreads();
+    if (t < WAVE) {  // exclusive scan of the 256 digit totals, 4 per lane
+      u32 x[4], sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[j] = lstart[4 * t + j];
+        sum += x[j];
+      }
+      u32 run = wave_incl_sum(sum) - sum;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lstart[4 * t + j] = run;
+        run += x[j];
+      }
+    }
+    __syncthreads();
+    if (t < RGA_NDIG) {
+      u32 acc = lstart[t];
+#pragma unroll
+      for (int q = 0; q < RR_NW; ++q) {
+        const u32 c = wc[q][t];
+        wc[q][t] = (u16)acc;
+        acc += c;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < RREC_ITEMS; ++it) {
+      const u32 li = (u32)(w * RREC_SEG + it * WAVE + lane);
+      const i64 i = base + li;
+      if (i >= n) continue;
+      const u32 d = dr[it] & 255u, p = wc[w][d] + (dr[it] >> 8);
+      skey[p] = key[it];
+      if constexpr (FIRST) {
+        u64* r = &srec[p * RGA_REC];
+        const u64 tt = (u64)T.t[it] ^ 0x8000000000000000ull;
+        r[0] = ((u64)T.anchor[it] << 32) | (tt >> 32);
+        r[1] = (tt << 32) | T.author[it];
+        r[2] = T.hi[it];
+        r[3] = T.lo[it];
+        const u32 op = T.op[it] > 2 ? 0u : T.op[it];
+        r[4] = ((u64)T.value[it] << 32) | (op << 30) | (u32)i;
+      } else {
+        spos[li] = (u16)p;
+      }
+    }
+    if constexpr (!FIRST) {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < RREC_V4; ++i) {
+        const u32 c = t + (u32)i * RR_NT;  // words 2c, 2c + 1
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const u32 x = 2 * c + h;
+          if (x < cnt * RGA_REC) {
+            const u32 r = x / RGA_REC, k = x - r * RGA_REC;
+            srec[spos[r] * RGA_REC + k] = h ? ((u64)T.w[i].w << 32 | T.w[i].z) : ((u64)T.w[i].y << 32 | T.w[i].x);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // the next tile's loads fly while this tile's runs are written
+    if (tile + gridDim.x < ntiles) rrec_load<FIRST>(T, o, kin, rin, (i64)(tile + gridDim.x) * RREC_TILE, t, w, lane);
+#pragma unroll 1
+    for (u32 p = t; p < cnt; p += RR_NT) {
+      const u32 d = (skey[p] >> shift) & 255u;
+      kout[gofs[d] + p - lstart[d]] = skey[p];
+    }
+#pragma unroll 1
+    for (u32 x = t; x < cnt * RGA_REC; x += RR_NT) {  // word-wise: consecutive lanes, consecutive words
+      const u32 p = x / RGA_REC, k = x - p * RGA_REC;
+      const u32 d = (skey[p] >> shift) & 255u;
+      rout[(u64)(gofs[d] + p - lstart[d]) * RGA_REC + k] = srec[x];
+    }
+    __syncthreads();  // LDS is rewritten by the next tile
   }
 }
 
@@ -213,237 +293,371 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b) {
   return (u32)a[4] < (u32)b[4];  // index bits (the op bits above them are fixed per index)
 }
 
-// Bitonic sort across a 256-thread block, one (key, payload) per thread, ascending by
-// key (all-ascending network: the lower index of each pair keeps the minimum).  Stages
-// whose pairs lie within a wave exchange through cross-lane permutes; the three
-// stages that cross waves go through LDS.
-__device__ __forceinline__ void bitonic_block256(u64& key, u32& pay, u64* lk, u32* lp) {
-  const u32 i = threadIdx.x;
-#pragma unroll
-  for (u32 k = 2; k <= 256; k <<= 1) {
-#pragma unroll
-    for (u32 j = k >> 1; j > 0; j >>= 1) {
-      const u32 mask = j == (k >> 1) ? k - 1 : j;
-      u64 ok;
-      u32 op;
-      if (mask < WAVE) {
-        ok = __shfl_xor(key, (int)mask);
-        op = __shfl_xor(pay, (int)mask);
-      } else {
-        lk[i] = key;
-        lp[i] = pay;
-        __syncthreads();
-        ok = lk[i ^ mask];
-        op = lp[i ^ mask];
-        __syncthreads();
-      }
-      const bool lower = (i & j) == 0;
-      if (lower ? ok < key : key < ok) {
-        key = ok;
-        pay = op;
-      }
-    }
+// ---------------------------------------------------------------------------
+// Lists of at most RW_CAP events: one wave per list, no block barriers.  Lane x owns
+// the list's events x, x + 64, ... (K = ceil(cnt / 64) of them; the partition keeps
+// each list's events in stream order, so event position = creation order).
+//  1. value groups by an LDS hash table (CAS insert, a member chain per group);
+//  2. the lane that inserted a group's value replays the group in stream order
+//     (crdt.py:29-43);
+//  3. the survivors, compacted, ordered by key word 0 with an in-register bitonic
+//     network (DPP / swizzle lane exchanges); runs of equal word 0 are re-sorted on
+//     the rest of the key and the index (crdt.py:45-57).
+#define RW_CAP 256   // k_rga_wave; the deferred lists' kernel takes up to 2 * RW_CAP
+#define RW_WAVES 2   // lists per block
+#define RW_EMPTY 0xffffffffu
+#define RW_NIL 0xffffu
+#define RW_DEAD 0x400u
+#ifndef RW_ABL
+#define RW_ABL 0  // timing ablations (wrong results): bit0 no replay, bit1 no grouping / replay,
+                  // bit2 no key order, bit3 load only
+#endif
+
+__device__ __forceinline__ void wave_lds_sync() {  // LDS writes of this wave visible to its lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// v from lane ^ lm (lm a constant after unrolling): DPP for 1, 2, 3, 7, 15, a swizzle
+// within 32 lanes for 4, 8, 16, 31, a permute otherwise.
+__device__ __forceinline__ u32 xshfl(u32 v, u32 lm) {
+  switch (lm) {
+    case 1: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    case 2: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    case 3: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x1B, 0xF, 0xF, false);
+    case 7: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    case 15: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+    case 4: return (u32)__builtin_amdgcn_ds_swizzle((int)v, (4 << 10) | 0x1f);
+    case 8: return (u32)__builtin_amdgcn_ds_swizzle((int)v, (8 << 10) | 0x1f);
+    case 16: return (u32)__builtin_amdgcn_ds_swizzle((int)v, (16 << 10) | 0x1f);
+    case 31: return (u32)__builtin_amdgcn_ds_swizzle((int)v, (31 << 10) | 0x1f);
+    default: return (u32)__shfl_xor((int)v, (int)lm);
   }
 }
 
-// Lists of at most CAP events, one block each, everything in LDS:
-//  1. load the list's records (contiguous);
-//  2. order the events by (value, index) — block bitonic sort when CAP == NT == 256,
-//     ranking by counting for the larger tier — and let one thread per value group
-//     replay the group in stream order (crdt.py:29-43): insert creates a live element,
-//     move pops the live element with the smallest (key, index) and creates one,
-//     delete tombstones every present element;
-//  3. compact the survivors' keys (wave-aggregated) into contiguous LDS columns;
-//  4. order them by (key, index) (crdt.py:45-57): CAP == NT == 256: block bitonic sort
-//     on word 0, then each run of equal word 0 (rare) is insertion-sorted on the rest
-//     of the key and the index; larger tier: rank by counting.  Write (value, index) in
-//     list order at the list's range start; scnt[l] = survivors.
-// Grid: list l = blockIdx.x when `todo` is null, else a loop over todo[0..*ntodo).
-// Longer lists are appended to defer[] for the next kernel.
-template <int CAP, int NT>
-__global__ void __launch_bounds__(NT) k_rga_list(const u64* __restrict__ R, const u32* __restrict__ lstart, i64 n,
-                                                 i64 nl, const u32* __restrict__ todo, const u32* __restrict__ ntodo,
-                                                 u32* __restrict__ defer, u32* __restrict__ ndefer,
-                                                 u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
-                                                 u32* __restrict__ scnt) {
-  constexpr bool SMALL = CAP == 256 && NT == 256;
-  __shared__ u64 rec[CAP * RGA_REC];
-  // larger tier: (value << 30 | index) by record, then the survivors' words 0 .. 4
-  __shared__ u64 gk[SMALL ? 1 : CAP];
-  __shared__ u64 sk[4][SMALL ? 1 : CAP];
-  __shared__ u16 perm[CAP];              // (value, index) order -> record
-  __shared__ u16 surv[SMALL ? CAP : 1];  // SMALL: surviving records
-  __shared__ u64 gs[SMALL ? CAP : 1];    // SMALL: (value << 30 | index), sorted
-  __shared__ u8 st[CAP];        // bit0 present, bit1 tombstoned (by record, or by (value, index) position)
-  __shared__ u64 lk[SMALL ? 256 : 1];
-  __shared__ u32 lp[SMALL ? 256 : 1];
-  __shared__ u32 ns;
-  const u32 t = threadIdx.x, lane = t & (WAVE - 1);
-  const u64 lanes_lt = lanemask_lt();
-  const u32 nwork = todo ? *ntodo : (u32)gridDim.x;
-  for (u32 item = blockIdx.x; item < nwork; item += todo ? gridDim.x : nwork) {
-    const u32 l = todo ? todo[item] : item;
+// Ascending bitonic network (all-ascending form: the first step of each merge compares
+// e with its mirror e ^ (kk - 1)) over 64 * K (key, payload) pairs, e = k * 64 + lane;
+// the partner of (lane, k) under mask m is (lane ^ (m & 63), k ^ (m >> 6)).  Steps are
+// template-expanded so every exchange pattern is a constant.
+template <int K, u32 KK, u32 J>
+__device__ __forceinline__ void wave_bitonic_step(u64 (&key)[8], u32 (&pay)[8], u32 lane) {
+  constexpr u32 mask = J == (KK >> 1) ? KK - 1 : J;
+  constexpr u32 lm = mask & 63u, sm = mask >> 6;
+  u64 nk[K];
+  u32 np[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int src = k ^ (int)sm;
+    u64 ok = key[src];
+    u32 op = pay[src];
+    if (lm) {
+      ok = ((u64)xshfl((u32)(ok >> 32), lm) << 32) | xshfl((u32)ok, lm);
+      op = xshfl(op, lm);
+    }
+    const bool lower = (((u32)k * 64u + lane) & J) == 0;
+    const bool take = lower ? ok < key[k] : key[k] < ok;
+    nk[k] = take ? ok : key[k];
+    np[k] = take ? op : pay[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    key[k] = nk[k];
+    pay[k] = np[k];
+  }
+  if constexpr (J > 1) wave_bitonic_step<K, KK, (J >> 1)>(key, pay, lane);
+}
+
+template <int K, u32 KK = 2>
+__device__ __forceinline__ void wave_bitonic(u64 (&key)[8], u32 (&pay)[8], u32 lane) {
+  wave_bitonic_step<K, KK, (KK >> 1)>(key, pay, lane);
+  if constexpr (KK < 64u * K) wave_bitonic<K, KK * 2>(key, pay, lane);
+}
+
+template <int CAP>
+struct RwLds {
+  static constexpr int HT = 2 * CAP;  // hash slots
+  u64 w0[CAP];          // key word 0 of each event (words 1-3 stay in global memory / L2)
+  u64 w4[CAP];          // value << 32 | op << 30 | index
+  union {
+    struct {
+      u32 hkey[HT];     // the slot's value, RW_EMPTY
+      u32 hcnt[HT];     // members of the slot's group
+      u32 hbase[HT];    // first member position (exclusive scan of hcnt)
+    } h;
+    u64 gs[CAP];        // step 3: survivors' word 0, sorted
+  };
+  u16 mem[CAP];         // group members, group by group, each in event order
+  u16 gp[CAP];          // step 3: survivors' events, sorted
+  u8 st[CAP];           // bit0 present, bit1 tombstoned
+};
+
+// Event a before event b of one list in (key, index) order (crdt.py:48-57); key
+// words 1-3 from the list's records in global memory (rare: equal word 0).
+template <class LDS>
+__device__ __forceinline__ bool ev_lt(const LDS& S, const u64* __restrict__ src, u32 a, u32 b) {
+  if (S.w0[a] != S.w0[b]) return S.w0[a] < S.w0[b];
+  const u64* ka = src + (u64)a * RGA_REC;
+  const u64* kb = src + (u64)b * RGA_REC;
+  return ka[1] != kb[1] ? ka[1] < kb[1] : ka[2] != kb[2] ? ka[2] < kb[2] : ka[3] != kb[3] ? ka[3] < kb[3] : a < b;
+}
+
+// Step 3 over the survivors' (word 0, event) pairs held K2 per lane.
+template <int K2, class LDS>
+__device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, u64 (&key)[8], u32 (&pay)[8], u32 m,
+                                         u32 s0, u32 lane, u32* __restrict__ tmp_v, u32* __restrict__ tmp_s) {
+  constexpr u32 N = 64u * K2;
+  wave_bitonic<K2>(key, pay, lane);
+#pragma unroll
+  for (int k = 0; k < K2; ++k) {
+    const u32 q = (u32)k * 64u + lane;
+    S.gs[q] = key[k];
+    S.gp[q] = (u16)pay[k];
+  }
+  wave_lds_sync();
+  auto tail_lt = [&](u32 b, u32 a) {  // events b, a with equal word 0; dead ones last
+    if ((a | b) & RW_DEAD) return (a & RW_DEAD) && !(b & RW_DEAD);
+    return ev_lt(S, src, b, a);
+  };
+#pragma unroll
+  for (int k = 0; k < K2; ++k) {
+    const u32 q = (u32)k * 64u + lane;
+    if (q < m && q + 1 < N && S.gs[q + 1] == key[k] && (q == 0 || S.gs[q - 1] != key[k])) {
+      u32 e = q + 2;  // the run [q, e) of equal word 0: insertion sort on the rest
+      while (e < N && S.gs[e] == key[k]) ++e;
+      for (u32 x = q + 1; x < e; ++x) {
+        const u32 v = S.gp[x];
+        u32 y = x;
+        while (y > q && tail_lt(v, S.gp[y - 1])) {
+          S.gp[y] = S.gp[y - 1];
+          --y;
+        }
+        S.gp[y] = (u16)v;
+      }
+    }
+  }
+  wave_lds_sync();
+  for (u32 q = lane; q < m; q += WAVE) {
+    const u64 w4 = S.w4[S.gp[q] & (RW_DEAD - 1)];
+    tmp_v[s0 + q] = (u32)(w4 >> 32);
+    tmp_s[s0 + q] = (u32)w4 & RGA_IDX_MASK;
+  }
+}
+
+template <int K, int CAP>
+__device__ __forceinline__ void rga_wave_list(const u64* __restrict__ R, u32 l, u32 s0, u32 cnt, RwLds<CAP>& S, u32 lane,
+                                              u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
+                                              u32* __restrict__ scnt) {
+  const u64* src = R + (u64)s0 * RGA_REC;
+  {  // every load in flight at once; words 0 and 4 of each event to LDS
+    u64 v[RGA_REC * K];
+#pragma unroll
+    for (int i = 0; i < RGA_REC * K; ++i) {
+      const u32 x = lane + (u32)i * WAVE;
+      v[i] = x < cnt * RGA_REC ? src[x] : 0ull;
+    }
+    for (u32 t = lane; t < RwLds<CAP>::HT; t += WAVE) {
+      S.h.hkey[t] = RW_EMPTY;
+      S.h.hcnt[t] = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < RGA_REC * K; ++i) {
+      const u32 x = lane + (u32)i * WAVE;
+      const u32 e = x / RGA_REC, wd = x - e * RGA_REC;
+      if (x < cnt * RGA_REC) {
+        if (wd == 0) S.w0[e] = v[i];
+        if (wd == 4) S.w4[e] = v[i];
+      }
+    }
+  }
+  wave_lds_sync();
+  if (RW_ABL & 8) {
+    if (lane == 0) scnt[l] = (u32)S.w0[lane] & 1u;
+    return;
+  }
+  const u64 lt = lanemask_lt();
+  constexpr int HB = CAP == 256 ? 9 : 10;  // log2 of the hash slots
+  static_assert(RwLds<CAP>::HT == 1 << HB, "hash slots");
+  u32 slot[8], rk[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) slot[k] = rk[k] = 0;
+  if (RW_ABL & 2) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const u32 e = (u32)k * 64u + lane;
+      S.st[e] = e < cnt && ((u32)(S.w4[e] >> 30) & 3u) != 2;
+    }
+  } else {
+    // 1. value groups: each event's value into the hash table (CAS), its rank among
+    //    the group's events (match within the wave, running counts across slots),
+    //    then the groups laid out contiguously, each in event order
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const u32 e = (u32)k * 64u + lane;
+      S.st[e] = 0;
+      if (e < cnt) {
+        const u32 v = (u32)(S.w4[e] >> 32);
+        u32 h = (v * 0x9E3779B1u) >> (32 - HB);
+        for (;;) {
+          const u32 old = atomicCAS(&S.h.hkey[h], RW_EMPTY, v);
+          if (old == RW_EMPTY || old == v) break;
+          h = (h + 1) & (RwLds<CAP>::HT - 1);
+        }
+        slot[k] = h;
+      }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const u32 e = (u32)k * 64u + lane;
+      const bool valid = e < cnt;
+      const u64 peers = wave_peers<HB>(slot[k], valid);
+      const u32 base = valid ? S.h.hcnt[slot[k]] : 0u;
+      rk[k] = base + (u32)__popcll(peers & lt);
+      wave_lds_sync();
+      if (valid && (peers & lt) == 0) S.h.hcnt[slot[k]] = base + (u32)__popcll(peers);
+      wave_lds_sync();
+    }
+    {  // exclusive scan of the group sizes, HT / 64 slots per lane
+      constexpr int PL = RwLds<CAP>::HT / WAVE;
+      u32 c[PL], tot = 0;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) {
+        c[i] = S.h.hcnt[lane * PL + i];
+        tot += c[i];
+      }
+      u32 run = wave_incl_sum(tot) - tot;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) {
+        S.h.hbase[lane * PL + i] = run;
+        run += c[i];
+      }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const u32 e = (u32)k * 64u + lane;
+      if (e < cnt) S.mem[S.h.hbase[slot[k]] + rk[k]] = (u16)e;
+    }
+    wave_lds_sync();
+    // 2. the group's first event's lane replays the group in event order (crdt.py:29-43)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const u32 e = (u32)k * 64u + lane;
+      if (e >= cnt || rk[k] != 0) continue;
+      const u32 b = S.h.hbase[slot[k]], c = S.h.hcnt[slot[k]];
+      if (c == 1 || (RW_ABL & 1)) {
+        S.st[e] = ((u32)(S.w4[e] >> 30) & 3u) != 2;
+        continue;
+      }
+      for (u32 i = 0; i < c; ++i) {
+        const u32 x = S.mem[b + i];
+        const u32 op = (u32)(S.w4[x] >> 30) & 3u;
+        if (op == 2) {  // delete: every present element is tombstoned; creates nothing
+          for (u32 j = 0; j < i; ++j) {
+            const u32 y = S.mem[b + j];
+            if (S.st[y] & 1) S.st[y] |= 2;
+          }
+          continue;
+        }
+        if (op == 1) {  // move: pops the live element first in list order
+          u32 best = RW_NIL;
+          for (u32 j = 0; j < i; ++j) {
+            const u32 y = S.mem[b + j];
+            if (S.st[y] == 1 && (best == RW_NIL || ev_lt(S, src, y, best))) best = y;
+          }
+          if (best != RW_NIL) S.st[best] = 0;
+        }
+        S.st[x] = 1;
+      }
+    }
+  }
+  wave_lds_sync();
+  // 3. survivors (event order) -> K2 (word 0, event) pairs per lane, ordered by key
+  u32 m = 0;
+  u64 key[8];
+  u32 pay[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    key[k] = ~0ull;
+    pay[k] = RW_DEAD;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const u32 e = (u32)k * 64u + lane;
+    const bool live = e < cnt && S.st[e] == 1;
+    const u64 ball = __ballot(live);
+    if (live) S.gp[m + (u32)__popcll(ball & lt)] = (u16)e;
+    m += (u32)__popcll(ball);
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const u32 a = (u32)k * 64u + lane;
+    if (a < m) {
+      pay[k] = S.gp[a];
+      key[k] = S.w0[pay[k]];
+    }
+  }
+  wave_lds_sync();  // gp / the hash table are rewritten below
+  if (RW_ABL & 4) {
+    for (u32 q = lane; q < m; q += WAVE) {
+      const u64 w4 = S.w4[S.gp[q]];
+      tmp_v[s0 + q] = (u32)(w4 >> 32);
+      tmp_s[s0 + q] = (u32)w4 & RGA_IDX_MASK;
+    }
+  } else if (m <= 64) {
+    rw_order<1>(S, src, key, pay, m, s0, lane, tmp_v, tmp_s);
+  } else if (m <= 128) {
+    rw_order<2>(S, src, key, pay, m, s0, lane, tmp_v, tmp_s);
+  } else if (K <= 4 || m <= 256) {
+    rw_order<(K <= 4 ? K : 4)>(S, src, key, pay, m, s0, lane, tmp_v, tmp_s);
+  } else {
+    rw_order<8>(S, src, key, pay, m, s0, lane, tmp_v, tmp_s);
+  }
+  if (lane == 0) scnt[l] = m;
+}
+
+__global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave(const u64* __restrict__ R, const u32* __restrict__ lstart,
+                                                             i64 n, i64 nl, u32* __restrict__ defer,
+                                                             u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
+                                                             u32* __restrict__ tmp_s, u32* __restrict__ scnt) {
+  __shared__ RwLds<RW_CAP> lds[RW_WAVES];
+  const u32 lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const u32 l = blockIdx.x * RW_WAVES + w;
+  if (l >= (u64)nl) return;
+  const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
+  if (cnt > RW_CAP) {
+    if (lane == 0) defer[atomicAdd(ndefer, 1u)] = l;
+    return;
+  }
+  if (cnt <= 64)
+    rga_wave_list<1>(R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+  else if (cnt <= 128)
+    rga_wave_list<2>(R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+  else
+    rga_wave_list<4>(R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+}
+
+// The deferred lists of RW_CAP + 1 .. 2 * RW_CAP events: the same wave per list with
+// twice the slots; longer ones go on to k_rga_big.
+__global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(const u64* __restrict__ R, const u32* __restrict__ lstart,
+                                                              i64 n, i64 nl, const u32* __restrict__ todo,
+                                                              const u32* __restrict__ ntodo, u32* __restrict__ defer,
+                                                              u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
+                                                              u32* __restrict__ tmp_s, u32* __restrict__ scnt) {
+  __shared__ RwLds<2 * RW_CAP> lds[RW_WAVES];
+  const u32 lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const u32 nt = *ntodo;
+  for (u32 i = blockIdx.x * RW_WAVES + w; i < nt; i += gridDim.x * RW_WAVES) {
+    const u32 l = todo[i];
     const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
-    if (cnt > (u32)CAP) {
-      if (t == 0) defer[atomicAdd(ndefer, 1u)] = l;
+    if (cnt > 2 * RW_CAP) {
+      if (lane == 0) defer[atomicAdd(ndefer, 1u)] = l;
       continue;
     }
-    __syncthreads();  // the previous list's LDS reads are done
-    if (t == 0) ns = 0;
-    for (u32 w = t; w < cnt * RGA_REC; w += NT) rec[w] = R[(u64)s0 * RGA_REC + w];
-    __syncthreads();
-    // survivor: record position when SMALL, else (value, index) position -> perm
-    if constexpr (SMALL) {  // (value, index) order by a block bitonic sort; gk, perm by position
-      u64 key = ~0ull;
-      u32 pay = t;
-      if (t < cnt) {
-        const u64 w4 = rec[t * RGA_REC + 4];
-        key = ((w4 >> 32) << 30) | (w4 & RGA_IDX_MASK);
-      }
-      bitonic_block256(key, pay, lk, lp);
-      gs[t] = key;
-      perm[t] = (u16)pay;
-      st[t] = 0;
-      __syncthreads();
-#if RGA_ABL & 1
-      if (t < cnt) st[t] = t % 3 != 0;
-      if (0)
-#endif
-      if (t < cnt && (t == 0 || (gs[t - 1] >> 30) != (key >> 30))) {  // group head: replay in stream order
-        const u64 v = key >> 30;
-        u32 end = t + 1;
-        while (end < cnt && (gs[end] >> 30) == v) ++end;
-        for (u32 x = t; x < end; ++x) {
-          const u32 op = (u32)(rec[perm[x] * RGA_REC + 4] >> 30) & 3u;
-          if (op == 2) {
-            for (u32 y = t; y < x; ++y)
-              if (st[y] & 1) st[y] |= 2;
-            continue;  // a delete creates nothing
-          }
-          if (op == 1) {
-            int best = -1;
-            for (u32 y = t; y < x; ++y)
-              if (st[y] == 1 && (best < 0 || rec_lt(&rec[perm[y] * RGA_REC], &rec[perm[best] * RGA_REC])))
-                best = (int)y;
-            if (best >= 0) st[best] = 0;
-          }
-          st[x] = 1;
-        }
-      }
-    } else {
-      for (u32 i = t; i < cnt; i += NT) {
-        const u64 w4 = rec[i * RGA_REC + 4];
-        gk[i] = ((w4 >> 32) << 30) | (w4 & RGA_IDX_MASK);
-        st[i] = 0;
-      }
-      __syncthreads();
-      for (u32 i = t; i < cnt; i += NT) {
-        const u64 k = gk[i];
-        u32 r = 0, j = 0;
-        for (; j + 4 <= cnt; j += 4) r += (gk[j] < k) + (gk[j + 1] < k) + (gk[j + 2] < k) + (gk[j + 3] < k);
-        for (; j < cnt; ++j) r += gk[j] < k;
-        perm[r] = (u16)i;
-      }
-      __syncthreads();
-      for (u32 j = t; j < cnt; j += NT) {
-        const u64 v = gk[perm[j]] >> 30;
-        if (j != 0 && (gk[perm[j - 1]] >> 30) == v) continue;
-        u32 end = j + 1;
-        while (end < cnt && (gk[perm[end]] >> 30) == v) ++end;
-        for (u32 x = j; x < end; ++x) {
-          const u32 op = (u32)(rec[perm[x] * RGA_REC + 4] >> 30) & 3u;
-          if (op == 2) {
-            for (u32 y = j; y < x; ++y)
-              if (st[y] & 1) st[y] |= 2;
-            continue;
-          }
-          if (op == 1) {
-            int best = -1;
-            for (u32 y = j; y < x; ++y)
-              if (st[y] == 1 && (best < 0 || rec_lt(&rec[perm[y] * RGA_REC], &rec[perm[best] * RGA_REC])))
-                best = (int)y;
-            if (best >= 0) st[best] = 0;
-          }
-          st[x] = 1;
-        }
-      }
-    }
-    __syncthreads();
-    for (u32 j0 = 0; j0 < cnt; j0 += NT) {
-      const u32 j = j0 + t;
-      const bool live = j < cnt && st[j] == 1;
-      const u64 ball = __ballot(live);
-      u32 got = 0;
-      if (lane == 0 && ball) got = atomicAdd(&ns, (u32)__popcll(ball));
-      const u32 base = __shfl(got, 0);
-      if (live) {
-        const u32 a = base + (u32)__popcll(ball & lanes_lt);
-        if constexpr (SMALL) {
-          surv[a] = perm[j];
-        } else {
-          const u32 p = perm[j];
-          gk[a] = rec[p * RGA_REC];
-          sk[0][a] = rec[p * RGA_REC + 1];
-          sk[1][a] = rec[p * RGA_REC + 2];
-          sk[2][a] = rec[p * RGA_REC + 3];
-          sk[3][a] = rec[p * RGA_REC + 4];
-        }
-      }
-    }
-    __syncthreads();
-    const u32 m = ns;
-    if constexpr (SMALL) {
-      // survivors a, b (record positions) that tie on word 0: the rest of the key, the index
-      auto tail_lt = [&](u32 b, u32 a) {
-        const u64* ka = &rec[a * RGA_REC];
-        const u64* kb = &rec[b * RGA_REC];
-        const u32 ia = (u32)ka[4] & RGA_IDX_MASK, ib = (u32)kb[4] & RGA_IDX_MASK;
-        return kb[1] != ka[1] ? kb[1] < ka[1] : kb[2] != ka[2] ? kb[2] < ka[2] : kb[3] != ka[3] ? kb[3] < ka[3] : ib < ia;
-      };
-      u32 pay = t < m ? surv[t] : 0u;
-      u64 key = t < m ? rec[pay * RGA_REC] : ~0ull;
-      if (!(RGA_ABL & 2)) bitonic_block256(key, pay, lk, lp);
-      lk[t] = key;
-      lp[t] = pay;
-      __syncthreads();
-      if (t < m && t + 1 < m && lk[t + 1] == key && (t == 0 || lk[t - 1] != key)) {
-        u32 e = t + 2;  // run [t, e) of equal word 0: insertion sort on the rest
-        while (e < m && lk[e] == key) ++e;
-        for (u32 x = t + 1; x < e; ++x) {
-          const u32 v = lp[x];
-          u32 y = x;
-          while (y > t && tail_lt(v, lp[y - 1])) {
-            lp[y] = lp[y - 1];
-            --y;
-          }
-          lp[y] = v;
-        }
-      }
-      __syncthreads();
-      if (t < m) {
-        const u64 w4 = rec[lp[t] * RGA_REC + 4];
-        tmp_v[s0 + t] = (u32)(w4 >> 32);
-        tmp_s[s0 + t] = (u32)w4 & RGA_IDX_MASK;
-      }
-    } else {
-      auto tail_lt = [&](u32 b, u32 a) {
-        const u64 a1 = sk[0][a], b1 = sk[0][b], a2 = sk[1][a], b2 = sk[1][b], a3 = sk[2][a], b3 = sk[2][b];
-        const u32 ia = (u32)sk[3][a] & RGA_IDX_MASK, ib = (u32)sk[3][b] & RGA_IDX_MASK;
-        return b1 != a1 ? b1 < a1 : b2 != a2 ? b2 < a2 : b3 != a3 ? b3 < a3 : ib < ia;
-      };
-      for (u32 a = t; a < m; a += NT) {
-        const u64 k0 = gk[a];
-        u32 r = 0;
-        for (u32 b = 0; b < m; ++b) {
-          const u64 x = gk[b];
-          r += x < k0 || (x == k0 && b != a && tail_lt(b, a));
-        }
-        const u64 w4 = sk[3][a];
-        tmp_v[s0 + r] = (u32)(w4 >> 32);
-        tmp_s[s0 + r] = (u32)w4 & RGA_IDX_MASK;
-      }
-    }
-    if (t == 0) scnt[l] = m;
+    rga_wave_list<8>(R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+    wave_lds_sync();  // the next list reuses the slice
   }
 }
 
@@ -471,7 +685,7 @@ __device__ void block_sort_positions(u32* p, u32 cnt, Less less) {
   }
 }
 
-// Lists longer than RGA_MID: the same replay from global memory, one block per list
+// Lists longer than 2 * RW_CAP: the same replay from global memory, one block per list
 // (such lists are rare — a whole file's history in one list).  Per list, in its
 // record range: gp = positions sorted by (value, index), bst = state by that order;
 // then the survivors' positions sorted by (key, index).
@@ -560,6 +774,8 @@ __global__ void k_rga_fin(const u32* __restrict__ soff_total, i64 n_lists, smx_r
   out.counts[0] = *soff_total;
 }
 
+static int g_rr_grid = 0;  // persistent scatter grid (CUs of the device)
+
 static bool o_ok(const smx_rga_ops* o) {
   return o->list && o->op && o->value && o->anchor && o->t && o->author && o->opid_hi && o->opid_lo;
 }
@@ -637,6 +853,12 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   const int grid = (int)(SMX_CEIL_DIV(n, (i64)BLOCK) < 8192 ? SMX_CEIL_DIV(n, (i64)BLOCK) : 8192);
 
   RGA_TRY(hipMemsetAsync(err, 0, 32, st));
+  if (g_rr_grid == 0) {  // one persistent scatter workgroup per CU
+    int dev = 0, cus = 0;
+    RGA_TRY(hipGetDevice(&dev));
+    RGA_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    g_rr_grid = cus > 0 ? cus : 256;
+  }
   {  // records grouped by list: LSD passes over the list id, ping-pong into rec
     int npass = 1;
     while (npass < 4 && ((u64)(nl - 1) >> (8 * npass)) != 0) ++npass;
@@ -652,18 +874,19 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
         hipLaunchKernelGGL(k_rrec_hist<false>, dim3(nblk), dim3(BLOCK), 0, st, o, kbuf[(p - 1) & 1], 8 * p, rhist,
                            err);
       hscan(rhist, nblk, 256u, tsum, dstart, st);
+      const int sgrid = nblk < g_rr_grid ? nblk : g_rr_grid;
       if (p == 0)
-        hipLaunchKernelGGL(k_rrec_scatter<true>, dim3(nblk), dim3(RR_NT), 0, st, o, nullptr, nullptr, kbuf[0],
-                           rbuf[0], 0, rhist);
+        hipLaunchKernelGGL(k_rrec_scatter<true>, dim3(sgrid), dim3(RR_NT), 0, st, o, nullptr, nullptr, kbuf[0],
+                           rbuf[0], 0, rhist, err, (u32)nblk);
       else
-        hipLaunchKernelGGL(k_rrec_scatter<false>, dim3(nblk), dim3(RR_NT), 0, st, o, kbuf[(p - 1) & 1],
-                           rbuf[(p - 1) & 1], kbuf[p & 1], rbuf[p & 1], 8 * p, rhist);
+        hipLaunchKernelGGL(k_rrec_scatter<false>, dim3(sgrid), dim3(RR_NT), 0, st, o, kbuf[(p - 1) & 1],
+                           rbuf[(p - 1) & 1], kbuf[p & 1], rbuf[p & 1], 8 * p, rhist, err, (u32)nblk);
     }
     hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, kbuf[(npass - 1) & 1], n, nl, lstart);
   }
-  hipLaunchKernelGGL((k_rga_list<RGA_SMALL, 256>), dim3(nl), dim3(256), 0, st, rec, lstart, n, nl, nullptr, nullptr,
-                     def1, ndef, tmp_v, tmp_s, scnt);
-  hipLaunchKernelGGL((k_rga_list<RGA_MID, 512>), dim3(512), dim3(512), 0, st, rec, lstart, n, nl, def1, ndef, def2,
+  hipLaunchKernelGGL(k_rga_wave, dim3(SMX_CEIL_DIV(nl, (i64)RW_WAVES)), dim3(WAVE * RW_WAVES), 0, st, rec, lstart, n,
+                     nl, def1, ndef, tmp_v, tmp_s, scnt);
+  hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, rec, lstart, n, nl, def1, ndef, def2,
                      ndef + 1, tmp_v, tmp_s, scnt);
   hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
                      tmp_s, scnt);

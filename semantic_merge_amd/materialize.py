@@ -98,6 +98,24 @@ def smx_host_ctor_mode(cls: type, names: Tuple[str, ...]) -> int:
     return 2 if cls.__dataclass_params__.frozen else 1
 
 
+_REF_DR = None
+
+
+def conflict_factory():
+    """The reference's own ``conflict_divergent_rename`` (semmerge/conflict.py:34-49) when
+    the reference package is importable -- so callers get its ``Conflict`` class back --
+    else this package's restatement (conflict.py here, same fields and payload)."""
+    global _REF_DR
+    if _REF_DR is None:
+        try:
+            from semmerge.conflict import conflict_divergent_rename as f
+        except ImportError:
+            f = divergent_rename
+        _REF_DR = f
+    return _REF_DR
+
+
 def materialize_conflicts(ops: Sequence[Any], pairs: np.ndarray) -> List[Any]:
     """``pairs`` is an (n, 2) array of (A source index, B source index) in walk order."""
-    return [divergent_rename(ops[a], ops[b]) for a, b in pairs.tolist()]
+    make = conflict_factory()
+    return [make(ops[a], ops[b]) for a, b in pairs.tolist()]
