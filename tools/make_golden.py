@@ -248,12 +248,68 @@ def make_rga_cases(crdt, n_cases: int, seed: int):
     return cases
 
 
+# ---------------------------------------------------------------------------
+# OpLog.from_json cases (ops.py:106-121): JSON texts of op dicts with the coercions
+# Op.from_dict applies (ops.py:89-100), and the reference's decoded ops -- or the
+# exception class it raises.
+def make_oplog_cases(ops_mod, n_cases: int, seed: int):
+    rng = random.Random(seed)
+    cases = []
+    for c in range(n_cases):
+        pool = []
+        syms = ["s0", "s1", "sé"]
+        items = [rand_op(rng, "iso" if c % 2 else "any", ["uuid", "short", "long"][c % 3], syms, pool)
+                 for _ in range(rng.choice([0, 1, 2, 5, 9]))]
+        for d in items:
+            r = rng.random()
+            if r < 0.1:
+                d["schemaVersion"] = rng.choice(["2", 3.0, True, "7"])
+            elif r < 0.2:
+                del d["schemaVersion"]
+            elif r < 0.3:
+                d["id"] = rng.choice([123, 4.5, True, None, "ü-id"])
+            for k in ("params", "guards", "effects", "provenance"):
+                if rng.random() < 0.08:
+                    del d[k]
+            if rng.random() < 0.1 and "params" in d:
+                d["params"]["unicode"] = "naïve ☃ \U0001f600"
+                d["params"]["float"] = rng.choice([0.1, -2.5e-8, 1e300, 12345678901234567])
+        bad = None
+        if c % 10 == 9 and items:  # malformed input: the reference's exception
+            bad = rng.choice(["type", "target", "symbolId", "schemaVersion", "id"])
+            d = items[0]
+            if bad == "type":
+                del d["type"]
+            elif bad == "target":
+                del d["target"]
+            elif bad == "symbolId":
+                d["target"] = {"addressId": "x"}
+            elif bad == "schemaVersion":
+                d["schemaVersion"] = "v1"
+            else:
+                del d["id"]
+        text = json.dumps(items, ensure_ascii=rng.random() < 0.5,
+                          separators=rng.choice([(",", ":"), (", ", ": ")]),
+                          indent=rng.choice([None, None, 2]))
+        try:
+            log = ops_mod.OpLog.from_json(text)
+            cases.append({"text": text, "ops": [o.to_dict() for o in log.ops]})
+        except Exception as e:  # noqa: BLE001 - the class name is the fixture
+            cases.append({"text": text, "error": type(e).__name__})
+    return cases
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
+    ap.add_argument("--only", choices=["oplog"], help="regenerate one fixture file only")
     args = ap.parse_args()
     compose, crdt, ops_mod = _import_reference()
     os.makedirs(GOLD, exist_ok=True)
+    with open(os.path.join(GOLD, "oplog_cases.json"), "w") as fh:
+        json.dump(make_oplog_cases(ops_mod, 300, seed=112), fh, separators=(",", ":"), ensure_ascii=False)
+    if args.only == "oplog":
+        return
 
     cases = make_cases(compose, ops_mod, 600, seed=20251114)
     with open(os.path.join(GOLD, "compose_cases.json"), "w") as fh:

@@ -7,7 +7,7 @@ OUT=${1:-$R/gpurun_out/pmc}
 mkdir -p "$OUT"
 make -s -C tools || exit 1
 cd /tmp && export TMPDIR=/tmp
-RX='k_window_f|k_emit|k_tb_scatter|k_tb_reduce|k_flags|k_calib'
+RX='k_window_f|k_emit|k_tb_scatter|k_tb_reduce|k_calib'
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \

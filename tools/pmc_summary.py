@@ -22,7 +22,7 @@ def load(dirs):
                 short = name.split("(")[0].split("<")[0].strip()
                 if short.startswith("void "):
                     short = short[5:]
-                if "k_calib_read" in name or "k_calib_write" in name:
+                if "k_calib_read" in name or "k_calib_write" in name or "k_calib_gather" in name:
                     short = name.split("(")[0].strip()
                 vals[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return vals
@@ -43,6 +43,11 @@ def main():
             cal["w4"] = cs["WRITE_SIZE"] * 1024 / CALIB_BYTES
         if k.startswith("void k_calib_write<uint4") and "WRITE_SIZE" in cs:
             cal["w16"] = cs["WRITE_SIZE"] * 1024 / CALIB_BYTES
+        for tag, name in (("0", "g8_8MB"), ("1", "g8_1GB")):  # 2^25 random 8-B gathers
+            if k.startswith("void k_calib_gather<" + tag) and "FETCH_SIZE" in cs:
+                cal[name] = cs["FETCH_SIZE"] * 1024 / (8 << 25)
+            if k.startswith("void k_calib_gather<" + tag) and "TCC_MISS_sum" in cs:
+                cal[name + "_miss_per_gather"] = cs["TCC_MISS_sum"] / (1 << 25)
     out["calibration_counter_per_byte"] = cal
     win = out["kernels"].get("k_window_f", {})
     if "FETCH_SIZE" in win and "WRITE_SIZE" in win and cal:
