@@ -18,7 +18,9 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 namespace {
@@ -203,93 +205,80 @@ struct Interner {  // value -> dense id, first-seen order
 
 // ---------------------------------------------------------------- marshal
 
-// marshal_ops(ops, kind_rank, unknown, kmove, krename, default_ts, eq_key,
-//             kind, ts, hi, lo, sym, v0, v1)
-//   -> (n_sym, strings, ts_ok, id_mode, ts_strs | None, ids | None)
-// ts_ok False: ts_strs holds every timestamp string for the rank encoder.
-// id_mode 0 UUID, 1 packed, -1: ids holds every id for the Python encoder.
-PyObject* marshal_ops(PyObject*, PyObject* args) {
-  PyObject *ops, *kind_rank, *default_ts, *eq_key;
+// One op at a time into growing SoA columns (marshal.py; compose.py:16-18 sort key,
+// :64-82 chain values).
+struct Marshaler {
+  PyObject *kind_rank, *default_ts, *eq_key;
   int unknown, kmove, krename;
-  PyObject *okind, *ots, *ohi, *olo, *osym, *ov0, *ov1;
-  if (!PyArg_ParseTuple(args, "O!O!iiiUOOOOOOOO", &PyList_Type, &ops, &PyDict_Type, &kind_rank, &unknown,
-                        &kmove, &krename, &default_ts, &eq_key, &okind, &ots, &ohi, &olo, &osym, &ov0, &ov1))
-    return nullptr;
-  const Py_ssize_t n = PyList_GET_SIZE(ops);
-  Buf bk, bts, bhi, blo, bsym, bv0, bv1;
-  if (!get_buf(okind, bk, 1, n, true, "kind") || !get_buf(ots, bts, 8, n, true, "ts") ||
-      !get_buf(ohi, bhi, 8, n, true, "oid_hi") || !get_buf(olo, blo, 8, n, true, "oid_lo") ||
-      !get_buf(osym, bsym, 4, n, true, "sym") || !get_buf(ov0, bv0, 4, n, true, "v0") ||
-      !get_buf(ov1, bv1, 4, n, true, "v1"))
-    return nullptr;
-  auto* kind = (uint8_t*)bk.v.buf;
-  auto* ts = (uint64_t*)bts.v.buf;
-  auto* hi = (uint64_t*)bhi.v.buf;
-  auto* lo = (uint64_t*)blo.v.buf;
-  auto* sym = (uint32_t*)bsym.v.buf;
-  auto* v0 = (int32_t*)bv0.v.buf;
-  auto* v1 = (int32_t*)bv1.v.buf;
-
   Interner syms, strings, eq;
-  if (!syms.init(false) || !strings.init(true) || !eq.init(false)) return nullptr;
-  Ref ts_list(PyList_New(n)), id_list(PyList_New(n));
-  if (!ts_list || !id_list) return nullptr;
+  std::vector<uint8_t> kind;
+  std::vector<uint64_t> ts, hi, lo;
+  std::vector<uint32_t> sym;
+  std::vector<int32_t> v0, v1;
+  Ref ts_list, id_list;
   bool ts_ok = true, all_uuid = true;
 
-  auto sid = [&](PyObject* v, int32_t* dst) -> bool {  // strings[str(v)]
+  bool init() {
+    ts_list.reset(PyList_New(0));
+    id_list.reset(PyList_New(0));
+    return syms.init(false) && strings.init(true) && eq.init(false) && ts_list && id_list;
+  }
+  bool sid(PyObject* v, int32_t* dst) {  // strings[str(v)]
     Ref s(PyObject_Str(v));
     if (!s) return false;
     const long long id = strings(s.p);
     if (id < 0) return false;
     *dst = (int32_t)id;
     return true;
-  };
-
-  for (Py_ssize_t k = 0; k < n; ++k) {
-    PyObject* op = PyList_GET_ITEM(ops, k);
+  }
+  bool add(PyObject* op) {
+    const size_t k = kind.size();
+    kind.push_back(0);
+    ts.push_back(0);
+    hi.push_back(0);
+    lo.push_back(0);
+    sym.push_back(0);
+    v0.push_back(-1);
+    v1.push_back(-1);
     // precedence.get(op.type, 99) (compose.py:18)
     Ref type(PyObject_GetAttr(op, N.type));
-    if (!type) return nullptr;
+    if (!type) return false;
     PyObject* r = PyDict_GetItemWithError(kind_rank, type.p);
-    if (!r && PyErr_Occurred()) return nullptr;
+    if (!r && PyErr_Occurred()) return false;
     const int kr = r ? (int)PyLong_AsLong(r) : unknown;
     kind[k] = (uint8_t)kr;
     // str(op.provenance.get("timestamp", "1970-01-01T00:00:00Z")) (compose.py:17)
     Ref prov(PyObject_GetAttr(op, N.provenance));
-    if (!prov) return nullptr;
+    if (!prov) return false;
     Ref tso(map_get(prov.p, N.timestamp, default_ts));
-    if (!tso) return nullptr;
-    PyObject* tss = PyObject_Str(tso.p);
-    if (!tss) return nullptr;
-    PyList_SET_ITEM(ts_list.p, k, tss);
-    if (ts_ok && !iso_key(tss, &ts[k])) ts_ok = false;
+    if (!tso) return false;
+    Ref tss(PyObject_Str(tso.p));
+    if (!tss || PyList_Append(ts_list.p, tss.p) < 0) return false;
+    if (ts_ok && !iso_key(tss.p, &ts[k])) ts_ok = false;
     // op.id (compose.py:18)
-    PyObject* id = PyObject_GetAttr(op, N.id);
-    if (!id) return nullptr;
-    PyList_SET_ITEM(id_list.p, k, id);
-    if (all_uuid && !uuid_key(id, &hi[k], &lo[k])) all_uuid = false;
+    Ref id(PyObject_GetAttr(op, N.id));
+    if (!id || PyList_Append(id_list.p, id.p) < 0) return false;
+    if (all_uuid && !uuid_key(id.p, &hi[k], &lo[k])) all_uuid = false;
     // target.symbolId: dict key / == (compose.py:33,64)
     Ref tgt(PyObject_GetAttr(op, N.target));
-    if (!tgt) return nullptr;
+    if (!tgt) return false;
     Ref s(PyObject_GetAttr(tgt.p, N.symbolId));
-    if (!s) return nullptr;
+    if (!s) return false;
     const long long si = syms(s.p);
-    if (si < 0) return nullptr;
+    if (si < 0) return false;
     sym[k] = (uint32_t)si;
-    v0[k] = -1;
-    v1[k] = -1;
-    if (kr != kmove && kr != krename) continue;
+    if (kr != kmove && kr != krename) return true;
     Ref params(PyObject_GetAttr(op, N.params));
-    if (!params) return nullptr;
+    if (!params) return false;
     if (kr == krename) {  // newName: '!=' class (compose.py:66) and str(newName) (compose.py:72)
       Ref name(map_get(params.p, N.newName, Py_None));
-      if (!name) return nullptr;
+      if (!name) return false;
       bool nan = false;
       if (PyFloat_CheckExact(name.p)) {
         nan = std::isnan(PyFloat_AS_DOUBLE(name.p));
       } else if (PyFloat_Check(name.p)) {
         const int ne = PyObject_RichCompareBool(name.p, name.p, Py_NE);
-        if (ne < 0) return nullptr;
+        if (ne < 0) return false;
         nan = ne == 1;
       }
       if (nan) {
@@ -301,40 +290,83 @@ PyObject* marshal_ops(PyObject*, PyObject* args) {
           key.reset(name.p);
         } else {
           key.reset(PyObject_CallOneArg(eq_key, name.p));
-          if (!key) return nullptr;
+          if (!key) return false;
         }
         const long long c = eq(key.p);
-        if (c < 0) return nullptr;
+        if (c < 0) return false;
         v0[k] = (int32_t)c;
       }
-      if (!sid(name.p, &v1[k])) return nullptr;
-    } else {  // moves: str(newAddress), str(newFile or file) (compose.py:75-82)
-      Ref addr(map_get(params.p, N.newAddress, Py_None));
-      if (!addr) return nullptr;
-      if (addr.p != Py_None && !sid(addr.p, &v0[k])) return nullptr;
-      Ref nfile(map_get(params.p, N.newFile, Py_None));
-      if (!nfile) return nullptr;
-      const int truthy = PyObject_IsTrue(nfile.p);
-      if (truthy < 0) return nullptr;
-      if (!truthy) {
-        nfile.reset(map_get(params.p, N.file, Py_None));
-        if (!nfile) return nullptr;
+      return sid(name.p, &v1[k]);
+    }
+    // moves: str(newAddress), str(newFile or file) (compose.py:75-82)
+    Ref addr(map_get(params.p, N.newAddress, Py_None));
+    if (!addr) return false;
+    if (addr.p != Py_None && !sid(addr.p, &v0[k])) return false;
+    Ref nfile(map_get(params.p, N.newFile, Py_None));
+    if (!nfile) return false;
+    const int truthy = PyObject_IsTrue(nfile.p);
+    if (truthy < 0) return false;
+    if (!truthy) {
+      nfile.reset(map_get(params.p, N.file, Py_None));
+      if (!nfile) return false;
+    }
+    if (nfile.p != Py_None && !sid(nfile.p, &v1[k])) return false;
+    return true;
+  }
+  // (n_sym, strings, ts_ok, id_mode, ts_strs | None, ids | None)
+  PyObject* summary() {
+    const Py_ssize_t n = (Py_ssize_t)kind.size();
+    int id_mode = 0;
+    if (!all_uuid) {
+      id_mode = 1;
+      for (Py_ssize_t k = 0; k < n && id_mode == 1; ++k) {
+        const int p = packed_key(PyList_GET_ITEM(id_list.p, k), &hi[k], &lo[k]);
+        if (p != 1) id_mode = -1;
       }
-      if (nfile.p != Py_None && !sid(nfile.p, &v1[k])) return nullptr;
     }
+    const Py_ssize_t n_sym = PyDict_GET_SIZE(syms.map);
+    return Py_BuildValue("nOOiOO", n_sym, strings.list, ts_ok ? Py_True : Py_False, id_mode,
+                         ts_ok ? Py_None : ts_list.p, id_mode >= 0 ? Py_None : id_list.p);
   }
+};
 
-  int id_mode = 0;
-  if (!all_uuid) {
-    id_mode = 1;
-    for (Py_ssize_t k = 0; k < n && id_mode == 1; ++k) {
-      const int p = packed_key(PyList_GET_ITEM(id_list.p, k), &hi[k], &lo[k]);
-      if (p != 1) id_mode = -1;
-    }
-  }
-  const Py_ssize_t n_sym = PyDict_GET_SIZE(syms.map);
-  return Py_BuildValue("nOOiOO", n_sym, strings.list, ts_ok ? Py_True : Py_False, id_mode,
-                       ts_ok ? Py_None : ts_list.p, id_mode >= 0 ? Py_None : id_list.p);
+template <typename T>
+bool copy_col(const std::vector<T>& v, PyObject* o, const char* what) {
+  Buf b;
+  if (!get_buf(o, b, sizeof(T), (Py_ssize_t)v.size(), true, what)) return false;
+  if (!v.empty()) std::memcpy(b.v.buf, v.data(), v.size() * sizeof(T));
+  return true;
+}
+
+bool parse_marshal_args(PyObject* args, PyObject** ops, Marshaler& M, PyObject** cols) {
+  return PyArg_ParseTuple(args, "O!O!iiiUOOOOOOOO", &PyList_Type, ops, &PyDict_Type, &M.kind_rank, &M.unknown,
+                          &M.kmove, &M.krename, &M.default_ts, &M.eq_key, &cols[0], &cols[1], &cols[2], &cols[3],
+                          &cols[4], &cols[5], &cols[6]);
+}
+
+bool store_cols(const Marshaler& M, PyObject** cols) {
+  return copy_col(M.kind, cols[0], "kind") && copy_col(M.ts, cols[1], "ts") && copy_col(M.hi, cols[2], "oid_hi") &&
+         copy_col(M.lo, cols[3], "oid_lo") && copy_col(M.sym, cols[4], "sym") && copy_col(M.v0, cols[5], "v0") &&
+         copy_col(M.v1, cols[6], "v1");
+}
+
+// marshal_ops(ops, kind_rank, unknown, kmove, krename, default_ts, eq_key,
+//             kind, ts, hi, lo, sym, v0, v1)
+//   -> (n_sym, strings, ts_ok, id_mode, ts_strs | None, ids | None)
+// ts_ok False: ts_strs holds every timestamp string for the rank encoder.
+// id_mode 0 UUID, 1 packed, -1: ids holds every id for the Python encoder.
+PyObject* marshal_ops(PyObject*, PyObject* args) {
+  PyObject* ops;
+  PyObject* cols[7];
+  Marshaler M;
+  if (!parse_marshal_args(args, &ops, M, cols) || !M.init()) return nullptr;
+  const Py_ssize_t n = PyList_GET_SIZE(ops);
+  M.kind.reserve(n);
+  for (Py_ssize_t k = 0; k < n; ++k)
+    if (!M.add(PyList_GET_ITEM(ops, k))) return nullptr;
+  Ref sum(M.summary());  // (packs the short ids into hi / lo)
+  if (!sum || !store_cols(M, cols)) return nullptr;
+  return sum.release();
 }
 
 // ---------------------------------------------------------------- deepcopy of JSON trees
@@ -569,10 +601,73 @@ PyObject* dict_of(PyObject* x) {
   return PyObject_CallOneArg((PyObject*)&PyDict_Type, x);
 }
 
-// ops_from_dicts(items, op_cls, target_cls, ctor_mode) -> List[Op]: Op.from_dict of every
-// item (ops.py:89-100), in the same evaluation order and with the same coercions:
+// Op.from_dict(d) (ops.py:89-100) in the same evaluation order and with the same
+// coercions (new reference):
 //   id=str(d["id"]), schemaVersion=int(d.get("schemaVersion", 1)), type=d["type"],
 //   target=Target(**d["target"]), params/guards/effects/provenance=dict(d.get(k, {}))
+PyObject* op_from_dict(PyObject* d, Ctor& ctor, PyObject* op_cls, PyObject* tcls, PyObject* one) {
+  PyObject* const k4[4] = {N.params, N.guards, N.effects, N.provenance};
+  Ref id_raw(PyObject_GetItem(d, N.id));
+  if (!id_raw) return nullptr;
+  Ref id(PyObject_Str(id_raw.p));
+  if (!id) return nullptr;
+  Ref sv_raw(map_get(d, N.schemaVersion, one));
+  if (!sv_raw) return nullptr;
+  Ref sv(PyNumber_Long(sv_raw.p));
+  if (!sv) return nullptr;
+  Ref ty(PyObject_GetItem(d, N.type));
+  if (!ty) return nullptr;
+  Ref tg_raw(PyObject_GetItem(d, N.target));
+  if (!tg_raw) return nullptr;
+  Ref tg;
+  {  // Target(**target): the plain-dataclass fast path needs exactly symbolId and addressId
+    PyObject *sym = nullptr, *addr = nullptr;
+    if (PyDict_CheckExact(tg_raw.p) && PyDict_GET_SIZE(tg_raw.p) == 2) {
+      sym = PyDict_GetItemWithError(tg_raw.p, N.symbolId);
+      if (!sym && PyErr_Occurred()) return nullptr;
+      addr = sym ? PyDict_GetItemWithError(tg_raw.p, N.addressId) : nullptr;
+      if (!addr && PyErr_Occurred()) return nullptr;
+    }
+    const int mode = sym && addr ? ctor.mode((PyTypeObject*)tcls, N.kw_target) : 0;
+    if (mode < 0) return nullptr;
+    if (mode > 0) {
+      PyObject* a[2] = {sym, addr};
+      tg.reset(ctor.make((PyTypeObject*)tcls, a, N.kw_target));
+    } else {
+      Ref kw(PyDict_New());
+      if (!kw) return nullptr;
+      if (PyDict_Update(kw.p, tg_raw.p) < 0) {  // `**` of a non-mapping: the same TypeError text
+        if (PyErr_ExceptionMatches(PyExc_AttributeError)) {
+          PyErr_Clear();
+          PyErr_Format(PyExc_TypeError, "%.200s() argument after ** must be a mapping, not %.200s",
+                       ((PyTypeObject*)tcls)->tp_name, Py_TYPE(tg_raw.p)->tp_name);
+        }
+        return nullptr;
+      }
+      tg.reset(PyObject_Call(tcls, N.empty, kw.p));
+    }
+    if (!tg) return nullptr;
+  }
+  Ref vals[4];
+  for (int q = 0; q < 4; ++q) {  // dict(d.get(k, {}))
+    if (PyDict_CheckExact(d)) {
+      PyObject* v = PyDict_GetItemWithError(d, k4[q]);
+      if (!v && PyErr_Occurred()) return nullptr;
+      vals[q].reset(v ? dict_of(v) : PyDict_New());
+    } else {
+      Ref dflt(PyDict_New());
+      if (!dflt) return nullptr;
+      Ref raw(PyObject_CallMethodObjArgs(d, N.get, k4[q], dflt.p, nullptr));
+      if (!raw) return nullptr;
+      vals[q].reset(dict_of(raw.p));
+    }
+    if (!vals[q]) return nullptr;
+  }
+  PyObject* a8[8] = {id.p, sv.p, ty.p, tg.p, vals[0].p, vals[1].p, vals[2].p, vals[3].p};
+  return ctor.make((PyTypeObject*)op_cls, a8, N.kw_op);
+}
+
+// ops_from_dicts(items, op_cls, target_cls, ctor_mode) -> List[Op]: Op.from_dict of every item.
 PyObject* ops_from_dicts(PyObject*, PyObject* args) {
   PyObject *items, *op_cls, *tcls;
   Ctor ctor;
@@ -585,71 +680,383 @@ PyObject* ops_from_dicts(PyObject*, PyObject* args) {
   if (!one) return nullptr;
   Ref out(PyList_New(n));
   if (!out) return nullptr;
-  PyObject* const keys4[4] = {N.params, N.guards, N.effects, N.provenance};
   for (Py_ssize_t k = 0; k < n; ++k) {
-    PyObject* d = PyList_GET_ITEM(items, k);
-    Ref id_raw(PyObject_GetItem(d, N.id));
-    if (!id_raw) return nullptr;
-    Ref id(PyObject_Str(id_raw.p));
-    if (!id) return nullptr;
-    Ref sv_raw(map_get(d, N.schemaVersion, one.p));
-    if (!sv_raw) return nullptr;
-    Ref sv(PyNumber_Long(sv_raw.p));
-    if (!sv) return nullptr;
-    Ref ty(PyObject_GetItem(d, N.type));
-    if (!ty) return nullptr;
-    Ref tg_raw(PyObject_GetItem(d, N.target));
-    if (!tg_raw) return nullptr;
-    Ref tg;
-    {  // Target(**target): the plain-dataclass fast path needs exactly symbolId and addressId
-      PyObject *sym = nullptr, *addr = nullptr;
-      if (PyDict_CheckExact(tg_raw.p) && PyDict_GET_SIZE(tg_raw.p) == 2) {
-        sym = PyDict_GetItemWithError(tg_raw.p, N.symbolId);
-        if (!sym && PyErr_Occurred()) return nullptr;
-        addr = sym ? PyDict_GetItemWithError(tg_raw.p, N.addressId) : nullptr;
-        if (!addr && PyErr_Occurred()) return nullptr;
-      }
-      const int mode = sym && addr ? ctor.mode((PyTypeObject*)tcls, N.kw_target) : 0;
-      if (mode < 0) return nullptr;
-      if (mode > 0) {
-        PyObject* a[2] = {sym, addr};
-        tg.reset(ctor.make((PyTypeObject*)tcls, a, N.kw_target));
-      } else {
-        Ref kw(PyDict_New());
-        if (!kw) return nullptr;
-        if (PyDict_Update(kw.p, tg_raw.p) < 0) {  // `**` of a non-mapping: the same TypeError text
-          if (PyErr_ExceptionMatches(PyExc_AttributeError)) {
-            PyErr_Clear();
-            PyErr_Format(PyExc_TypeError, "%.200s() argument after ** must be a mapping, not %.200s",
-                         ((PyTypeObject*)tcls)->tp_name, Py_TYPE(tg_raw.p)->tp_name);
-          }
-          return nullptr;
-        }
-        tg.reset(PyObject_Call(tcls, N.empty, kw.p));
-      }
-      if (!tg) return nullptr;
-    }
-    Ref vals[4];
-    for (int q = 0; q < 4; ++q) {  // dict(d.get(k, {}))
-      if (PyDict_CheckExact(d)) {
-        PyObject* v = PyDict_GetItemWithError(d, keys4[q]);
-        if (!v && PyErr_Occurred()) return nullptr;
-        vals[q].reset(v ? dict_of(v) : PyDict_New());
-      } else {
-        Ref dflt(PyDict_New());
-        if (!dflt) return nullptr;
-        Ref raw(PyObject_CallMethodObjArgs(d, N.get, keys4[q], dflt.p, nullptr));
-        if (!raw) return nullptr;
-        vals[q].reset(dict_of(raw.p));
-      }
-      if (!vals[q]) return nullptr;
-    }
-    PyObject* a8[8] = {id.p, sv.p, ty.p, tg.p, vals[0].p, vals[1].p, vals[2].p, vals[3].p};
-    PyObject* op = ctor.make((PyTypeObject*)op_cls, a8, N.kw_op);
+    PyObject* op = op_from_dict(PyList_GET_ITEM(items, k), ctor, op_cls, tcls, one.p);
     if (!op) return nullptr;
     PyList_SET_ITEM(out.p, k, op);
   }
   return out.release();
+}
+
+// ---------------------------------------------------------------- JSON (ops.py:112-118)
+
+// A strict JSON reader with the standard json module's results (dict / list / str /
+// int / float / True / False / None; duplicate keys: the last wins; big integers
+// exact; float(token) for the rest) and orjson's input rules: NaN / Infinity rejected,
+// no control characters inside strings, nesting up to 1024, nothing after the value.
+struct JsonReader {
+  const char* p;
+  const char* b;
+  const char* e;
+  PyObject* memo;  // key strings seen so far (json's memo)
+  int depth = 0;
+  // raw key text (no escapes, <= 32 bytes) -> its str: one object per distinct key
+  // without building a str per occurrence
+  struct KeySlot {
+    const char* s = nullptr;
+    int n = 0;
+    PyObject* k = nullptr;  // borrowed from memo
+  };
+  KeySlot keys[256];
+
+  PyObject* key() {  // p at the opening quote; new reference
+    const char* s0 = p + 1;
+    const char* q = s0;
+    while (q < e && q - s0 <= 32 && *q != '"' && *q != '\\' && (unsigned char)*q >= 0x20) ++q;
+    if (q < e && *q == '"' && q - s0 <= 32) {
+      const int n = (int)(q - s0);
+      uint32_t h = 2166136261u;
+      for (int i = 0; i < n; ++i) h = (h ^ (unsigned char)s0[i]) * 16777619u;
+      for (int probe = 0; probe < 8; ++probe) {
+        KeySlot& ks = keys[(h + probe) & 255];
+        if (ks.k && ks.n == n && std::memcmp(ks.s, s0, (size_t)n) == 0) {
+          p = q + 1;
+          Py_INCREF(ks.k);
+          return ks.k;
+        }
+        if (!ks.k) {
+          Ref k(string());
+          if (!k) return nullptr;
+          PyObject* m = PyDict_SetDefault(memo, k.p, k.p);
+          if (!m) return nullptr;
+          ks.s = s0;
+          ks.n = n;
+          ks.k = m;
+          Py_INCREF(m);
+          return m;
+        }
+      }
+    }
+    Ref k(string());
+    if (!k) return nullptr;
+    PyObject* m = PyDict_SetDefault(memo, k.p, k.p);  // one object per key text
+    if (!m) return nullptr;
+    Py_INCREF(m);
+    return m;
+  }
+
+  bool fail(const char* what) {
+    if (!PyErr_Occurred())
+      PyErr_Format(PyExc_ValueError, "JSON decode error: %s at offset %zd", what, (Py_ssize_t)(p - b));
+    return false;
+  }
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+  static int hex4(const char* q) {
+    int v = 0;
+    for (int i = 0; i < 4; ++i) {
+      const int h = hexval((unsigned char)(q[i] | ((q[i] >= 'A' && q[i] <= 'F') ? 0x20 : 0)));
+      if (h < 0) return -1;
+      v = v << 4 | h;
+    }
+    return v;
+  }
+  PyObject* string() {  // p at the opening quote
+    ++p;
+    const char* s0 = p;
+    bool esc = false;
+    while (p < e && *p != '"') {
+      const unsigned char c = (unsigned char)*p;
+      if (c < 0x20) return fail("control character in string"), nullptr;
+      if (c == '\\') {
+        esc = true;
+        if (++p >= e) break;
+      }
+      ++p;
+    }
+    if (p >= e) return fail("unterminated string"), nullptr;
+    const char* s1 = p++;
+    if (!esc) return PyUnicode_DecodeUTF8(s0, s1 - s0, "strict");
+    std::vector<Py_UCS4> u;
+    u.reserve((size_t)(s1 - s0));
+    for (const char* q = s0; q < s1;) {
+      const unsigned char c = (unsigned char)*q;
+      if (c == '\\') {
+        const char x = q[1];
+        q += 2;
+        switch (x) {
+          case '"': u.push_back('"'); break;
+          case '\\': u.push_back('\\'); break;
+          case '/': u.push_back('/'); break;
+          case 'b': u.push_back('\b'); break;
+          case 'f': u.push_back('\f'); break;
+          case 'n': u.push_back('\n'); break;
+          case 'r': u.push_back('\r'); break;
+          case 't': u.push_back('\t'); break;
+          case 'u': {
+            if (s1 - q < 4) return p = q, fail("truncated \\u escape"), nullptr;
+            int cp = hex4(q);
+            if (cp < 0) return p = q, fail("invalid \\u escape"), nullptr;
+            q += 4;
+            if (cp >= 0xD800 && cp <= 0xDBFF && s1 - q >= 6 && q[0] == '\\' && q[1] == 'u') {
+              const int lo2 = hex4(q + 2);  // a surrogate pair (json pairs them; a lone one stays)
+              if (lo2 >= 0xDC00 && lo2 <= 0xDFFF) {
+                cp = 0x10000 + ((cp - 0xD800) << 10) + (lo2 - 0xDC00);
+                q += 6;
+              }
+            }
+            u.push_back((Py_UCS4)cp);
+            break;
+          }
+          default:
+            return p = q - 1, fail("invalid escape"), nullptr;
+        }
+        continue;
+      }
+      // one UTF-8 sequence (validated by the decoder)
+      int len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+      if (!len || q + len > s1) return p = q, fail("invalid UTF-8"), nullptr;
+      Ref one_cp(PyUnicode_DecodeUTF8(q, len, "strict"));
+      if (!one_cp) return nullptr;
+      u.push_back(PyUnicode_READ_CHAR(one_cp.p, 0));
+      q += len;
+    }
+    return PyUnicode_FromKindAndData(PyUnicode_4BYTE_KIND, u.data(), (Py_ssize_t)u.size());
+  }
+  PyObject* number() {
+    const char* s0 = p;
+    bool isf = false;
+    if (p < e && *p == '-') ++p;
+    if (p < e && *p == '0') {
+      ++p;
+    } else if (p < e && *p >= '1' && *p <= '9') {
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+    } else {
+      return fail("invalid number"), nullptr;
+    }
+    if (p < e && *p == '.') {
+      isf = true;
+      ++p;
+      if (!(p < e && *p >= '0' && *p <= '9')) return fail("invalid number"), nullptr;
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+    }
+    if (p < e && (*p == 'e' || *p == 'E')) {
+      isf = true;
+      ++p;
+      if (p < e && (*p == '+' || *p == '-')) ++p;
+      if (!(p < e && *p >= '0' && *p <= '9')) return fail("invalid number"), nullptr;
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+    }
+    const size_t len = (size_t)(p - s0);
+    if (!isf && len <= 18) {  // fits int64: digits straight from the text
+      long long v = 0;
+      const char* q = s0 + (*s0 == '-');
+      for (; q < p; ++q) v = v * 10 + (*q - '0');
+      return PyLong_FromLongLong(*s0 == '-' ? -v : v);
+    }
+    std::string tok(s0, len);
+    if (isf) {
+      const double v = PyOS_string_to_double(tok.c_str(), nullptr, nullptr);
+      if (v == -1.0 && PyErr_Occurred()) return nullptr;
+      return PyFloat_FromDouble(v);
+    }
+    return PyLong_FromString(tok.c_str(), nullptr, 10);
+  }
+  bool lit(const char* w) {
+    const size_t n = std::strlen(w);
+    if ((size_t)(e - p) >= n && std::memcmp(p, w, n) == 0) {
+      p += n;
+      return true;
+    }
+    return false;
+  }
+  PyObject* value() {
+    ws();
+    if (p >= e) return fail("unexpected end"), nullptr;
+    switch (*p) {
+      case '{': {
+        if (++depth > 1024) return fail("nesting too deep"), nullptr;
+        ++p;
+        Ref d(PyDict_New());
+        if (!d) return nullptr;
+        ws();
+        if (p < e && *p == '}') {
+          ++p;
+          --depth;
+          return d.release();
+        }
+        for (;;) {
+          ws();
+          if (p >= e || *p != '"') return fail("expected a key"), nullptr;
+          Ref k(key());
+          if (!k) return nullptr;
+          ws();
+          if (p >= e || *p != ':') return fail("expected ':'"), nullptr;
+          ++p;
+          Ref v(value());
+          if (!v || PyDict_SetItem(d.p, k.p, v.p) < 0) return nullptr;
+          ws();
+          if (p < e && *p == ',') {
+            ++p;
+            continue;
+          }
+          if (p < e && *p == '}') {
+            ++p;
+            break;
+          }
+          return fail("expected ',' or '}'"), nullptr;
+        }
+        --depth;
+        return d.release();
+      }
+      case '[': {
+        if (++depth > 1024) return fail("nesting too deep"), nullptr;
+        ++p;
+        Ref l(PyList_New(0));
+        if (!l) return nullptr;
+        ws();
+        if (p < e && *p == ']') {
+          ++p;
+          --depth;
+          return l.release();
+        }
+        for (;;) {
+          Ref v(value());
+          if (!v || PyList_Append(l.p, v.p) < 0) return nullptr;
+          ws();
+          if (p < e && *p == ',') {
+            ++p;
+            continue;
+          }
+          if (p < e && *p == ']') {
+            ++p;
+            break;
+          }
+          return fail("expected ',' or ']'"), nullptr;
+        }
+        --depth;
+        return l.release();
+      }
+      case '"':
+        return string();
+      case 't':
+        if (lit("true")) Py_RETURN_TRUE;
+        break;
+      case 'f':
+        if (lit("false")) Py_RETURN_FALSE;
+        break;
+      case 'n':
+        if (lit("null")) Py_RETURN_NONE;
+        break;
+      case 'N':
+      case 'I':
+        return fail("NaN / Infinity are not JSON"), nullptr;
+      default:
+        if (*p == '-' && p + 1 < e && p[1] == 'I') return fail("NaN / Infinity are not JSON"), nullptr;
+        if (*p == '-' || (*p >= '0' && *p <= '9')) return number();
+    }
+    return fail("unexpected character"), nullptr;
+  }
+  PyObject* document() {
+    Ref v(value());
+    if (!v) return nullptr;
+    ws();
+    if (p != e) return fail("extra data"), nullptr;
+    return v.release();
+  }
+};
+
+// UTF-8 view of a str / bytes-like argument (bytes are taken as UTF-8).
+bool utf8_of(PyObject* x, Ref& hold, const char** s, Py_ssize_t* n) {
+  if (PyUnicode_Check(x)) {
+    *s = PyUnicode_AsUTF8AndSize(x, n);
+    return *s != nullptr;
+  }
+  hold.reset(PyBytes_FromObject(x));
+  if (!hold) return false;
+  *s = PyBytes_AS_STRING(hold.p);
+  *n = PyBytes_GET_SIZE(hold.p);
+  return true;
+}
+
+PyObject* json_loads(PyObject*, PyObject* x) {
+  GcPause gc_pause;
+  Ref hold, memo(PyDict_New());
+  const char* s;
+  Py_ssize_t n;
+  if (!memo || !utf8_of(x, hold, &s, &n)) return nullptr;
+  JsonReader R{s, s, s + n, memo.p};
+  return R.document();
+}
+
+// decode_oplogs(texts, op_cls, target_cls, ctor_mode, kind_rank, unknown, kmove, krename,
+//               default_ts, eq_key)
+//   -> (per-text op lists, marshal summary (as marshal_ops), kind, ts, hi, lo, sym, v0, v1)
+// OpLog.from_json of each text (ops.py:116-118) and the compose SoA of all of them
+// together (marshal_ops over the concatenation) in one pass: each parsed op object
+// is built and marshalled before the next is read.
+PyObject* decode_oplogs(PyObject*, PyObject* args) {
+  PyObject *texts, *op_cls, *tcls;
+  Ctor ctor;
+  Marshaler M;
+  if (!PyArg_ParseTuple(args, "O!O!O!OO!iiiUO", &PyTuple_Type, &texts, &PyType_Type, &op_cls, &PyType_Type, &tcls,
+                        &ctor.mode_fn, &PyDict_Type, &M.kind_rank, &M.unknown, &M.kmove, &M.krename,
+                        &M.default_ts, &M.eq_key) ||
+      !M.init())
+    return nullptr;
+  GcPause gc_pause;
+  Ref one(PyLong_FromLong(1)), lists(PyTuple_New(PyTuple_GET_SIZE(texts)));
+  if (!one || !lists) return nullptr;
+  for (Py_ssize_t t = 0; t < PyTuple_GET_SIZE(texts); ++t) {
+    Ref hold, memo(PyDict_New());
+    const char* s;
+    Py_ssize_t n;
+    if (!memo || !utf8_of(PyTuple_GET_ITEM(texts, t), hold, &s, &n)) return nullptr;
+    JsonReader R{s, s, s + n, memo.p};
+    Ref out(PyList_New(0));
+    if (!out) return nullptr;
+    R.ws();
+    if (R.p < R.e && *R.p == '[') {  // the usual document: ops decoded as they are read
+      ++R.p;
+      R.ws();
+      bool first = true;
+      while (!(R.p < R.e && *R.p == ']')) {
+        if (!first) {
+          if (!(R.p < R.e && *R.p == ',')) return R.fail("expected ',' or ']'"), nullptr;
+          ++R.p;
+        }
+        first = false;
+        Ref item(R.value());
+        if (!item) return nullptr;
+        Ref op(op_from_dict(item.p, ctor, op_cls, tcls, one.p));
+        if (!op || !M.add(op.p) || PyList_Append(out.p, op.p) < 0) return nullptr;
+        R.ws();
+      }
+      ++R.p;
+      R.ws();
+      if (R.p != R.e) return R.fail("extra data"), nullptr;
+    } else {  // any other document: iterate it as the reference's list comprehension does
+      Ref doc(R.document());
+      if (!doc) return nullptr;
+      Ref it(PyObject_GetIter(doc.p));
+      if (!it) return nullptr;
+      while (PyObject* raw = PyIter_Next(it.p)) {
+        Ref item(raw);
+        Ref op(op_from_dict(item.p, ctor, op_cls, tcls, one.p));
+        if (!op || !M.add(op.p) || PyList_Append(out.p, op.p) < 0) return nullptr;
+      }
+      if (PyErr_Occurred()) return nullptr;
+    }
+    PyTuple_SET_ITEM(lists.p, t, out.release());
+  }
+  Ref sum(M.summary());
+  if (!sum) return nullptr;
+  auto col = [](const void* d, size_t bytes) { return PyByteArray_FromStringAndSize((const char*)d, (Py_ssize_t)bytes); };
+  return Py_BuildValue("OONNNNNNN", lists.p, sum.p, col(M.kind.data(), M.kind.size()),
+                       col(M.ts.data(), M.ts.size() * 8), col(M.hi.data(), M.hi.size() * 8),
+                       col(M.lo.data(), M.lo.size() * 8), col(M.sym.data(), M.sym.size() * 4),
+                       col(M.v0.data(), M.v0.size() * 4), col(M.v1.data(), M.v1.size() * 4));
 }
 
 PyMethodDef methods[] = {
@@ -657,6 +1064,8 @@ PyMethodDef methods[] = {
     {"marshal_ops", marshal_ops, METH_VARARGS, "List[Op] -> SoA columns (see marshal.py)."},
     {"materialize_ops", materialize_ops, METH_VARARGS, "device results -> List[Op] (see materialize.py)."},
     {"deep_copy", py_deep_copy, METH_VARARGS, "copy.deepcopy with a native JSON-tree path."},
+    {"json_loads", json_loads, METH_O, "strict JSON -> Python objects (orjson's input rules)."},
+    {"decode_oplogs", decode_oplogs, METH_VARARGS, "OpLog.from_json of each text + their compose SoA."},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef module = {PyModuleDef_HEAD_INIT, "_smx_host", "Native host marshal / materialise.", -1, methods};

@@ -12,6 +12,10 @@ the input side of compose.
   orjson itself when it is importable, the standard json module held to those rules
   when it is not; ``from_json`` decodes through ``ops_from_dicts``.
 * ``oplog_from_json(text)`` is ``OpLog.from_json(text).ops``.
+* ``decode_pair(text_a, text_b)`` is both ``OpLog.from_json`` calls plus the compose SoA
+  of their ops (``marshal.marshal_native``) in one native pass over the texts
+  (the wire format straight into SoA); ``compose_json`` runs the
+  drop-in compose on it.
 * ``ops_from_worker_result(result)`` is what ``TSWorker.build_and_diff`` does with the
   worker's JSON-RPC result (``semmerge/lang/ts/bridge.py:36-40``).
 
@@ -78,13 +82,19 @@ def _reject_constant(name: str):
 
 
 def loads(data: Any) -> Any:
-    """``orjson.loads(data)`` (ops.py:117): str or bytes, NaN / Infinity rejected."""
+    """``orjson.loads(data)`` (ops.py:117): str or bytes, NaN / Infinity rejected.
+    Without orjson: the native strict reader (csrc/smx_host.cpp JsonReader; the json
+    module's results), or the json module for str the reader cannot view as UTF-8
+    (lone surrogates)."""
     oj = _orjson()
     if oj is not None:
         return oj.loads(data)
-    if isinstance(data, (bytes, bytearray, memoryview)):
-        data = bytes(data).decode("utf-8")
-    return json.loads(data, parse_constant=_reject_constant)
+    if isinstance(data, str):
+        try:
+            data.encode("utf-8")
+        except UnicodeEncodeError:
+            return json.loads(data, parse_constant=_reject_constant)
+    return host().json_loads(data)
 
 
 @dataclass
@@ -106,6 +116,47 @@ class OpLog:
 
 def oplog_from_json(data: Any, op_cls: type = Op, target_cls: type = Target) -> List[Any]:
     return OpLog.from_json(data, op_cls, target_cls).ops
+
+
+def decode_pair(text_a: Any, text_b: Any, op_cls: type = Op, target_cls: type = Target):
+    """(ops_a, ops_b, soa): ``OpLog.from_json`` of both branch logs and the compose SoA
+    of ``ops_a + ops_b`` (equal to ``marshal_native(ops_a, ops_b)``), in one pass."""
+    import numpy as np
+    from .marshal import (DEFAULT_TIMESTAMP, SoA, TS_ISO, _encode_ids, _encode_ts, eq_key)
+    from .ops import KIND_MOVE, KIND_RANK, KIND_RENAME, KIND_UNKNOWN
+    if _orjson() is not None:  # orjson's own reader decides what parses
+        from .marshal import marshal_native
+        ops_a = OpLog.from_json(text_a, op_cls, target_cls).ops
+        ops_b = OpLog.from_json(text_b, op_cls, target_cls).ops
+        return ops_a, ops_b, marshal_native(ops_a, ops_b)
+    (ops_a, ops_b), summ, kind, ts, hi, lo, sym, v0, v1 = host().decode_oplogs(
+        (text_a, text_b), op_cls, target_cls, smx_host_ctor_mode, KIND_RANK, KIND_UNKNOWN, KIND_MOVE,
+        KIND_RENAME, DEFAULT_TIMESTAMP, eq_key)
+    n_sym, strings, ts_ok, id_mode, ts_str, ids = summ
+    kind = np.frombuffer(kind, np.uint8)
+    ts = np.frombuffer(ts, np.uint64)
+    hi, lo = np.frombuffer(hi, np.uint64), np.frombuffer(lo, np.uint64)
+    ts_mode = TS_ISO
+    if not ts_ok:
+        ts_mode, ts = _encode_ts(ts_str)
+    if id_mode < 0:
+        id_mode, hi, lo = _encode_ids(ids)
+    soa = SoA(len(ops_a), len(ops_b), kind, ts, hi, lo, np.frombuffer(sym, np.uint32),
+              np.frombuffer(v0, np.int32), np.frombuffer(v1, np.int32), max(n_sym, 1), strings, ts_mode,
+              id_mode)
+    return ops_a, ops_b, soa
+
+
+def compose_json(text_a: Any, text_b: Any, op_cls: type = Op, target_cls: type = Target):
+    """compose_oplogs(OpLog.from_json(text_a).ops, OpLog.from_json(text_b).ops) with the
+    decode and the marshal fused (decode_pair)."""
+    from ._lib import compose_soa
+    from .materialize import materialize_conflicts, materialize_ops_native
+    ops_a, ops_b, soa = decode_pair(text_a, text_b, op_cls, target_cls)
+    order, addr, file, ctx, pairs = compose_soa(soa)
+    ops = ops_a + ops_b
+    return materialize_ops_native(ops, soa.kind, soa.strings, order, addr, file, ctx), \
+        materialize_conflicts(ops, pairs)
 
 
 def ops_from_worker_result(result: Dict[str, Any], op_cls: type = Op,

@@ -1,5 +1,7 @@
 set -o pipefail
-O=gpurun_out/r02x; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_compose.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 1000 bash tools/pmc_passes.sh $PWD/$O/pmc > $O/pmc.log 2>&1; rc=$?; tail -8 $O/pmc.log; [ $rc -eq 0 ] || exit $rc
-python3 -c "import json; d=json.load(open('$O/pmc/summary.json')); print(json.dumps(d['calibration_counter_per_byte']))"
+O=gpurun_out/r02y; mkdir -p $O
+R=$PWD
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err; rc=$?; tail -3 $O/bench.err; cat $O/bench.json; [ $rc -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o p -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-pmc --no-e2e > $R/$O/prof.log 2>&1; rc=$?; [ $rc -eq 0 ] || { tail -5 $R/$O/prof.log; exit $rc; }
+cd $R && python3 tools/prof_export.py $O/prof $O/kernel_stats.csv && head -12 $O/kernel_stats.csv | cut -c1-150

@@ -6,6 +6,8 @@ shape: a synthetic two-branch lift log), split into its host and device parts.
 Legs (seconds, median of --reps):
   python_from_dict / native_from_dicts  decoding the worker's op dicts into Op objects
                                         (Op.from_dict per op vs oplog.ops_from_dicts)
+  json_python / json_native_pair        both branch logs' JSON texts -> Op lists + SoA: json.loads +
+                                        Op.from_dict + marshal vs oplog.decode_pair (one native pass)
   python_marshal / python_materialize   the Python restatement (marshal.py, materialize.py)
   native_marshal / native_materialize   csrc/smx_host.cpp (what compose_oplogs runs)
   gpu_compose                           compose_soa on cuda:0, SoA already on the host (--gpu),
@@ -75,6 +77,13 @@ def one(a, n_ops):
     assert na_ == oa and nb_ == ob
     del na_, nb_
     ops = oa + ob
+    ta, tb = json.dumps(A), json.dumps(B)
+    res["json_python"], _ = timed(lambda: marshal([Op.from_dict(d) for d in json.loads(ta)],
+                                                  [Op.from_dict(d) for d in json.loads(tb)]), reps)
+    from semantic_merge_amd.oplog import decode_pair
+    res["json_native_pair"], (ja, jb, jsoa) = timed(lambda: decode_pair(ta, tb), reps)
+    assert ja == oa and jb == ob
+    del ja, jb, jsoa
 
     res["python_marshal"], soa = timed(lambda: marshal(oa, ob), reps)
     res["native_marshal"], soa_n = timed(lambda: marshal_native(oa, ob), reps)
