@@ -192,3 +192,17 @@ def test_long_same_symbol_chain_is_linear(interleave):
     dt = time.perf_counter() - t0
     _eq_soa(got, ref, f"chain interleave={interleave}")
     assert dt < 1.0, f"{dt:.3f} s for 200k chained renames"
+
+
+def test_compose_json_matches_dropin():
+    """oplog.compose_json (JSON texts -> one-pass decode + SoA -> GPU -> Op objects)
+    equals compose_oplogs on OpLog.from_json's ops, on the reference's own cases."""
+    import json
+    from semantic_merge_amd.oplog import OpLog, compose_json
+    for i, case in enumerate(load("compose_cases.json")[:120]):
+        ta, tb = json.dumps(case["A"]), json.dumps(case["B"])
+        out, conf = compose_json(ta, tb)
+        assert [o.to_dict() for o in out] == case["out"], f"case {i}"
+        assert [c.to_dict() for c in conf] == case["conflicts"], f"case {i}"
+        ref = compose_oplogs(OpLog.from_json(ta).ops, OpLog.from_json(tb).ops)
+        assert [o.to_dict() for o in ref[0]] == case["out"]

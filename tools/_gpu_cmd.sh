@@ -1,7 +1,4 @@
 set -o pipefail
-O=gpurun_out/r02y; mkdir -p $O
-R=$PWD
-timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err; rc=$?; tail -3 $O/bench.err; cat $O/bench.json; [ $rc -eq 0 ] || exit $rc
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o p -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-pmc --no-e2e > $R/$O/prof.log 2>&1; rc=$?; [ $rc -eq 0 ] || { tail -5 $R/$O/prof.log; exit $rc; }
-cd $R && python3 tools/prof_export.py $O/prof $O/kernel_stats.csv && head -12 $O/kernel_stats.csv | cut -c1-150
+O=gpurun_out/r02z; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?; grep -E "PASSED|FAILED|ERROR" $O/tests.log | tail -80; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1; rc=$?; tail -2 $O/smoke.txt; exit $rc
