@@ -299,16 +299,104 @@ def make_oplog_cases(ops_mod, n_cases: int, seed: int):
     return cases
 
 
+# ---------------------------------------------------------------------------
+# applier cases (applier.py:14-104): a base tree, an op sequence, and the reference's
+# merged tree (or the exception it raised, with the tree as it left it).  Paths stay
+# inside the tree (no "..": the reference would write outside its temp directory).
+def _tree(root):
+    files, dirs = {}, []
+    for dp, dn, fn in os.walk(root):
+        rel = os.path.relpath(dp, root)
+        if rel != ".":
+            dirs.append(rel)
+        for f in fn:
+            with open(os.path.join(dp, f), "rb") as fh:
+                files[os.path.normpath(os.path.join(rel, f))] = fh.read().decode("latin-1")
+    return files, sorted(dirs)
+
+
+def make_applier_cases(applier_mod, ops_mod, n_cases: int, seed: int):
+    import shutil
+    import tempfile
+    rng = random.Random(seed)
+    names = ["foo", "bar", "a.b", "$x", "x1", "foo_bar", "élan", "if", "Foo", "o"]
+    paths = ["src/a.ts", "src/b.ts", "lib/c.ts", "d.ts", "src/deep/e.ts", "/abs/src/a.ts"]
+    cases = []
+    for c in range(n_cases):
+        base = {}
+        for pth in ("src/a.ts", "src/b.ts", "lib/c.ts", "d.ts"):
+            if rng.random() < 0.85:
+                words = [rng.choice(names + ["import x from 'y';", "(", ")", ".", "=", "1"])
+                         for _ in range(rng.randint(0, 40))]
+                text = " ".join(words)
+                if rng.random() < 0.2:
+                    text = text.replace(" ", "\r\n", 3)
+                base[pth] = text
+        ops = []
+        for k in range(rng.randint(0, 14)):
+            t = rng.choice(["renameSymbol"] * 5 + ["modifyImport"] * 2 + ["moveDecl"] * 2 + ["moveFile", "addDecl"])
+            params = {}
+            if t == "renameSymbol":
+                params = {"file": rng.choice(paths + [None, ""]), "oldName": rng.choice(names + [None]),
+                          "newName": rng.choice(names + ["\\g<0>!", "n\\n", None, 7])}
+                if rng.random() < 0.2:
+                    params["newFile"] = rng.choice(paths)
+            elif t == "modifyImport":
+                params = {"file": rng.choice(paths), "oldImport": rng.choice(["'y'", "x", None]),
+                          "newImport": rng.choice(["'z'", "w", None])}
+            elif t == "moveDecl":
+                params = {"oldFile": rng.choice(paths + [None]), "newFile": rng.choice(paths + ["src/new/f.ts"]),
+                          "file": rng.choice(paths + [None])}
+            elif t == "moveFile":
+                params = {"oldPath": rng.choice(paths + ["src", "lib"]),
+                          "newPath": rng.choice(paths + ["moved", "src/deep", "lib2/c.ts"])}
+            ops.append({"id": f"op{c}-{k}", "type": t, "target": {"symbolId": "s", "addressId": None},
+                        "params": params})
+        tmp = tempfile.mkdtemp(prefix="smx_gold_")
+        try:
+            for pth, text in base.items():
+                full = os.path.join(tmp, "base", pth)
+                os.makedirs(os.path.dirname(full), exist_ok=True)
+                with open(full, "w", encoding="utf-8", newline="") as fh:
+                    fh.write(text)
+            os.makedirs(os.path.join(tmp, "base"), exist_ok=True)
+            op_objs = [ops_mod.Op.from_dict(d) for d in ops]
+            before = set(os.listdir(tempfile.gettempdir()))
+            err = None
+            try:
+                out = applier_mod.apply_ops(os.path.join(tmp, "base"), op_objs)
+            except Exception as e:  # noqa: BLE001 - the class name is the fixture
+                err = type(e).__name__
+                new = [d for d in set(os.listdir(tempfile.gettempdir())) - before
+                       if d.startswith("semmerge_merged_")]
+                out = os.path.join(tempfile.gettempdir(), new[0])
+            files, dirs = _tree(out)
+            shutil.rmtree(out)
+        finally:
+            shutil.rmtree(tmp)
+        rec = {"base": base, "ops": ops, "files": files, "dirs": dirs}
+        if err:
+            rec["error"] = err
+        cases.append(rec)
+    return cases
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
-    ap.add_argument("--only", choices=["oplog"], help="regenerate one fixture file only")
+    ap.add_argument("--only", choices=["oplog", "applier"], help="regenerate one fixture file only")
     args = ap.parse_args()
     compose, crdt, ops_mod = _import_reference()
     os.makedirs(GOLD, exist_ok=True)
-    with open(os.path.join(GOLD, "oplog_cases.json"), "w") as fh:
-        json.dump(make_oplog_cases(ops_mod, 300, seed=112), fh, separators=(",", ":"), ensure_ascii=False)
-    if args.only == "oplog":
+    if args.only in (None, "oplog"):
+        with open(os.path.join(GOLD, "oplog_cases.json"), "w") as fh:
+            json.dump(make_oplog_cases(ops_mod, 300, seed=112), fh, separators=(",", ":"), ensure_ascii=False)
+    if args.only in (None, "applier"):
+        from semmerge import applier as applier_mod
+        with open(os.path.join(GOLD, "applier_cases.json"), "w") as fh:
+            json.dump(make_applier_cases(applier_mod, ops_mod, 400, seed=77), fh, separators=(",", ":"),
+                      ensure_ascii=False)
+    if args.only:
         return
 
     cases = make_cases(compose, ops_mod, 600, seed=20251114)
