@@ -756,17 +756,19 @@ __global__ void __launch_bounds__(1024) k_rga_big(const u64* __restrict__ R, con
   }
 }
 
-// Per list: its survivors, in list order, to their place in the output.
-__global__ void k_rga_out(const u32* __restrict__ tmp_v, const u32* __restrict__ tmp_s,
-                          const u32* __restrict__ lstart, const u32* __restrict__ scnt, const u32* __restrict__ soff,
-                          smx_rga_out out) {
-  const u32 l = blockIdx.x;
+// Per list (one wave each): its survivors, in list order, to their place in the output.
+__global__ void __launch_bounds__(BLOCK) k_rga_out(const u32* __restrict__ tmp_v, const u32* __restrict__ tmp_s,
+                                                  const u32* __restrict__ lstart, const u32* __restrict__ scnt,
+                                                  const u32* __restrict__ soff, i64 nl, smx_rga_out out) {
+  const u32 lane = threadIdx.x & (WAVE - 1);
+  const i64 l = (i64)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE;
+  if (l >= nl) return;
   const u32 s0 = lstart[l], m = scnt[l], d = soff[l];
-  for (u32 x = threadIdx.x; x < m; x += BLOCK) {
-    out.out_value[d + x] = tmp_v[s0 + x];
-    out.out_src[d + x] = (i32)tmp_s[s0 + x];
+  for (u32 x = lane; x < m; x += WAVE) {
+    out.out_value[d + x] = __builtin_nontemporal_load(&tmp_v[s0 + x]);
+    out.out_src[d + x] = (i32)__builtin_nontemporal_load(&tmp_s[s0 + x]);
   }
-  if (threadIdx.x == 0) out.out_offsets[l] = d;
+  if (lane == 0) out.out_offsets[l] = d;
 }
 
 __global__ void k_rga_fin(const u32* __restrict__ soff_total, i64 n_lists, smx_rga_out out) {
@@ -891,7 +893,8 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
                      tmp_s, scnt);
   RGA_TRY((scan_excl<OpSum, u32, u32>(scnt, soff, nl, nullptr, part, totals, st)));
-  hipLaunchKernelGGL(k_rga_out, dim3(nl), dim3(BLOCK), 0, st, tmp_v, tmp_s, lstart, scnt, soff, *out);
+  hipLaunchKernelGGL(k_rga_out, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE))), dim3(BLOCK), 0, st, tmp_v, tmp_s, lstart,
+                     scnt, soff, nl, *out);
   hipLaunchKernelGGL(k_rga_fin, dim3(1), dim3(1), 0, st, totals, nl, *out);
   RGA_TRY(hipGetLastError());
   i32 herr = 0;

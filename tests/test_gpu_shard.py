@@ -29,6 +29,8 @@ def _make(case):
         spec = synth.LiftSpec(**{**synth.CONFIGS["c2s"].__dict__, "n_total": n, "n_sym": n_sym,
                                  "seed": seed})
         return synth.lift_soa(synth.lift_logs(spec))
+    if kind == "hollow":  # 4 ranks: a run of equal timestamps makes shard 1 empty
+        return _hollow_soa(n, seed)
     if kind == "dense":  # long equal-timestamp groups: windows overflow, ORDER_FIX repairs
         spec = synth.LiftSpec(n, n_sym, seed, ops_per_ms=4096)
         return synth.lift_soa(synth.lift_logs(spec))
@@ -73,6 +75,27 @@ def _chain_soa(n_ren, seed):
     v0[:n_ren], v1[:n_ren] = 0, 0
     v0[na:na + n_ren], v1[na:na + n_ren] = 1, 1
     return SoA(na, nb, kind, ts, hi, lo, sym, v0, v1, 5, ["a", "b"])
+
+
+def _hollow_soa(n_ren, seed):
+    """A renames symbol 0 n_ren times (name class 0), B n_ren times (class 1) after all
+    of A: one DivergentRename region from shard 0 to the last shard.  A's ops
+    n_ren/4 .. n_ren/2 share one timestamp, so with 4 ranks the splitters of shards 1 and
+    2 coincide and shard 1 is empty: the open region must pass through it, and what it
+    hands on changes between walk rounds."""
+    from semantic_merge_amd.marshal import SoA
+    rng = np.random.default_rng(seed)
+    na = nb = n_ren
+    ts_a = np.arange(na, dtype=np.uint64) * 2
+    q1, q2 = na // 4, na // 2
+    ts_a[q1:q2 + 1] = ts_a[q1]
+    ts = np.concatenate([ts_a, np.uint64(10 * na) + np.arange(nb, dtype=np.uint64) * 2])
+    hi = rng.integers(0, 2**63, size=na + nb, dtype=np.int64).astype(np.uint64)
+    lo = rng.integers(0, 2**63, size=na + nb, dtype=np.int64).astype(np.uint64)
+    kind = np.full(na + nb, 1, np.uint8)
+    sym = np.zeros(na + nb, np.uint32)
+    v0 = np.concatenate([np.zeros(na, np.int32), np.ones(nb, np.int32)])
+    return SoA(na, nb, kind, ts, hi, lo, sym, v0, v0.copy(), 1, ["a", "b"])
 
 
 def _worker(rank, world, port, case, halo, q, mode="auto"):
@@ -168,6 +191,13 @@ def test_shard_tiny_with_empty_shards():
     _check(("lift", 40, 5, 2), 3)
 
 
+def test_shard_open_region_through_empty_middle_shard():
+    got, ref = _check(("hollow", 4000, 0, 5), 4)
+    assert len(ref[4]) == 4000
+    assert got[1][0][0].size == 0, "shard 1 must be empty"
+    assert got[2][1] != (0, 0) and got[3][1] != (0, 0), "the region must reach shards 2 and 3"
+
+
 def test_shard_sample_sort_shuffled_c2s():
     """Branch logs in any order (config 2s's shape): the sample-sort exchange on the full
     T key, the generic plan per shard, global sources through src_map."""
@@ -206,3 +236,66 @@ def test_bench_two_ranks_sharded():
         assert out["n_gpus"] == 2 and out["config"]["n_ops_total"] == total
         assert out["scaling"] == scaling
         assert out["value"] > 0 and "key-range shards" in out["config"]["parallelism"]
+
+
+def _full_worker(rank, world, port, q):
+    import hashlib
+    import json
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from semantic_merge_amd import shard, synth
+        soa = synth.lift_soa(synth.lift_logs(synth.CONFIGS["c3"]))
+        a, b, na, nb = shard.slices_from_soa(soa, rank, world, "cuda:0")
+        del soa
+        sc = shard.ShardedCompose(a, b, na, nb, 1_000_000, shard.Comm(), "cuda:0", mode="range")
+        del a, b
+        sc.run()
+        res = sc.results()
+        del sc
+        torch.cuda.empty_cache()
+        if rank == 0:  # gather the other shards' outputs, assemble, digest
+            parts = [res]
+            for r in range(1, world):
+                got = [None]
+                dist.recv_object_list(got, src=r)
+                parts.append(got[0])
+            glob = shard.assemble(parts)
+            h = hashlib.sha256()
+            for arr in glob:
+                h.update(np.ascontiguousarray(arr, dtype=np.int32).tobytes())
+            q.put((rank, (len(glob[0]), len(glob[4]), h.hexdigest())))
+        else:
+            dist.send_object_list([res], dst=0)
+            q.put((rank, None))
+    except Exception as e:  # report to the parent instead of hanging the collective
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_shard_full_size_c3_two_ranks():
+    """Config 3 at full size (100M ops, 1M symbols) as one merge over two shards: the
+    assembled output's sha256 equals the C oracle's digest of the single merge
+    (tests/golden/full_digests.json)."""
+    import json
+    rec = {r["name"]: r for r in json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                                             "full_digests.json")))}["c3"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_full_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=800) for _ in range(2))
+    for p in procs:
+        p.join(120)
+    assert not isinstance(got[1], str), got[1]
+    assert not isinstance(got[0], str), got[0]
+    n_out, n_conf, digest = got[0]
+    assert (n_out, n_conf) == (rec["n_out"], rec["n_conflicts"])
+    assert digest == rec["sha256"]
