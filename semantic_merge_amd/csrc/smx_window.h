@@ -537,18 +537,27 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   __syncthreads();
   WSTAMP(10);
   // 6. renames: rank among the window's renames of the same branch (final order).
-  //    Computed in the collision-check phase; redone after a (rare) exact re-rank.
+  //    Computed in the collision-check phase into registers (rown aliases fin, which
+  //    the exact re-rank still reads) and stored once no tie is known; redone after a
+  //    (rare) exact re-rank.
   const int R0 = kbase[KREN], RN = wck[KREN];
   const int nrc = (RN + WAVE - 1) / WAVE;
-  auto rename_ranks = [&]() {
-    for (int c = wv; c < nrc; c += WF_WAVES) {
+  constexpr int RQ = (NCHUNK + WF_WAVES - 1) / WF_WAVES;  // rename chunks per wave
+  u32 rown_r[RQ];
+  auto rename_ranks = [&](bool store) {
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const int c = wv + q * WF_WAVES;
+      rown_r[q] = 0;
+      if (c >= nrc) continue;  // wave-uniform
       const int x = c * WAVE + lane;
       const bool valid = x < RN;
       const int e = valid ? sord[R0 + x] : 0;
       const bool sb = valid && e >= na;
       const u64 bm = __ballot(sb), vm = __ballot(valid);
       const u64 lt = lanemask_lt();
-      if (valid) rown[x] = (u16)(sb ? __popcll(bm & lt) : __popcll(vm & ~bm & lt));
+      rown_r[q] = (u32)(sb ? __popcll(bm & lt) : __popcll(vm & ~bm & lt));
+      if (store && valid) rown[x] = (u16)rown_r[q];
       if (lane == 0) {
         rc[c][0] = (u16)__popcll(vm & ~bm);
         rc[c][1] = (u16)__popcll(bm);
@@ -561,7 +570,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     const int r = t + WF_NT * j;
     if (r < sz) tie |= sl[r] == 0xffffu;
   }
-  rename_ranks();
+  rename_ranks(false);
   const bool any_tie = __syncthreads_or(tie);
   WSTAMP(21);
   if (any_tie) {
@@ -585,8 +594,14 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     __syncthreads();
     for (int r = t; r < sz; r += WF_NT) sord[r] = fin[sl[r]];
     __syncthreads();
-    rename_ranks();
+    rename_ranks(true);
     __syncthreads();
+  } else {
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {  // fin is dead now: the ranks go to rown
+      const int x = (wv + q * WF_WAVES) * WAVE + lane;
+      if (wv + q * WF_WAVES < nrc && x < RN) rown[x] = (u16)rown_r[q];
+    }
   }
   WSTAMP(11);
   if (wv == 0) {

@@ -206,3 +206,23 @@ def test_compose_json_matches_dropin():
         assert [c.to_dict() for c in conf] == case["conflicts"], f"case {i}"
         ref = compose_oplogs(OpLog.from_json(ta).ops, OpLog.from_json(tb).ops)
         assert [o.to_dict() for o in ref[0]] == case["out"]
+
+
+@pytest.mark.parametrize("frac,dup", [(0.3, False), (1.0, True)])
+def test_gpu_presorted_id_prefix_ties(frac, dup):
+    """Ops whose ids share their top 32 bits (and, with dup, whole ids) inside equal-
+    (kind, timestamp) groups: the presorted window's 32-bit group rank collides and the
+    window re-ranks exactly on the full ids -- with the renames' ranks computed around
+    it (a window with ties and renames)."""
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(300_000, 3_000, 21)))
+    rng = np.random.default_rng(5)
+    sel = rng.random(soa.n) < frac
+    soa.oid_hi[sel] = (soa.oid_hi[sel] & np.uint64(0xFFFFFFFF)) | np.uint64(0x4242424200000000)
+    if dup:
+        soa.oid_lo[sel] = np.uint64(7)
+        soa.oid_hi[sel] &= np.uint64(0xFFFFFFFFFFFF000F)  # many exact duplicates
+    dc = DeviceCompose(soa)
+    dc.run()
+    got = dc.results()
+    assert DeviceCompose.last_plan() == "presorted"
+    _eq_soa(got, oracle.compose(soa), f"id prefix ties frac={frac} dup={dup}")
