@@ -24,11 +24,14 @@
       return smx_set_error(SMX_E_HIP, (std::string(#x) + ": " + hipGetErrorString(_e)).c_str()); \
   } while (0)
 
-// Event record, 5 u64 words, grouped by list by the partition below:
+// Event record, 3 u64 words, grouped by list by the partition below:
 //   w0 = anchor << 32 | t' >> 32,  w1 = t' << 32 | author   (t' = t with the sign bit flipped)
-//   w2 = opid_hi, w3 = opid_lo                              -> (w0..w3) is the crdt.py:48-57 key order
-//   w4 = value << 32 | op << 30 | event index              (index = creation order, the tie-break)
-#define RGA_REC 5
+//   w2 = value << 32 | op << 30 | event index              (index = creation order)
+// (w0, w1, opid, index) is the crdt.py:48-57 key order; the opid breaks a tie on
+// (anchor, t, author) only, so it stays in the input columns and is read by the
+// event index when two keys tie that far.
+#define RGA_REC 3
+#define RGA_WV 2  // the value / op / index word
 #define RGA_IDX_MASK 0x3fffffffu
 
 // Grouping the events by list: a stable LSD radix partition of whole records on the
@@ -83,7 +86,6 @@ struct RTile<true> {
   u32 list[RREC_ITEMS], value[RREC_ITEMS], anchor[RREC_ITEMS], author[RREC_ITEMS];
   u32 op[RREC_ITEMS];
   i64 t[RREC_ITEMS];
-  u64 hi[RREC_ITEMS], lo[RREC_ITEMS];
 };
 #define RREC_V4 ((RREC_TILE * RGA_REC * 8 / 16 + RR_NT - 1) / RR_NT)  // 16-byte loads per thread
 typedef u32 v4u32 __attribute__((ext_vector_type(4)));
@@ -112,8 +114,6 @@ __device__ __forceinline__ void rrec_load(RTile<FIRST>& T, const smx_rga_ops& o,
       T.anchor[it] = v ? o.anchor[i] : 0u;
       T.t[it] = v ? o.t[i] : 0;
       T.author[it] = v ? o.author[i] : 0u;
-      T.hi[it] = v ? o.opid_hi[i] : 0ull;
-      T.lo[it] = v ? o.opid_lo[i] : 0ull;
     }
   } else {
 #pragma unroll
@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
                                                         u64* __restrict__ rout, int shift,
                                                         const u32* __restrict__ offs, i32* __restrict__ err,
                                                         u32 ntiles) {
-  __shared__ u64 srec[RREC_TILE * RGA_REC];  // 120 KB
+  __shared__ u64 srec[RREC_TILE * RGA_REC];  // 72 KB
   __shared__ u32 skey[RREC_TILE];
   __shared__ u16 spos[RREC_TILE];            // tile record -> staged slot (pass 2+)
   __shared__ u16 wc[RR_NW][RGA_NDIG];        // per-wave digit counts, then offsets
@@ -227,10 +227,8 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
         const u64 tt = (u64)T.t[it] ^ 0x8000000000000000ull;
         r[0] = ((u64)T.anchor[it] << 32) | (tt >> 32);
         r[1] = (tt << 32) | T.author[it];
-        r[2] = T.hi[it];
-        r[3] = T.lo[it];
         const u32 op = T.op[it] > 2 ? 0u : T.op[it];
-        r[4] = ((u64)T.value[it] << 32) | (op << 30) | (u32)i;
+        r[RGA_WV] = ((u64)T.value[it] << 32) | (op << 30) | (u32)i;
       } else {
         spos[li] = (u16)p;
       }
@@ -285,12 +283,15 @@ __device__ __forceinline__ u32 rga_lend(const u32* lstart, u32 l, i64 nl, i64 n)
 }
 
 // a before b in (key, creation index) order; records as above
-__device__ __forceinline__ bool rec_lt(const u64* a, const u64* b) {
+__device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga_ops& o) {
   if (a[0] != b[0]) return a[0] < b[0];
   if (a[1] != b[1]) return a[1] < b[1];
-  if (a[2] != b[2]) return a[2] < b[2];
-  if (a[3] != b[3]) return a[3] < b[3];
-  return (u32)a[4] < (u32)b[4];  // index bits (the op bits above them are fixed per index)
+  const u32 ia = (u32)a[RGA_WV] & RGA_IDX_MASK, ib = (u32)b[RGA_WV] & RGA_IDX_MASK;
+  const u64 ha = (u64)o.opid_hi[ia], hb = (u64)o.opid_hi[ib];
+  if (ha != hb) return ha < hb;
+  const u64 la = (u64)o.opid_lo[ia], lb = (u64)o.opid_lo[ib];
+  if (la != lb) return la < lb;
+  return ia < ib;
 }
 
 // ---------------------------------------------------------------------------
@@ -378,7 +379,7 @@ template <int CAP>
 struct RwLds {
   static constexpr int HT = 2 * CAP;  // hash slots
   u64 w0[CAP];          // key word 0 of each event (words 1-3 stay in global memory / L2)
-  u64 w4[CAP];          // value << 32 | op << 30 | index
+  u64 wv[CAP];          // value << 32 | op << 30 | index (record word RGA_WV)
   union {
     struct {
       u32 hkey[HT];     // the slot's value, RW_EMPTY
@@ -392,19 +393,27 @@ struct RwLds {
   u8 st[CAP];           // bit0 present, bit1 tombstoned
 };
 
-// Event a before event b of one list in (key, index) order (crdt.py:48-57); key
-// words 1-3 from the list's records in global memory (rare: equal word 0).
+// Event a before event b of one list in (key, index) order (crdt.py:48-57): word 0
+// from LDS; on a tie word 1 from the list's records and the opids by event index
+// (rare: equal word 0).
 template <class LDS>
-__device__ __forceinline__ bool ev_lt(const LDS& S, const u64* __restrict__ src, u32 a, u32 b) {
+__device__ __forceinline__ bool ev_lt(const LDS& S, const u64* __restrict__ src, const smx_rga_ops& o, u32 a,
+                                      u32 b) {
   if (S.w0[a] != S.w0[b]) return S.w0[a] < S.w0[b];
-  const u64* ka = src + (u64)a * RGA_REC;
-  const u64* kb = src + (u64)b * RGA_REC;
-  return ka[1] != kb[1] ? ka[1] < kb[1] : ka[2] != kb[2] ? ka[2] < kb[2] : ka[3] != kb[3] ? ka[3] < kb[3] : a < b;
+  const u64 a1 = src[(u64)a * RGA_REC + 1], b1 = src[(u64)b * RGA_REC + 1];
+  if (a1 != b1) return a1 < b1;
+  const u32 ia = (u32)S.wv[a] & RGA_IDX_MASK, ib = (u32)S.wv[b] & RGA_IDX_MASK;
+  const u64 ha = (u64)o.opid_hi[ia], hb = (u64)o.opid_hi[ib];
+  if (ha != hb) return ha < hb;
+  const u64 la = (u64)o.opid_lo[ia], lb = (u64)o.opid_lo[ib];
+  if (la != lb) return la < lb;
+  return a < b;
 }
 
 // Step 3 over the survivors' (word 0, event) pairs held K2 per lane.
 template <int K2, class LDS>
-__device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, u64 (&key)[8], u32 (&pay)[8], u32 m,
+__device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, const smx_rga_ops& o, u64 (&key)[8],
+                                         u32 (&pay)[8], u32 m,
                                          u32 s0, u32 lane, u32* __restrict__ tmp_v, u32* __restrict__ tmp_s) {
   constexpr u32 N = 64u * K2;
   wave_bitonic<K2>(key, pay, lane);
@@ -417,7 +426,7 @@ __device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, u6
   wave_lds_sync();
   auto tail_lt = [&](u32 b, u32 a) {  // events b, a with equal word 0; dead ones last
     if ((a | b) & RW_DEAD) return (a & RW_DEAD) && !(b & RW_DEAD);
-    return ev_lt(S, src, b, a);
+    return ev_lt(S, src, o, b, a);
   };
 #pragma unroll
   for (int k = 0; k < K2; ++k) {
@@ -438,14 +447,15 @@ __device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, u6
   }
   wave_lds_sync();
   for (u32 q = lane; q < m; q += WAVE) {
-    const u64 w4 = S.w4[S.gp[q] & (RW_DEAD - 1)];
-    tmp_v[s0 + q] = (u32)(w4 >> 32);
-    tmp_s[s0 + q] = (u32)w4 & RGA_IDX_MASK;
+    const u64 w = S.wv[S.gp[q] & (RW_DEAD - 1)];
+    tmp_v[s0 + q] = (u32)(w >> 32);
+    tmp_s[s0 + q] = (u32)w & RGA_IDX_MASK;
   }
 }
 
 template <int K, int CAP>
-__device__ __forceinline__ void rga_wave_list(const u64* __restrict__ R, u32 l, u32 s0, u32 cnt, RwLds<CAP>& S, u32 lane,
+__device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* __restrict__ R, u32 l, u32 s0, u32 cnt,
+                                              RwLds<CAP>& S, u32 lane,
                                               u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
                                               u32* __restrict__ scnt) {
   const u64* src = R + (u64)s0 * RGA_REC;
@@ -466,7 +476,7 @@ __device__ __forceinline__ void rga_wave_list(const u64* __restrict__ R, u32 l, 
       const u32 e = x / RGA_REC, wd = x - e * RGA_REC;
       if (x < cnt * RGA_REC) {
         if (wd == 0) S.w0[e] = v[i];
-        if (wd == 4) S.w4[e] = v[i];
+        if (wd == RGA_WV) S.wv[e] = v[i];
       }
     }
   }
@@ -485,7 +495,7 @@ __device__ __forceinline__ void rga_wave_list(const u64* __restrict__ R, u32 l, 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const u32 e = (u32)k * 64u + lane;
-      S.st[e] = e < cnt && ((u32)(S.w4[e] >> 30) & 3u) != 2;
+      S.st[e] = e < cnt && ((u32)(S.wv[e] >> 30) & 3u) != 2;
     }
   } else {
     // 1. value groups: each event's value into the hash table (CAS), its rank among
@@ -496,7 +506,7 @@ __device__ __forceinline__ void rga_wave_list(const u64* __restrict__ R, u32 l, 
       const u32 e = (u32)k * 64u + lane;
       S.st[e] = 0;
       if (e < cnt) {
-        const u32 v = (u32)(S.w4[e] >> 32);
+        const u32 v = (u32)(S.wv[e] >> 32);
         u32 h = (v * 0x9E3779B1u) >> (32 - HB);
         for (;;) {
           const u32 old = atomicCAS(&S.h.hkey[h], RW_EMPTY, v);
@@ -547,12 +557,12 @@ __device__ __forceinline__ void rga_wave_list(const u64* __restrict__ R, u32 l, 
       if (e >= cnt || rk[k] != 0) continue;
       const u32 b = S.h.hbase[slot[k]], c = S.h.hcnt[slot[k]];
       if (c == 1 || (RW_ABL & 1)) {
-        S.st[e] = ((u32)(S.w4[e] >> 30) & 3u) != 2;
+        S.st[e] = ((u32)(S.wv[e] >> 30) & 3u) != 2;
         continue;
       }
       for (u32 i = 0; i < c; ++i) {
         const u32 x = S.mem[b + i];
-        const u32 op = (u32)(S.w4[x] >> 30) & 3u;
+        const u32 op = (u32)(S.wv[x] >> 30) & 3u;
         if (op == 2) {  // delete: every present element is tombstoned; creates nothing
           for (u32 j = 0; j < i; ++j) {
             const u32 y = S.mem[b + j];
@@ -564,7 +574,7 @@ __device__ __forceinline__ void rga_wave_list(const u64* __restrict__ R, u32 l, 
           u32 best = RW_NIL;
           for (u32 j = 0; j < i; ++j) {
             const u32 y = S.mem[b + j];
-            if (S.st[y] == 1 && (best == RW_NIL || ev_lt(S, src, y, best))) best = y;
+            if (S.st[y] == 1 && (best == RW_NIL || ev_lt(S, src, o, y, best))) best = y;
           }
           if (best != RW_NIL) S.st[best] = 0;
         }
@@ -602,23 +612,24 @@ __device__ __forceinline__ void rga_wave_list(const u64* __restrict__ R, u32 l, 
   wave_lds_sync();  // gp / the hash table are rewritten below
   if (RW_ABL & 4) {
     for (u32 q = lane; q < m; q += WAVE) {
-      const u64 w4 = S.w4[S.gp[q]];
-      tmp_v[s0 + q] = (u32)(w4 >> 32);
-      tmp_s[s0 + q] = (u32)w4 & RGA_IDX_MASK;
+      const u64 w = S.wv[S.gp[q]];
+      tmp_v[s0 + q] = (u32)(w >> 32);
+      tmp_s[s0 + q] = (u32)w & RGA_IDX_MASK;
     }
   } else if (m <= 64) {
-    rw_order<1>(S, src, key, pay, m, s0, lane, tmp_v, tmp_s);
+    rw_order<1>(S, src, o, key, pay, m, s0, lane, tmp_v, tmp_s);
   } else if (m <= 128) {
-    rw_order<2>(S, src, key, pay, m, s0, lane, tmp_v, tmp_s);
+    rw_order<2>(S, src, o, key, pay, m, s0, lane, tmp_v, tmp_s);
   } else if (K <= 4 || m <= 256) {
-    rw_order<(K <= 4 ? K : 4)>(S, src, key, pay, m, s0, lane, tmp_v, tmp_s);
+    rw_order<(K <= 4 ? K : 4)>(S, src, o, key, pay, m, s0, lane, tmp_v, tmp_s);
   } else {
-    rw_order<8>(S, src, key, pay, m, s0, lane, tmp_v, tmp_s);
+    rw_order<8>(S, src, o, key, pay, m, s0, lane, tmp_v, tmp_s);
   }
   if (lane == 0) scnt[l] = m;
 }
 
-__global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave(const u64* __restrict__ R, const u32* __restrict__ lstart,
+__global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave(smx_rga_ops o, const u64* __restrict__ R,
+                                                             const u32* __restrict__ lstart,
                                                              i64 n, i64 nl, u32* __restrict__ defer,
                                                              u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
                                                              u32* __restrict__ tmp_s, u32* __restrict__ scnt) {
@@ -632,16 +643,17 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave(const u64* __restr
     return;
   }
   if (cnt <= 64)
-    rga_wave_list<1>(R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+    rga_wave_list<1>(o, R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
   else if (cnt <= 128)
-    rga_wave_list<2>(R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+    rga_wave_list<2>(o, R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
   else
-    rga_wave_list<4>(R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+    rga_wave_list<4>(o, R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
 }
 
 // The deferred lists of RW_CAP + 1 .. 2 * RW_CAP events: the same wave per list with
 // twice the slots; longer ones go on to k_rga_big.
-__global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(const u64* __restrict__ R, const u32* __restrict__ lstart,
+__global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(smx_rga_ops o, const u64* __restrict__ R,
+                                                              const u32* __restrict__ lstart,
                                                               i64 n, i64 nl, const u32* __restrict__ todo,
                                                               const u32* __restrict__ ntodo, u32* __restrict__ defer,
                                                               u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
@@ -656,7 +668,7 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(const u64* __rest
       if (lane == 0) defer[atomicAdd(ndefer, 1u)] = l;
       continue;
     }
-    rga_wave_list<8>(R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+    rga_wave_list<8>(o, R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
     wave_lds_sync();  // the next list reuses the slice
   }
 }
@@ -689,7 +701,7 @@ __device__ void block_sort_positions(u32* p, u32 cnt, Less less) {
 // (such lists are rare — a whole file's history in one list).  Per list, in its
 // record range: gp = positions sorted by (value, index), bst = state by that order;
 // then the survivors' positions sorted by (key, index).
-__device__ void rga_big_list(const u64* __restrict__ R, u32 l, const u32* __restrict__ lstart, i64 n, i64 nl,
+__device__ void rga_big_list(const smx_rga_ops& o, const u64* __restrict__ R, u32 l, const u32* __restrict__ lstart, i64 n, i64 nl,
                              u8* __restrict__ bst, u32* __restrict__ gp, u32* __restrict__ tmp_v,
                              u32* __restrict__ tmp_s, u32* __restrict__ scnt) {
   __shared__ u32 ns;
@@ -698,7 +710,7 @@ __device__ void rga_big_list(const u64* __restrict__ R, u32 l, const u32* __rest
   const u64* L = R + (u64)s0 * RGA_REC;
   u8* S = bst + s0;
   u32* G = gp + s0;
-  auto gkey = [&](u32 x) { const u64 w = L[x * RGA_REC + 4]; return ((w >> 32) << 30) | (w & RGA_IDX_MASK); };
+  auto gkey = [&](u32 x) { const u64 w = L[x * RGA_REC + RGA_WV]; return ((w >> 32) << 30) | (w & RGA_IDX_MASK); };
   for (u32 x = t; x < cnt; x += NT) {
     G[x] = x;
     S[x] = 0;
@@ -711,7 +723,7 @@ __device__ void rga_big_list(const u64* __restrict__ R, u32 l, const u32* __rest
     u32 end = j + 1;
     while (end < cnt && (gkey(G[end]) >> 30) == v) ++end;
     for (u32 x = j; x < end; ++x) {
-      const u32 op = (u32)(L[G[x] * RGA_REC + 4] >> 30) & 3u;
+      const u32 op = (u32)(L[G[x] * RGA_REC + RGA_WV] >> 30) & 3u;
       if (op == 2) {
         for (u32 y = j; y < x; ++y)
           if (S[y] & 1) S[y] |= 2;
@@ -720,7 +732,7 @@ __device__ void rga_big_list(const u64* __restrict__ R, u32 l, const u32* __rest
       if (op == 1) {
         int best = -1;
         for (u32 y = j; y < x; ++y)
-          if (S[y] == 1 && (best < 0 || rec_lt(&L[G[y] * RGA_REC], &L[G[best] * RGA_REC]))) best = (int)y;
+          if (S[y] == 1 && (best < 0 || rec_lt(&L[G[y] * RGA_REC], &L[G[best] * RGA_REC], o))) best = (int)y;
         if (best >= 0) S[best] = 0;
       }
       S[x] = 1;
@@ -736,23 +748,24 @@ __device__ void rga_big_list(const u64* __restrict__ R, u32 l, const u32* __rest
   }
   __syncthreads();
   const u32 m = ns;
-  block_sort_positions(G, m, [&](u32 a, u32 b) { return rec_lt(&L[a * RGA_REC], &L[b * RGA_REC]); });
+  block_sort_positions(G, m, [&](u32 a, u32 b) { return rec_lt(&L[a * RGA_REC], &L[b * RGA_REC], o); });
   for (u32 j = t; j < m; j += NT) {
-    const u64 w4 = L[G[j] * RGA_REC + 4];
-    tmp_v[s0 + j] = (u32)(w4 >> 32);
-    tmp_s[s0 + j] = (u32)w4 & RGA_IDX_MASK;
+    const u64 w = L[G[j] * RGA_REC + RGA_WV];
+    tmp_v[s0 + j] = (u32)(w >> 32);
+    tmp_s[s0 + j] = (u32)w & RGA_IDX_MASK;
   }
   if (t == 0) scnt[l] = m;
 }
 
-__global__ void __launch_bounds__(1024) k_rga_big(const u64* __restrict__ R, const u32* __restrict__ lstart, i64 n,
+__global__ void __launch_bounds__(1024) k_rga_big(smx_rga_ops o, const u64* __restrict__ R,
+                                                  const u32* __restrict__ lstart, i64 n,
                                                   i64 nl, const u32* __restrict__ todo, const u32* __restrict__ ntodo,
                                                   u8* __restrict__ bst, u32* __restrict__ gp,
                                                   u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
                                                   u32* __restrict__ scnt) {
   for (u32 item = blockIdx.x; item < *ntodo; item += gridDim.x) {
     __syncthreads();
-    rga_big_list(R, todo[item], lstart, n, nl, bst, gp, tmp_v, tmp_s, scnt);
+    rga_big_list(o, R, todo[item], lstart, n, nl, bst, gp, tmp_v, tmp_s, scnt);
   }
 }
 
@@ -886,11 +899,11 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
     }
     hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, kbuf[(npass - 1) & 1], n, nl, lstart);
   }
-  hipLaunchKernelGGL(k_rga_wave, dim3(SMX_CEIL_DIV(nl, (i64)RW_WAVES)), dim3(WAVE * RW_WAVES), 0, st, rec, lstart, n,
+  hipLaunchKernelGGL(k_rga_wave, dim3(SMX_CEIL_DIV(nl, (i64)RW_WAVES)), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n,
                      nl, def1, ndef, tmp_v, tmp_s, scnt);
-  hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, rec, lstart, n, nl, def1, ndef, def2,
+  hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, def1, ndef, def2,
                      ndef + 1, tmp_v, tmp_s, scnt);
-  hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
+  hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
                      tmp_s, scnt);
   RGA_TRY((scan_excl<OpSum, u32, u32>(scnt, soff, nl, nullptr, part, totals, st)));
   hipLaunchKernelGGL(k_rga_out, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE))), dim3(BLOCK), 0, st, tmp_v, tmp_s, lstart,

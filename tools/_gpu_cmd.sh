@@ -1,5 +1,14 @@
 set -o pipefail
-O=gpurun_out/r02zg; mkdir -p $O
+O=gpurun_out/r02zh; mkdir -p $O
 R=$PWD
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/stage_ab.py 2>/dev/null | tail -1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_rga.py -x -q --timeout 200 --timeout-method thread > $O/rga_tests.log 2>&1; rc=$?; tail -2 $O/rga_tests.log; [ $rc -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp
+for v in base t2048; do
+  if [ $v = base ]; then L=$R/semantic_merge_amd/libsmx.so; else L=$R/tools/_build/var_$v/libsmx.so; fi
+  SMX_LIB=$L RGA_NO_CPU=1 RGA_STEPS=5 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/p_$v -o r -- python3 $R/tools/bench_rga.py > $R/$O/$v.log 2>&1 || exit 1
+  (cd $R && python3 tools/prof_export.py $O/p_$v $O/$v.csv && python3 -c "
+import csv
+r=list(csv.reader(open('$O/$v.csv')))
+print('$v', [(x[0][:22], x[3]) for x in r[1:6]])
+print('  total', round(sum(float(x[2]) for x in r[1:] if 'rga' in x[0] or 'rrec' in x[0] or 'scan' in x[0])/int(r[1][1]),1))")
+done
