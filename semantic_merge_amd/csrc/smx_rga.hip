@@ -24,14 +24,14 @@
       return smx_set_error(SMX_E_HIP, (std::string(#x) + ": " + hipGetErrorString(_e)).c_str()); \
   } while (0)
 
-// Event record, 3 u64 words, grouped by list by the partition below:
-//   w0 = anchor << 32 | t' >> 32,  w1 = t' << 32 | author   (t' = t with the sign bit flipped)
-//   w2 = value << 32 | op << 30 | event index              (index = creation order)
-// (w0, w1, opid, index) is the crdt.py:48-57 key order; the opid breaks a tie on
-// (anchor, t, author) only, so it stays in the input columns and is read by the
-// event index when two keys tie that far.
-#define RGA_REC 3
-#define RGA_WV 2  // the value / op / index word
+// Event record, 2 u64 words, grouped by list by the partition below:
+//   w0 = anchor << 32 | t' >> 32   (t' = t with the sign bit flipped: order-preserving)
+//   w1 = value << 32 | op << 30 | event index   (index = creation order)
+// (anchor, t, author, opid, index) is the crdt.py:48-57 key order; w0 decides it
+// unless two events share anchor and the top half of t, and only then are t, author
+// and opid read from the input columns by event index (rga_key_lt).
+#define RGA_REC 2
+#define RGA_WV 1  // the value / op / index word
 #define RGA_IDX_MASK 0x3fffffffu
 
 // Grouping the events by list: a stable LSD radix partition of whole records on the
@@ -43,6 +43,9 @@
 #define RR_NT 512                         // scatter workgroup (persistent, one per CU)
 #endif
 #define RR_NW (RR_NT / WAVE)
+#ifndef RR_PER_CU
+#define RR_PER_CU 2  // persistent scatter workgroups per CU (LDS ~74 KB each)
+#endif
 #ifndef RREC_ITEMS
 #define RREC_ITEMS 6
 #endif
@@ -83,7 +86,7 @@ template <bool FIRST>
 struct RTile;
 template <>
 struct RTile<true> {
-  u32 list[RREC_ITEMS], value[RREC_ITEMS], anchor[RREC_ITEMS], author[RREC_ITEMS];
+  u32 list[RREC_ITEMS], value[RREC_ITEMS], anchor[RREC_ITEMS];
   u32 op[RREC_ITEMS];
   i64 t[RREC_ITEMS];
 };
@@ -113,7 +116,7 @@ __device__ __forceinline__ void rrec_load(RTile<FIRST>& T, const smx_rga_ops& o,
       T.value[it] = v ? o.value[i] : 0u;
       T.anchor[it] = v ? o.anchor[i] : 0u;
       T.t[it] = v ? o.t[i] : 0;
-      T.author[it] = v ? o.author[i] : 0u;
+
     }
   } else {
 #pragma unroll
@@ -145,7 +148,7 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
                                                         u64* __restrict__ rout, int shift,
                                                         const u32* __restrict__ offs, i32* __restrict__ err,
                                                         u32 ntiles) {
-  __shared__ u64 srec[RREC_TILE * RGA_REC];  // 72 KB
+  __shared__ u64 srec[RREC_TILE * RGA_REC];  // 48 KB
   __shared__ u32 skey[RREC_TILE];
   __shared__ u16 spos[RREC_TILE];            // tile record -> staged slot (pass 2+)
   __shared__ u16 wc[RR_NW][RGA_NDIG];        // per-wave digit counts, then offsets
@@ -226,7 +229,6 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
         u64* r = &srec[p * RGA_REC];
         const u64 tt = (u64)T.t[it] ^ 0x8000000000000000ull;
         r[0] = ((u64)T.anchor[it] << 32) | (tt >> 32);
-        r[1] = (tt << 32) | T.author[it];
         const u32 op = T.op[it] > 2 ? 0u : T.op[it];
         r[RGA_WV] = ((u64)T.value[it] << 32) | (op << 30) | (u32)i;
       } else {
@@ -282,16 +284,24 @@ __device__ __forceinline__ u32 rga_lend(const u32* lstart, u32 l, i64 nl, i64 n)
   return l + 1 < nl ? lstart[l + 1] : (u32)n;
 }
 
-// a before b in (key, creation index) order; records as above
-__device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga_ops& o) {
-  if (a[0] != b[0]) return a[0] < b[0];
-  if (a[1] != b[1]) return a[1] < b[1];
-  const u32 ia = (u32)a[RGA_WV] & RGA_IDX_MASK, ib = (u32)b[RGA_WV] & RGA_IDX_MASK;
+// Events ia, ib (stream indices) whose record words 0 are equal: the rest of the
+// crdt.py:48-57 key -- t (signed), author, opid -- then the creation index.
+__device__ __forceinline__ bool rga_key_lt(const smx_rga_ops& o, u32 ia, u32 ib) {
+  const i64 ta = o.t[ia], tb = o.t[ib];
+  if (ta != tb) return ta < tb;
+  const u32 aa = o.author[ia], ab = o.author[ib];
+  if (aa != ab) return aa < ab;
   const u64 ha = (u64)o.opid_hi[ia], hb = (u64)o.opid_hi[ib];
   if (ha != hb) return ha < hb;
   const u64 la = (u64)o.opid_lo[ia], lb = (u64)o.opid_lo[ib];
   if (la != lb) return la < lb;
   return ia < ib;
+}
+
+// record a before record b in (key, creation index) order
+__device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga_ops& o) {
+  if (a[0] != b[0]) return a[0] < b[0];
+  return rga_key_lt(o, (u32)a[RGA_WV] & RGA_IDX_MASK, (u32)b[RGA_WV] & RGA_IDX_MASK);
 }
 
 // ---------------------------------------------------------------------------
@@ -394,20 +404,12 @@ struct RwLds {
 };
 
 // Event a before event b of one list in (key, index) order (crdt.py:48-57): word 0
-// from LDS; on a tie word 1 from the list's records and the opids by event index
-// (rare: equal word 0).
+// from LDS, the rest from the input columns by stream index (rare: equal word 0).
 template <class LDS>
 __device__ __forceinline__ bool ev_lt(const LDS& S, const u64* __restrict__ src, const smx_rga_ops& o, u32 a,
                                       u32 b) {
   if (S.w0[a] != S.w0[b]) return S.w0[a] < S.w0[b];
-  const u64 a1 = src[(u64)a * RGA_REC + 1], b1 = src[(u64)b * RGA_REC + 1];
-  if (a1 != b1) return a1 < b1;
-  const u32 ia = (u32)S.wv[a] & RGA_IDX_MASK, ib = (u32)S.wv[b] & RGA_IDX_MASK;
-  const u64 ha = (u64)o.opid_hi[ia], hb = (u64)o.opid_hi[ib];
-  if (ha != hb) return ha < hb;
-  const u64 la = (u64)o.opid_lo[ia], lb = (u64)o.opid_lo[ib];
-  if (la != lb) return la < lb;
-  return a < b;
+  return rga_key_lt(o, (u32)S.wv[a] & RGA_IDX_MASK, (u32)S.wv[b] & RGA_IDX_MASK);
 }
 
 // Step 3 over the survivors' (word 0, event) pairs held K2 per lane.
@@ -789,7 +791,7 @@ __global__ void k_rga_fin(const u32* __restrict__ soff_total, i64 n_lists, smx_r
   out.counts[0] = *soff_total;
 }
 
-static int g_rr_grid = 0;  // persistent scatter grid (CUs of the device)
+static int g_rr_grid = 0;  // persistent scatter grid (RR_PER_CU per CU of the device)
 
 static bool o_ok(const smx_rga_ops* o) {
   return o->list && o->op && o->value && o->anchor && o->t && o->author && o->opid_hi && o->opid_lo;
@@ -868,11 +870,11 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   const int grid = (int)(SMX_CEIL_DIV(n, (i64)BLOCK) < 8192 ? SMX_CEIL_DIV(n, (i64)BLOCK) : 8192);
 
   RGA_TRY(hipMemsetAsync(err, 0, 32, st));
-  if (g_rr_grid == 0) {  // one persistent scatter workgroup per CU
+  if (g_rr_grid == 0) {  // persistent scatter workgroups
     int dev = 0, cus = 0;
     RGA_TRY(hipGetDevice(&dev));
     RGA_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    g_rr_grid = cus > 0 ? cus : 256;
+    g_rr_grid = (cus > 0 ? cus : 256) * RR_PER_CU;
   }
   {  // records grouped by list: LSD passes over the list id, ping-pong into rec
     int npass = 1;
