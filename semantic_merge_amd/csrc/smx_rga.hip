@@ -786,6 +786,30 @@ __global__ void __launch_bounds__(BLOCK) k_rga_out(const u32* __restrict__ tmp_v
   if (lane == 0) out.out_offsets[l] = d;
 }
 
+// Exclusive scan of the survivor counts in one workgroup (n_lists up to RS_MAX), and
+// the output's total: out_offsets[n_lists] = counts[0] = survivors.
+#define RS_NT 1024
+#define RS_MAX (RS_NT * 64)
+__global__ void __launch_bounds__(RS_NT) k_rga_scnt_scan(const u32* __restrict__ scnt, u32* __restrict__ soff,
+                                                         i64 nl, smx_rga_out out) {
+  __shared__ u32 sh[RS_NT / WAVE + 1];
+  const i64 per = SMX_CEIL_DIV(nl, (i64)RS_NT);
+  const i64 b0 = (i64)threadIdx.x * per, b1 = b0 + per < nl ? b0 + per : nl;
+  u32 sum = 0;
+  for (i64 i = b0; i < b1; ++i) sum += scnt[i];
+  u32 tot;
+  u32 run = block_excl_scan<OpSum, u32, RS_NT / WAVE>(sum, sh, &tot);
+  for (i64 i = b0; i < b1; ++i) {
+    const u32 c = scnt[i];
+    soff[i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) {
+    out.out_offsets[nl] = tot;
+    out.counts[0] = tot;
+  }
+}
+
 __global__ void k_rga_fin(const u32* __restrict__ soff_total, i64 n_lists, smx_rga_out out) {
   out.out_offsets[n_lists] = *soff_total;
   out.counts[0] = *soff_total;
@@ -907,10 +931,14 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
                      ndef + 1, tmp_v, tmp_s, scnt);
   hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
                      tmp_s, scnt);
-  RGA_TRY((scan_excl<OpSum, u32, u32>(scnt, soff, nl, nullptr, part, totals, st)));
+  if (nl <= RS_MAX) {
+    hipLaunchKernelGGL(k_rga_scnt_scan, dim3(1), dim3(RS_NT), 0, st, scnt, soff, nl, *out);
+  } else {
+    RGA_TRY((scan_excl<OpSum, u32, u32>(scnt, soff, nl, nullptr, part, totals, st)));
+  }
   hipLaunchKernelGGL(k_rga_out, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE))), dim3(BLOCK), 0, st, tmp_v, tmp_s, lstart,
                      scnt, soff, nl, *out);
-  hipLaunchKernelGGL(k_rga_fin, dim3(1), dim3(1), 0, st, totals, nl, *out);
+  if (nl > RS_MAX) hipLaunchKernelGGL(k_rga_fin, dim3(1), dim3(1), 0, st, totals, nl, *out);
   RGA_TRY(hipGetLastError());
   i32 herr = 0;
   RGA_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
