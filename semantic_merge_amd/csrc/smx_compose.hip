@@ -1048,7 +1048,7 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   C.tm->begin(ST_PLAN);
   HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
   if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
-  if (tgt > WIN_CAP) tgt = WIN_CAP;
+  if (tgt > WF_CAP) tgt = WF_CAP;
   tgt -= tgt % CH;  // chunk-aligned diagonals (k_fpart's sampled first level)
   const i64 W = SMX_CEIL_DIV(C.n, tgt);
   const i64 CM = SMX_CEIL_DIV(C.na > C.nb ? C.na : C.nb, (i64)CH) + 1;
@@ -1083,11 +1083,12 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   P.W = W;
   P.ablate = env_int("SMX_ABLATE", 0);
   C.tm->begin(ST_WINDOW);
-  if (g_phase_dbg && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
+  if (g_phase_dbg && !P.src_map && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
     P.dbg = (u64*)g_phase_dbg;
-    hipLaunchKernelGGL(k_window_f<true>, dim3(W), dim3(WF_NT), 0, st, P);
+    hipLaunchKernelGGL((k_window_f<true, false>), dim3(W), dim3(WF_NT), 0, st, P);
   } else {
-    hipLaunchKernelGGL(k_window_f<false>, dim3(W), dim3(WF_NT), 0, st, P);
+    if (P.src_map) hipLaunchKernelGGL((k_window_f<false, true>), dim3(W), dim3(WF_NT), 0, st, P);
+    else hipLaunchKernelGGL((k_window_f<false, false>), dim3(W), dim3(WF_NT), 0, st, P);
   }
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_WINDOW);

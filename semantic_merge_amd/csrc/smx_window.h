@@ -36,7 +36,9 @@
 #include "smx_common.h"
 
 #define WIN_CAP 2048               // max ops per window held in LDS
+#ifndef WIN_TGT
 #define WIN_TGT 1792               // default target window size, presorted path (SMX_WIN_TGT)
+#endif
 #define WIN_TGT_MIN 256
 #define NCNT (SMX_N_KINDS + 3)     // kinds, renames per branch, moves with a None value
 #define CNT_REN_A SMX_N_KINDS
@@ -105,6 +107,15 @@ __device__ __forceinline__ void win_publish_widths(ComposeMeta* meta, const u32*
     for (int w = 0; w < nw; ++w) m |= vbw[w * 3 + q];
     const u32 cur = __hip_atomic_load(&meta->vbits[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((cur | m) != cur) atomicOr(&meta->vbits[q], m);
+  }
+}
+// ... with the published widths read beforehand (cur[3]): no global round trip here
+__device__ __forceinline__ void win_publish_widths(ComposeMeta* meta, const u32* vbw, int nw, const u32* cur) {
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    u32 m = 0;
+    for (int w = 0; w < nw; ++w) m |= vbw[w * 3 + q];
+    if ((cur[q] | m) != cur[q]) atomicOr(&meta->vbits[q], m);
   }
 }
 
@@ -181,8 +192,13 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_NT
 #define WF_NT 512
 #endif
+#ifndef WF_CAP
+#define WF_CAP WIN_CAP              // max ops per presorted window
+#endif
+#define WF_NCH (WF_CAP / WAVE)
 #define WF_WAVES (WF_NT / WAVE)
-#define WF_ITEMS (WIN_CAP / WF_NT)
+#define WF_ITEMS (WF_CAP / WF_NT)
+#define WF_KP ((2 * CH + WF_NT - 1) / WF_NT)  // partial-chunk kinds per lane
 
 // LDS ~34 KB (buffers are reused across phases) so 4 workgroups fit a CU: while
 // some workgroups run their LDS phases, others stream their windows from HBM.
@@ -194,17 +210,19 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
     if (DBG && t == 0) P.dbg[w * WF_NSTAMP + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
-template <bool DBG>
+// MAP: the sample-sorted shard's source map (P.src_map) is read; a separate instance so
+// that the plain path's store loop has no load whose wait would also drain its stores
+template <bool DBG, bool MAP>
 __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
-  __shared__ __attribute__((aligned(16))) u64 sts[WIN_CAP];  // element space: timestamps; later slot-space rank keys
-  __shared__ u16 sord[WIN_CAP];       // S order (merge), later the final order
-  __shared__ u16 fin[WIN_CAP];        // slot -> element, later rename ranks
-  __shared__ u16 sl[WIN_CAP];         // element -> slot, later rank -> slot, later posl
-  __shared__ u8 skind[WIN_CAP];
-  __shared__ u8 skS[WIN_CAP];         // kinds in S order
-  __shared__ u64 gbits[NCHUNK];       // group-start bits over slots, later candidate ballots
-  __shared__ u16 ccnt[NCHUNK][SMX_N_KINDS];
-  __shared__ u16 rc[NCHUNK][2];
+  __shared__ __attribute__((aligned(16))) u64 sts[WF_CAP];  // element space: timestamps; later slot-space rank keys
+  __shared__ u16 sord[WF_CAP];       // S order (merge), later the final order
+  __shared__ u16 fin[WF_CAP];        // slot -> element, later rename ranks
+  __shared__ u16 sl[WF_CAP];         // element -> slot, later rank -> slot, later posl
+  __shared__ u8 skind[WF_CAP];
+  __shared__ u8 skS[WF_CAP];         // kinds in S order
+  __shared__ u64 gbits[WF_NCH];       // group-start bits over slots, later candidate ballots
+  __shared__ u16 ccnt[WF_NCH][SMX_N_KINDS];
+  __shared__ u16 rc[WF_NCH][2];
   __shared__ u32 kbase[SMX_N_KINDS + 1];
   __shared__ u32 wck[SMX_N_KINDS];
   __shared__ u64 base[SMX_N_KINDS + 1];
@@ -221,7 +239,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   const int na = (int)(P.bnd[2 * w + 2] - a0);
   const int nb = (int)(P.bnd[2 * w + 3] - b0);
   const int sz = na + nb;
-  if (na < 0 || nb < 0 || sz > WIN_CAP) {  // the presorted plan does not hold
+  if (na < 0 || nb < 0 || sz > WF_CAP) {  // the presorted plan does not hold
     // bit 0: branch logs not timestamp-ordered; bit 1: window too large for LDS;
     // bit 2: ... and it holds one timestamp only, so smaller windows cannot help
     if (threadIdx.x == 0) {
@@ -247,6 +265,44 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   i32 v0_r[WF_ITEMS], v1_r[WF_ITEMS];
   u32 k_r[WF_ITEMS];
   bool bad = false;
+  // every global read of the window is issued here, before any loaded value is used:
+  // the load phase is one round trip to memory, and the later phases find their
+  // operands in registers (no dependent global reads between barriers).  The few side
+  // reads go first, so that their address arithmetic never waits on the bulk loads.
+  // kinds of the <= 255 ops between each branch's chunk start and the window start
+  // (window offsets below); entries 0..255 branch A, 256..511 branch B
+  u32 kpart[WF_KP];
+#pragma unroll
+  for (int u = 0; u < WF_KP; ++u) {
+    const int x = t + WF_NT * u;
+    const int pa = (int)(a0 % CH), pb = (int)(b0 % CH);
+    const int side = x >= CH;
+    const int q = x - side * CH;
+    kpart[u] = 0xffffffffu;
+    if (x < 2 * CH && q < (side ? pb : pa)) kpart[u] = P.kind[side ? (P.na + P.bgap + b0 - pb + q) : (a0 - pa + q)];
+  }
+  // timestamps just before the window on each branch
+  u64 prev_a = 0, prev_b = 0;
+  if (t == 0 && a0 > 0) prev_a = P.kts[a0 - 1];
+  if (t == 0 && b0 > 0) prev_b = P.kts[P.na + P.bgap + b0 - 1];
+  // T-order segment starts; window offsets = chunk prefix at the window start + kinds
+  // of the <= 255 ops between that chunk start and the window start (per branch)
+  const u64 base_v = t <= SMX_N_KINDS ? P.meta->base[t] : 0ull;
+  u32 woff_x = 0, woff_y = 0;  // (added where stored: an add here would wait for every load)
+  // (32-bit chunk indices: 2 * kinds * CM < 2^32 for any n < 2^31, the i32 output limit)
+  if (t < SMX_N_KINDS) {
+    woff_x = P.cpre[(u32)t * (u32)P.CM + (u32)(a0 / CH)];
+    woff_y = P.cpre[(u32)(SMX_N_KINDS + t) * (u32)P.CM + (u32)(b0 / CH)];
+  } else if (t < SMX_N_KINDS + 2) {
+    const int sd = t - SMX_N_KINDS;
+    woff_x = P.cpre[(u32)(sd * SMX_N_KINDS + KREN) * (u32)P.CM + (u32)((sd ? b0 : a0) / CH)];
+  }
+  // value widths published so far (a stale read only costs a redundant atomicOr)
+  u32 vcur[3] = {0u, 0u, 0u};
+  if (t == 0) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) vcur[q] = __hip_atomic_load(&P.meta->vbits[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // all loads are issued unconditionally (clamped to a valid op) so that the
   // loads of a lane are in flight together; the guards apply to the LDS stores only
   u64 ts_r[WF_ITEMS];
@@ -294,31 +350,11 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     vbw[wv][1] = vb_f;
     vbw[wv][2] = vb_c;
   }
-  // kinds of the <= 255 ops between each branch's chunk start and the window start
-  // (window offsets below); lanes 0..255 branch A, 256..511 branch B
-  u32 kpart = 0xffffffffu;
-  {
-    const int pa = (int)(a0 % CH), pb = (int)(b0 % CH);
-    const int side = t >= CH;
-    const int q = t - side * CH;
-    if (q < (side ? pb : pa)) kpart = P.kind[side ? (P.na + P.bgap + b0 - pb + q) : (a0 - pa + q)];
-  }
-  // timestamps just before the window on each branch (issued with the loads above)
-  u64 prev_a = 0, prev_b = 0;
-  if (t == 0 && a0 > 0) prev_a = P.kts[a0 - 1];
-  if (t == 0 && b0 > 0) prev_b = P.kts[P.na + P.bgap + b0 - 1];
   if (bad) P.meta->bad_sym = 1;
-  for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
-  if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
+  for (int i = t; i < WF_NCH * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
+  if (t <= SMX_N_KINDS) base[t] = base_v;
   if (t < SMX_N_KINDS) wck[t] = 0;
-  // window offsets = chunk prefix at the window start + kinds of the <= 255 ops
-  // between that chunk start and the window start (per branch)
-  if (t < SMX_N_KINDS) {
-    woffk[t] = P.cpre[(i64)t * P.CM + a0 / CH] + P.cpre[(i64)(SMX_N_KINDS + t) * P.CM + b0 / CH];
-  } else if (t < SMX_N_KINDS + 2) {
-    const int sd = t - SMX_N_KINDS;
-    woffk[t] = P.cpre[(i64)(sd * SMX_N_KINDS + KREN) * P.CM + (sd ? b0 : a0) / CH];
-  }
+  if (t < SMX_N_KINDS + 2) woffk[t] = woff_x + woff_y;
   __syncthreads();
   WSTAMP(1);
   if (P.ablate & 16) {  // diagnostics: load only (keeps every load live)
@@ -329,10 +365,13 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     return;
   }
   // window offsets: the partial-chunk kinds
-  if (kpart != 0xffffffffu) {
-    const u32 k = kpart < SMX_N_KINDS ? kpart : SMX_N_KINDS - 1;
-    atomicAdd(&woffk[k], 1u);
-    if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + (t >= CH)], 1u);
+#pragma unroll
+  for (int u = 0; u < WF_KP; ++u) {
+    if (kpart[u] != 0xffffffffu) {
+      const u32 k = kpart[u] < SMX_N_KINDS ? kpart[u] : SMX_N_KINDS - 1;
+      atomicAdd(&woffk[k], 1u);
+      if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + (t + WF_NT * u >= CH)], 1u);
+    }
   }
 
   // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties
@@ -343,8 +382,8 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   //    the merge.
   bool dec = false;
   if (t == 0) {
-    dec = (a0 > 0 && na > 0 && prev_a > ts_r[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
-    win_publish_widths(P.meta, &vbw[0][0], WF_WAVES);
+    dec = (a0 > 0 && na > 0 && prev_a > sts[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
+    win_publish_widths(P.meta, &vbw[0][0], WF_WAVES, vcur);
   }
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
@@ -440,7 +479,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
       f = (p == (int)kbase[skind[e]]) || (sts[fin[p - 1]] != sts[e]);
     }
     const u64 b = __ballot(f);
-    if (lane == 0 && (p >> 6) < NCHUNK) gbits[p >> 6] = b;
+    if (lane == 0 && (p >> 6) < WF_NCH) gbits[p >> 6] = b;
   }
   __syncthreads();
   WSTAMP(8);
@@ -542,7 +581,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   //    (rare) exact re-rank.
   const int R0 = kbase[KREN], RN = wck[KREN];
   const int nrc = (RN + WAVE - 1) / WAVE;
-  constexpr int RQ = (NCHUNK + WF_WAVES - 1) / WF_WAVES;  // rename chunks per wave
+  constexpr int RQ = (WF_NCH + WF_WAVES - 1) / WF_WAVES;  // rename chunks per wave
   u32 rown_r[RQ];
   auto rename_ranks = [&](bool store) {
 #pragma unroll
@@ -624,8 +663,8 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
   // 7. payload by element, round 1: sym (| the move's has-value bits) and v0; the
   //    position of each rename in its branch's list (posl)
   if (P.ablate & 4) return;
-  u32* st_a = (u32*)sts;             // [WIN_CAP] sym | flags
-  i32* st_b = (i32*)sts + WIN_CAP;   // [WIN_CAP] v0, then v1
+  u32* st_a = (u32*)sts;             // [WF_CAP] sym | flags
+  i32* st_b = (i32*)sts + WF_CAP;   // [WF_CAP] v0, then v1
   u16* posl = sl;
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
@@ -673,7 +712,7 @@ __global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
     const i64 j = e < na ? a0 + e : bpos + e;
     const u32 sa = st_a[e];
     if (k == KMOVE) {
-      P.out_order[T] = win_gsrc(P, j);
+      P.out_order[T] = MAP ? P.src_map[j] : (j < P.na ? (i32)(P.src_a + j) : (i32)(P.src_b + (j - P.na)));
       P.out_addr[T] = st_b[e];
       P.out_ctx[T] = -1;
       P.msym[T] = sa;
