@@ -267,18 +267,17 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 // kinds of at most 255 ops before it.  Coalesced: iteration j of a block reads
 // chunk j, lane t its byte t.
 #define CH_PER_BLOCK (BLOCK / 16)   // 16 lanes x 16 kind bytes per 256-op chunk
-#define KH_COPIES 8                 // counter copies (lane & 7) against LDS atomic conflicts
 
 // Block b counts global chunks [b*CH_PER_BLOCK, ...) (A chunks, then B chunks):
 // lane t reads bytes [16*(t%16), +16) of chunk t/16 (one 16-byte load when
-// aligned) and adds each byte to its (chunk, kind) counter with an LDS atomic
-// into one of KH_COPIES copies.
+// aligned), so a chunk is one 16-lane DPP row.  No atomics: each lane counts its 16
+// kinds in packed 5-bit fields (6 kinds per word), widens them to 10-bit fields and
+// the row adds them up with DPP shifts; the row's last lane holds the chunk's counts.
 __global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, const u64* __restrict__ ts,
                                                  i64 na, i64 nb, i64 bgap, i64 CM, u32* __restrict__ cnt,
                                                  u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta) {
-  __shared__ u32 c[KH_COPIES][CH_PER_BLOCK][SMX_N_KINDS];
+  __shared__ u32 c[CH_PER_BLOCK][SMX_N_KINDS];
   const i64 CA = SMX_CEIL_DIV(na, (i64)CH), CB = SMX_CEIL_DIV(nb, (i64)CH);
-  for (int i = threadIdx.x; i < KH_COPIES * CH_PER_BLOCK * SMX_N_KINDS; i += BLOCK) (&c[0][0][0])[i] = 0;
   const int j = threadIdx.x / 16, q = threadIdx.x % 16;
   const i64 g = (i64)blockIdx.x * CH_PER_BLOCK + j;
   const int side = g >= CA;
@@ -301,8 +300,7 @@ __global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, co
     for (int y = 0; y < 16; ++y)
       if (y < nv) w[y >> 2] |= (u32)src[y] << (8 * (y & 3));
   }
-  __syncthreads();
-  u32* ck = c[threadIdx.x & (KH_COPIES - 1)][j];
+  u32 pk[3] = {0u, 0u, 0u};  // kind k: bits 5 * (k % 6) of word k / 6
   bool bad = false;
 #pragma unroll
   for (int y = 0; y < 16; ++y) {
@@ -310,19 +308,41 @@ __global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, co
     u32 k = (w[y >> 2] >> (8 * (y & 3))) & 0xffu;
     bad |= k >= SMX_N_KINDS;
     k = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
-    atomicAdd(&ck[k], 1u);
+    const u32 wd = (k * 43u) >> 8;  // k / 6 for k < 18
+    const u32 inc = 1u << (5u * (k - 6u * wd));
+    pk[0] += wd == 0 ? inc : 0u;
+    pk[1] += wd == 1 ? inc : 0u;
+    pk[2] += wd == 2 ? inc : 0u;
   }
-  if (bad) meta->bad_sym = 1;
+  if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) meta->bad_sym = 1;
+  // 10-bit fields (a chunk count is at most 256), three kinds per word; row sums
+  u32 f[6];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    f[2 * i] = (pk[i] & 31u) | ((pk[i] >> 5) & 31u) << 10 | ((pk[i] >> 10) & 31u) << 20;
+    f[2 * i + 1] = ((pk[i] >> 15) & 31u) | ((pk[i] >> 20) & 31u) << 10 | ((pk[i] >> 25) & 31u) << 20;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    u32 v = f[i];
+    v += dpp_u32<0x111, 0xf>(v);  // row_shr:1
+    v += dpp_u32<0x112, 0xf>(v);  // row_shr:2
+    v += dpp_u32<0x114, 0xf>(v);  // row_shr:4
+    v += dpp_u32<0x118, 0xf>(v);  // row_shr:8
+    f[i] = v;
+  }
+  if (q == 15) {
+#pragma unroll
+    for (int k = 0; k < SMX_N_KINDS; ++k) c[j][k] = (f[k / 3] >> (10 * (k % 3))) & 1023u;
+  }
   __syncthreads();
+  // column-major output: consecutive threads write consecutive chunks of one column
   for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += BLOCK) {
-    const int jj = i / SMX_N_KINDS, k = i % SMX_N_KINDS;
+    const int jj = i % CH_PER_BLOCK, k = i / CH_PER_BLOCK;
     const i64 gg = (i64)blockIdx.x * CH_PER_BLOCK + jj;
     if (gg >= CA + CB) continue;
-    u32 s = 0;
-#pragma unroll
-    for (int cp = 0; cp < KH_COPIES; ++cp) s += c[cp][jj][k];
     const int sd = gg >= CA;
-    cnt[((i64)sd * SMX_N_KINDS + k) * CM + (sd ? gg - CA : gg)] = s;
+    cnt[((i64)sd * SMX_N_KINDS + k) * CM + (sd ? gg - CA : gg)] = c[jj][k];
   }
 }
 
