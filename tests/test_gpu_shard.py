@@ -98,11 +98,14 @@ def _hollow_soa(n_ren, seed):
     return SoA(na, nb, kind, ts, hi, lo, sym, v0, v0.copy(), 1, ["a", "b"])
 
 
-def _worker(rank, world, port, case, halo, q, mode="auto"):
+def _worker(rank, world, port, case, halo, q, mode="auto", backend="gloo"):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: one rank per GPU
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from semantic_merge_amd import shard
         soa = _make(case)
@@ -123,11 +126,12 @@ def _worker(rank, world, port, case, halo, q, mode="auto"):
         dist.destroy_process_group()
 
 
-def _run(case, world, halo=4096, mode="auto"):
+def _run(case, world, halo=4096, mode="auto", backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, halo, q, mode)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, halo, q, mode, backend))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -141,10 +145,10 @@ def _run(case, world, halo=4096, mode="auto"):
     return [got[r][0] for r in range(world)], got
 
 
-def _check(case, world, halo=4096, mode="auto", want_mode=None):
+def _check(case, world, halo=4096, mode="auto", want_mode=None, backend="gloo"):
     from oracle import oracle
     from semantic_merge_amd import shard
-    parts, got = _run(case, world, halo, mode)
+    parts, got = _run(case, world, halo, mode, backend)
     glob = shard.assemble(parts)
     ref = oracle.compose(_make(case))
     names = ("order", "addr", "file", "ctx", "conflicts")
@@ -158,6 +162,16 @@ def _check(case, world, halo=4096, mode="auto", want_mode=None):
         if want_mode:
             assert emode == want_mode, emode
     return got, ref
+
+
+@pytest.mark.parametrize("mode", ["range", "sample"])
+def test_shard_rccl_single_rank(mode):
+    """The RCCL branch of shard.Comm (collectives on device tensors: all_gather_into_tensor,
+    MAX all_reduce on int64, all_to_all_single of packed uint8 records) on one GPU: a
+    one-rank "nccl" group runs the whole sharded step sequence, checked against the oracle.
+    (More ranks need one GPU each: the driver's node.)"""
+    _check(("lift", 60_000, 2_000, 5), 1, mode=mode, backend="nccl",
+           want_mode=None)
 
 
 def test_shard_lift_two_ranks():
