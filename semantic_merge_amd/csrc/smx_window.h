@@ -777,6 +777,11 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   __shared__ u64 cb[NCHUNK];
   __shared__ u32 wtot[2];
   __shared__ u32 vbw[WG_NT / WAVE][3];
+  __shared__ u32 woffk[NCNT];
+  // after the merge the id words are dead: the payload by element takes their place
+  u32* st_sym = reinterpret_cast<u32*>(shi);
+  i32* st_v0 = reinterpret_cast<i32*>(shi) + WIN_CAP;
+  i32* st_v1 = reinterpret_cast<i32*>(slo);
 
   const int t = threadIdx.x;
   const int lane = t & (WAVE - 1);
@@ -787,23 +792,49 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   const int nb = (int)(P.bnd[2 * w + 3] - b0);
   const int sz = na + nb;
 
+  // loads: the sorted keys and the permutation, then the op fields through it (two
+  // round trips, every item's loads in flight together; the payload stays in registers
+  // until the merge is done)
   bool bad = false;
   u32 vb_a = 0, vb_f = 0, vb_c = 0;
-  for (int e = t; e < sz; e += WG_NT) {
-    const i64 j = e < na ? a0 + e : P.na + b0 + (e - na);
-    const u32 src = P.perm[j];
-    sts[e] = P.kts[j];
-    shi[e] = P.khi[j];
-    slo[e] = P.klo[j];
-    ssrc[e] = src;
-    const u32 k = P.kind[src];
-    bad |= (k >= SMX_N_KINDS) || (P.sym[src] >= (u64)P.n_sym);
+  u32 src_r[WG_ITEMS], k_r[WG_ITEMS], sym_r[WG_ITEMS];
+  i32 v0_r[WG_ITEMS], v1_r[WG_ITEMS];
+  u64 kt_r[WG_ITEMS], kh_r[WG_ITEMS], kl_r[WG_ITEMS];
+#pragma unroll
+  for (int i = 0; i < WG_ITEMS; ++i) {
+    const int e = t + WG_NT * i;
+    const int ec = e < sz ? e : 0;
+    const i64 j = sz == 0 ? 0 : (ec < na ? a0 + ec : P.na + b0 + (ec - na));
+    src_r[i] = P.perm[j];
+    kt_r[i] = P.kts[j];
+    kh_r[i] = P.khi[j];
+    kl_r[i] = P.klo[j];
+  }
+  if (t < NCNT) woffk[t] = P.woff[(i64)t * P.W + w];
+#pragma unroll
+  for (int i = 0; i < WG_ITEMS; ++i) {
+    const u32 src = src_r[i];
+    k_r[i] = P.kind[src];
+    sym_r[i] = P.sym[src];
+    v0_r[i] = P.v0[src];
+    v1_r[i] = P.v1[src];
+  }
+#pragma unroll
+  for (int i = 0; i < WG_ITEMS; ++i) {
+    const int e = t + WG_NT * i;
+    if (e >= sz) continue;
+    sts[e] = kt_r[i];
+    shi[e] = kh_r[i];
+    slo[e] = kl_r[i];
+    ssrc[e] = src_r[i];
+    const u32 k = k_r[i];
+    bad |= (k >= SMX_N_KINDS) || (sym_r[i] >= (u64)P.n_sym);
     skind[e] = (u8)(k < SMX_N_KINDS ? k : SMX_N_KINDS - 1);
     if (k == KMOVE) {
-      vb_a |= (u32)(P.v0[src] + 1);
-      vb_f |= (u32)(P.v1[src] + 1);
+      vb_a |= (u32)(v0_r[i] + 1);
+      vb_f |= (u32)(v1_r[i] + 1);
     } else if (k == KREN) {
-      vb_c |= (u32)(P.v1[src] + 1);
+      vb_c |= (u32)(v1_r[i] + 1);
     }
   }
   vb_a = wave_or_to_last(vb_a);
@@ -843,6 +874,15 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
     }
   }
   __syncthreads();
+#pragma unroll
+  for (int i = 0; i < WG_ITEMS; ++i) {  // (visible after the multisplit's barriers)
+    const int e = t + WG_NT * i;
+    if (e < sz) {
+      st_sym[e] = sym_r[i];
+      st_v0[e] = v0_r[i];
+      st_v1[e] = v1_r[i];
+    }
+  }
 
   const int nch = (sz + WAVE - 1) / WAVE;
   for (int c = wv; c < nch; c += WG_NT / WAVE) {
@@ -917,20 +957,20 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
     posl[(s ? cntA : 0) + rc[x >> 6][s] + rown[x]] = (u16)x;
   }
   if (t == 0) {
-    P.wren[2 * w] = P.woff[(i64)KREN * P.W + w];
-    P.wren[2 * w + 1] = P.woff[(i64)CNT_REN_A * P.W + w];
+    P.wren[2 * w] = woffk[KREN];
+    P.wren[2 * w + 1] = woffk[CNT_REN_A];
   }
   __syncthreads();
   win_rename_flags<WG_NT>(
-      P, w, P.woff[(i64)KREN * P.W + w], RN, cntA, cntB, posl, cb,
+      P, w, woffk[KREN], RN, cntA, cntB, posl, cb,
       [&](int x, int* s, int* own) {
         const int e = fin[R0 + x];
         *s = e >= na;
         *own = rc[x >> 6][*s] + rown[x];
       },
       [&](int x) -> uint2 {
-        const u32 src = ssrc[fin[R0 + x]];
-        return make_uint2(P.sym[src], (u32)P.v0[src]);
+        const int e = fin[R0 + x];
+        return make_uint2(st_sym[e], (u32)st_v0[e]);
       });
 
   const u64 nall = (u64)(P.na + P.nb);
@@ -939,11 +979,11 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
     const int e = fin[x];
     const u32 k = skind[e];
     const u32 src = ssrc[e];
-    const u64 T = base[k] + P.woff[(i64)k * P.W + w] + (u32)(x - kbase[k]);
+    const u64 T = base[k] + woffk[k] + (u32)(x - kbase[k]);
     if (T >= nall) continue;
-    const u32 s = P.sym[src];
+    const u32 s = st_sym[e];
     if (k == KMOVE) {
-      const i32 a = P.v0[src], f = P.v1[src];
+      const i32 a = st_v0[e], f = st_v1[e];
       P.out_order[T] = win_gsrc(P, src);
       P.out_addr[T] = a;
       P.out_file[T] = f;
@@ -952,7 +992,7 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
     } else {
       P.tsrc[T - nmv] = (i32)src;
       P.tsym[T - nmv] = s;
-      if (k == KREN) P.Rstr[T - nmv] = P.v1[src];
+      if (k == KREN) P.Rstr[T - nmv] = st_v1[e];
     }
   }
 }
