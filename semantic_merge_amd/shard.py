@@ -230,6 +230,15 @@ class ShardedCompose:
         self.glob = self.part[3 * max(n_sym, 1):]
         self.n_xchg = 0      # ops this rank received from other ranks in the last exchange
         self.order_fixes = 0  # ORDER_FIX runs (dense timestamp ties) on this rank
+        # every timestamp below 2^63 (ISO keys, dense ranks): the signed int64 order of
+        # the stored words is the u64 order, so the splitter search needs no key copy
+        self._ts_signed = [bool((self._orig(br, "ts") >= 0).all()) for br in range(2)]
+        self._sizes = torch.tensor([self.na_s, self.nb_s], dtype=torch.int64, device=dv)
+        self._one = torch.ones(1, dtype=torch.int64, device=dv)
+        self._zero2 = torch.zeros(2, dtype=torch.int64, device=dv)
+        self._signed = torch.tensor([int(x) for x in self._ts_signed], dtype=torch.int64, device=dv)
+        self._bind_key = None
+        self._halo_key = None
 
     def _alloc(self, hd: int, a, b) -> None:
         """Field buffers [hd | A slice | 2 hd | B slice | hd]; a, b: BranchSlices or the
@@ -254,54 +263,80 @@ class ShardedCompose:
         return self.buf[f][self._oa: self._oa + self.na_s] if br == 0 else \
             self.buf[f][self._ob: self._ob + self.nb_s]
 
-    def _range_counts(self):
-        """Device: timestamp splitters from one all_gather of each slice's first / last
-        keys, this rank's op counts per (branch, destination) and the ordered flag:
-        int64 [2 * world + 1]."""
+    def _range_info(self):
+        """Device int64 [9]: this rank's slice sizes, first / last key of each slice
+        (u64 order as int64), whether the slices are ordered, and per branch whether
+        every timestamp is below 2^63 (the cut search below runs on the stored words)."""
         torch = self.torch
-        dv, W = self.dev, self.world
-        info = torch.zeros(7, dtype=torch.int64, device=dv)
-        info[0], info[1] = self.na_s, self.nb_s
-        ok = torch.ones((), dtype=torch.bool, device=dv)
+        parts = [self._sizes]
+        ok = self._one
         for br, n in ((0, self.na_s), (1, self.nb_s)):
             if n:
-                k = _u64_key(self._orig(br, "ts"))
-                info[2 + 2 * br], info[3 + 2 * br] = k[0], k[-1]
+                ts = self._orig(br, "ts")
+                parts.append(_u64_key(torch.stack([ts[0], ts[-1]])))
                 if n > 1 and self.mode == "auto":  # "range": the ORDER plan checks the order itself
-                    ok &= (k[1:] >= k[:-1]).all()
-        info[6] = ok.to(torch.int64)
-        g = self.comm.all_gather(info)                                     # [W, 7]
-        ordered = g[:, 6].min() == 1
+                    k = _u64_key(ts)
+                    ok = (k[1:] >= k[:-1]).all().to(torch.int64).view(1)
+            else:
+                parts.append(self._zero2)
+        return torch.cat(parts + [ok, self._signed])
+
+    @staticmethod
+    def _range_plan(g: np.ndarray):
+        """Host, from every rank's _range_info (g [W, 7]): (ordered, tau) -- the key
+        ranges' lower bounds tau[1..W-1] (shard r owns keys [tau_r, tau_r+1)), the
+        running maximum of the ranks' first keys."""
+        W = g.shape[0]
+        ordered = bool(g[:, 6].min() == 1)
         for br in range(2):                 # slices of a branch must follow each other
             nz = g[:, br] > 0
-            first, last = g[:, 2 + 2 * br], g[:, 3 + 2 * br]
-            lmax = torch.cummax(torch.where(nz, last, torch.full_like(last, I64_MIN)), 0).values
-            prev = torch.cat([torch.full((1,), I64_MIN, dtype=torch.int64, device=dv), lmax[:-1]])
-            ordered &= (~nz | (first >= prev)).all()
-        cand = torch.where(g[:, 0] > 0, g[:, 2], torch.where(g[:, 1] > 0, g[:, 4],
-                                                              torch.full_like(g[:, 2], I64_MIN)))
+            last = np.where(nz, g[:, 3 + 2 * br], I64_MIN)
+            prev = np.concatenate([[I64_MIN], np.maximum.accumulate(last)[:-1]])
+            ordered &= bool((~nz | (g[:, 2 + 2 * br] >= prev)).all())
+        cand = np.where(g[:, 0] > 0, g[:, 2], np.where(g[:, 1] > 0, g[:, 4], I64_MIN)).astype(np.int64)
         cand[0] = I64_MIN
-        tau = torch.cummax(cand, 0).values                                 # shard r owns [tau_r, tau_r+1)
-        counts = []
-        for br, n in ((0, self.na_s), (1, self.nb_s)):
-            if n:
-                cut = torch.searchsorted(_u64_key(self._orig(br, "ts")).contiguous(), tau[1:].contiguous())
-                edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=dv), cut,
-                                   torch.full((1,), n, dtype=torch.int64, device=dv)])
-                counts.append(edges[1:] - edges[:-1])
-            else:
-                counts.append(torch.zeros(W, dtype=torch.int64, device=dv))
-        return torch.cat(counts + [ordered.view(1).to(torch.int64)])
+        return ordered, np.maximum.accumulate(cand)[1:] if W > 1 else np.zeros(0, np.int64)
+
+    def _range_counts(self):
+        """allc [W, 2, W] (src, branch, dest) op counts of the key-range split, or None when
+        the logs are not timestamp-ordered.  Two small host syncs: the ranks' slice ends,
+        then every rank's cut positions (binary searches on the device)."""
+        torch = self.torch
+        W = self.world
+        g = self.comm.all_gather(self._range_info()).cpu().numpy()        # [W, 9]
+        ordered, tau = self._range_plan(g)
+        if not ordered:
+            return None
+        cuts = torch.zeros((2, max(W - 1, 1)), dtype=torch.int64, device=self.dev)
+        if W > 1:
+            tk = torch.from_numpy(tau).to(self.dev)
+            for br, n in ((0, self.na_s), (1, self.nb_s)):
+                if n:
+                    ts = self._orig(br, "ts")
+                    # every timestamp below 2^63: search the stored words (int64 order =
+                    # u64 order); a splitter above 2^63 (key >= 0) is fixed on the host
+                    cuts[br] = torch.searchsorted(ts, _u64_key(tk)) if self._ts_signed[br] else \
+                        torch.searchsorted(_u64_key(ts).contiguous(), tk)
+        gc = self.comm.all_gather(cuts).cpu().numpy()                      # [W, 2, W-1]
+        allc = np.zeros((W, 2, W), np.int64)
+        for q in range(W):
+            for br in range(2):
+                n = int(g[q, br])
+                c = gc[q, br, : W - 1].copy()
+                if W > 1 and g[q, 7 + br]:  # a splitter above every stored word
+                    c[tau >= 0] = n
+                edges = np.concatenate([[0], np.clip(c, 0, n), [n]]) if W > 1 else np.array([0, n])
+                allc[q, br] = np.diff(edges)
+        return allc
 
     def exchange(self) -> None:
         """Every op to the shard owning its key (collective)."""
         self._saved = []
-        W = self.world
         if self.mode != "sample":
-            allc = self.comm.all_gather(self._range_counts()).cpu().numpy()  # the host sync
-            if allc[:, 2 * W].min() == 1:
+            allc = self._range_counts()
+            if allc is not None:
                 self.exchange_mode = "range"
-                self._exchange_range(allc[:, :2 * W].reshape(W, 2, W))
+                self._exchange_range(allc)
                 return
             if self.mode == "range":
                 raise ValueError("sharded merge (mode 'range') needs timestamp-ordered branch logs "
@@ -466,6 +501,11 @@ class ShardedCompose:
     # -- device structs -----------------------------------------------------------------
     def _bind(self) -> None:
         torch = self.torch
+        key = (self.n_a, self.n_b, tuple(map(tuple, self.rng)), self._fields["kind"].data_ptr(),
+               self._map_on, self.src_a, self.src_b)
+        if key == self._bind_key:  # the same layout as the last step (a repeated merge)
+            return
+        self._bind_key = key
         n = self.n_a + self.n_b
         if n > self._outn:
             nn = max(n, 1)
@@ -564,29 +604,37 @@ class ShardedCompose:
 
     def _order_exchange(self) -> None:
         """One all_gather of every shard's summary and halo exports; this shard's halo
-        (the first H renames of each branch on the following shards) assembled on the
-        device."""
+        (the first H renames of each branch on the following shards) gathered from them
+        on the device by indices computed on the host from the (small) summaries."""
         torch = self.torch
         H, r, W, dv = self.H, self.rank, self.world, self.dev
         g = self.comm.all_gather(torch.cat([self.summary, self.xport.reshape(-1).view(torch.int64)]))
         if H <= 0:
             self.halo_dev.zero_()
             return
-        summ = g[:, :SUM]
-        X = g[:, SUM:].contiguous().view(torch.int32).reshape(W, 3, 2 * H)
-        later = (torch.arange(W, device=dv) > r).to(torch.int64)
-        i = torch.arange(H, device=dv)
-        st = []
-        for b in range(2):
-            after = summ[:, S_REN + b] * later
-            c = after.clamp(max=H)
-            cum = torch.cumsum(c, 0)
-            got = cum[-1].clamp(max=H)
-            q = torch.searchsorted(cum, i, right=True).clamp(max=W - 1)
-            off = (i - (cum[q] - c[q])).clamp(min=0, max=H - 1)
-            self.halo[b].copy_(X[q, :, b * H + off].t())
-            st.append((got, (after.sum() > got).to(torch.int64)))
-        self.halo_dev.copy_(torch.stack([st[0][0], st[1][0], st[0][1], st[1][1]]))
+        summ = g[:, :SUM].cpu().numpy()
+        key = summ[:, S_REN:S_REN + 2].tobytes()
+        if key != self._halo_key:  # (a repeated merge reuses its indices)
+            idx = np.zeros((2, 3, H), np.int64)
+            st = []
+            i = np.arange(H)
+            for b in range(2):
+                after = summ[:, S_REN + b] * (np.arange(W) > r)
+                c = np.minimum(after, H)
+                cum = np.cumsum(c)
+                got = int(min(cum[-1], H))
+                q = np.minimum(np.searchsorted(cum, i, side="right"), W - 1)
+                off = np.clip(i - (cum[q] - c[q]), 0, H - 1)
+                for f in range(3):  # X[q, f, b * H + off] of the [W, 3, 2H] int32 exports
+                    idx[b, f] = (q * 3 + f) * 2 * H + b * H + off
+                st.append((got, int(after.sum() > got)))
+            self._halo_idx = torch.from_numpy(idx.reshape(-1)).to(dv)
+            self._halo_st = torch.tensor([st[0][0], st[1][0], st[0][1], st[1][1]], dtype=torch.int64,
+                                         device=dv)
+            self._halo_key = key
+        X = g[:, SUM:].contiguous().view(torch.int32).reshape(-1)
+        self.halo.view(-1).copy_(X[self._halo_idx])
+        self.halo_dev.copy_(self._halo_st)
 
     def _walk(self) -> np.ndarray:
         """Walk with the incoming open region of the previous shards (device-held); one
