@@ -247,7 +247,7 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
   const i64 k = (i64)blockIdx.x * BLOCK + threadIdx.x;
   if (k > W) return;
   const i64 n = na + nb;
-  const i64 d = k * WIN_CAP;
+  const i64 d = k * WG_CAP;
   if (k == 0) { bnd[0] = 0; bnd[1] = 0; return; }
   if (d >= n || k == W) { bnd[2 * k] = na; bnd[2 * k + 1] = nb; return; }
   i64 lo = d - nb > 0 ? d - nb : 0, hi = d < na ? d : na;
@@ -1390,7 +1390,7 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
     }
     if (!with_lo) hipLaunchKernelGGL(k_dupcheck, dim3(grid_for(n)), dim3(BLOCK), 0, st, sts, shi, na, n, meta);
   }
-  const i64 W = SMX_CEIL_DIV(n, (i64)WIN_CAP);
+  const i64 W = SMX_CEIL_DIV(n, (i64)WG_CAP);
   hipLaunchKernelGGL(k_gpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, sts, shi, slo, na, nb,
                      W, bnd);
   hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, C.ops->kind, C.ops->v0, C.ops->v1, perm, bnd, na, W,

@@ -754,33 +754,39 @@ __device__ __forceinline__ bool key_le(u64 ta, u64 ha, u64 la, u64 tb, u64 hb, u
   return la <= lb;
 }
 
-#ifndef WG_NT
-#define WG_NT 1024
+// 1024-op windows on 512 threads: 38 KB of LDS, four windows per CU (2048-op windows
+// took 75 KB, two per CU; config 5 window stage 0.80 -> 0.61 ms, profiles/r02_i)
+#ifndef WG_CAP
+#define WG_CAP 1024                 // ops per generic window (fixed diagonals, k_gpart)
 #endif
-#define WG_ITEMS (WIN_CAP / WG_NT)
+#ifndef WG_NT
+#define WG_NT 512
+#endif
+#define WG_ITEMS (WG_CAP / WG_NT)
+#define WG_NCH (WG_CAP / WAVE)
 
 __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
-  __shared__ u64 sts[WIN_CAP];
-  __shared__ u64 shi[WIN_CAP];
-  __shared__ u64 slo[WIN_CAP];
-  __shared__ u32 ssrc[WIN_CAP];
-  __shared__ u16 sord[WIN_CAP];       // merge order, later posl
-  __shared__ u16 fin[WIN_CAP];
-  __shared__ u16 rown[WIN_CAP];
-  __shared__ u8 skind[WIN_CAP];
-  __shared__ u8 srank[WIN_CAP];
-  __shared__ u16 ccnt[NCHUNK][SMX_N_KINDS];
-  __shared__ u16 rc[NCHUNK][2];
+  __shared__ u64 sts[WG_CAP];
+  __shared__ u64 shi[WG_CAP];
+  __shared__ u64 slo[WG_CAP];
+  __shared__ u32 ssrc[WG_CAP];
+  __shared__ u16 sord[WG_CAP];       // merge order, later posl
+  __shared__ u16 fin[WG_CAP];
+  __shared__ u16 rown[WG_CAP];
+  __shared__ u8 skind[WG_CAP];
+  __shared__ u8 srank[WG_CAP];
+  __shared__ u16 ccnt[WG_NCH][SMX_N_KINDS];
+  __shared__ u16 rc[WG_NCH][2];
   __shared__ u32 kbase[SMX_N_KINDS + 1];
   __shared__ u32 wck[SMX_N_KINDS];
   __shared__ u64 base[SMX_N_KINDS + 1];
-  __shared__ u64 cb[NCHUNK];
+  __shared__ u64 cb[WG_NCH];
   __shared__ u32 wtot[2];
   __shared__ u32 vbw[WG_NT / WAVE][3];
   __shared__ u32 woffk[NCNT];
   // after the merge the id words are dead: the payload by element takes their place
   u32* st_sym = reinterpret_cast<u32*>(shi);
-  i32* st_v0 = reinterpret_cast<i32*>(shi) + WIN_CAP;
+  i32* st_v0 = reinterpret_cast<i32*>(shi) + WG_CAP;
   i32* st_v1 = reinterpret_cast<i32*>(slo);
 
   const int t = threadIdx.x;
@@ -846,7 +852,7 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
     vbw[wv][2] = vb_c;
   }
   if (bad) P.meta->bad_sym = 1;
-  for (int i = t; i < NCHUNK * SMX_N_KINDS; i += WG_NT) (&ccnt[0][0])[i] = 0;
+  for (int i = t; i < WG_NCH * SMX_N_KINDS; i += WG_NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = P.meta->base[t];
   __syncthreads();
 
