@@ -20,9 +20,14 @@ def _free_port():
     return port
 
 
-def _soa(n, seed, ops_per_ms):
+def _soa(n, seed, ops_per_ms, high=False):
     from semantic_merge_amd import synth
-    return synth.lift_soa(synth.lift_logs(synth.LiftSpec(n, 50, seed, ops_per_ms=ops_per_ms)))
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(n, 50, seed, ops_per_ms=ops_per_ms)))
+    if high:  # the later half of each branch above 2^63: still ordered as u64, and the
+        # ranks holding it take the unsigned splitter search, the others the signed one
+        for lo, m in ((0, soa.n_a), (soa.n_a, soa.n_b)):
+            soa.ts[lo + m // 2: lo + m] |= np.uint64(1 << 63)
+    return soa
 
 
 def _worker(rank, world, port, args, q):
@@ -32,8 +37,8 @@ def _worker(rank, world, port, args, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from semantic_merge_amd import shard
-        n, seed, opm, headroom = args
-        soa = _soa(n, seed, opm)
+        n, seed, opm, headroom, high = args
+        soa = _soa(n, seed, opm, high)
         a, b, na, nb = shard.slices_from_soa(soa, rank, world, "cpu")
         sc = shard.ShardedCompose(a, b, na, nb, soa.n_sym, shard.Comm(), "cpu", halo_cap=64,
                                   headroom=headroom)
@@ -54,14 +59,16 @@ def _worker(rank, world, port, args, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,opm,headroom", [(2, 20_000, 64, None), (3, 30_000, 7, None),
-                                                  (3, 9_000, 1000, 0)])
-def test_exchange_key_ranges(world, n, opm, headroom):
+@pytest.mark.parametrize("world,n,opm,headroom,high", [(2, 20_000, 64, None, False),
+                                                       (3, 30_000, 7, None, False),
+                                                       (3, 9_000, 1000, 0, False),
+                                                       (4, 24_000, 64, None, True)])
+def test_exchange_key_ranges(world, n, opm, headroom, high):
     from semantic_merge_amd import shard
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    args = (n, 3, opm, headroom)
+    args = (n, 3, opm, headroom, high)
     procs = [ctx.Process(target=_worker, args=(r, world, port, args, q)) for r in range(world)]
     for p in procs:
         p.start()
@@ -73,7 +80,7 @@ def test_exchange_key_ranges(world, n, opm, headroom):
         p.join(60)
     errs = [res[r][1] for r in range(world) if isinstance(res[r][1], str)]
     assert not errs, errs
-    soa = _soa(n, 3, opm)
+    soa = _soa(n, 3, opm, high)
     na, nb = soa.n_a, soa.n_b
     cols = {"kind": soa.kind, "ts": soa.ts.view(np.int64), "hi": soa.oid_hi.view(np.int64),
             "lo": soa.oid_lo.view(np.int64), "sym": soa.sym.view(np.int32), "v0": soa.v0, "v1": soa.v1}
