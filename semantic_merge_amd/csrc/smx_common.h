@@ -43,6 +43,7 @@ struct ComposeMeta {
   u64 dup_key;               // generic plan: equal (ts, oid_hi) pair seen -> sort with oid_lo
   u64 seg_over;              // segmented plan: a timestamp group too long, or a branch not ordered
   u64 n_win;                 // windows of the plan that ran
+  u32 kmask[2];              // presorted plan: kinds present per branch (k_khist)
 };
 
 // Per-symbol final states (addr, file, ctx).  When the bit widths of (value + 1)

@@ -277,8 +277,10 @@ __global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, co
                                                  i64 na, i64 nb, i64 bgap, i64 CM, u32* __restrict__ cnt,
                                                  u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta) {
   __shared__ u32 c[CH_PER_BLOCK][SMX_N_KINDS];
+  __shared__ u32 km[2];
   const i64 CA = SMX_CEIL_DIV(na, (i64)CH), CB = SMX_CEIL_DIV(nb, (i64)CH);
   const int j = threadIdx.x / 16, q = threadIdx.x % 16;
+  if (threadIdx.x < 2) km[threadIdx.x] = 0;
   const i64 g = (i64)blockIdx.x * CH_PER_BLOCK + j;
   const int side = g >= CA;
   const i64 cc = side ? g - CA : g;
@@ -336,14 +338,35 @@ __global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, co
     for (int k = 0; k < SMX_N_KINDS; ++k) c[j][k] = (f[k / 3] >> (10 * (k % 3))) & 1023u;
   }
   __syncthreads();
-  // column-major output: consecutive threads write consecutive chunks of one column
+  // column-major output: consecutive threads write consecutive chunks of one column;
+  // the kinds present per branch (the scans skip the all-zero columns)
+  u32 m0 = 0, m1 = 0;
   for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += BLOCK) {
     const int jj = i % CH_PER_BLOCK, k = i / CH_PER_BLOCK;
     const i64 gg = (i64)blockIdx.x * CH_PER_BLOCK + jj;
     if (gg >= CA + CB) continue;
     const int sd = gg >= CA;
-    cnt[((i64)sd * SMX_N_KINDS + k) * CM + (sd ? gg - CA : gg)] = c[jj][k];
+    const u32 v = c[jj][k];
+    cnt[((i64)sd * SMX_N_KINDS + k) * CM + (sd ? gg - CA : gg)] = v;
+    if (v) (sd ? m1 : m0) |= 1u << k;
   }
+  m0 = wave_or_to_last(m0);
+  m1 = wave_or_to_last(m1);
+  if ((threadIdx.x & (WAVE - 1)) == WAVE - 1) {
+    if (m0) atomicOr(&km[0], m0);
+    if (m1) atomicOr(&km[1], m1);
+  }
+  __syncthreads();
+  // published only when it adds bits (a stale read costs a redundant atomic): the
+  // blocks would otherwise serialise on two words
+  if (threadIdx.x < 2 && km[threadIdx.x]) {
+    const u32 cur = __hip_atomic_load(&meta->kmask[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cur | km[threadIdx.x]) != cur) atomicOr(&meta->kmask[threadIdx.x], km[threadIdx.x]);
+  }
+}
+
+__device__ __forceinline__ bool cs_present(const ComposeMeta* meta, int col) {
+  return (meta->kmask[col >= SMX_N_KINDS] >> (col % SMX_N_KINDS)) & 1u;
 }
 
 // Exclusive scan of each (side, kind) column of chunk counts in three fully
@@ -352,9 +375,10 @@ __global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, co
 #define CS_TILE (BLOCK * 8)
 
 __global__ void __launch_bounds__(BLOCK) k_cscan_up(const u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
-                                                    i64 NT, u32* __restrict__ tsum) {
+                                                    i64 NT, u32* __restrict__ tsum, const ComposeMeta* meta) {
   __shared__ u32 s[NWAVES + 1];
   const int col = blockIdx.y;
+  if (!cs_present(meta, col)) return;  // all-zero column: its prefixes are its counts
   const i64 C = SMX_CEIL_DIV(col >= SMX_N_KINDS ? nb : na, (i64)CH);
   const i64 t0 = (i64)blockIdx.x * CS_TILE;
   if (t0 >= C) return;
@@ -374,7 +398,7 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_mid(u32* __restrict__ tsum, i64
   const int col = blockIdx.x;
   const int side = col / SMX_N_KINDS, k = col % SMX_N_KINDS;
   const i64 C = SMX_CEIL_DIV(side ? nb : na, (i64)CH);
-  const i64 nt = SMX_CEIL_DIV(C, (i64)CS_TILE);
+  const i64 nt = cs_present(meta, col) ? SMX_CEIL_DIV(C, (i64)CS_TILE) : 0;  // (absent: total 0)
   u32 carry = 0;
   for (i64 r0 = 0; r0 < nt; r0 += BLOCK) {
     const i64 r = r0 + threadIdx.x;
@@ -392,9 +416,10 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_mid(u32* __restrict__ tsum, i64
 }
 
 __global__ void __launch_bounds__(BLOCK) k_cscan_down(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM, i64 NT,
-                                                      const u32* __restrict__ tsum) {
+                                                      const u32* __restrict__ tsum, const ComposeMeta* meta) {
   __shared__ u32 s[NWAVES + 1];
   const int col = blockIdx.y;
+  if (!cs_present(meta, col)) return;
   const i64 C = SMX_CEIL_DIV(col >= SMX_N_KINDS ? nb : na, (i64)CH);
   const i64 t0 = (i64)blockIdx.x * CS_TILE;
   if (t0 >= C) return;
@@ -1084,11 +1109,12 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   {
     const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);
     u32* tsum = C.ws<u32>(B_TSUM);
-    hipLaunchKernelGGL(k_cscan_up, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT, tsum);
+    hipLaunchKernelGGL(k_cscan_up, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT, tsum,
+                       meta);
     hipLaunchKernelGGL(k_cscan_mid, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, tsum, C.na, C.nb, CM, NT, ccnt,
                        meta);
     hipLaunchKernelGGL(k_cscan_down, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT,
-                       tsum);
+                       tsum, meta);
   }
   hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta, (u64)W);
   HIP_TRY(hipGetLastError());

@@ -1,8 +1,6 @@
 set -o pipefail
 O=gpurun_out/${TAG:-r02s}; mkdir -p $O
-timeout -k 10 300 python -u bench.py --config c5 --no-pmc --no-e2e > $O/bench_c5.json 2> $O/bench_c5.err || { tail -5 $O/bench_c5.err; exit 1; }
-cut -c1-300 $O/bench_c5.json
-timeout -k 10 300 python -u bench.py --config c2 --no-pmc --no-e2e --steps 50 > $O/bench_c2.json 2> $O/bench_c2.err || { tail -5 $O/bench_c2.err; exit 1; }
-cut -c1-300 $O/bench_c2.json
-timeout -k 10 300 python -u tools/bench_rga.py > $O/bench_rga.json 2>&1 || { tail -5 $O/bench_rga.json; exit 1; }
-tail -1 $O/bench_rga.json | cut -c1-300
+timeout -k 10 400 python -u -m pytest tests/test_gpu_compose.py tests/test_gpu_full.py tests/test_gpu_async.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+for r in 1 2 3; do
+  echo -n "c3: "; timeout -k 10 200 python -u tools/stage_ab.py 2>&1 | tail -1 | tee -a $O/ab.txt || exit 1
+done
