@@ -1063,18 +1063,94 @@ static int launch_emit(const Ctx& C, bool packable, const smx_shard* sh) {
   return SMX_OK;
 }
 
-// Walk, tables, emit of a single merge.
+static int env_int(const char* name, int dflt);
+
+// A second stream per device (and its two fork/join events) for the table scatter,
+// which runs beside the walk: the walk is a chain of small, latency-bound launches
+// that leaves most of the chip idle.  Created once; the fork/join is by events, so
+// it also works inside a HIP graph capture of the caller's stream.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static std::mutex g_side_mu;
+static SideStream g_side[64];
+
+static int side_stream(SideStream** out) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return set_err(SMX_E_HIP, "device index out of range");
+  std::lock_guard<std::mutex> g(g_side_mu);
+  SideStream& S = g_side[dev];
+  if (!S.s) {
+    HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&S.fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&S.join, hipEventDisableTiming));
+  }
+  *out = &S;
+  return SMX_OK;
+}
+
+#ifndef SMX_TB_OVERLAP
+#define SMX_TB_OVERLAP 1
+#endif
+
+// Walk, tables, emit of a single merge.  The bucketed tables' scatter keeps every
+// rename and runs on the side stream while the walk runs; k_tb_unskip then kills
+// the records of the renames the walk skipped (compose.py:60-70: a skipped rename
+// never enters rename_chain) before the reduce.
 static int launch_tail(const Ctx& C) {
-  C.tm->begin(ST_WALK);
-  int rc = launch_walk(C, nullptr);
+  const i64 n_sym = C.n_sym;
+  u64 width = SMX_CEIL_DIV((u64)n_sym, (u64)TB_NBK_TGT);
+  if (width < 1) width = 1;
+  if (width > TB_WIDTH) width = TB_WIDTH;
+  const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);
+  const bool overlap = SMX_TB_OVERLAP && nbk <= TB_MAXBK && C.n > 0 && !env_int("SMX_TB_SERIAL", 0);
+  if (!overlap) {
+    C.tm->begin(ST_WALK);
+    int rc = launch_walk(C, nullptr);
+    if (rc) return rc;
+    C.tm->end(ST_WALK);
+    C.tm->begin(ST_TABLES);
+    bool bucketed = false;
+    if ((rc = launch_tables(C, nullptr, 0, &bucketed))) return rc;
+    C.tm->end(ST_TABLES);
+    C.tm->begin(ST_EMIT);
+    if ((rc = launch_emit(C, bucketed, nullptr))) return rc;
+    C.tm->end(ST_EMIT);
+    return SMX_OK;
+  }
+  SideStream* S = nullptr;
+  int rc = side_stream(&S);
   if (rc) return rc;
+  hipStream_t st = C.st;
+  TbArgs A = tb_args(C);
+  A.width = (u32)width;
+  A.nbk = (u32)nbk;
+  A.keep_skip = 1u;
+  u32* lst = C.ws<u32>(B_TBHIST);
+  u32* rec = C.ws<u32>(B_REC);
+  const int nblk = (int)SMX_CEIL_DIV((u64)C.n, (u64)TB_TILE);
+  HIP_TRY(hipEventRecord(S->fork, st));
+  HIP_TRY(hipStreamWaitEvent(S->s, S->fork, 0));
+  hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, S->s, A, lst, rec);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(S->join, S->s));
+  C.tm->begin(ST_WALK);
+  if ((rc = launch_walk(C, nullptr))) {
+    (void)hipStreamWaitEvent(st, S->join, 0);  // never leave the side stream unjoined
+    return rc;
+  }
   C.tm->end(ST_WALK);
+  HIP_TRY(hipStreamWaitEvent(st, S->join, 0));
   C.tm->begin(ST_TABLES);
-  bool bucketed = false;
-  if ((rc = launch_tables(C, nullptr, 0, &bucketed))) return rc;
+  hipLaunchKernelGGL(k_tb_unskip, dim3(64), dim3(BLOCK), 0, st, A, lst, rec, C.ws<u32>(B_SKIPLIST));
+  hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, lst, rec, n_sym, C.ws<int4>(B_FIN),
+                     (u64*)nullptr, 0u);
+  HIP_TRY(hipGetLastError());
   C.tm->end(ST_TABLES);
   C.tm->begin(ST_EMIT);
-  if ((rc = launch_emit(C, bucketed, nullptr))) return rc;
+  if ((rc = launch_emit(C, true, nullptr))) return rc;
   C.tm->end(ST_EMIT);
   return SMX_OK;
 }

@@ -50,6 +50,8 @@ struct TbArgs {
   u32 width;        // symbols per bucket
   u32 nbk;          // buckets
   u32 smax;         // n_sym - 1 (clamp)
+  u32 keep_skip;    // k_tb_scatter keeps every rename (it runs beside the walk; the
+                    // skipped renames' records are killed afterwards by k_tb_unskip)
   u64 nMv, nR;      // filled on the device by tb_load
 };
 
@@ -75,7 +77,7 @@ __device__ __forceinline__ bool tb_record(const TbArgs& A, u64 r, u32* sym, u32*
     return (x & (MS_HAS_A | MS_HAS_F)) != 0;
   }
   const u64 m = r - A.nMv;
-  if (tb_skipped(A, m)) return false;
+  if (!A.keep_skip && tb_skipped(A, m)) return false;
   *sym = min(A.tsym[m], A.smax);
   *flags = 0;
   return true;
@@ -104,7 +106,7 @@ __device__ __forceinline__ void tb_items(const TbArgs& A, u64 base, u32 (&sym)[T
     for (int it = 0; it < TB_ITEMS; ++it) s[it] = A.tsym[m0 + (u64)it * TB_NT + threadIdx.x];
 #pragma unroll
     for (int it = 0; it < TB_ITEMS; ++it) {
-      ok[it] = !tb_skipped(A, m0 + (u64)it * TB_NT + threadIdx.x);
+      ok[it] = A.keep_skip || !tb_skipped(A, m0 + (u64)it * TB_NT + threadIdx.x);
       fl[it] = 0;
       sym[it] = min(s[it], A.smax);
     }
@@ -189,6 +191,34 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
   for (u32 i = threadIdx.x; i < total; i += TB_NT) rec[base + i] = stage[i];
 }
 
+#define REC_DEAD 0xffffffffu
+// After a keep_skip scatter (which ran beside the walk): the record of every rename
+// the walk skipped is found in its tile's bucket run (64 records on average) and
+// marked dead, so that k_tb_reduce never sees it.  One lane per skip.
+__global__ void k_tb_unskip(TbArgs A0, const u32* __restrict__ lst, u32* __restrict__ rec,
+                            const u32* __restrict__ skiplist) {
+  const TbArgs A = tb_load(A0);
+  const u64 nskip = min(A.meta->n_skip, A.nR);
+  const u32 nb1 = A.nbk + 1;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nskip; i += (u64)gridDim.x * blockDim.x) {
+    const u64 m = skiplist[i];
+    if (m >= A.nR) continue;
+    const u64 r = A.nMv + m;
+    const u64 tile = r / TB_TILE;
+    const u32 loc = (u32)(r - tile * TB_TILE);
+    const u32 sym = min(A.tsym[m], A.smax);
+    const u32 b = sym / A.width;
+    const u32* lt = lst + tile * nb1;
+    const u64 rb = tile * TB_TILE;
+    for (u32 j = lt[b], e = lt[b + 1]; j < e; ++j) {
+      if ((rec[rb + j] & 0x3fffu) == loc && rec[rb + j] != REC_DEAD) {
+        rec[rb + j] = REC_DEAD;
+        break;
+      }
+    }
+  }
+}
+
 #define TBR_NT 1024
 #ifndef TBR_TK
 #define TBR_TK 16
@@ -253,7 +283,10 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
     for (int k = 0; k < TBR_TK; ++k) {
       const u32 lk = __builtin_amdgcn_readlane(lo, k), hk = __builtin_amdgcn_readlane(hi, k);
       const u64 rb = (u64)(t0 + k) * TB_TILE;
-      for (u32 i = lk + 2 * WAVE + (u32)lane; i < hk; i += WAVE) put(rec[rb + i], rb);
+      for (u32 i = lk + 2 * WAVE + (u32)lane; i < hk; i += WAVE) {
+        const u32 x = rec[rb + i];
+        if (x != REC_DEAD) put(x, rb);
+      }
     }
   }
   __syncthreads();

@@ -212,8 +212,16 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 
 // MAP: the sample-sorted shard's source map (P.src_map) is read; a separate instance so
 // that the plain path's store loop has no load whose wait would also drain its stores
+#ifndef WF_MINB
+#define WF_MINB 8
+#endif
+#ifdef WF_WPE
+#define WF_BOUNDS __launch_bounds__(WF_NT) __attribute__((amdgpu_waves_per_eu(WF_WPE, WF_WPE)))
+#else
+#define WF_BOUNDS __launch_bounds__(WF_NT, WF_MINB)
+#endif
 template <bool DBG, bool MAP>
-__global__ void __launch_bounds__(WF_NT, 8) k_window_f(WinArgs P) {
+__global__ void WF_BOUNDS k_window_f(WinArgs P) {
   __shared__ __attribute__((aligned(16))) u64 sts[WF_CAP];  // element space: timestamps; later slot-space rank keys
   __shared__ u16 sord[WF_CAP];       // S order (merge), later the final order
   __shared__ u16 fin[WF_CAP];        // slot -> element, later rename ranks
