@@ -1083,6 +1083,7 @@ static int side_stream(SideStream** out) {
   std::lock_guard<std::mutex> g(g_side_mu);
   SideStream& S = g_side[dev];
   if (!S.s) {
+    // (the lowest stream priority for it measured the same, profiles/r02_k/side_prio_ab.txt)
     HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&S.fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&S.join, hipEventDisableTiming));
@@ -1262,7 +1263,22 @@ __device__ __forceinline__ void seg_pass(u64 (&v)[8], u32 base, u32 b, u32 k, in
   }
 }
 
+#ifndef SEG_BUCKET
+#define SEG_BUCKET 1
+#endif
+#if SEG_BUCKET
+// Interpolation buckets (the default): element x of group [gs, ge) goes to bucket
+// (gs + (ge - gs) * hi32 / 2^32) / 2, i.e. two elements per bucket on random ids;
+// buckets are ordered like (group, hi), a counting sort places them and each element
+// ranks itself on the full key inside its bucket.  A bucket above SEG_BKMAX (ids that
+// cluster) sends the tile to the bitonic network.  The key array is unpadded so that two
+// blocks (64 KB keys + 8 KB of 16-bit bucket counters each) fit a CU.
+#define SEGPAD(i) (i)
+#define SEG_NBK (SEG_CAP / 2)
+#define SEG_BKMAX 32
+#else
 #define SEGPAD(i) ((i) + ((i) >> 3))  // one pad word per 8 keys: spreads a thread's 8 keys over banks
+#endif
 
 // One tile of one branch (ts, hi, lo: the branch's columns; outputs at the branch's
 // offset; off: the branch's first op index in A||B).  Sort key, one u64 per element:
@@ -1279,8 +1295,11 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
   constexpr int PER = SEG_CAP / SEG_NT;  // 8 keys per thread
   static_assert(PER == 8, "the register passes assume 8 keys per thread");
   __shared__ u64 key[SEGPAD(SEG_CAP)];
-  __shared__ u32 wsum[SEG_NT / WAVE];
+  __shared__ u32 wsum[SEG_NT / WAVE + 1];
   __shared__ i64 se[2];
+#if SEG_BUCKET
+  __shared__ u32 bcnt[SEG_NBK / 2];  // two 16-bit bucket counters per word
+#endif
   const int t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
   const i64 p0 = (i64)blockIdx.x * SEG_H;
   // Layout: every adjacent pair of the nominal range (the nominal ranges cover the
@@ -1342,12 +1361,86 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
   u32 g = inc - run;
   for (int q = 0; q < wv; ++q) g += wsum[q];
   u64 v[PER];
+  u32 gk[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const u32 x = t * PER + k;
     g += f[k];
+    gk[k] = g;
     v[k] = x < (u32)size ? ((u64)g << 51) | ((hi[s + x] >> 26) << 13) | x : ~0ull;  // padding sorts last
   }
+#if SEG_BUCKET
+  bool bitonic = false;
+  {
+    u32 ng = 1;  // groups in the tile
+    for (int q = 0; q < SEG_NT / WAVE; ++q) ng += wsum[q];
+    u16* gst = reinterpret_cast<u16*>(key);  // group starts (the key array is free until the scatter)
+    for (int i = t; i < SEG_NBK / 2; i += SEG_NT) bcnt[i] = 0u;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const u32 x = t * PER + k;
+      if (x < (u32)size && (x == 0 || f[k])) gst[gk[k]] = (u16)x;
+    }
+    __syncthreads();
+    u32 bk[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const u32 x = t * PER + k;
+      bk[k] = 0;
+      if (x < (u32)size) {
+        const u32 gs = gst[gk[k]], ge = gk[k] + 1 < ng ? (u32)gst[gk[k] + 1] : (u32)size;
+        const u32 h32 = (u32)(v[k] >> 19);  // the top 32 of the 38 id bits
+        bk[k] = (gs + (u32)(((u64)(ge - gs) * h32) >> 32)) >> 1;
+        atomicAdd(&bcnt[bk[k] >> 1], 1u << (16 * (bk[k] & 1)));
+      }
+    }
+    __syncthreads();
+    // exclusive scan of the counters (4 per thread), largest bucket -> fallback
+    const u32 nbw = ((u32)size + 3) / 4;  // counter words in use: 2 words per thread
+    u32 w0 = 2 * t < nbw ? bcnt[2 * t] : 0u, w1 = 2 * t + 1 < nbw ? bcnt[2 * t + 1] : 0u;
+    const u32 c0 = w0 & 0xffffu, c1 = w0 >> 16, c2 = w1 & 0xffffu, c3 = w1 >> 16;
+    const u32 mx = max(max(c0, c1), max(c2, c3));
+    u32 tot;
+    const u32 e0 = block_excl_scan<OpSum, u32, SEG_NT / WAVE>(c0 + c1 + c2 + c3, wsum, &tot);
+    const u32 e1 = e0 + c0, e2 = e1 + c1, e3 = e2 + c2;
+    if (2 * t < nbw) bcnt[2 * t] = e0 | (e1 << 16);
+    if (2 * t + 1 < nbw) bcnt[2 * t + 1] = e2 | (e3 << 16);
+    bitonic = __syncthreads_or(mx > SEG_BKMAX);
+    if (!bitonic) {
+      // scatter: the counters become bucket ends
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const u32 x = t * PER + k;
+        if (x < (u32)size) {
+          const u32 sh = 16 * (bk[k] & 1);
+          const u32 old = atomicAdd(&bcnt[bk[k] >> 1], 1u << sh);
+          key[(old >> sh) & 0xffffu] = v[k];
+        }
+      }
+      __syncthreads();
+      u32 fp[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const u32 x = t * PER + k;
+        fp[k] = 0;
+        if (x < (u32)size) {
+          const u32 b = bk[k];
+          const u32 e = (bcnt[b >> 1] >> (16 * (b & 1))) & 0xffffu;
+          const u32 lo = b ? (bcnt[(b - 1) >> 1] >> (16 * ((b - 1) & 1))) & 0xffffu : 0u;
+          u32 c = 0;
+          for (u32 q = lo; q < e; ++q) c += key[q] < v[k];
+          fp[k] = lo + c;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        if (t * PER + k < (u32)size) key[fp[k]] = v[k];
+      __syncthreads();
+    }
+  }
+  if (bitonic) {
+#endif
   // merge levels k = 2, 4, 8: keys 8t .. 8t+7 (b = 0)
   seg_pass(v, (u32)t * 8, 0, 2, 0, 1);
   seg_pass(v, (u32)t * 8, 0, 4, 1, 2);
@@ -1386,6 +1479,9 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
     for (int m = 0; m < PER; ++m) key[SEGPAD(bo | ((u32)m << cur))] = v[m];
   }
   __syncthreads();
+#if SEG_BUCKET
+  }
+#endif
   // runs of equal (group, hi38): exact order on (oid_hi, oid_lo, index)
   for (u32 x = t; x + 1 < (u32)size; x += SEG_NT) {
     const u64 kx = key[SEGPAD(x)] >> 13;

@@ -111,6 +111,20 @@ def test_gpu_segmented_plan_duplicate_ids():
     _eq_soa(compose_soa(soa), oracle.compose(soa), "segmented plan, duplicate ids")
 
 
+def test_gpu_segmented_plan_clustered_ids():
+    """Segmented plan with ids whose top bits cluster (sequential ids in the first half of
+    each branch, as short string ids give; distinct in the 38 sorted bits, so no tie
+    runs): those tiles' interpolation buckets overflow and take the bitonic network; the
+    random-id tiles keep the buckets."""
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(400_000, 1_000, 71, ops_per_ms=4096,
+                                                         mix=synth.ADVERSARIAL_MIX)))
+    for lo, hi in ((0, soa.n_a // 2), (soa.n_a, soa.n_a + soa.n_b // 2)):
+        seq = np.arange(hi - lo, dtype=np.uint64)
+        soa.oid_hi[lo:hi] = ((seq * np.uint64(2654435761)) & np.uint64(0xFFFFF)) << np.uint64(26)
+    _eq_soa(compose_soa(soa), oracle.compose(soa), "segmented plan, clustered ids")
+    assert DeviceCompose.last_plan() == "segmented"
+
+
 @pytest.mark.parametrize("bits", [15, 20, 31], ids=["packed48", "packed64", "wide"])
 def test_gpu_value_widths(bits):
     """Value ids of `bits` bits: 3 x 15 fits the 6-byte final-state table entries,
