@@ -500,28 +500,51 @@ __global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, c
       }
     }
   } else {
+    // a window holds at most WG_CAP ops: WC_ITEMS per thread, every load issued before
+    // any is used (the perm -> kind -> value chain is one round trip per level, not one
+    // per item); the item count is fixed, so the ballots stay wave-uniform
+    constexpr int WC_ITEMS = (WG_CAP + BLOCK - 1) / BLOCK;
     const u64 lt = lanemask_lt();
-    for (int side = 0; side < 2; ++side) {
-      const i64 lo = side ? b0 : a0, hi = side ? b1 : a1, off = side ? na : 0;
-      for (i64 j0 = lo; j0 < hi; j0 += BLOCK) {  // wave-uniform trip count for the ballots
-        const i64 j = j0 + threadIdx.x;
-        const bool valid = j < hi;
-        u32 k = 0;
-        bool none_mv = false;
-        if (valid) {
-          const u32 src = perm[off + j];
-          const u32 k0 = kind[src];
-          bad |= k0 >= SMX_N_KINDS;
-          k = k0 < SMX_N_KINDS ? k0 : SMX_N_KINDS - 1;
-          none_mv = k == KMOVE && (v0[src] < 0 || v1[src] < 0);
-        }
-        const u64 peers = wave_peers<5>(k, valid);
-        if (valid && (peers & lt) == 0) atomicAdd(&c[k], (u32)__popcll(peers));
-        const u64 nm = __ballot(none_mv);
-        if (nm && (threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&c[CNT_NONE_MV], (u32)__popcll(nm));
-        if (valid && k == KREN && (peers & lt) == 0) atomicAdd(&c[CNT_REN_A + side], (u32)__popcll(peers));
+    const i64 nA = a1 - a0, nW = nA + (b1 - b0);
+    u32 src[WC_ITEMS], kv[WC_ITEMS];
+    i32 x0[WC_ITEMS], x1[WC_ITEMS];
+    bool val[WC_ITEMS], sd[WC_ITEMS];
+#pragma unroll
+    for (int i = 0; i < WC_ITEMS; ++i) {
+      const i64 e = (i64)i * BLOCK + threadIdx.x;
+      val[i] = e < nW && e < WG_CAP;
+      sd[i] = e >= nA;
+      src[i] = val[i] ? perm[sd[i] ? na + b0 + (e - nA) : a0 + e] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < WC_ITEMS; ++i) kv[i] = kind[src[i]];
+#pragma unroll
+    for (int i = 0; i < WC_ITEMS; ++i) {  // the values of the moves only
+      const bool mv = val[i] && kv[i] == KMOVE;
+      x0[i] = mv ? v0[src[i]] : 0;
+      x1[i] = mv ? v1[src[i]] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < WC_ITEMS; ++i) {
+      u32 k = 0;
+      bool none_mv = false;
+      if (val[i]) {
+        bad |= kv[i] >= SMX_N_KINDS;
+        k = kv[i] < SMX_N_KINDS ? kv[i] : SMX_N_KINDS - 1;
+        none_mv = k == KMOVE && (x0[i] < 0 || x1[i] < 0);
+      }
+      const u64 peers = wave_peers<5>(k, val[i]);
+      if (val[i] && (peers & lt) == 0) atomicAdd(&c[k], (u32)__popcll(peers));
+      const u64 nm = __ballot(none_mv);
+      if (nm && (threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&c[CNT_NONE_MV], (u32)__popcll(nm));
+      // renames per branch (a wave may straddle the A/B boundary: split the peers)
+      if (val[i] && k == KREN) {
+        const u64 sb = __ballot(sd[i]);
+        const u64 mine = peers & (sd[i] ? sb : ~sb);
+        if ((mine & lt) == 0) atomicAdd(&c[CNT_REN_A + (sd[i] ? 1 : 0)], (u32)__popcll(mine));
       }
     }
+    if (nW > WG_CAP) bad = true;  // cannot happen: k_gpart cuts windows of at most WG_CAP ops
   }
   if (bad) meta->bad_sym = 1;
   __syncthreads();

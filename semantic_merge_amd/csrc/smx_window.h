@@ -296,6 +296,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   // T-order segment starts; window offsets = chunk prefix at the window start + kinds
   // of the <= 255 ops between that chunk start and the window start (per branch)
   const u64 base_v = t <= SMX_N_KINDS ? P.meta->base[t] : 0ull;
+  // a window that already failed the plan (dense groups: every window does) makes the
+  // rest of the launch pointless: checked after the load phase, no extra round trip
+  const u64 failed = t == 0 ? P.meta->f_fail : 0ull;
   u32 woff_x = 0, woff_y = 0;  // (added where stored: an add here would wait for every load)
   // (32-bit chunk indices: 2 * kinds * CM < 2^32 for any n < 2^31, the i32 output limit)
   if (t < SMX_N_KINDS) {
@@ -363,7 +366,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   if (t <= SMX_N_KINDS) base[t] = base_v;
   if (t < SMX_N_KINDS) wck[t] = 0;
   if (t < SMX_N_KINDS + 2) woffk[t] = woff_x + woff_y;
+  if (t == 0) wtot[0] = failed != 0;
   __syncthreads();
+  if (wtot[0]) return;  // (wtot is written again in step 6)
   WSTAMP(1);
   if (P.ablate & 16) {  // diagnostics: load only (keeps every load live)
     u32 x = 0;
