@@ -1118,6 +1118,9 @@ static int side_stream(SideStream** out) {
 #ifndef SMX_TB_OVERLAP
 #define SMX_TB_OVERLAP 1
 #endif
+#ifndef SMX_TB_OVERLAP_MIN
+#define SMX_TB_OVERLAP_MIN (1 << 22)  // ops
+#endif
 
 // Walk, tables, emit of a single merge.  The bucketed tables' scatter keeps every
 // rename and runs on the side stream while the walk runs; k_tb_unskip then kills
@@ -1129,7 +1132,8 @@ static int launch_tail(const Ctx& C) {
   if (width < 1) width = 1;
   if (width > TB_WIDTH) width = TB_WIDTH;
   const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);
-  const bool overlap = SMX_TB_OVERLAP && nbk <= TB_MAXBK && C.n > 0 && !env_int("SMX_TB_SERIAL", 0);
+  // small merges are launch-bound: the fork/join costs more than the overlap saves
+  const bool overlap = SMX_TB_OVERLAP && nbk <= TB_MAXBK && C.n >= SMX_TB_OVERLAP_MIN && !env_int("SMX_TB_SERIAL", 0);
   if (!overlap) {
     C.tm->begin(ST_WALK);
     int rc = launch_walk(C, nullptr);

@@ -215,6 +215,9 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_MINB
 #define WF_MINB 8
 #endif
+#ifndef WF_BUCKET
+#define WF_BUCKET 1  // step 5 by interpolation buckets (0: counting rank over each group)
+#endif
 #ifdef WF_WPE
 #define WF_BOUNDS __launch_bounds__(WF_NT) __attribute__((amdgpu_waves_per_eu(WF_WPE, WF_WPE)))
 #else
@@ -537,6 +540,18 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
            ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), l) << 32);
   };
   const u64 le_mask = lanemask_lt() | (1ull << lane);
+#if WF_BUCKET
+  // interpolation buckets over slot space: slot p of group [gs, ge) goes to bucket
+  // gs + (ge - gs) * key / 2^32 (one op per bucket on random ids); 16-bit counters,
+  // two per word, in the upper half of sts (free until step 7)
+  u32* bcnt = reinterpret_cast<u32*>(sts) + WF_CAP;
+  for (int i = t; i < WF_CAP / 2; i += WF_NT) bcnt[i] = 0u;
+  __syncthreads();
+  u32 bk_r[WF_ITEMS];
+  u32 kp_r[WF_ITEMS];
+#pragma unroll
+  for (int j = 0; j < WF_ITEMS; ++j) bk_r[j] = 0xffffffffu, kp_r[j] = 0u;
+#endif
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {
     const int wi = __builtin_amdgcn_readfirstlane((WF_NT * j) / WAVE + wv);  // this wave's slot chunk
@@ -564,6 +579,16 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       ge = ge < sz ? ge : sz;
     }
     if (p >= sz) continue;
+#if WF_BUCKET
+    {
+      const u32 kp = pkey[p];
+      const u32 b = (u32)gs + (u32)(((u64)(u32)(ge - gs) * kp) >> 32);
+      kp_r[j] = kp;
+      bk_r[j] = b;
+      atomicAdd(&bcnt[b >> 1], 1u << (16 * (b & 1)));
+      continue;
+    }
+#endif
     int r = p;
     if (ge - gs > 1 && !(P.ablate & 2)) {
       const u32 kp = pkey[p];
@@ -586,6 +611,58 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     sord[r] = fin[p];
     sl[r] = (u16)p;  // sl now maps rank -> slot
   }
+#if WF_BUCKET
+  bool btie = false;  // two equal 32-bit keys in one group (the exact re-rank below)
+  {
+    __syncthreads();
+    // exclusive scan of the counters, 4 per thread (2 words)
+    const u32 w0 = bcnt[2 * t], w1 = bcnt[2 * t + 1];
+    const u32 c0 = w0 & 0xffffu, c1 = w0 >> 16, c2 = w1 & 0xffffu, c3 = w1 >> 16;
+    u32 tot;
+    const u32 e0 = block_excl_scan<OpSum, u32, WF_WAVES>(c0 + c1 + c2 + c3, &vbw[0][0], &tot);  // (vbw is dead after step 2)
+    bcnt[2 * t] = e0 | ((e0 + c0) << 16);
+    bcnt[2 * t + 1] = (e0 + c0 + c1) | ((e0 + c0 + c1 + c2) << 16);
+    __syncthreads();
+    // scatter the slots into their buckets (sl: bucket position -> slot); the counters
+    // become the bucket ends
+#pragma unroll
+    for (int j = 0; j < WF_ITEMS; ++j) {
+      const u32 b = bk_r[j];
+      if (b == 0xffffffffu) continue;
+      const u32 sh = 16 * (b & 1);
+      const u32 old = atomicAdd(&bcnt[b >> 1], 1u << sh);
+      sl[(old >> sh) & 0xffffu] = (u16)((WF_NT * j) / WAVE * WAVE + wv * WAVE + lane);
+    }
+    __syncthreads();
+    // rank inside the bucket on the 32-bit key
+    int rr[WF_ITEMS];
+#pragma unroll
+    for (int j = 0; j < WF_ITEMS; ++j) {
+      const u32 b = bk_r[j];
+      rr[j] = -1;
+      if (b == 0xffffffffu) continue;
+      const u32 e = (bcnt[b >> 1] >> (16 * (b & 1))) & 0xffffu;
+      const u32 lo = b ? (bcnt[(b - 1) >> 1] >> (16 * ((b - 1) & 1))) & 0xffffu : 0u;
+      const u32 kp = kp_r[j];
+      u32 c = 0, eq = 0;
+      for (u32 q = lo; q < e; ++q) {
+        const u32 k = pkey[sl[q]];
+        c += k < kp;
+        eq += k == kp;
+      }
+      btie |= eq > 1;
+      rr[j] = (int)(lo + c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < WF_ITEMS; ++j) {
+      if (rr[j] < 0) continue;
+      const int p = (WF_NT * j) / WAVE * WAVE + wv * WAVE + lane;
+      sord[rr[j]] = fin[p];
+      sl[rr[j]] = (u16)p;  // sl now maps rank -> slot
+    }
+  }
+#endif
   __syncthreads();
   WSTAMP(10);
   // 6. renames: rank among the window's renames of the same branch (final order).
@@ -617,11 +694,15 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     }
   };
   bool tie = false;
+#if WF_BUCKET
+  tie = btie;
+#else
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {
     const int r = t + WF_NT * j;
     if (r < sz) tie |= sl[r] == 0xffffu;
   }
+#endif
   rename_ranks(false);
   const bool any_tie = __syncthreads_or(tie);
   WSTAMP(21);
