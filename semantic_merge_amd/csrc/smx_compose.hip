@@ -266,14 +266,17 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 // A window derives its T offsets from the chunk prefixes at its start plus the
 // kinds of at most 255 ops before it.  Coalesced: iteration j of a block reads
 // chunk j, lane t its byte t.
-#define CH_PER_BLOCK (BLOCK / 16)   // 16 lanes x 16 kind bytes per 256-op chunk
+#ifndef KH_NT
+#define KH_NT 512                  // 32 chunks per block: a column's counts fill a 128-byte line
+#endif
+#define CH_PER_BLOCK (KH_NT / 16)   // 16 lanes x 16 kind bytes per 256-op chunk
 
 // Block b counts global chunks [b*CH_PER_BLOCK, ...) (A chunks, then B chunks):
 // lane t reads bytes [16*(t%16), +16) of chunk t/16 (one 16-byte load when
 // aligned), so a chunk is one 16-lane DPP row.  No atomics: each lane counts its 16
 // kinds in packed 5-bit fields (6 kinds per word), widens them to 10-bit fields and
 // the row adds them up with DPP shifts; the row's last lane holds the chunk's counts.
-__global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, const u64* __restrict__ ts,
+__global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, const u64* __restrict__ ts,
                                                  i64 na, i64 nb, i64 bgap, i64 CM, u32* __restrict__ cnt,
                                                  u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta) {
   __shared__ u32 c[CH_PER_BLOCK][SMX_N_KINDS];
@@ -341,7 +344,7 @@ __global__ void __launch_bounds__(BLOCK) k_khist(const u8* __restrict__ kind, co
   // column-major output: consecutive threads write consecutive chunks of one column;
   // the kinds present per branch (the scans skip the all-zero columns)
   u32 m0 = 0, m1 = 0;
-  for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += BLOCK) {
+  for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += KH_NT) {
     const int jj = i % CH_PER_BLOCK, k = i / CH_PER_BLOCK;
     const i64 gg = (i64)blockIdx.x * CH_PER_BLOCK + jj;
     if (gg >= CA + CB) continue;
@@ -1172,7 +1175,7 @@ static int launch_tail(const Ctx& C) {
   C.tm->end(ST_WALK);
   HIP_TRY(hipStreamWaitEvent(st, S->join, 0));
   C.tm->begin(ST_TABLES);
-  hipLaunchKernelGGL(k_tb_unskip, dim3(64), dim3(BLOCK), 0, st, A, lst, rec, C.ws<u32>(B_SKIPLIST));
+  hipLaunchKernelGGL(k_tb_unskip, dim3(1024), dim3(BLOCK), 0, st, A, lst, rec, C.ws<u32>(B_SKIPLIST));
   hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, lst, rec, n_sym, C.ws<int4>(B_FIN),
                      (u64*)nullptr, 0u);
   HIP_TRY(hipGetLastError());
@@ -1205,7 +1208,7 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   u32* ccnt = C.ws<u32>(B_CCNT);
   u64* sA = C.ws<u64>(B_SMP);
   u64* sB = sA + SMX_CEIL_DIV(C.na, (i64)CH) + 1;
-  hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK)), dim3(BLOCK), 0, st, C.ops->kind,
+  hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK)), dim3(KH_NT), 0, st, C.ops->kind,
                      C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta);
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
                      C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na,

@@ -194,13 +194,16 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
 #define REC_DEAD 0xffffffffu
 // After a keep_skip scatter (which ran beside the walk): the record of every rename
 // the walk skipped is found in its tile's bucket run (64 records on average) and
-// marked dead, so that k_tb_reduce never sees it.  One lane per skip.
+// marked dead, so that k_tb_reduce never sees it.  One wave per skip, its lanes
+// test 64 records of the run per step.
 __global__ void k_tb_unskip(TbArgs A0, const u32* __restrict__ lst, u32* __restrict__ rec,
                             const u32* __restrict__ skiplist) {
   const TbArgs A = tb_load(A0);
   const u64 nskip = min(A.meta->n_skip, A.nR);
   const u32 nb1 = A.nbk + 1;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nskip; i += (u64)gridDim.x * blockDim.x) {
+  const u32 lane = threadIdx.x & (WAVE - 1);
+  const u64 nwv = (u64)gridDim.x * (blockDim.x / WAVE);
+  for (u64 i = (u64)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; i < nskip; i += nwv) {
     const u64 m = skiplist[i];
     if (m >= A.nR) continue;
     const u64 r = A.nMv + m;
@@ -210,11 +213,10 @@ __global__ void k_tb_unskip(TbArgs A0, const u32* __restrict__ lst, u32* __restr
     const u32 b = sym / A.width;
     const u32* lt = lst + tile * nb1;
     const u64 rb = tile * TB_TILE;
-    for (u32 j = lt[b], e = lt[b + 1]; j < e; ++j) {
-      if ((rec[rb + j] & 0x3fffu) == loc && rec[rb + j] != REC_DEAD) {
-        rec[rb + j] = REC_DEAD;
-        break;
-      }
+    const u32 e = lt[b + 1];
+    for (u32 j = lt[b] + lane; j < e; j += WAVE) {
+      const u32 q = rec[rb + j];
+      if (q != REC_DEAD && (q & 0x3fffu) == loc) rec[rb + j] = REC_DEAD;
     }
   }
 }
