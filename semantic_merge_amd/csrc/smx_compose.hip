@@ -686,6 +686,7 @@ struct EmitArgs {
 #ifndef EMIT_B
 #define EMIT_B 8      // wave steps whose loads are issued together
 #endif
+static_assert(EMIT_WT % (WAVE * EMIT_B) == 0, "a wave's output range is whole batches of steps");
 
 // Every op after the move block (the moves' records came from the window
 // kernel).  Each wave owns EMIT_WT consecutive OUTPUT indices (aligned: no output
@@ -695,7 +696,12 @@ struct EmitArgs {
 // found by one binary search per wave and a scalar walk over the (few) skips of
 // each 64-output step.  Renames see their symbol's final move state, the rest
 // also its last rename (compose.py:30-49).  Block 0 writes the call's counts.
-__global__ void __launch_bounds__(BLOCK) k_emit(EmitArgs E) {
+#ifdef EMIT_WPE
+#define EMIT_BOUNDS __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EMIT_WPE, EMIT_WPE)))
+#else
+#define EMIT_BOUNDS __launch_bounds__(BLOCK)
+#endif
+__global__ void EMIT_BOUNDS k_emit(EmitArgs E) {
   const ComposeMeta* M = E.meta;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     // -1 invalid input (sym >= n_sym or kind >= 18); -2 the plan failed, -3 moves
