@@ -131,6 +131,17 @@ __device__ __forceinline__ u64 wave_peers(u32 d, bool valid) {
   return m;
 }
 
+// wave_peers over the low `nbits` bits (wave-uniform at run time)
+__device__ __forceinline__ u64 wave_peers_n(u32 d, bool valid, int nbits) {
+  u64 m = __ballot(valid);
+  for (int b = 0; b < nbits; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const u64 x = __ballot(bit);
+    m &= bit ? x : ~x;
+  }
+  return m;
+}
+
 // Inclusive wave64 prefix scans on the DPP network (VALU only; __shfl_up would be
 // a chain of six ds_bpermute LDS round trips): row_shr 1, 2, 4, 8 inside each
 // 16-lane row, then row_bcast:15 and row_bcast:31 carry across rows.

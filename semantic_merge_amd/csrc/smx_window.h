@@ -215,6 +215,9 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_MINB
 #define WF_MINB 8
 #endif
+#ifndef WF_DENSE_KINDS
+#define WF_DENSE_KINDS 1  // step 3's ballots over the dense index of the present kinds
+#endif
 #ifndef WF_BUCKET
 #define WF_BUCKET 1  // step 5 by interpolation buckets (0: counting rank over each group)
 #endif
@@ -299,6 +302,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   // T-order segment starts; window offsets = chunk prefix at the window start + kinds
   // of the <= 255 ops between that chunk start and the window start (per branch)
   const u64 base_v = t <= SMX_N_KINDS ? P.meta->base[t] : 0ull;
+#if WF_DENSE_KINDS
+  const u32 kmask_r = P.meta->kmask[0] | P.meta->kmask[1];
+#endif
   // a window that already failed the plan (dense groups: every window does) makes the
   // rest of the launch pointless: checked after the load phase, no extra round trip
   const u64 failed = t == 0 ? P.meta->f_fail : 0ull;
@@ -442,13 +448,23 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     mkr[j] = m < sz ? skS[m] : 0u;
   }
   const u64 ltm = lanemask_lt();
+#if WF_DENSE_KINDS
+  // the ballots run over the dense index of the kinds present in the merge (k_khist's
+  // kind masks): 6 kinds take 3 ballots instead of 5
+  const u32 kpres = __builtin_amdgcn_readfirstlane(kmask_r);
+  const int kbits = 32 - __clz((int)(max(__popc(kpres), 1u) - 1u));
+#endif
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {
     const int m = t + WF_NT * j;
     const int c = wv + WF_WAVES * j;
     const bool valid = m < sz;
     const u32 k = mkr[j];
+#if WF_DENSE_KINDS
+    const u64 peers = wave_peers_n((u32)__popc(kpres & ((1u << k) - 1u)), valid, kbits);
+#else
     const u64 peers = wave_peers<5>(k, valid);
+#endif
     const u32 r = __popcll(peers & ltm);
     mkr[j] = k | (r << 8);
     if (valid && r == 0) {
