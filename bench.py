@@ -1,7 +1,7 @@
 """Benchmark: op-log compose+conflict throughput on device-resident synthetic logs.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--n-ops N]
-                    [--weak | --independent] [--no-pmc] [--no-cpu-baseline] [--no-e2e]
+                    [--weak | --independent] [--no-pmc] [--no-cpu-baseline] [--no-e2e] [--no-async]
 
 One step = one composition (semmerge/compose.py:11-114 restated on the GPU) of
 SURVEY §8(d) config 3: 100M lift-shaped ops (50M per branch), 1M symbols, seed 11.
@@ -69,7 +69,7 @@ def pmc_traffic(args) -> dict:
         cmd = [exe, "--pmc", counter, "--kernel-include-regex", "k_", "-d", d, "-o", "p",
                "--output-format", "csv", "--", sys.executable, os.path.join(REPO, "bench.py"),
                "--steps", "2", "--warmup", "1", "--config", args.config, "--no-cpu-baseline",
-               "--no-pmc", "--no-e2e"]
+               "--no-pmc", "--no-e2e", "--no-async"]
         if args.n_ops:
             cmd += ["--n-ops", str(args.n_ops)]
         if args.n_sym:
@@ -198,6 +198,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
     ap.add_argument("--no-e2e", action="store_true", help="skip the drop-in end-to-end leg")
+    ap.add_argument("--no-async", action="store_true", help="skip the smx_compose_async pipeline leg")
     ap.add_argument("--e2e-ops", type=int, default=100_000)
     ap.add_argument("--verify", action="store_true", help="check GPU == oracle (slow, N = 1)")
     ap.add_argument("--weak", action="store_true", help="N > 1: N x the config's ops (weak scaling)")
@@ -287,7 +288,7 @@ def main() -> None:
     # smx_compose_finish after the last: what a caller pipelining merges gets (no host
     # sync between merges).  Reported beside the headline, outside its timed region.
     async_api = None
-    if not sharded and world == 1:
+    if not sharded and world == 1 and not args.no_async:
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         for _ in range(args.steps):

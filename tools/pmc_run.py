@@ -22,7 +22,7 @@ def main():
     assert rc == 0
     torch.cuda.synchronize()
     del buf
-    sys.argv = ["bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-pmc", "--no-e2e"] + sys.argv[1:]
+    sys.argv = ["bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-pmc", "--no-e2e", "--no-async"] + sys.argv[1:]
     import runpy
     runpy.run_path(os.path.join(REPO, "bench.py"), run_name="__main__")
 
