@@ -270,6 +270,9 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 #define KH_NT 512                  // 32 chunks per block: a column's counts fill a 128-byte line
 #endif
 #define CH_PER_BLOCK (KH_NT / 16)   // 16 lanes x 16 kind bytes per 256-op chunk
+#ifndef KH_R
+#define KH_R 1                     // chunk rounds per block (4 measured slower: profiles/r02_k/khist_rounds_ab.txt)
+#endif
 
 // Block b counts global chunks [b*CH_PER_BLOCK, ...) (A chunks, then B chunks):
 // lane t reads bytes [16*(t%16), +16) of chunk t/16 (one 16-byte load when
@@ -279,74 +282,85 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, const u64* __restrict__ ts,
                                                  i64 na, i64 nb, i64 bgap, i64 CM, u32* __restrict__ cnt,
                                                  u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta) {
-  __shared__ u32 c[CH_PER_BLOCK][SMX_N_KINDS];
+  __shared__ u32 c[CH_PER_BLOCK * KH_R][SMX_N_KINDS];
   __shared__ u32 km[2];
   const i64 CA = SMX_CEIL_DIV(na, (i64)CH), CB = SMX_CEIL_DIV(nb, (i64)CH);
   const int j = threadIdx.x / 16, q = threadIdx.x % 16;
   if (threadIdx.x < 2) km[threadIdx.x] = 0;
-  const i64 g = (i64)blockIdx.x * CH_PER_BLOCK + j;
-  const int side = g >= CA;
-  const i64 cc = side ? g - CA : g;
-  const i64 len = side ? nb : na;
-  const i64 r0 = cc * CH + q * 16;  // branch position of this lane's first byte
-  const int nv = g < CA + CB ? (int)(len - r0 < 0 ? 0 : (len - r0 < 16 ? len - r0 : 16)) : 0;
-  const u8* src = kind + (side ? na + bgap : 0) + r0;
-  // timestamp samples for k_fpart: first op of each A chunk, last op of each full B chunk
-  if (g < CA + CB) {
-    if (!side && q == 0) sA[cc] = ts[cc * CH];
-    if (side && q == 15 && nv == 16) sB[cc] = ts[na + bgap + cc * CH + CH - 1];
-  }
-  u32 w[4] = {0u, 0u, 0u, 0u};
-  if (nv == 16 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-    const uint4 v = *reinterpret_cast<const uint4*>(src);
-    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-  } else {
+  // KH_R rounds of CH_PER_BLOCK chunks per block; every round's loads are issued first
+  u32 w[KH_R][4];
+  int nvr[KH_R];
 #pragma unroll
-    for (int y = 0; y < 16; ++y)
-      if (y < nv) w[y >> 2] |= (u32)src[y] << (8 * (y & 3));
+  for (int rd = 0; rd < KH_R; ++rd) {
+    const i64 g = ((i64)blockIdx.x * KH_R + rd) * CH_PER_BLOCK + j;
+    const int side = g >= CA;
+    const i64 cc = side ? g - CA : g;
+    const i64 len = side ? nb : na;
+    const i64 r0 = cc * CH + q * 16;  // branch position of this lane's first byte
+    const int nv = g < CA + CB ? (int)(len - r0 < 0 ? 0 : (len - r0 < 16 ? len - r0 : 16)) : 0;
+    nvr[rd] = nv;
+    const u8* src = kind + (side ? na + bgap : 0) + r0;
+    // timestamp samples for k_fpart: first op of each A chunk, last op of each full B chunk
+    if (g < CA + CB) {
+      if (!side && q == 0) sA[cc] = ts[cc * CH];
+      if (side && q == 15 && nv == 16) sB[cc] = ts[na + bgap + cc * CH + CH - 1];
+    }
+    w[rd][0] = w[rd][1] = w[rd][2] = w[rd][3] = 0u;
+    if (nv == 16 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src);
+      w[rd][0] = v.x; w[rd][1] = v.y; w[rd][2] = v.z; w[rd][3] = v.w;
+    } else {
+#pragma unroll
+      for (int y = 0; y < 16; ++y)
+        if (y < nv) w[rd][y >> 2] |= (u32)src[y] << (8 * (y & 3));
+    }
   }
-  u32 pk[3] = {0u, 0u, 0u};  // kind k: bits 5 * (k % 6) of word k / 6
   bool bad = false;
 #pragma unroll
-  for (int y = 0; y < 16; ++y) {
-    if (y >= nv) break;
-    u32 k = (w[y >> 2] >> (8 * (y & 3))) & 0xffu;
-    bad |= k >= SMX_N_KINDS;
-    k = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
-    const u32 wd = (k * 43u) >> 8;  // k / 6 for k < 18
-    const u32 inc = 1u << (5u * (k - 6u * wd));
-    pk[0] += wd == 0 ? inc : 0u;
-    pk[1] += wd == 1 ? inc : 0u;
-    pk[2] += wd == 2 ? inc : 0u;
+  for (int rd = 0; rd < KH_R; ++rd) {
+    const int nv = nvr[rd];
+    u32 pk[3] = {0u, 0u, 0u};  // kind k: bits 5 * (k % 6) of word k / 6
+#pragma unroll
+    for (int y = 0; y < 16; ++y) {
+      if (y >= nv) break;
+      u32 k = (w[rd][y >> 2] >> (8 * (y & 3))) & 0xffu;
+      bad |= k >= SMX_N_KINDS;
+      k = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
+      const u32 wd = (k * 43u) >> 8;  // k / 6 for k < 18
+      const u32 inc = 1u << (5u * (k - 6u * wd));
+      pk[0] += wd == 0 ? inc : 0u;
+      pk[1] += wd == 1 ? inc : 0u;
+      pk[2] += wd == 2 ? inc : 0u;
+    }
+    // 10-bit fields (a chunk count is at most 256), three kinds per word; row sums
+    u32 f[6];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      f[2 * i] = (pk[i] & 31u) | ((pk[i] >> 5) & 31u) << 10 | ((pk[i] >> 10) & 31u) << 20;
+      f[2 * i + 1] = ((pk[i] >> 15) & 31u) | ((pk[i] >> 20) & 31u) << 10 | ((pk[i] >> 25) & 31u) << 20;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      u32 v = f[i];
+      v += dpp_u32<0x111, 0xf>(v);  // row_shr:1
+      v += dpp_u32<0x112, 0xf>(v);  // row_shr:2
+      v += dpp_u32<0x114, 0xf>(v);  // row_shr:4
+      v += dpp_u32<0x118, 0xf>(v);  // row_shr:8
+      f[i] = v;
+    }
+    if (q == 15) {
+#pragma unroll
+      for (int k = 0; k < SMX_N_KINDS; ++k) c[rd * CH_PER_BLOCK + j][k] = (f[k / 3] >> (10 * (k % 3))) & 1023u;
+    }
   }
   if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) meta->bad_sym = 1;
-  // 10-bit fields (a chunk count is at most 256), three kinds per word; row sums
-  u32 f[6];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    f[2 * i] = (pk[i] & 31u) | ((pk[i] >> 5) & 31u) << 10 | ((pk[i] >> 10) & 31u) << 20;
-    f[2 * i + 1] = ((pk[i] >> 15) & 31u) | ((pk[i] >> 20) & 31u) << 10 | ((pk[i] >> 25) & 31u) << 20;
-  }
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    u32 v = f[i];
-    v += dpp_u32<0x111, 0xf>(v);  // row_shr:1
-    v += dpp_u32<0x112, 0xf>(v);  // row_shr:2
-    v += dpp_u32<0x114, 0xf>(v);  // row_shr:4
-    v += dpp_u32<0x118, 0xf>(v);  // row_shr:8
-    f[i] = v;
-  }
-  if (q == 15) {
-#pragma unroll
-    for (int k = 0; k < SMX_N_KINDS; ++k) c[j][k] = (f[k / 3] >> (10 * (k % 3))) & 1023u;
-  }
   __syncthreads();
   // column-major output: consecutive threads write consecutive chunks of one column;
   // the kinds present per branch (the scans skip the all-zero columns)
   u32 m0 = 0, m1 = 0;
-  for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += KH_NT) {
-    const int jj = i % CH_PER_BLOCK, k = i / CH_PER_BLOCK;
-    const i64 gg = (i64)blockIdx.x * CH_PER_BLOCK + jj;
+  for (int i = threadIdx.x; i < CH_PER_BLOCK * KH_R * SMX_N_KINDS; i += KH_NT) {
+    const int jj = i % (CH_PER_BLOCK * KH_R), k = i / (CH_PER_BLOCK * KH_R);
+    const i64 gg = (i64)blockIdx.x * CH_PER_BLOCK * KH_R + jj;
     if (gg >= CA + CB) continue;
     const int sd = gg >= CA;
     const u32 v = c[jj][k];
@@ -1214,7 +1228,7 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   u32* ccnt = C.ws<u32>(B_CCNT);
   u64* sA = C.ws<u64>(B_SMP);
   u64* sB = sA + SMX_CEIL_DIV(C.na, (i64)CH) + 1;
-  hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK)), dim3(KH_NT), 0, st, C.ops->kind,
+  hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK * KH_R)), dim3(KH_NT), 0, st, C.ops->kind,
                      C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta);
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
                      C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na,
