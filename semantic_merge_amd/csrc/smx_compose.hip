@@ -1130,7 +1130,18 @@ static int side_stream(SideStream** out) {
   SideStream& S = g_side[dev];
   if (!S.s) {
     // (the lowest stream priority for it measured the same, profiles/r02_k/side_prio_ab.txt)
-    HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+    // SMX_SIDE_CUS = k > 0: the side stream runs on the first k CUs only, so that the
+    // walk's small launches always find free CUs (A/B knob)
+    int ncu = 0;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int k = env_int("SMX_SIDE_CUS", 0);
+    if (k > 0 && k < ncu) {
+      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+      for (int i = 0; i < k; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+      HIP_TRY(hipExtStreamCreateWithCUMask(&S.s, (uint32_t)mask.size(), mask.data()));
+    } else {
+      HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+    }
     HIP_TRY(hipEventCreateWithFlags(&S.fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&S.join, hipEventDisableTiming));
   }
