@@ -131,17 +131,22 @@ def cpu_baseline(soa, args) -> dict:
     oracle.compose(s1)
     dt = time.perf_counter() - t0
     res = {"value": round(s1.n / dt, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+           "host_cpu_count": os.cpu_count(),
            "sample": f"first {s1.n_a:,} ops of each branch of the same workload ({s1.n:,} ops) "
                      f"through oracle/compose_ref.c, 1 thread, {dt:.1f}s"}
     legs = {}
-    # every host thread at once: independent merges (ctypes releases the GIL)
-    threads = min(16, os.cpu_count() or 1)
+    # every host thread this job may use at once: independent merges (ctypes releases
+    # the GIL).  On the GPU box os.cpu_count() reports the whole machine while the job's
+    # CPU share is OMP_NUM_THREADS (16); both are reported.
+    host_cpus = os.cpu_count() or 1
+    threads = max(1, min(host_cpus, int(os.environ.get("OMP_NUM_THREADS") or host_cpus)))
     sN = sample(args.cpu_sample // 8)
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
         list(ex.map(lambda _: oracle.compose(sN), range(threads)))
     dtN = time.perf_counter() - t0
     legs["c_port_all_threads"] = {"value": round(threads * sN.n / dtN, 1), "cores": threads,
+                                  "host_cpu_count": host_cpus,
                                   "sample": f"{threads} independent {sN.n:,}-op merges, {dtN:.1f}s"}
     sp = sample(200_000)
     t0 = time.perf_counter()
@@ -351,7 +356,9 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if strong else "weak",
+        # N > 1 splits one merge over the ranks by default (strong); N = 1 is that
+        # curve's first point.  --weak / --independent keep the per-GPU work fixed.
+        "scaling": "weak" if (args.weak or args.independent) else "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (lift-shaped op logs generated from a seed, SURVEY §8(d))",

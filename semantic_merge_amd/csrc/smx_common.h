@@ -6,6 +6,12 @@
 
 #include "../../include/smx.h"
 
+// Diagnostic build (-DSMX_DIAG=1, tools/build_variants.sh): environment knobs and the
+// window kernel's phase ablations.  The release library compiles them out.
+#ifndef SMX_DIAG
+#define SMX_DIAG 0
+#endif
+
 typedef uint64_t u64;
 typedef uint32_t u32;
 typedef int64_t i64;

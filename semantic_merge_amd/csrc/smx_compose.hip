@@ -932,7 +932,9 @@ struct Ctx {
   T* ws(int b) const { return (T*)(base + L.off[b]); }
 };
 
-// Diagnostics (tools/window_phases.py): a device buffer for k_window_f phase stamps.
+// Diagnostic builds only (tools/window_phases.py): a device buffer for k_window_f
+// phase stamps.
+#if SMX_DIAG
 static void* g_phase_dbg = nullptr;
 static size_t g_phase_dbg_bytes = 0;
 extern "C" int smx_debug_phase_buffer(void* p, size_t bytes) {
@@ -940,6 +942,10 @@ extern "C" int smx_debug_phase_buffer(void* p, size_t bytes) {
   g_phase_dbg_bytes = bytes;
   return SMX_OK;
 }
+#else
+static constexpr void* g_phase_dbg = nullptr;
+static constexpr size_t g_phase_dbg_bytes = 0;
+#endif
 
 static WinArgs win_args(const Ctx& C) {
   WinArgs P{};
@@ -1109,43 +1115,71 @@ static int launch_emit(const Ctx& C, bool packable, const smx_shard* sh) {
   return SMX_OK;
 }
 
-static int env_int(const char* name, int dflt);
+// Diagnostic knobs (SMX_ABLATE, SMX_WIN_TGT, SMX_TB_SERIAL, SMX_SIDE_CUS) are read
+// from the environment only in a diagnostic build (-DSMX_DIAG=1, tools/build_variants.sh);
+// the release library always takes the compiled defaults, so no environment variable
+// can change what smx_compose computes.
+#if SMX_DIAG
+static int knob(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+#else
+static constexpr int knob(const char*, int dflt) { return dflt; }
+#endif
 
-// A second stream per device (and its two fork/join events) for the table scatter,
-// which runs beside the walk: the walk is a chain of small, latency-bound launches
-// that leaves most of the chip idle.  Created once; the fork/join is by events, so
-// it also works inside a HIP graph capture of the caller's stream.
+// A second stream (and its fork/join events) for the table scatter, which runs beside
+// the walk: the walk is a chain of small, latency-bound launches that leaves most of
+// the chip idle.  One per (device, caller stream), created on first use, so that calls
+// on distinct streams never share one (and a graph capture of one caller's stream
+// pulls in only that caller's side stream).  `mu` is held from the fork record to the
+// join wait: two threads that share a caller stream cannot interleave their records.
+// The fork/join is by events, so it also works inside a HIP graph capture.
 struct SideStream {
+  std::mutex mu;
+  int dev = -1;
+  hipStream_t caller = nullptr;
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
 };
+#define SIDE_MAX 256  // distinct caller streams with a side stream; beyond: no overlap
 static std::mutex g_side_mu;
-static SideStream g_side[64];
+static SideStream* g_side[SIDE_MAX];
+static int g_nside = 0;
 
-static int side_stream(SideStream** out) {
+// *out = the side stream of (current device, caller), or nullptr when the table is
+// full (the caller then runs the tables on its own stream).
+static int side_stream(hipStream_t caller, SideStream** out) {
+  *out = nullptr;
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) return set_err(SMX_E_HIP, "device index out of range");
   std::lock_guard<std::mutex> g(g_side_mu);
-  SideStream& S = g_side[dev];
-  if (!S.s) {
-    // (the lowest stream priority for it measured the same, profiles/r02_k/side_prio_ab.txt)
-    // SMX_SIDE_CUS = k > 0: the side stream runs on the first k CUs only, so that the
-    // walk's small launches always find free CUs (A/B knob)
-    int ncu = 0;
-    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    const int k = env_int("SMX_SIDE_CUS", 0);
-    if (k > 0 && k < ncu) {
-      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-      for (int i = 0; i < k; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-      HIP_TRY(hipExtStreamCreateWithCUMask(&S.s, (uint32_t)mask.size(), mask.data()));
-    } else {
-      HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+  for (int i = 0; i < g_nside; ++i)
+    if (g_side[i]->dev == dev && g_side[i]->caller == caller) {
+      *out = g_side[i];
+      return SMX_OK;
     }
-    HIP_TRY(hipEventCreateWithFlags(&S.fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&S.join, hipEventDisableTiming));
+  if (g_nside == SIDE_MAX) return SMX_OK;
+  SideStream* S = new SideStream;
+  S->dev = dev;
+  S->caller = caller;
+  // (the lowest stream priority for it measured the same, profiles/r02_k/side_prio_ab.txt)
+  // SMX_SIDE_CUS = k > 0 (diagnostic builds): the side stream runs on the first k CUs
+  // only (measured slower, profiles/r02_k/side_cumask_ab.txt)
+  int ncu = 0;
+  HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int k = knob("SMX_SIDE_CUS", 0);
+  if (k > 0 && k < ncu) {
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+    for (int i = 0; i < k; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+    HIP_TRY(hipExtStreamCreateWithCUMask(&S->s, (uint32_t)mask.size(), mask.data()));
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&S->s, hipStreamNonBlocking));
   }
-  *out = &S;
+  HIP_TRY(hipEventCreateWithFlags(&S->fork, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&S->join, hipEventDisableTiming));
+  g_side[g_nside++] = S;
+  *out = S;
   return SMX_OK;
 }
 
@@ -1167,8 +1201,12 @@ static int launch_tail(const Ctx& C) {
   if (width > TB_WIDTH) width = TB_WIDTH;
   const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);
   // small merges are launch-bound: the fork/join costs more than the overlap saves
-  const bool overlap = SMX_TB_OVERLAP && nbk <= TB_MAXBK && C.n >= SMX_TB_OVERLAP_MIN && !env_int("SMX_TB_SERIAL", 0);
-  if (!overlap) {
+  SideStream* S = nullptr;
+  if (SMX_TB_OVERLAP && nbk <= TB_MAXBK && C.n >= SMX_TB_OVERLAP_MIN && !knob("SMX_TB_SERIAL", 0)) {
+    int rc = side_stream(C.st, &S);
+    if (rc) return rc;
+  }
+  if (!S) {
     C.tm->begin(ST_WALK);
     int rc = launch_walk(C, nullptr);
     if (rc) return rc;
@@ -1182,9 +1220,8 @@ static int launch_tail(const Ctx& C) {
     C.tm->end(ST_EMIT);
     return SMX_OK;
   }
-  SideStream* S = nullptr;
-  int rc = side_stream(&S);
-  if (rc) return rc;
+  std::lock_guard<std::mutex> own(S->mu);  // fork record .. join wait
+  int rc;
   hipStream_t st = C.st;
   TbArgs A = tb_args(C);
   A.width = (u32)width;
@@ -1219,10 +1256,6 @@ static int launch_tail(const Ctx& C) {
 
 // Presorted plan: branch logs with non-decreasing timestamps (what lift.ts
 // emits).  Speculative: k_window_f verifies the layout and flags f_fail.
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
 
 static int run_presorted(const Ctx& C, i64 tgt) {
   hipStream_t st = C.st;
@@ -1265,7 +1298,7 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   P.klo = C.ops->oid_lo;
   P.perm = nullptr;
   P.W = W;
-  P.ablate = env_int("SMX_ABLATE", 0);
+  P.ablate = knob("SMX_ABLATE", 0);
   C.tm->begin(ST_WINDOW);
   if (g_phase_dbg && !P.src_map && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
     P.dbg = (u64*)g_phase_dbg;
@@ -1747,7 +1780,7 @@ static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeM
 // tail launched behind it when `tail` -- every tail kernel is a no-op if the window
 // kernel flags the plan as failed -- then the fallbacks.  hm: the meta after it.
 static int run_order(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm) {
-  const i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
+  const i64 tgt = knob("SMX_WIN_TGT", WIN_TGT);
   int rc = run_presorted(C, tgt);
   if (rc) return rc;
   if (tail && (rc = launch_tail(C))) return rc;
@@ -1799,8 +1832,8 @@ static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, vo
   }
   StageTimer tm(st, profiling_on() != 0);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
-  if ((rc = run_presorted(C, env_int("SMX_WIN_TGT", WIN_TGT)))) return rc;
-  if (!env_int("SMX_ABLATE", 0) && (rc = launch_tail(C))) return rc;  // SMX_ABLATE: window stage only
+  if ((rc = run_presorted(C, knob("SMX_WIN_TGT", WIN_TGT)))) return rc;
+  if (!knob("SMX_ABLATE", 0) && (rc = launch_tail(C))) return rc;  // SMX_ABLATE (diagnostic builds): window only
   tm.flush();
   return SMX_OK;
 }
@@ -1813,13 +1846,13 @@ static int compose_finish_impl(const smx_ops* ops, const smx_compose_out* out, v
   int rc = check_args(ops, out, ws, ws_bytes, &L);
   if (rc) return rc;
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
-  if (n == 0 || env_int("SMX_ABLATE", 0)) return SMX_OK;
+  if (n == 0 || knob("SMX_ABLATE", 0)) return SMX_OK;
   StageTimer tm(st, profiling_on() != 0);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
   ComposeMeta hm;
   if ((rc = read_meta(C, &hm))) return rc;
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
-  if (hm.f_fail && (rc = order_fallbacks(C, true, true, &hm, env_int("SMX_WIN_TGT", WIN_TGT)))) return rc;
+  if (hm.f_fail && (rc = order_fallbacks(C, true, true, &hm, knob("SMX_WIN_TGT", WIN_TGT)))) return rc;
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
   if (hm.n_move_none && hm.kcnt[KMOVE]) {
     tm.begin(ST_MVPREFIX);
@@ -1923,7 +1956,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
     case SMX_SHARD_ORDER_FIX: {
       if (sh->halo_cap < 0 || (sh->halo_cap > 0 && (!sh->export_sym || !sh->export_cls || !sh->export_src)))
         return set_err(SMX_E_ARG, "bad export buffers");
-      const i64 tgt = env_int("SMX_WIN_TGT", WIN_TGT);
+      const i64 tgt = knob("SMX_WIN_TGT", WIN_TGT);
       if (step == SMX_SHARD_ORDER && !sh->src_map) {  // asynchronous: failures show in summary[21]
         g_plan = SMX_PLAN_PRESORTED;
         if ((rc = run_presorted(C, tgt))) return rc;

@@ -77,7 +77,7 @@ struct WinArgs {
   i64 n_sym;
   i64 src_a, src_b; // global source index of local op j (sharded merge; 0 / na otherwise)
   const i32* src_map;  // sample-sorted shard: global source of local op j, or null
-  int ablate;       // diagnostics only (SMX_ABLATE): skip phases, results invalid
+  int ablate;       // diagnostic builds only (SMX_ABLATE): skip phases, results invalid
   const i64* bnd;
   const u32* woff;  // [NCNT][W] exclusive offsets over windows (generic plan)
   const u32* cpre;  // presorted plan: [2][kinds][CM] chunk prefixes (256-op chunks)
@@ -379,7 +379,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   __syncthreads();
   if (wtot[0]) return;  // (wtot is written again in step 6)
   WSTAMP(1);
-  if (P.ablate & 16) {  // diagnostics: load only (keeps every load live)
+  if (SMX_DIAG && (P.ablate & 16)) {  // diagnostics: load only (keeps every load live)
     u32 x = 0;
 #pragma unroll
     for (int i = 0; i < WF_ITEMS; ++i) x += sym_r[i] + (u32)v0_r[i] + (u32)v1_r[i] + (u32)hi_r[i];
@@ -411,7 +411,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
     if (e >= sz) continue;
-    if (!(P.ablate & 1) && e != 0 && e != na && sts[e - 1] > ts_r[i]) dec = true;
+    if (!(SMX_DIAG && (P.ablate & 1)) && e != 0 && e != na && sts[e - 1] > ts_r[i]) dec = true;
   }
   {
     const int d0 = t * WF_ITEMS < sz ? t * WF_ITEMS : sz;
@@ -606,7 +606,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     }
 #endif
     int r = p;
-    if (ge - gs > 1 && !(P.ablate & 2)) {
+    if (ge - gs > 1 && !(SMX_DIAG && (P.ablate & 2))) {
       const u32 kp = pkey[p];
       const uint4* pv = reinterpret_cast<const uint4*>(pkey);
       const int q0 = gs & ~3;
@@ -772,7 +772,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
 
   // 7. payload by element, round 1: sym (| the move's has-value bits) and v0; the
   //    position of each rename in its branch's list (posl)
-  if (P.ablate & 4) return;
+  if (SMX_DIAG && (P.ablate & 4)) return;
   u32* st_a = (u32*)sts;             // [WF_CAP] sym | flags
   i32* st_b = (i32*)sts + WF_CAP;   // [WF_CAP] v0, then v1
   u16* posl = sl;

@@ -276,7 +276,7 @@ class ShardedCompose:
                 parts.append(_u64_key(torch.stack([ts[0], ts[-1]])))
                 if n > 1 and self.mode == "auto":  # "range": the ORDER plan checks the order itself
                     k = _u64_key(ts)
-                    ok = (k[1:] >= k[:-1]).all().to(torch.int64).view(1)
+                    ok = ok & (k[1:] >= k[:-1]).all().to(torch.int64).view(1)  # both branches
             else:
                 parts.append(self._zero2)
         return torch.cat(parts + [ok, self._signed])

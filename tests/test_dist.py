@@ -1,6 +1,7 @@
 """Multi-process path of bench.py on CPU: world_size 2 over gloo (127.0.0.1)."""
 import os
-import socket
+import shutil
+import tempfile
 
 import pytest
 import torch.multiprocessing as mp
@@ -8,19 +9,11 @@ import torch.multiprocessing as mp
 from semantic_merge_amd import dist as smx_dist
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
-def _worker(rank, world, port, q):
+def _worker(rank, world, store_path, q):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
-                      RANK=str(rank), LOCAL_RANK=str(rank))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank))
+    # FileStore rendezvous: no bound-then-freed port for the children to race for
+    dist.init_process_group("gloo", store=dist.FileStore(store_path, world), rank=rank, world_size=world)
     info = smx_dist.rank_info()
     dist.barrier()
     elapsed = smx_dist.max_over_ranks(1.0 + rank)  # rank 1 is the slowest
@@ -34,13 +27,14 @@ def _worker(rank, world, port, q):
 def test_two_rank_gloo():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    tmp = tempfile.mkdtemp(prefix="smx_store_")
+    procs = [ctx.Process(target=_worker, args=(r, 2, os.path.join(tmp, "store"), q)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
+    shutil.rmtree(tmp, ignore_errors=True)
     res = sorted(q.get(timeout=5) for _ in range(2))
     assert [r[0] for r in res] == [0, 1] and all(r[1] == 2 for r in res)
     assert all(r[2] == 2.0 for r in res)            # MAX over ranks seen by every rank

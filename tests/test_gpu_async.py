@@ -73,3 +73,68 @@ def test_async_reports_pending_work():
     assert int(dc.counts[0].item()) == -3
     dc.finish()
     _check(dc, soa, "none moves")
+
+
+def test_async_captured_in_a_graph_forked_tail():
+    # >= 4M ops: the table scatter runs on the caller's side stream (event fork/join),
+    # so the capture holds both streams
+    import torch
+    soa = _lift(5_000_000, 100_000, 8)
+    dc = _lib.DeviceCompose(soa)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        dc.run_async()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        dc.run_async()
+    dc.counts.fill_(-7)
+    dc.order.fill_(-7)
+    dc.addr.fill_(-7)
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    assert int(dc.counts[0].item()) >= 0
+    _check(dc, soa, "graph replay, forked tail")
+
+
+def test_two_threads_compose_concurrently():
+    # smx_compose is reentrant across distinct buffers and streams (include/smx.h):
+    # two host threads, each with its own stream, each composing two 5M-op merges
+    # (forked table scatter) at the same time on one device
+    import threading
+    import torch
+    soas = [[_lift(5_000_000, 50_000 + 7 * t + k, 20 + 2 * t + k) for k in range(2)] for t in range(2)]
+    dcs = [[_lib.DeviceCompose(x) for x in row] for row in soas]
+    bar = threading.Barrier(2)
+    errors, results = [], {}
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for rep in range(3):
+                    for k in range(2):
+                        bar.wait()
+                        dcs[t][k].run(s)
+                s.synchronize()
+            for k in range(2):
+                results[(t, k)] = dcs[t][k].results()
+        except BaseException as e:  # noqa: BLE001 -- reported below
+            errors.append(e)
+            bar.abort()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not any(x.is_alive() for x in th), "a compose thread did not finish"
+    assert not errors, errors
+    for t in range(2):
+        for k in range(2):
+            ref = oracle.compose(soas[t][k])
+            for name, g, r in zip(("order", "addr", "file", "ctx", "conflicts"), results[(t, k)], ref):
+                assert np.array_equal(g, r), f"thread {t} merge {k}: {name}"

@@ -54,6 +54,38 @@ def test_dropin_compose_oplogs_matches_reference():
     assert all(o is not a for o in out for a in A + B)
 
 
+def test_config1_e2e_compose_then_apply(tmp_path):
+    """Config 1 (/root/reference/tests/e2e_rename_move_decl.sh:14-74) on the box: the GPU
+    drop-in compose_oplogs, then the fast apply_ops (semantic_merge_amd/applier.py), give
+    the composed log and the merged tree the reference's compose_oplogs + apply_ops gave
+    (tests/golden/e2e_tree.json, tools/make_golden.py --only e2e)."""
+    import os
+    import shutil
+    from semantic_merge_amd import applier
+    case = load("e2e_tree.json")
+    base = tmp_path / "base"
+    for pth, text in case["base"].items():
+        (base / pth).parent.mkdir(parents=True, exist_ok=True)
+        (base / pth).write_text(text, encoding="utf-8")
+    out, conf = compose_oplogs(to_ops(case["A"]), to_ops(case["B"]))
+    assert jline([o.to_dict() for o in out]) == jline(case["out"])
+    assert [c.to_dict() for c in conf] == case["conflicts"] == []
+    merged = applier.apply_ops(base, out)
+    try:
+        files, dirs = {}, []
+        for dp, _, fn in os.walk(merged):
+            rel = os.path.relpath(dp, merged)
+            if rel != ".":
+                dirs.append(rel)
+            for f in fn:
+                with open(os.path.join(dp, f), "rb") as fh:
+                    files[os.path.normpath(os.path.join(rel, f))] = fh.read().decode("latin-1")
+        assert files == case["files"] and sorted(dirs) == case["dirs"]
+        assert "function bar" in files["lib/util.ts"]
+    finally:
+        shutil.rmtree(merged)
+
+
 def _digest(dicts):
     h = hashlib.sha256()
     for d in dicts:
@@ -63,7 +95,7 @@ def _digest(dicts):
 
 
 @pytest.mark.parametrize("name", ["lift_20k", "lift_100k_shuffled", "adversarial_100k",
-                                  "lift_200k"])
+                                  "lift_200k", "c2_1M"])
 def test_synthetic_digests_gpu(name):
     rec = {r["name"]: r for r in load("compose_digests.json")}[name]
     kw = dict(rec["spec"])

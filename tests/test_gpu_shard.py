@@ -3,7 +3,10 @@ GPU over gloo (collectives through host copies; RCCL runs the same code on a nod
 Each rank starts from an index slice of the global logs; the assembled per-shard outputs
 must equal the CPU oracle's composition of the whole merge, bit for bit."""
 import os
+import queue
+import shutil
 import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -13,11 +16,63 @@ pytestmark = pytest.mark.gpu
 
 
 def _free_port():
+    # only for torch.distributed.run's --master-port (test_bench_two_ranks_sharded);
+    # the spawned workers below rendezvous through a FileStore instead
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     return port
+
+
+def _init(rank, world, store_path, backend="gloo"):
+    """Process group over a FileStore: no port to race for (a bound-then-freed port
+    handed to the children can be taken before rank 0 listens on it), and no eager
+    communicator set-up for RCCL (it is created by the first collective)."""
+    import torch
+    import torch.distributed as dist
+    store = dist.FileStore(store_path, world)
+    if backend == "nccl":  # RCCL: one rank per GPU
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, store=store, rank=rank, world_size=world)
+
+
+def _phase(q, rank, name):
+    q.put(("phase", rank, name))
+
+
+def _spawn(target, world, extra, timeout):
+    """Start `world` ranks of target(rank, world, store_path, q, *extra) and collect one
+    ("done", rank, payload) per rank.  Ranks report ("phase", rank, name) as they go;
+    if nothing arrives for `timeout` seconds the ranks are killed and the failure names
+    each rank's last phase."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    tmp = tempfile.mkdtemp(prefix="smx_store_")
+    store_path = os.path.join(tmp, "store")
+    procs = [ctx.Process(target=target, args=(r, world, store_path, q) + tuple(extra)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, last = {}, {r: "spawned" for r in range(world)}
+    try:
+        while len(got) < world:
+            try:
+                msg = q.get(timeout=timeout)
+            except queue.Empty:
+                raise AssertionError(f"no progress for {timeout} s; last phase per rank: {last}") from None
+            if msg[0] == "phase":
+                last[msg[1]] = msg[2]
+            else:
+                got[msg[1]] = msg[2]
+        for p in procs:
+            p.join(60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(10)
+        shutil.rmtree(tmp, ignore_errors=True)
+    return got
 
 
 def _make(case):
@@ -98,48 +153,37 @@ def _hollow_soa(n_ren, seed):
     return SoA(na, nb, kind, ts, hi, lo, sym, v0, v0.copy(), 1, ["a", "b"])
 
 
-def _worker(rank, world, port, case, halo, q, mode="auto", backend="gloo"):
-    import torch
+def _worker(rank, world, store_path, q, case, halo, mode="auto", backend="gloo"):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    if backend == "nccl":  # RCCL: one rank per GPU
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
-    else:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    _phase(q, rank, "init_process_group")
+    _init(rank, world, store_path, backend)
     try:
         from semantic_merge_amd import shard
+        _phase(q, rank, "make inputs")
         soa = _make(case)
         a, b, na, nb = shard.slices_from_soa(soa, rank, world, "cuda:0")
+        _phase(q, rank, "ShardedCompose")
         sc = shard.ShardedCompose(a, b, na, nb, soa.n_sym, shard.Comm(), "cuda:0", halo_cap=halo,
                                   mode=mode)
+        _phase(q, rank, "run 1")
         sc.run()
         res = sc.results()
         first = (res, sc.totals())
+        _phase(q, rank, "run 2")
         sc.run()  # a second run on the same buffers (bench.py's steps) gives the same results
         res2 = sc.results()
         same = all(np.array_equal(x, y) for x, y in zip(first[0][:5], res2[:5]))
-        q.put((rank, res, sc.in_state, (sc.exchange_mode, same, first[1], sc.order_fixes)))
+        _phase(q, rank, "destroy_process_group")
+        q.put(("done", rank, (res, sc.in_state, (sc.exchange_mode, same, first[1], sc.order_fixes))))
     except Exception as e:  # report to the parent instead of hanging the collective
-        q.put((rank, repr(e), None, None))
+        q.put(("done", rank, (repr(e), None, None)))
         raise
     finally:
         dist.destroy_process_group()
 
 
 def _run(case, world, halo=4096, mode="auto", backend="gloo"):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, halo, q, mode, backend))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    got = {}
-    for _ in range(world):
-        r, res, st, nopen = q.get(timeout=240)
-        got[r] = (res, st, nopen)
-    for p in procs:
-        p.join(60)
+    got = _spawn(_worker, world, (case, halo, mode, backend), timeout=180)
     for r in range(world):
         assert not isinstance(got[r][0], str), f"rank {r}: {got[r][0]}"
     return [got[r][0] for r in range(world)], got
@@ -164,13 +208,7 @@ def _check(case, world, halo=4096, mode="auto", want_mode=None, backend="gloo"):
     return got, ref
 
 
-@pytest.mark.parametrize("mode", [
-    "range",
-    # all_to_all_single on RCCL: passed on the box (profiles/r02_i), but one of three runs
-    # hung at start-up, so it is opt-in (SMX_TEST_RCCL=1) rather than in the round-end suite
-    pytest.param("sample", marks=pytest.mark.skipif(os.environ.get("SMX_TEST_RCCL") != "1",
-                                                    reason="opt-in: SMX_TEST_RCCL=1")),
-])
+@pytest.mark.parametrize("mode", ["range", "sample"])
 def test_shard_rccl_single_rank(mode):
     """The RCCL branch of shard.Comm (collectives on device tensors: all_gather_into_tensor,
     MAX all_reduce on int64, all_to_all_single of packed uint8 records) on one GPU: a
@@ -258,24 +296,26 @@ def test_bench_two_ranks_sharded():
         assert out["value"] > 0 and "key-range shards" in out["config"]["parallelism"]
 
 
-def _full_worker(rank, world, port, q):
+def _full_worker(rank, world, store_path, q):
     import hashlib
-    import json
     import torch
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _phase(q, rank, "init_process_group")
+    _init(rank, world, store_path)
     try:
+        _phase(q, rank, "generate c3")
         from semantic_merge_amd import shard, synth
         soa = synth.lift_soa(synth.lift_logs(synth.CONFIGS["c3"]))
         a, b, na, nb = shard.slices_from_soa(soa, rank, world, "cuda:0")
         del soa
         sc = shard.ShardedCompose(a, b, na, nb, 1_000_000, shard.Comm(), "cuda:0", mode="range")
         del a, b
+        _phase(q, rank, "run")
         sc.run()
         res = sc.results()
         del sc
         torch.cuda.empty_cache()
+        _phase(q, rank, "gather outputs")
         if rank == 0:  # gather the other shards' outputs, assemble, digest
             parts = [res]
             for r in range(1, world):
@@ -286,12 +326,12 @@ def _full_worker(rank, world, port, q):
             h = hashlib.sha256()
             for arr in glob:
                 h.update(np.ascontiguousarray(arr, dtype=np.int32).tobytes())
-            q.put((rank, (len(glob[0]), len(glob[4]), h.hexdigest())))
+            q.put(("done", rank, (len(glob[0]), len(glob[4]), h.hexdigest())))
         else:
             dist.send_object_list([res], dst=0)
-            q.put((rank, None))
+            q.put(("done", rank, None))
     except Exception as e:  # report to the parent instead of hanging the collective
-        q.put((rank, repr(e)))
+        q.put(("done", rank, repr(e)))
         raise
     finally:
         dist.destroy_process_group()
@@ -305,15 +345,7 @@ def test_shard_full_size_c3_two_ranks():
     import json
     rec = {r["name"]: r for r in json.load(open(os.path.join(os.path.dirname(__file__), "golden",
                                                              "full_digests.json")))}["c3"]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_full_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    got = dict(q.get(timeout=800) for _ in range(2))
-    for p in procs:
-        p.join(120)
+    got = _spawn(_full_worker, 2, (), timeout=400)
     assert not isinstance(got[1], str), got[1]
     assert not isinstance(got[0], str), got[0]
     n_out, n_conf, digest = got[0]

@@ -42,7 +42,7 @@ def spec_of(rec):
 
 
 @pytest.mark.parametrize("name", ["lift_20k", "lift_100k_shuffled", "adversarial_100k",
-                                  "lift_200k"])
+                                  "lift_200k", "c2_1M"])
 def test_synthetic_digests_match_reference(name):
     rec = {r["name"]: r for r in load("compose_digests.json")}[name]
     logs = synth.lift_logs(spec_of(rec))

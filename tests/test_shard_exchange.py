@@ -5,19 +5,22 @@ back for the next step.  The sample-sort exchange (logs in any order) puts every
 the shard owning its full T key, with its global source index.  The compute steps need
 a GPU (tests/test_gpu_shard.py)."""
 import os
-import socket
+import shutil
+import tempfile
 
 import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+def _init(rank, world, store_path):
+    # FileStore rendezvous: no bound-then-freed port for the children to race for
+    import torch.distributed as dist
+    dist.init_process_group("gloo", store=dist.FileStore(store_path, world), rank=rank, world_size=world)
+
+
+def _store_path():
+    return os.path.join(tempfile.mkdtemp(prefix="smx_store_"), "store")
 
 
 def _soa(n, seed, ops_per_ms, high=False):
@@ -30,11 +33,10 @@ def _soa(n, seed, ops_per_ms, high=False):
     return soa
 
 
-def _worker(rank, world, port, args, q):
+def _worker(rank, world, port, args, q):  # port: the FileStore path
     import torch
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world, port)
     try:
         from semantic_merge_amd import shard
         n, seed, opm, headroom, high = args
@@ -67,7 +69,7 @@ def test_exchange_key_ranges(world, n, opm, headroom, high):
     from semantic_merge_amd import shard
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    port = _store_path()
     args = (n, 3, opm, headroom, high)
     procs = [ctx.Process(target=_worker, args=(r, world, port, args, q)) for r in range(world)]
     for p in procs:
@@ -78,6 +80,7 @@ def test_exchange_key_ranges(world, n, opm, headroom, high):
         res[item[0]] = item
     for p in procs:
         p.join(60)
+    shutil.rmtree(os.path.dirname(port), ignore_errors=True)
     errs = [res[r][1] for r in range(world) if isinstance(res[r][1], str)]
     assert not errs, errs
     soa = _soa(n, 3, opm, high)
@@ -109,7 +112,7 @@ def test_exchange_key_ranges(world, n, opm, headroom, high):
 def _spawn(target, world, args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    port = _store_path()
     procs = [ctx.Process(target=target, args=(r, world, port, args, q)) for r in range(world)]
     for p in procs:
         p.start()
@@ -119,24 +122,33 @@ def _spawn(target, world, args):
         res[item[0]] = item
     for p in procs:
         p.join(60)
+    shutil.rmtree(os.path.dirname(port), ignore_errors=True)
     errs = [res[r][1] for r in range(world) if isinstance(res[r][1], str)]
     assert not errs, errs
     return res
 
 
-def _shuffled(n, seed):
+def _shuffled(n, seed, only_a=False):
     from semantic_merge_amd import synth
-    return synth.lift_soa(synth.lift_logs(synth.LiftSpec(n, 40, seed, ops_per_ms=3, shuffle=True)))
+    if not only_a:
+        return synth.lift_soa(synth.lift_logs(synth.LiftSpec(n, 40, seed, ops_per_ms=3, shuffle=True)))
+    # branch A in random order, branch B timestamp-ordered (the order flags
+    # of the two branches must be combined, not overwritten by B's)
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(n, 40, seed, ops_per_ms=3)))
+    perm = np.random.default_rng(seed).permutation(soa.n_a)
+    for f in ("kind", "ts", "oid_hi", "oid_lo", "sym", "v0", "v1"):
+        col = getattr(soa, f)
+        col[:soa.n_a] = col[:soa.n_a][perm]
+    return soa
 
 
 def _sample_worker(rank, world, port, args, q):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world, port)
     try:
         from semantic_merge_amd import shard
-        n, seed, mode = args
-        soa = _shuffled(n, seed)
+        n, seed, mode, only_a = args
+        soa = _shuffled(n, seed, only_a)
         a, b, na, nb = shard.slices_from_soa(soa, rank, world, "cpu")
         sc = shard.ShardedCompose(a, b, na, nb, soa.n_sym, shard.Comm(), "cpu", halo_cap=64,
                                   mode=mode, oversample=32)
@@ -151,13 +163,15 @@ def _sample_worker(rank, world, port, args, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,mode", [(2, 6_000, "sample"), (3, 9_001, "auto")])
-def test_exchange_sample_sort(world, n, mode):
+@pytest.mark.parametrize("world,n,mode,only_a", [(2, 6_000, "sample", False), (3, 9_001, "auto", False),
+                                                (2, 6_000, "auto", True)])
+def test_exchange_sample_sort(world, n, mode, only_a):
     """Unordered branch logs: every op lands exactly once on the shard owning its full T
-    key (kind, ts, oid, side, index), A' and B' in global index order, shards balanced."""
+    key (kind, ts, oid, side, index), A' and B' in global index order, shards balanced.
+    With mode "auto", one unordered branch is enough to choose the sample sort."""
     from semantic_merge_amd import shard
-    res = _spawn(_sample_worker, world, (n, 5, mode))
-    soa = _shuffled(n, 5)
+    res = _spawn(_sample_worker, world, (n, 5, mode, only_a))
+    soa = _shuffled(n, 5, only_a)
     cols = {"kind": soa.kind, "ts": soa.ts.view(np.int64), "hi": soa.oid_hi.view(np.int64),
             "lo": soa.oid_lo.view(np.int64), "sym": soa.sym.view(np.int32), "v0": soa.v0, "v1": soa.v1}
     seen = np.zeros(soa.n, np.int64)
@@ -204,8 +218,7 @@ def test_packed_records_round_trip():
 
 def _strong_worker(rank, world, port, args, q):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world, port)
     try:
         from semantic_merge_amd import shard, synth
         n_total, = args

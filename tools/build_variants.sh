@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build libsmx variants with extra -D flags for A/B timing on the GPU box:
 #   tools/build_variants.sh name1:"-DX=1 -DY=0" name2:"..."
+# (environment knobs such as SMX_ABLATE / SMX_WIN_TGT need "-DSMX_DIAG=1")
 # -> tools/_build/var_<name>/libsmx.so  (run with SMX_LIB=<that path>)
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)

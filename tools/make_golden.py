@@ -7,9 +7,12 @@ crdt never do).  Nothing from the reference is copied: the committed fixtures ar
 inputs and the reference's outputs (JSON), plus sha256 digests for the large
 synthetic configs.  The GPU box never reads /root/reference.
 
-    python tools/make_golden.py [--big]
+    python tools/make_golden.py [--big] [--only oplog|applier|big|e2e]
 
-``--big`` also composes the 1M-op config 2 (~25 s of reference CPU time).
+``--big`` also composes the 1M-op config 2 (~25 s of reference CPU time);
+``--only big`` composes only that.  ``--only e2e`` records config 1 (the
+reference's tests/e2e_rename_move_decl.sh scenario) end to end: base tree, both op
+logs, and the tree the reference's compose_oplogs + apply_ops leave.
 """
 from __future__ import annotations
 
@@ -315,6 +318,36 @@ def _tree(root):
     return files, sorted(dirs)
 
 
+def make_e2e_tree(compose, applier_mod, ops_mod):
+    """Config 1: tests/e2e_rename_move_decl.sh:14-74 with fixed ids -- base tree
+    src/util.ts, A renames foo -> bar, B moves the declaration to lib/util.ts; the
+    reference's composed log and the merged tree its apply_ops leaves."""
+    import pathlib
+    import shutil
+    import tempfile
+    sc = scenarios(compose, ops_mod)["e2e_rename_move_decl"]
+    base_files = {"src/util.ts": "export function foo(x: number) {\n  return x + 1;\n}\n"}
+    tmp = tempfile.mkdtemp(prefix="smx_e2e_")
+    try:
+        for pth, text in base_files.items():
+            full = pathlib.Path(tmp) / pth
+            full.parent.mkdir(parents=True, exist_ok=True)
+            full.write_text(text, encoding="utf-8")
+        oa = [ops_mod.Op.from_dict(d) for d in sc["A"]]
+        ob = [ops_mod.Op.from_dict(d) for d in sc["B"]]
+        out, conf = compose.compose_oplogs(oa, ob)
+        merged = applier_mod.apply_ops(pathlib.Path(tmp), out)
+        try:
+            files, dirs = _tree(merged)
+        finally:
+            shutil.rmtree(merged, ignore_errors=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    assert "function bar" in files["lib/util.ts"]
+    return {"base": base_files, "A": sc["A"], "B": sc["B"], "out": [o.to_dict() for o in out],
+            "conflicts": [c.to_dict() for c in conf], "files": files, "dirs": dirs}
+
+
 def make_applier_cases(applier_mod, ops_mod, n_cases: int, seed: int):
     import shutil
     import tempfile
@@ -384,7 +417,8 @@ def make_applier_cases(applier_mod, ops_mod, n_cases: int, seed: int):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
-    ap.add_argument("--only", choices=["oplog", "applier"], help="regenerate one fixture file only")
+    ap.add_argument("--only", choices=["oplog", "applier", "big", "e2e"],
+                    help="regenerate one fixture only")
     args = ap.parse_args()
     compose, crdt, ops_mod = _import_reference()
     os.makedirs(GOLD, exist_ok=True)
@@ -396,6 +430,13 @@ def main() -> None:
         with open(os.path.join(GOLD, "applier_cases.json"), "w") as fh:
             json.dump(make_applier_cases(applier_mod, ops_mod, 400, seed=77), fh, separators=(",", ":"),
                       ensure_ascii=False)
+    if args.only == "e2e":
+        from semmerge import applier as applier_mod
+        with open(os.path.join(GOLD, "e2e_tree.json"), "w") as fh:
+            json.dump(make_e2e_tree(compose, applier_mod, ops_mod), fh, indent=1, ensure_ascii=False)
+    if args.only == "big":
+        from semantic_merge_amd import synth
+        _save_digests([synth_digest(compose, ops_mod, "c2_1M", synth.CONFIGS["c2"])])
     if args.only:
         return
 
@@ -420,7 +461,10 @@ def main() -> None:
     ]
     if args.big:
         specs.append(("c2_1M", synth.CONFIGS["c2"]))
-    recs = [synth_digest(compose, ops_mod, name, spec) for name, spec in specs]
+    _save_digests([synth_digest(compose, ops_mod, name, spec) for name, spec in specs])
+
+
+def _save_digests(recs) -> None:
     path = os.path.join(GOLD, "compose_digests.json")
     old = {}
     if os.path.exists(path):
