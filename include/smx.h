@@ -144,7 +144,11 @@ int smx_last_plan(void);
  *                     may be re-run when the incoming region changes;
  *                     writes summary[22..27]
  *   SMX_SHARD_TABLES  this shard's last writers -> part_tab (MAX-reduce them
- *                     over shards next); writes summary[28..30]
+ *                     over shards next); writes summary[28..30].  ORDER and
+ *                     ORDER_FIX already bucket the table records (beside the
+ *                     walk); TABLES applies the walk's skips to them, which it can
+ *                     do once:
+ *   SMX_SHARD_SCATTER re-buckets the records, for a TABLES after a WALK re-run
  *   SMX_SHARD_EMIT    composed output from the reduced tables (fin_tab) and
  *                     the global value widths (glob[0..2]); mv_prefix (or NULL
  *                     when no move has a None value) = [2][n_sym] last non-None
@@ -164,6 +168,7 @@ int smx_last_plan(void);
 #define SMX_SHARD_TABLES 2
 #define SMX_SHARD_EMIT 3
 #define SMX_SHARD_ORDER_FIX 4
+#define SMX_SHARD_SCATTER 5
 #define SMX_SHARD_SUMMARY 32
 
 typedef struct smx_shard {
@@ -200,6 +205,13 @@ typedef struct smx_shard {
   const int32_t* src_map;
   /* host memory: this shard's summary [SMX_SHARD_SUMMARY] after WALK, or NULL */
   const int64_t* summary_host;
+  /* Device, or NULL: the all-gather of every shard's ORDER outputs, row q =
+   * shard q's summary [SMX_SHARD_SUMMARY] then its exports (export_sym, export_cls,
+   * export_src, each [2][halo_cap] 32-bit) -- [world][SMX_SHARD_SUMMARY + 3 * halo_cap]
+   * int64.  When set, the WALK step first assembles this shard's halo from it on the
+   * device: halo_sym / halo_cls / halo_src ([halo_cap] each, writable) and halo_dev
+   * (writable) are then outputs, so the host needs no read of the summaries. */
+  const int64_t* order_gather;
 } smx_shard;
 
 int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const smx_compose_out* out,
@@ -249,6 +261,11 @@ typedef struct smx_rga_out {
   int32_t* out_src;
   int64_t* out_offsets;
   int64_t* counts; /* counts[0] = surviving elements */
+  /* NULL: the output is materialize() (live elements only).  Non-NULL: the output is
+   * the whole list state RGA.list (crdt.py:26-27) -- the live elements and the ones
+   * delete() tombstoned, in list order -- and out_tomb[k] = 1 marks the tombstoned
+   * ones (0 the live ones); counts[0] = elements in the lists. */
+  uint8_t* out_tomb;
 } smx_rga_out;
 
 int smx_rga_workspace_bytes(int64_t n_ops, int64_t n_lists, size_t* bytes);

@@ -64,11 +64,13 @@ class SmxShard(C.Structure):
         ("in_state_dev", C.c_void_p),
         ("src_map", C.c_void_p),
         ("summary_host", C.c_void_p),
+        ("order_gather", C.c_void_p),
     ]
 
 
 SHARD_ORDER, SHARD_WALK, SHARD_TABLES, SHARD_EMIT = 0, 1, 2, 3
 SHARD_ORDER_FIX = 4
+SHARD_SCATTER = 5
 PLAN_NAMES = ("presorted", "segmented", "radix", "radix+oid_lo")  # smx_last_plan()
 SHARD_SUMMARY = 32
 
@@ -94,6 +96,7 @@ class SmxRgaOut(C.Structure):
         ("out_src", C.c_void_p),
         ("out_offsets", C.c_void_p),
         ("counts", C.c_void_p),
+        ("out_tomb", C.c_void_p),
     ]
 
 

@@ -231,14 +231,16 @@ def stage_times():
     return {L.smx_stage_name(i).decode(): (ms[i], calls[i]) for i in range(n)}
 
 
-def rga_replay_device(batch, device: str = "cuda"):
-    """(values, src, offsets) of a batched RGA replay computed on the GPU."""
+def rga_replay_device(batch, device: str = "cuda", tombstones: bool = False):
+    """(values, src, offsets) of a batched RGA replay computed on the GPU; with
+    tombstones=True the whole list state (live and tombstoned elements, crdt.py RGA.list)
+    and a fourth array, the tombstone flags."""
     torch = _torch()
     dev = torch.device(device)
     n = batch.n
     if n == 0:
-        return (np.zeros(0, np.uint32), np.zeros(0, np.int32),
-                np.zeros(batch.n_lists + 1, np.int64))
+        e = (np.zeros(0, np.uint32), np.zeros(0, np.int32), np.zeros(batch.n_lists + 1, np.int64))
+        return e + (np.zeros(0, np.bool_),) if tombstones else e
 
     def up(a, dt):
         return torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
@@ -250,14 +252,15 @@ def rga_replay_device(batch, device: str = "cuda"):
     src = torch.empty(n, dtype=torch.int32, device=dev)
     offs = torch.empty(batch.n_lists + 1, dtype=torch.int64, device=dev)
     counts = torch.zeros(1, dtype=torch.int64, device=dev)
+    tomb = torch.empty(n, dtype=torch.uint8, device=dev) if tombstones else None
     ws = C.c_size_t(0)
     check(lib().smx_rga_workspace_bytes(n, batch.n_lists, C.byref(ws)))
     wst = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=dev)
     ops = _abi.SmxRgaOps(n, batch.n_lists, *[_ptr(t) for t in ins])
-    out = _abi.SmxRgaOut(_ptr(vals), _ptr(src), _ptr(offs), _ptr(counts))
+    out = _abi.SmxRgaOut(_ptr(vals), _ptr(src), _ptr(offs), _ptr(counts), _ptr(tomb))
     check(lib().smx_rga_replay(C.byref(ops), C.byref(out), _ptr(wst), ws.value,
                                torch.cuda.current_stream(dev).cuda_stream))
     torch.cuda.synchronize(dev)
     k = int(counts.item())
-    return (vals[:k].cpu().numpy().view(np.uint32), src[:k].cpu().numpy(),
-            offs.cpu().numpy())
+    res = (vals[:k].cpu().numpy().view(np.uint32), src[:k].cpu().numpy(), offs.cpu().numpy())
+    return res + (tomb[:k].cpu().numpy().astype(np.bool_),) if tombstones else res

@@ -1,8 +1,10 @@
 """Ordered-list CRDT (RGA) entry points, batched onto the GPU.
 
-Reference: ``semmerge/crdt.py:8-57``.  ``Key`` and the ``RGA`` method names and
+Reference: ``semmerge/crdt.py:8-57``.  ``Key``, ``Elem`` and the ``RGA`` method names and
 argument meaning are unchanged; ``RGA`` records its event stream and
-``materialize()`` replays it through ``smx_rga_replay`` (include/smx.h).
+``materialize()`` replays it through ``smx_rga_replay`` (include/smx.h); ``RGA.list``
+(the reference's state, crdt.py:26-27) replays it in the library's list mode, which
+keeps the tombstoned elements.
 :func:`replay` is the batched entry point: many independent lists in one launch.
 
 Exact parallel restatement used by the device: the fate
@@ -31,6 +33,15 @@ class Key:
     t: int
     author: str
     opid: str
+
+
+@dataclass
+class Elem:
+    """List element (crdt.py:16-20)."""
+
+    key: Key
+    value: str
+    tombstone: bool = False
 
 
 Event = Tuple[int, Any, Any]  # (INSERT|MOVE|DELETE, key or None, value)
@@ -99,11 +110,31 @@ def replay(streams: Sequence[Sequence[Event]]) -> List[List[Any]]:
     return [[batch.values[s] for s in srcl[offl[i]:offl[i + 1]]] for i in range(len(streams))]
 
 
+def replay_lists(streams: Sequence[Sequence[Event]]) -> List[List[Elem]]:
+    """Every stream's final list state (crdt.py:26-27 ``RGA.list``) on the GPU: the
+    elements in list order, tombstoned ones included, each as ``Elem(key, value,
+    tombstone)`` with the key and value of the event that created it."""
+    from ._lib import rga_replay_device  # the HIP library; raises if missing
+    batch = marshal_streams(streams)
+    _, src, offsets, tomb = rga_replay_device(batch, tombstones=True)
+    events = [ev for stream in streams for ev in stream]
+    srcl, tl, offl = src.tolist(), tomb.tolist(), offsets.tolist()
+    return [[Elem(events[s][1], events[s][2], bool(tb)) for s, tb in
+             zip(srcl[offl[i]:offl[i + 1]], tl[offl[i]:offl[i + 1]])] for i in range(len(streams))]
+
+
 class RGA:
-    """Drop-in for crdt.py:23-46: same methods; state is the recorded stream."""
+    """Drop-in for crdt.py:23-46: same methods; state is the recorded stream.  ``list``
+    is the reference's ``List[Elem]`` state, computed on the GPU from the stream when it
+    is read (a fresh list of fresh ``Elem`` objects each time: mutating it does not
+    change the RGA, which is why it is read-only here)."""
 
     def __init__(self) -> None:
         self._events: List[Event] = []
+
+    @property
+    def list(self) -> List[Elem]:
+        return replay_lists([self._events])[0]
 
     def insert(self, key: Key, value: str) -> None:
         self._events.append((INSERT, key, value))

@@ -810,6 +810,142 @@ __global__ void EMIT_BOUNDS k_emit(EmitArgs E) {
   }
 }
 
+// k_emit with four consecutive outputs per lane: the streams move 16 bytes per lane
+// and instruction (the per-lane address work of the texture path is what bounds this
+// kernel: a fully divergent 64-lane table gather costs the CU ~150 cycles, a coalesced
+// 4-byte stream instruction about as many per byte as a 16-byte one per four).  Each
+// wave owns EMIT_WT consecutive output indices; a step is 256 outputs.  Four outputs
+// of a lane read four consecutive positions P unless a skipped rename falls between
+// them (rare): then each is read on its own.
+#ifndef EMIT_VEC
+#define EMIT_VEC 0
+#endif
+#define EMIT4_STEPS (EMIT_WT / (4 * WAVE))
+typedef u32 ev4u __attribute__((ext_vector_type(4)));
+typedef i32 ev4i __attribute__((ext_vector_type(4)));
+typedef ev4u __attribute__((aligned(4))) ev4u_a4;
+__global__ void EMIT_BOUNDS k_emit4(EmitArgs E) {
+  const ComposeMeta* M = E.meta;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const bool bad = M->bad_sym != 0;
+    E.counts[0] = bad ? -1 : M->f_fail ? -2 : (M->n_move_none && E.status_none) ? -3 : (i64)(E.n - M->n_skip);
+    E.counts[1] = bad ? -1 : (i64)M->n_conf;
+  }
+  if (M->f_fail | M->bad_sym) return;
+  const u64 nskip = M->n_skip;
+  const u64 nmv = min(M->kcnt[KMOVE], E.n);
+  const u64 nP = E.n - nmv;
+  const u64 nR = min(M->kcnt[KREN], nP);
+  const u64 nout = E.n - nskip, nRk = nR - nskip;
+  auto gsrc = [&](i32 j) -> i32 {
+    if (E.src_map) return E.src_map[j];
+    return (u64)j < E.na_loc ? (i32)(E.src_a + j) : (i32)(E.src_b + ((i64)j - (i64)E.na_loc));
+  };
+  const FinPack FP = fin_pack_of(M->vbits, E.allow_pack != 0);
+  const int lane = threadIdx.x & (WAVE - 1);
+  const u64 w0 = (((u64)blockIdx.x * BLOCK + threadIdx.x) / WAVE) * EMIT_WT;  // output index
+  if (w0 + EMIT_WT <= nmv || w0 >= nout || nP == 0) return;
+  u64 kk = 0;  // skips with S[j] - j below the next step's first rename output
+  {
+    const u64 o0 = w0 > nmv ? w0 - nmv : 0;
+    if (o0 < nRk) {
+      u64 lo = 0, hi = nskip;
+      while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if ((u64)E.skiplist[mid] - mid < o0) lo = mid + 1;
+        else hi = mid;
+      }
+      kk = lo;
+    }
+  }
+  u64 pp[EMIT4_STEPS][4];
+  bool vec[EMIT4_STEPS];
+#pragma unroll
+  for (int j = 0; j < EMIT4_STEPS; ++j) {
+    const u64 b = w0 + (u64)j * 4 * WAVE;  // the step's first output (wave-uniform)
+    const u64 o = b + 4 * (u64)lane;
+    u64 add[4] = {0, 0, 0, 0};
+    const u64 k0 = kk;
+    if (b + 4 * WAVE > nmv && (b > nmv ? b - nmv : 0) < nRk) {
+      const u64 ohi = b + 4 * WAVE - 1 - nmv;
+      while (kk < nskip) {
+        const u64 sj = (u64)(u32)__builtin_amdgcn_readfirstlane((int)E.skiplist[kk]) - kk;
+        if (sj > ohi) break;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) add[u] += (o + u >= nmv ? o + u - nmv : 0) >= sj;
+        ++kk;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const u64 ou = o + u;
+      const u64 op = ou >= nmv ? ou - nmv : 0;
+      const bool ok = ou >= nmv && ou < nout;
+      pp[j][u] = !ok ? 0 : (op < nRk ? op + k0 + add[u] : op + nskip);
+    }
+    vec[j] = o >= nmv && o + 3 < nout && pp[j][3] == pp[j][0] + 3;
+  }
+  i32 src[EMIT4_STEPS][4];
+  u32 sy[EMIT4_STEPS][4];
+#pragma unroll
+  for (int j = 0; j < EMIT4_STEPS; ++j) {
+    if (vec[j]) {
+      const ev4u s4 = __builtin_nontemporal_load(reinterpret_cast<const ev4u_a4*>(&E.tsrc[pp[j][0]]));
+      const ev4u y4 = __builtin_nontemporal_load(reinterpret_cast<const ev4u_a4*>(&E.tsym[pp[j][0]]));
+      src[j][0] = (i32)s4.x, src[j][1] = (i32)s4.y, src[j][2] = (i32)s4.z, src[j][3] = (i32)s4.w;
+      sy[j][0] = y4.x, sy[j][1] = y4.y, sy[j][2] = y4.z, sy[j][3] = y4.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        src[j][u] = NTLD(&E.tsrc[pp[j][u]]);
+        sy[j][u] = NTLD(&E.tsym[pp[j][u]]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sy[j][u] = min(sy[j][u], E.smax);
+  }
+#pragma unroll
+  for (int j = 0; j < EMIT4_STEPS; ++j) {
+    int4 F[4];
+    if (FP.packed) {
+      u64 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = fin_word(FP, E.fin, sy[j][u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) F[u] = fin_decode(FP, x[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) F[u] = E.fin[sy[j][u]];
+    }
+    const u64 o = w0 + (u64)j * 4 * WAVE + 4 * (u64)lane;
+    i32 vo[4], va[4], vf[4], vc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ren = o + u >= nmv && o + u - nmv < nRk;
+      vo[u] = gsrc(src[j][u]);
+      va[u] = F[u].x;
+      vf[u] = F[u].y;
+      vc[u] = ren ? -1 : F[u].z;
+    }
+    if (o >= nmv && o + 3 < nout) {  // o is a multiple of 4: 16-byte aligned stores
+      NTST((ev4i{vo[0], vo[1], vo[2], vo[3]}), reinterpret_cast<ev4i*>(&E.out_order[o]));
+      NTST((ev4i{va[0], va[1], va[2], va[3]}), reinterpret_cast<ev4i*>(&E.out_addr[o]));
+      NTST((ev4i{vf[0], vf[1], vf[2], vf[3]}), reinterpret_cast<ev4i*>(&E.out_file[o]));
+      NTST((ev4i{vc[0], vc[1], vc[2], vc[3]}), reinterpret_cast<ev4i*>(&E.out_ctx[o]));
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (o + u >= nmv && o + u < nout) {
+          E.out_order[o + u] = vo[u];
+          E.out_addr[o + u] = va[u];
+          E.out_file[o + u] = vf[u];
+          E.out_ctx[o + u] = vc[u];
+        }
+      }
+    }
+  }
+}
+
 // Moves whose newAddress or newFile is None see the symbol's inclusive prefix
 // (compose.py:73-82 + 37-41): moves grouped by symbol in T order, last-non-None
 // scan over the moves' own values (out_addr / out_file with msym's has-value bits);
@@ -928,6 +1064,7 @@ struct Ctx {
   i64 src_a, src_b;  // global source index of local op j (see WinArgs)
   StageTimer* tm;
   const i32* src_map = nullptr;
+  mutable bool ts64 = false;  // a window's timestamps span >= 2^32: u64 window keys
   template <typename T>
   T* ws(int b) const { return (T*)(base + L.off[b]); }
 };
@@ -1064,27 +1201,57 @@ static TbArgs tb_args(const Ctx& C) {
   return A;
 }
 
+// Bucket geometry of the per-symbol tables: the bucketed path when it returns true.
+static bool tb_geometry(const Ctx& C, u64* width_o, u64* nbk_o) {
+  u64 width = SMX_CEIL_DIV((u64)C.n_sym, (u64)TB_NBK_TGT);
+  if (width < 1) width = 1;
+  if (width > TB_WIDTH) width = TB_WIDTH;
+  *width_o = width;
+  *nbk_o = SMX_CEIL_DIV((u64)C.n_sym, width);
+  return *nbk_o <= TB_MAXBK;
+}
+
+// The table records bucketed with every rename kept (k_tb_scatter keep_skip): it needs
+// only the window outputs, so it can run before or beside the walk; k_tb_unskip then
+// applies the walk's skips.  No-op off the bucketed path.
+static int launch_tb_prescatter(const Ctx& C) {
+  u64 width, nbk;
+  if (!tb_geometry(C, &width, &nbk)) return SMX_OK;
+  TbArgs A = tb_args(C);
+  A.width = (u32)width;
+  A.nbk = (u32)nbk;
+  A.keep_skip = 1u;
+  hipLaunchKernelGGL(k_tb_scatter, dim3((int)SMX_CEIL_DIV((u64)C.n, (u64)TB_TILE)), dim3(TB_NT), 0, C.st, A,
+                     C.ws<u32>(B_TBHIST), C.ws<u32>(B_REC));
+  HIP_TRY(hipGetLastError());
+  return SMX_OK;
+}
+
 // Per-symbol last writers.  part == nullptr: the final-state table fin (packed
-// when the value widths allow); otherwise this shard's partial tables.
-static int launch_tables(const Ctx& C, u64* part_tab, u32 tag, bool* bucketed) {
+// when the value widths allow); otherwise this shard's partial tables.  prescattered:
+// launch_tb_prescatter already bucketed the records (then only the skips and the
+// reduce run here).
+static int launch_tables(const Ctx& C, u64* part_tab, u32 tag, bool* bucketed, bool prescattered = false) {
   hipStream_t st = C.st;
   const i64 n = C.n;
   int4* fin = C.ws<int4>(B_FIN);
   *bucketed = false;
   const i64 n_sym = C.n_sym;
   TbArgs A = tb_args(C);
-  u64 width = SMX_CEIL_DIV((u64)n_sym, (u64)TB_NBK_TGT);
-  if (width < 1) width = 1;
-  if (width > TB_WIDTH) width = TB_WIDTH;
-  const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);
-  if (nbk <= TB_MAXBK) {
+  u64 width, nbk;
+  if (tb_geometry(C, &width, &nbk)) {
     *bucketed = true;
     A.width = (u32)width;
     A.nbk = (u32)nbk;
     const int nblk = (int)SMX_CEIL_DIV((u64)n, (u64)TB_TILE);
     u32* lst = C.ws<u32>(B_TBHIST);
     u32* rec = C.ws<u32>(B_REC);
-    hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, lst, rec);
+    if (prescattered) {
+      A.keep_skip = 1u;
+      hipLaunchKernelGGL(k_tb_unskip, dim3(1024), dim3(BLOCK), 0, st, A, lst, rec, C.ws<u32>(B_SKIPLIST));
+    } else {
+      hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, lst, rec);
+    }
     hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, lst, rec, n_sym, fin, part_tab, tag);
   } else {
     // very large symbol spaces: device-scope atomics on the packed keys
@@ -1110,7 +1277,12 @@ static int launch_emit(const Ctx& C, bool packable, const smx_shard* sh) {
              C.ws<int4>(B_FIN), meta, (u64)n, (u32)(C.n_sym - 1), packable ? 1 : 0, (u64)C.na, C.src_a,
              C.src_b, C.src_map, C.out->order, C.out->addr, C.out->file, C.out->ctx, C.out->counts, sh ? 0 : 1};
   const i64 ewaves = SMX_CEIL_DIV(n, (i64)EMIT_WT);
-  hipLaunchKernelGGL(k_emit, dim3(SMX_CEIL_DIV(ewaves, (i64)NWAVES)), dim3(BLOCK), 0, st, E);
+  const bool al16 = ((uintptr_t)C.out->order | (uintptr_t)C.out->addr | (uintptr_t)C.out->file |
+                     (uintptr_t)C.out->ctx) % 16 == 0;
+  if (EMIT_VEC && al16)
+    hipLaunchKernelGGL(k_emit4, dim3(SMX_CEIL_DIV(ewaves, (i64)NWAVES)), dim3(BLOCK), 0, st, E);
+  else
+    hipLaunchKernelGGL(k_emit, dim3(SMX_CEIL_DIV(ewaves, (i64)NWAVES)), dim3(BLOCK), 0, st, E);
   HIP_TRY(hipGetLastError());
   return SMX_OK;
 }
@@ -1300,12 +1472,19 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   P.W = W;
   P.ablate = knob("SMX_ABLATE", 0);
   C.tm->begin(ST_WINDOW);
+  const bool ts32 = WF_TS32 && !C.ts64;
+#if SMX_DIAG
   if (g_phase_dbg && !P.src_map && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
     P.dbg = (u64*)g_phase_dbg;
-    hipLaunchKernelGGL((k_window_f<true, false>), dim3(W), dim3(WF_NT), 0, st, P);
+    hipLaunchKernelGGL((k_window_f<true, false, false>), dim3(W), dim3(WF_NT), 0, st, P);
+  } else
+#endif
+  if (P.src_map) {
+    if (ts32) hipLaunchKernelGGL((k_window_f<false, true, true>), dim3(W), dim3(WF_NT), 0, st, P);
+    else hipLaunchKernelGGL((k_window_f<false, true, false>), dim3(W), dim3(WF_NT), 0, st, P);
   } else {
-    if (P.src_map) hipLaunchKernelGGL((k_window_f<false, true>), dim3(W), dim3(WF_NT), 0, st, P);
-    else hipLaunchKernelGGL((k_window_f<false, false>), dim3(W), dim3(WF_NT), 0, st, P);
+    if (ts32) hipLaunchKernelGGL((k_window_f<false, false, true>), dim3(W), dim3(WF_NT), 0, st, P);
+    else hipLaunchKernelGGL((k_window_f<false, false, false>), dim3(W), dim3(WF_NT), 0, st, P);
   }
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_WINDOW);
@@ -1749,6 +1928,12 @@ static thread_local int g_plan = SMX_PLAN_PRESORTED;
 static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm, i64 tgt) {
   int rc;
   g_plan = SMX_PLAN_PRESORTED;
+  if ((hm->f_fail & WF_FAIL_TSRANGE) && !hm->bad_sym) {  // timestamps too far apart for 32-bit keys
+    C.ts64 = true;
+    if ((rc = run_presorted(C, tgt))) return rc;
+    if (tail && (rc = launch_tail(C))) return rc;
+    if ((rc = read_meta(C, hm))) return rc;
+  }
   while (hm->f_fail == 2 && !hm->bad_sym && tgt > WIN_TGT_MIN) {  // dense groups: smaller windows
     tgt = (tgt / 2) / CH * CH;
     if ((rc = run_presorted(C, tgt))) return rc;
@@ -1874,7 +2059,10 @@ __global__ void k_shard_summary(const ComposeMeta* meta, i64* summary) {
   summary[18] = (i64)meta->n_ren_side[0];
   summary[19] = (i64)meta->n_ren_side[1];
   summary[20] = (i64)meta->n_move_none;
-  summary[21] = (i64)((meta->f_fail & 1 ? 1 : 0) | (meta->bad_sym ? 2 : 0) | (meta->f_fail & 2 ? 4 : 0));
+  // (bit 2: repairable by SMX_SHARD_ORDER_FIX -- a window overflow or a timestamp range
+  // too wide for the 32-bit window keys)
+  summary[21] = (i64)((meta->f_fail & 1 ? 1 : 0) | (meta->bad_sym ? 2 : 0) |
+                      (meta->f_fail & (2 | WF_FAIL_TSRANGE) ? 4 : 0));
 }
 
 // An empty shard hands the incoming open region (device- or host-held) straight on.
@@ -1918,6 +2106,41 @@ __global__ void k_fin_from_tab(const u64* __restrict__ tab, const i64* __restric
   }
 }
 
+// This shard's halo from the all-gather of every shard's ORDER outputs (smx_shard
+// .order_gather): for each branch b, the first H renames of b on the following shards
+// in shard order -- entry i is taken from the shard q whose cumulative count first
+// exceeds i -- and halo_dev = (count, count, more, more).
+__global__ void k_halo_gather(const i64* __restrict__ g, int W, int r, i64 H, u32* hs0, u32* hs1, i32* hc0, i32* hc1,
+                              i32* hr0, i32* hr1, i64* halo_dev) {
+  const i64 row = SMX_SHARD_SUMMARY + 3 * H;  // int64 words per shard
+  for (int b = 0; b < 2; ++b) {
+    u32* hs = b ? hs1 : hs0;
+    i32* hc = b ? hc1 : hc0;
+    i32* hr = b ? hr1 : hr0;
+    i64 total = 0;
+    for (int q = r + 1; q < W; ++q) total += max(g[q * row + 18 + b], (i64)0);
+    const i64 got = min(total, H);
+    for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < got; i += (i64)gridDim.x * BLOCK) {
+      i64 cum = 0;
+      int q = r + 1;
+      for (; q < W; ++q) {
+        const i64 c = min(max(g[q * row + 18 + b], (i64)0), H);
+        if (i < cum + c) break;
+        cum += c;
+      }
+      const i64 off = i - cum;
+      const i32* X = reinterpret_cast<const i32*>(g + q * row + SMX_SHARD_SUMMARY);  // [3][2H] int32
+      hs[i] = (u32)X[b * H + off];
+      hc[i] = X[2 * H + b * H + off];
+      hr[i] = X[4 * H + b * H + off];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      halo_dev[b] = got;
+      halo_dev[2 + b] = total > got ? 1 : 0;
+    }
+  }
+}
+
 static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose_out* out, void* ws,
                       size_t ws_bytes, hipStream_t st, int step) {
   if (!sh || !sh->summary) return set_err(SMX_E_ARG, "null shard / summary");
@@ -1949,7 +2172,8 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       hipLaunchKernelGGL(k_halo_export, dim3(1), dim3(EX_NT), 0, st, walk_args(C, nullptr), sh->export_sym,
                          sh->export_cls, sh->export_src, (u64)sh->halo_cap);
     HIP_TRY(hipGetLastError());
-    return SMX_OK;
+    // the table records, bucketed while the host exchanges the summaries and walks
+    return launch_tb_prescatter(C);
   };
   switch (step) {
     case SMX_SHARD_ORDER:
@@ -1979,6 +2203,17 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
     }
     case SMX_SHARD_WALK: {
       tm.begin(ST_WALK);
+      if (sh->order_gather && sh->halo_cap > 0) {
+        if (!sh->halo_dev || !sh->halo_sym[0] || !sh->halo_sym[1] || !sh->halo_cls[0] || !sh->halo_cls[1] ||
+            !sh->halo_src[0] || !sh->halo_src[1] || sh->world < 1 || sh->rank < 0 || sh->rank >= sh->world)
+          return set_err(SMX_E_ARG, "order_gather needs writable halo buffers and halo_dev");
+        hipLaunchKernelGGL(k_halo_gather, dim3(SMX_CEIL_DIV(sh->halo_cap, (i64)BLOCK)), dim3(BLOCK), 0, st,
+                           sh->order_gather, (int)sh->world, (int)sh->rank, (i64)sh->halo_cap,
+                           (u32*)sh->halo_sym[0], (u32*)sh->halo_sym[1], (i32*)sh->halo_cls[0],
+                           (i32*)sh->halo_cls[1], (i32*)sh->halo_src[0], (i32*)sh->halo_src[1],
+                           (i64*)sh->halo_dev);
+        HIP_TRY(hipGetLastError());
+      }
       if ((rc = launch_walk(C, sh))) return rc;
       hipLaunchKernelGGL(k_shard_walk_sum, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary);
       HIP_TRY(hipGetLastError());
@@ -1989,11 +2224,16 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       if (!sh->part_tab) return set_err(SMX_E_ARG, "null part_tab");
       tm.begin(ST_TABLES);
       bool bucketed = false;
-      if ((rc = launch_tables(C, sh->part_tab, (u32)sh->rank + 1u, &bucketed))) return rc;
+      // (ORDER / ORDER_FIX / SCATTER bucketed the records)
+      if ((rc = launch_tables(C, sh->part_tab, (u32)sh->rank + 1u, &bucketed, true))) return rc;
       hipLaunchKernelGGL(k_shard_tab_sum, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary,
                          bucketed ? 1 : 0);
       HIP_TRY(hipGetLastError());
       tm.end(ST_TABLES);
+      break;
+    }
+    case SMX_SHARD_SCATTER: {
+      if ((rc = launch_tb_prescatter(C))) return rc;
       break;
     }
     case SMX_SHARD_EMIT: {

@@ -33,6 +33,7 @@
 #define RGA_REC 2
 #define RGA_WV 1  // the value / op / index word
 #define RGA_IDX_MASK 0x3fffffffu
+#define RGA_TOMB_BIT 0x80000000u  // tmp_s: the element is tombstoned (list mode, smx_rga_out.out_tomb)
 
 // Grouping the events by list: a stable LSD radix partition of whole records on the
 // list id, 8 bits per pass (one pass up to 256 lists, two up to 65536, ...).  The first
@@ -449,15 +450,17 @@ __device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, co
   }
   wave_lds_sync();
   for (u32 q = lane; q < m; q += WAVE) {
-    const u64 w = S.wv[S.gp[q] & (RW_DEAD - 1)];
+    const u32 e = S.gp[q] & (RW_DEAD - 1);
+    const u64 w = S.wv[e];
     tmp_v[s0 + q] = (u32)(w >> 32);
-    tmp_s[s0 + q] = (u32)w & RGA_IDX_MASK;
+    tmp_s[s0 + q] = ((u32)w & RGA_IDX_MASK) | (S.st[e] & 2 ? RGA_TOMB_BIT : 0u);
   }
 }
 
+// tomb: list mode (crdt.py RGA.list) -- the tombstoned elements stay, flagged
 template <int K, int CAP>
 __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* __restrict__ R, u32 l, u32 s0, u32 cnt,
-                                              RwLds<CAP>& S, u32 lane,
+                                              RwLds<CAP>& S, u32 lane, bool tomb,
                                               u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
                                               u32* __restrict__ scnt) {
   const u64* src = R + (u64)s0 * RGA_REC;
@@ -597,7 +600,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const u32 e = (u32)k * 64u + lane;
-    const bool live = e < cnt && S.st[e] == 1;
+    const bool live = e < cnt && (tomb ? (S.st[e] & 1) != 0 : S.st[e] == 1);
     const u64 ball = __ballot(live);
     if (live) S.gp[m + (u32)__popcll(ball & lt)] = (u16)e;
     m += (u32)__popcll(ball);
@@ -634,7 +637,8 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave(smx_rga_ops o, con
                                                              const u32* __restrict__ lstart,
                                                              i64 n, i64 nl, u32* __restrict__ defer,
                                                              u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
-                                                             u32* __restrict__ tmp_s, u32* __restrict__ scnt) {
+                                                             u32* __restrict__ tmp_s, u32* __restrict__ scnt,
+                                                             int tomb) {
   __shared__ RwLds<RW_CAP> lds[RW_WAVES];
   const u32 lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   const u32 l = blockIdx.x * RW_WAVES + w;
@@ -645,11 +649,11 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave(smx_rga_ops o, con
     return;
   }
   if (cnt <= 64)
-    rga_wave_list<1>(o, R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+    rga_wave_list<1>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
   else if (cnt <= 128)
-    rga_wave_list<2>(o, R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+    rga_wave_list<2>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
   else
-    rga_wave_list<4>(o, R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+    rga_wave_list<4>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
 }
 
 // The deferred lists of RW_CAP + 1 .. 2 * RW_CAP events: the same wave per list with
@@ -659,7 +663,8 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(smx_rga_ops o, co
                                                               i64 n, i64 nl, const u32* __restrict__ todo,
                                                               const u32* __restrict__ ntodo, u32* __restrict__ defer,
                                                               u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
-                                                              u32* __restrict__ tmp_s, u32* __restrict__ scnt) {
+                                                              u32* __restrict__ tmp_s, u32* __restrict__ scnt,
+                                                              int tomb) {
   __shared__ RwLds<2 * RW_CAP> lds[RW_WAVES];
   const u32 lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   const u32 nt = *ntodo;
@@ -670,7 +675,7 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(smx_rga_ops o, co
       if (lane == 0) defer[atomicAdd(ndefer, 1u)] = l;
       continue;
     }
-    rga_wave_list<8>(o, R, l, s0, cnt, lds[w], lane, tmp_v, tmp_s, scnt);
+    rga_wave_list<8>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
     wave_lds_sync();  // the next list reuses the slice
   }
 }
@@ -705,7 +710,7 @@ __device__ void block_sort_positions(u32* p, u32 cnt, Less less) {
 // then the survivors' positions sorted by (key, index).
 __device__ void rga_big_list(const smx_rga_ops& o, const u64* __restrict__ R, u32 l, const u32* __restrict__ lstart, i64 n, i64 nl,
                              u8* __restrict__ bst, u32* __restrict__ gp, u32* __restrict__ tmp_v,
-                             u32* __restrict__ tmp_s, u32* __restrict__ scnt) {
+                             u32* __restrict__ tmp_s, u32* __restrict__ scnt, bool tomb) {
   __shared__ u32 ns;
   const u32 t = threadIdx.x, NT = blockDim.x;
   const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
@@ -741,20 +746,23 @@ __device__ void rga_big_list(const smx_rga_ops& o, const u64* __restrict__ R, u3
     }
   }
   __syncthreads();
-  // survivors' positions to the front of G (their order is fixed by the sort below)
+  // survivors' positions to the front of G (their order is fixed by the sort below);
+  // the tombstone flag rides in bit 31 (positions < 2^30)
   if (t == 0) {
     u32 w = 0;
     for (u32 j = 0; j < cnt; ++j)
-      if (S[j] == 1) G[w++] = G[j];
+      if (tomb ? (S[j] & 1) : S[j] == 1) G[w++] = G[j] | (S[j] & 2 ? RGA_TOMB_BIT : 0u);
     ns = w;
   }
   __syncthreads();
   const u32 m = ns;
-  block_sort_positions(G, m, [&](u32 a, u32 b) { return rec_lt(&L[a * RGA_REC], &L[b * RGA_REC], o); });
+  block_sort_positions(G, m, [&](u32 a, u32 b) {
+    return rec_lt(&L[(a & ~RGA_TOMB_BIT) * RGA_REC], &L[(b & ~RGA_TOMB_BIT) * RGA_REC], o);
+  });
   for (u32 j = t; j < m; j += NT) {
-    const u64 w = L[G[j] * RGA_REC + RGA_WV];
+    const u64 w = L[(G[j] & ~RGA_TOMB_BIT) * RGA_REC + RGA_WV];
     tmp_v[s0 + j] = (u32)(w >> 32);
-    tmp_s[s0 + j] = (u32)w & RGA_IDX_MASK;
+    tmp_s[s0 + j] = ((u32)w & RGA_IDX_MASK) | (G[j] & RGA_TOMB_BIT);
   }
   if (t == 0) scnt[l] = m;
 }
@@ -764,10 +772,10 @@ __global__ void __launch_bounds__(1024) k_rga_big(smx_rga_ops o, const u64* __re
                                                   i64 nl, const u32* __restrict__ todo, const u32* __restrict__ ntodo,
                                                   u8* __restrict__ bst, u32* __restrict__ gp,
                                                   u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
-                                                  u32* __restrict__ scnt) {
+                                                  u32* __restrict__ scnt, int tomb) {
   for (u32 item = blockIdx.x; item < *ntodo; item += gridDim.x) {
     __syncthreads();
-    rga_big_list(o, R, todo[item], lstart, n, nl, bst, gp, tmp_v, tmp_s, scnt);
+    rga_big_list(o, R, todo[item], lstart, n, nl, bst, gp, tmp_v, tmp_s, scnt, tomb != 0);
   }
 }
 
@@ -781,7 +789,9 @@ __global__ void __launch_bounds__(BLOCK) k_rga_out(const u32* __restrict__ tmp_v
   const u32 s0 = lstart[l], m = scnt[l], d = soff[l];
   for (u32 x = lane; x < m; x += WAVE) {
     out.out_value[d + x] = __builtin_nontemporal_load(&tmp_v[s0 + x]);
-    out.out_src[d + x] = (i32)__builtin_nontemporal_load(&tmp_s[s0 + x]);
+    const u32 sx = __builtin_nontemporal_load(&tmp_s[s0 + x]);
+    out.out_src[d + x] = (i32)(sx & ~RGA_TOMB_BIT);
+    if (out.out_tomb) out.out_tomb[d + x] = sx & RGA_TOMB_BIT ? 1 : 0;
   }
   if (lane == 0) out.out_offsets[l] = d;
 }
@@ -925,12 +935,13 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
     }
     hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, kbuf[(npass - 1) & 1], n, nl, lstart);
   }
+  const int tomb = out->out_tomb != nullptr;
   hipLaunchKernelGGL(k_rga_wave, dim3(SMX_CEIL_DIV(nl, (i64)RW_WAVES)), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n,
-                     nl, def1, ndef, tmp_v, tmp_s, scnt);
+                     nl, def1, ndef, tmp_v, tmp_s, scnt, tomb);
   hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, def1, ndef, def2,
-                     ndef + 1, tmp_v, tmp_s, scnt);
+                     ndef + 1, tmp_v, tmp_s, scnt, tomb);
   hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
-                     tmp_s, scnt);
+                     tmp_s, scnt, tomb);
   if (nl <= RS_MAX) {
     hipLaunchKernelGGL(k_rga_scnt_scan, dim3(1), dim3(RS_NT), 0, st, scnt, soff, nl, *out);
   } else {

@@ -282,10 +282,23 @@ class ShardedCompose:
         return torch.cat(parts + [ok, self._signed])
 
     @staticmethod
-    def _range_plan(g: np.ndarray):
-        """Host, from every rank's _range_info (g [W, 7]): (ordered, tau) -- the key
-        ranges' lower bounds tau[1..W-1] (shard r owns keys [tau_r, tau_r+1)), the
-        running maximum of the ranks' first keys."""
+    def _range_plan(g):
+        """From every rank's _range_info (g [W, 9], numpy or a device tensor): (ordered,
+        tau) -- the key ranges' lower bounds tau[1..W-1] (shard r owns keys [tau_r,
+        tau_r+1)), the running maximum of the ranks' first keys."""
+        if not isinstance(g, np.ndarray):  # the same on the device (no host sync)
+            import torch
+            W = g.shape[0]
+            lo = torch.full((1,), I64_MIN, dtype=torch.int64, device=g.device)
+            ordered = g[:, 6].min() == 1
+            for br in range(2):             # slices of a branch must follow each other
+                nz = g[:, br] > 0
+                last = torch.where(nz, g[:, 3 + 2 * br], lo)
+                prev = torch.cat([lo, torch.cummax(last, 0).values[:-1]])
+                ordered = ordered & (~nz | (g[:, 2 + 2 * br] >= prev)).all()
+            cand = torch.where(g[:, 0] > 0, g[:, 2], torch.where(g[:, 1] > 0, g[:, 4], lo))
+            cand[0] = I64_MIN
+            return ordered, torch.cummax(cand, 0).values[1:]
         W = g.shape[0]
         ordered = bool(g[:, 6].min() == 1)
         for br in range(2):                 # slices of a branch must follow each other
@@ -299,25 +312,30 @@ class ShardedCompose:
 
     def _range_counts(self):
         """allc [W, 2, W] (src, branch, dest) op counts of the key-range split, or None when
-        the logs are not timestamp-ordered.  Two small host syncs: the ranks' slice ends,
-        then every rank's cut positions (binary searches on the device)."""
+        the logs are not timestamp-ordered.  One host sync: the ranks' slice ends are
+        gathered, the splitters and every rank's cut positions (binary searches) are
+        computed on the device, and the cuts are gathered with the slice ends."""
         torch = self.torch
         W = self.world
-        g = self.comm.all_gather(self._range_info()).cpu().numpy()        # [W, 9]
-        ordered, tau = self._range_plan(g)
-        if not ordered:
-            return None
+        g_dev = self.comm.all_gather(self._range_info())                  # [W, 9]
+        ordered_dev, tau = self._range_plan(g_dev)
         cuts = torch.zeros((2, max(W - 1, 1)), dtype=torch.int64, device=self.dev)
         if W > 1:
-            tk = torch.from_numpy(tau).to(self.dev)
             for br, n in ((0, self.na_s), (1, self.nb_s)):
                 if n:
                     ts = self._orig(br, "ts")
                     # every timestamp below 2^63: search the stored words (int64 order =
                     # u64 order); a splitter above 2^63 (key >= 0) is fixed on the host
-                    cuts[br] = torch.searchsorted(ts, _u64_key(tk)) if self._ts_signed[br] else \
-                        torch.searchsorted(_u64_key(ts).contiguous(), tk)
-        gc = self.comm.all_gather(cuts).cpu().numpy()                      # [W, 2, W-1]
+                    cuts[br] = torch.searchsorted(ts, _u64_key(tau)) if self._ts_signed[br] else \
+                        torch.searchsorted(_u64_key(ts).contiguous(), tau)
+        both = self.comm.all_gather(torch.cat([cuts.reshape(-1), ordered_dev.to(torch.int64).view(1)]))
+        host = torch.cat([g_dev.reshape(-1), both.reshape(-1)]).cpu().numpy()     # the one host sync
+        g = host[: W * 9].reshape(W, 9)
+        both = host[W * 9:].reshape(W, -1)
+        if not bool(both[0, -1]):
+            return None
+        _, tau = self._range_plan(g)
+        gc = both[:, :-1].reshape(W, 2, max(W - 1, 1))                     # [W, 2, W-1]
         allc = np.zeros((W, 2, W), np.int64)
         for q in range(W):
             for br in range(2):
@@ -555,13 +573,39 @@ class ShardedCompose:
                                    _ptr(self._ws), self._ws_bytes, s, step))
 
     # -- 2..5 -------------------------------------------------------------------------
-    def run(self) -> None:
-        """One sharded composition (collective: every rank calls it)."""
+    def _tables(self, summ: Optional[np.ndarray], rescatter: bool) -> None:
+        """TABLES (+ the lower shards' move tables when a move has a None value, which
+        needs the gathered summaries `summ`) and the MAX all_reduce of the partial
+        tables and value widths (collective).  rescatter: the records were consumed by
+        an earlier TABLES of this step (a WALK re-run) and are bucketed again."""
         torch = self.torch
+        if rescatter:
+            self._step(_abi.SHARD_SCATTER)
+        self._step(_abi.SHARD_TABLES)
+        n3 = 3 * max(self.n_sym, 1)
+        self.part[n3:].copy_(self.summary[S_WIDTH:S_WIDTH + 3])
+        mvpre = None
+        if summ is not None and summ[:, S_MVNONE].sum() > 0:
+            mv = self.comm.all_gather(self.part[: 2 * self.n_sym])      # [world, 2*n_sym]
+            mvpre = mv[: self.rank].max(dim=0).values if self.rank > 0 else torch.zeros_like(mv[0])
+            mvpre = mvpre.contiguous()
+        self._mvpre = mvpre
+        self._sh.mv_prefix = _ptr(mvpre) if mvpre is not None else None
+        self.comm.all_reduce_max(self.part)        # last writers and value widths together
+
+    def run(self) -> None:
+        """One sharded composition (collective: every rank calls it).  Host syncs: the
+        exchange's split sizes, then one read of the gathered walk summaries; the tables
+        and their all_reduce are enqueued before that read (speculatively: redone when
+        the walk re-ran, an ORDER failed or a move has a None value)."""
         self.exchange()
         self._step(_abi.SHARD_ORDER)
         self._order_exchange()
-        summ = self._walk()
+        self.in_dev.zero_()
+        self._step(_abi.SHARD_WALK)
+        self._tables(None, rescatter=False)
+        summ, reran = self._walk(first_done=True)
+        final = not reran and not summ[:, S_FAIL].any() and summ[:, S_MVNONE].sum() == 0
         if summ[:, S_FAIL].any():          # an asynchronous ORDER failed somewhere
             if int(np.bitwise_or.reduce(summ[:, S_FAIL])) & 3:
                 self._fail(summ)
@@ -574,21 +618,12 @@ class ShardedCompose:
                 except RuntimeError as e:   # reported by every rank below
                     err = e
             self._order_exchange()
-            summ = self._walk()
+            summ, _ = self._walk()
             if summ[:, S_FAIL].any():
                 self._fail(summ, err)
+        if not final:  # the speculative tables do not hold: every rank redoes them
+            self._tables(summ, rescatter=True)
         self.sum_walk = summ
-        self._step(_abi.SHARD_TABLES)
-        n3 = 3 * max(self.n_sym, 1)
-        self.part[n3:].copy_(self.summary[S_WIDTH:S_WIDTH + 3])
-        mvpre = None
-        if summ[:, S_MVNONE].sum() > 0:
-            mv = self.comm.all_gather(self.part[: 2 * self.n_sym])      # [world, 2*n_sym]
-            mvpre = mv[: self.rank].max(dim=0).values if self.rank > 0 else torch.zeros_like(mv[0])
-            mvpre = mvpre.contiguous()
-        self._mvpre = mvpre
-        self._sh.mv_prefix = _ptr(mvpre) if mvpre is not None else None
-        self.comm.all_reduce_max(self.part)        # last writers and value widths together
         self._sum_host = np.ascontiguousarray(summ[self.rank], dtype=np.int64)
         self._sh.summary_host = self._sum_host.ctypes.data
         self._step(_abi.SHARD_EMIT)
@@ -603,49 +638,30 @@ class ShardedCompose:
                            + (f" ({err})" if err else " (branch logs not timestamp-ordered)"))
 
     def _order_exchange(self) -> None:
-        """One all_gather of every shard's summary and halo exports; this shard's halo
-        (the first H renames of each branch on the following shards) gathered from them
-        on the device by indices computed on the host from the (small) summaries."""
+        """One all_gather of every shard's summary and halo exports; the WALK step
+        assembles this shard's halo (the first H renames of each branch on the
+        following shards) from it on the device (smx_shard.order_gather): no host read."""
         torch = self.torch
-        H, r, W, dv = self.H, self.rank, self.world, self.dev
-        g = self.comm.all_gather(torch.cat([self.summary, self.xport.reshape(-1).view(torch.int64)]))
-        if H <= 0:
+        if self.H <= 0:
             self.halo_dev.zero_()
+            self._sh.order_gather = None
             return
-        summ = g[:, :SUM].cpu().numpy()
-        key = summ[:, S_REN:S_REN + 2].tobytes()
-        if key != self._halo_key:  # (a repeated merge reuses its indices)
-            idx = np.zeros((2, 3, H), np.int64)
-            st = []
-            i = np.arange(H)
-            for b in range(2):
-                after = summ[:, S_REN + b] * (np.arange(W) > r)
-                c = np.minimum(after, H)
-                cum = np.cumsum(c)
-                got = int(min(cum[-1], H))
-                q = np.minimum(np.searchsorted(cum, i, side="right"), W - 1)
-                off = np.clip(i - (cum[q] - c[q]), 0, H - 1)
-                for f in range(3):  # X[q, f, b * H + off] of the [W, 3, 2H] int32 exports
-                    idx[b, f] = (q * 3 + f) * 2 * H + b * H + off
-                st.append((got, int(after.sum() > got)))
-            self._halo_idx = torch.from_numpy(idx.reshape(-1)).to(dv)
-            self._halo_st = torch.tensor([st[0][0], st[1][0], st[0][1], st[1][1]], dtype=torch.int64,
-                                         device=dv)
-            self._halo_key = key
-        X = g[:, SUM:].contiguous().view(torch.int32).reshape(-1)
-        self.halo.view(-1).copy_(X[self._halo_idx])
-        self.halo_dev.copy_(self._halo_st)
+        self._gathered = self.comm.all_gather(torch.cat([self.summary, self.xport.reshape(-1).view(torch.int64)]))
+        self._sh.order_gather = _ptr(self._gathered)
 
-    def _walk(self) -> np.ndarray:
+    def _walk(self, first_done: bool = False):
         """Walk with the incoming open region of the previous shards (device-held); one
         summary all_gather + host read per round; a shard whose incoming region changed
         re-runs, until none does (a region hand-off moves one shard per round).  Every
         rank sees every summary, so all take the same decisions without another
-        collective.  Returns the gathered summaries."""
+        collective.  first_done: this step's first WALK is already enqueued.  Returns
+        (the gathered summaries, whether any shard re-ran)."""
         W, r = self.world, self.rank
         used = [(0, 0)] * W
-        self.in_dev.zero_()
-        self._step(_abi.SHARD_WALK)
+        reran = False
+        if not first_done:
+            self.in_dev.zero_()
+            self._step(_abi.SHARD_WALK)
         for _ in range(W + 1):
             summ = self.comm.all_gather(self.summary).cpu().numpy()
             if summ[:, S_FAIL].any():
@@ -657,12 +673,13 @@ class ShardedCompose:
                     if q > 0 and summ[q - 1, S_OPEN] else (0, 0) for q in range(W)]
             if want == used:
                 break
+            reran = True
             if want[r] != used[r]:
                 self.in_dev.copy_(self.torch.tensor(want[r], dtype=self.torch.int64))
                 self._step(_abi.SHARD_WALK)
             used = want
         self.in_state = used[r]
-        return summ
+        return summ, reran
 
     def totals(self) -> Tuple[int, int]:
         """(composed ops, conflicts) of the whole merge after run() (collective)."""

@@ -126,6 +126,26 @@ def test_gpu_equals_oracle_soa(spec):
     _eq_soa(compose_soa(soa), oracle.compose(soa), str(spec))
 
 
+@pytest.mark.parametrize("stretch", ["all", "half"])
+def test_gpu_wide_timestamp_range(stretch):
+    """Timestamps whose window span exceeds the 32-bit window keys (k_window_f TS32):
+    the windows flag it and the presorted plan reruns on u64 keys -- every window
+    ("all") or only the windows of the later half of each branch ("half")."""
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(400_000, 2_000, 71)))
+    for lo, m in ((0, soa.n_a), (soa.n_a, soa.n_b)):
+        ts = soa.ts[lo:lo + m].copy()
+        rank = np.searchsorted(np.unique(ts), ts).astype(np.uint64)
+        if stretch == "all":
+            soa.ts[lo:lo + m] = rank * np.uint64(1 << 33) + np.uint64(5)
+        else:  # a jump of 2^40 halfway: the windows that straddle it span it
+            soa.ts[lo:lo + m] = rank + np.where(np.arange(m) >= m // 2, np.uint64(1 << 40), np.uint64(0))
+    assert np.all(np.diff(soa.ts[:soa.n_a].astype(np.float64)) >= 0)
+    dc = DeviceCompose(soa)
+    dc.run()
+    _eq_soa(dc.results(), oracle.compose(soa), f"wide timestamps ({stretch})")
+    assert dc.last_plan() == "presorted"
+
+
 def test_gpu_segmented_plan_duplicate_ids():
     """Config-5-shaped log (ordered, 4096-op timestamp groups: the segmented plan) with
     duplicate ids and ids equal in their top bits inside groups: the tie runs are

@@ -5,7 +5,7 @@ import pytest
 from oracle import oracle
 from semantic_merge_amd import synth
 from semantic_merge_amd._lib import rga_replay_device
-from semantic_merge_amd.crdt import RGA, Key, marshal_streams, replay
+from semantic_merge_amd.crdt import RGA, Elem, Key, marshal_streams, replay, replay_lists
 
 from _util import load
 from test_rga_oracle import to_streams
@@ -28,6 +28,45 @@ def test_rga_class_dropin():
     r.insert(Key("root", 5, "u1", "o4"), "c")
     r.delete("b")
     assert r.materialize() == ["a", "c"]
+
+
+def test_rga_list_state_golden_gpu():
+    """RGA.list (crdt.py:26-27) in the library's list mode: every element in list order,
+    tombstoned ones included, equals the reference's list after each golden stream
+    (tests/golden/rga_list_cases.json, tools/make_golden.py --only rga_list)."""
+    cases = load("rga_cases.json")
+    want = load("rga_list_cases.json")
+    got = replay_lists(to_streams(cases))
+    assert sum(e[2] for w in want for e in w) > 100  # tombstones present
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert [[[e.key.anchor, e.key.t, e.key.author, e.key.opid], e.value, e.tombstone] for e in g] == w, \
+            f"rga list case {i}"
+
+
+def test_rga_class_list_property():
+    r = RGA()
+    r.insert(Key("root", 1, "u1", "o1"), "a")
+    r.insert(Key("root", 0, "u1", "o2"), "b")
+    r.move("a", Key("root", -1, "u2", "o3"))
+    r.delete("b")
+    assert r.list == [Elem(Key("root", -1, "u2", "o3"), "a", False), Elem(Key("root", 0, "u1", "o2"), "b", True)]
+    assert [e.value for e in r.list if not e.tombstone] == r.materialize() == ["a"]
+
+
+@pytest.mark.parametrize("n_ops,n_lists,seed", [(1_000_000, 5_000, 14), (300_000, 30, 15)])
+def test_rga_list_mode_live_elements_match(n_ops, n_lists, seed):
+    """At scale (the oracle has no list mode): the list state's live elements are exactly
+    materialize()'s output, list by list, and its tombstoned ones are extra elements."""
+    batch = synth.rga_batch(n_ops, n_lists, seed)
+    lv, ls, lo = rga_replay_device(batch)
+    tv, ts, to, tomb = rga_replay_device(batch, tombstones=True)
+    assert tomb.any()
+    for i in range(batch.n_lists):
+        a, b = to[i], to[i + 1]
+        live = ~tomb[a:b]
+        assert np.array_equal(ts[a:b][live], ls[lo[i]:lo[i + 1]]), f"list {i}"
+        assert np.array_equal(tv[a:b][live], lv[lo[i]:lo[i + 1]])
+    assert np.all(batch.op[ts[tomb]] != 2)  # tombstoned elements were created by inserts / moves
 
 
 def _check(batch):

@@ -251,6 +251,25 @@ def make_rga_cases(crdt, n_cases: int, seed: int):
     return cases
 
 
+def make_rga_list_cases(crdt):
+    """The reference's RGA.list state (crdt.py:26-27: every element in list order, with
+    its key and tombstone) after each stream of tests/golden/rga_cases.json."""
+    cases = json.load(open(os.path.join(GOLD, "rga_cases.json")))
+    out = []
+    for case in cases:
+        rga = crdt.RGA()
+        for ev in case["events"]:
+            if ev[0] == "insert":
+                rga.insert(crdt.Key(*ev[2]), ev[1])
+            elif ev[0] == "move":
+                rga.move(ev[1], crdt.Key(*ev[2]))
+            else:
+                rga.delete(ev[1])
+        out.append([[[e.key.anchor, e.key.t, e.key.author, e.key.opid], e.value, e.tombstone]
+                    for e in rga.list])
+    return out
+
+
 # ---------------------------------------------------------------------------
 # OpLog.from_json cases (ops.py:106-121): JSON texts of op dicts with the coercions
 # Op.from_dict applies (ops.py:89-100), and the reference's decoded ops -- or the
@@ -417,7 +436,7 @@ def make_applier_cases(applier_mod, ops_mod, n_cases: int, seed: int):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
-    ap.add_argument("--only", choices=["oplog", "applier", "big", "e2e"],
+    ap.add_argument("--only", choices=["oplog", "applier", "big", "e2e", "rga_list"],
                     help="regenerate one fixture only")
     args = ap.parse_args()
     compose, crdt, ops_mod = _import_reference()
@@ -430,6 +449,9 @@ def main() -> None:
         with open(os.path.join(GOLD, "applier_cases.json"), "w") as fh:
             json.dump(make_applier_cases(applier_mod, ops_mod, 400, seed=77), fh, separators=(",", ":"),
                       ensure_ascii=False)
+    if args.only == "rga_list":
+        with open(os.path.join(GOLD, "rga_list_cases.json"), "w") as fh:
+            json.dump(make_rga_list_cases(crdt), fh, separators=(",", ":"))
     if args.only == "e2e":
         from semmerge import applier as applier_mod
         with open(os.path.join(GOLD, "e2e_tree.json"), "w") as fh:
