@@ -818,7 +818,7 @@ __global__ void EMIT_BOUNDS k_emit(EmitArgs E) {
 // of a lane read four consecutive positions P unless a skipped rename falls between
 // them (rare): then each is read on its own.
 #ifndef EMIT_VEC
-#define EMIT_VEC 0
+#define EMIT_VEC 1
 #endif
 #define EMIT4_STEPS (EMIT_WT / (4 * WAVE))
 typedef u32 ev4u __attribute__((ext_vector_type(4)));
@@ -1064,7 +1064,6 @@ struct Ctx {
   i64 src_a, src_b;  // global source index of local op j (see WinArgs)
   StageTimer* tm;
   const i32* src_map = nullptr;
-  mutable bool ts64 = false;  // a window's timestamps span >= 2^32: u64 window keys
   template <typename T>
   T* ws(int b) const { return (T*)(base + L.off[b]); }
 };
@@ -1472,20 +1471,14 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   P.W = W;
   P.ablate = knob("SMX_ABLATE", 0);
   C.tm->begin(ST_WINDOW);
-  const bool ts32 = WF_TS32 && !C.ts64;
 #if SMX_DIAG
   if (g_phase_dbg && !P.src_map && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
     P.dbg = (u64*)g_phase_dbg;
-    hipLaunchKernelGGL((k_window_f<true, false, false>), dim3(W), dim3(WF_NT), 0, st, P);
+    hipLaunchKernelGGL((k_window_f<true, false>), dim3(W), dim3(WF_NT), 0, st, P);
   } else
 #endif
-  if (P.src_map) {
-    if (ts32) hipLaunchKernelGGL((k_window_f<false, true, true>), dim3(W), dim3(WF_NT), 0, st, P);
-    else hipLaunchKernelGGL((k_window_f<false, true, false>), dim3(W), dim3(WF_NT), 0, st, P);
-  } else {
-    if (ts32) hipLaunchKernelGGL((k_window_f<false, false, true>), dim3(W), dim3(WF_NT), 0, st, P);
-    else hipLaunchKernelGGL((k_window_f<false, false, false>), dim3(W), dim3(WF_NT), 0, st, P);
-  }
+  if (P.src_map) hipLaunchKernelGGL((k_window_f<false, true>), dim3(W), dim3(WF_NT), 0, st, P);
+  else hipLaunchKernelGGL((k_window_f<false, false>), dim3(W), dim3(WF_NT), 0, st, P);
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_WINDOW);
   return SMX_OK;
@@ -1928,12 +1921,6 @@ static thread_local int g_plan = SMX_PLAN_PRESORTED;
 static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm, i64 tgt) {
   int rc;
   g_plan = SMX_PLAN_PRESORTED;
-  if ((hm->f_fail & WF_FAIL_TSRANGE) && !hm->bad_sym) {  // timestamps too far apart for 32-bit keys
-    C.ts64 = true;
-    if ((rc = run_presorted(C, tgt))) return rc;
-    if (tail && (rc = launch_tail(C))) return rc;
-    if ((rc = read_meta(C, hm))) return rc;
-  }
   while (hm->f_fail == 2 && !hm->bad_sym && tgt > WIN_TGT_MIN) {  // dense groups: smaller windows
     tgt = (tgt / 2) / CH * CH;
     if ((rc = run_presorted(C, tgt))) return rc;
@@ -2059,10 +2046,7 @@ __global__ void k_shard_summary(const ComposeMeta* meta, i64* summary) {
   summary[18] = (i64)meta->n_ren_side[0];
   summary[19] = (i64)meta->n_ren_side[1];
   summary[20] = (i64)meta->n_move_none;
-  // (bit 2: repairable by SMX_SHARD_ORDER_FIX -- a window overflow or a timestamp range
-  // too wide for the 32-bit window keys)
-  summary[21] = (i64)((meta->f_fail & 1 ? 1 : 0) | (meta->bad_sym ? 2 : 0) |
-                      (meta->f_fail & (2 | WF_FAIL_TSRANGE) ? 4 : 0));
+  summary[21] = (i64)((meta->f_fail & 1 ? 1 : 0) | (meta->bad_sym ? 2 : 0) | (meta->f_fail & 2 ? 4 : 0));
 }
 
 // An empty shard hands the incoming open region (device- or host-held) straight on.

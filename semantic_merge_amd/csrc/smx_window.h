@@ -205,6 +205,15 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 // DBG: phase timestamps of every window (diagnostics, tools/window_phases.py):
 // lane 0 of wave 0 stores s_memtime after each phase into P.dbg[w * WF_NSTAMP + i].
 #define WF_NSTAMP 24
+// Diagnostic builds: SMX_ABLATE = 100 + N leaves the kernel after phase N (timing of
+// the phases by difference, tools/window_ablate.py); results invalid.
+#define WF_EXIT(N)                                                         \
+  do {                                                                     \
+    if (SMX_DIAG && P.ablate == 100 + (N)) {                               \
+      if (t == 0 && sord[0] == 0xfffeu && fin[1] == 0xfffeu) P.meta->dup_key = 1; \
+      return;                                                              \
+    }                                                                      \
+  } while (0)
 #define WSTAMP(i)                                                                  \
   do {                                                                             \
     if (DBG && t == 0) P.dbg[w * WF_NSTAMP + (i)] = __builtin_amdgcn_s_memtime(); \
@@ -226,18 +235,9 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #else
 #define WF_BOUNDS __launch_bounds__(WF_NT, WF_MINB)
 #endif
-// TS32: the window's timestamps as 32-bit offsets from its smallest one (both branch
-// parts are sorted, so that is the first op of one of them): the merge and the group
-// bits compare and move 4-byte keys.  A window whose timestamps span 2^32 or more
-// flags f_fail bit 3 and the launch is redone with TS32 = false (u64 keys).
-#ifndef WF_TS32
-#define WF_TS32 1
-#endif
-#define WF_FAIL_TSRANGE 8
-template <bool DBG, bool MAP, bool TS32>
+template <bool DBG, bool MAP>
 __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   __shared__ __attribute__((aligned(16))) u64 sts[WF_CAP];  // element space: timestamps; later slot-space rank keys
-  u32* const sts32 = reinterpret_cast<u32*>(sts);             // TS32: the timestamps' 32-bit offsets
   __shared__ u16 sord[WF_CAP];       // S order (merge), later the final order
   __shared__ u16 fin[WF_CAP];        // slot -> element, later rename ranks
   __shared__ u16 sl[WF_CAP];         // element -> slot, later rank -> slot, later posl
@@ -308,15 +308,6 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   u64 prev_a = 0, prev_b = 0;
   if (t == 0 && a0 > 0) prev_a = P.kts[a0 - 1];
   if (t == 0 && b0 > 0) prev_b = P.kts[P.na + P.bgap + b0 - 1];
-  // TS32: the window's first and last timestamp of each branch part (uniform loads);
-  // a branch-ordered window spans [tmin, tmax]
-  u64 tmin = 0, tmax = 0;
-  if (TS32) {
-    const u64 af = na ? P.kts[a0] : ~0ull, bf = nb ? P.kts[bld + na] : ~0ull;
-    const u64 al = na ? P.kts[a0 + na - 1] : 0ull, bl = nb ? P.kts[bld + na + nb - 1] : 0ull;
-    tmin = af < bf ? af : bf;
-    tmax = al > bl ? al : bl;
-  }
   // T-order segment starts; window offsets = chunk prefix at the window start + kinds
   // of the <= 255 ops between that chunk start and the window start (per branch)
   const u64 base_v = t <= SMX_N_KINDS ? P.meta->base[t] : 0ull;
@@ -358,7 +349,6 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     v0_r[i] = P.v0[j];
     v1_r[i] = P.v1[j];
   }
-  bool out_of_range = false;  // TS32: a timestamp outside [tmin, tmax]: not branch-ordered
   u32 none_mv = 0;  // moves with a None value (prefix fix-up)
   u32 vb_a = 0, vb_f = 0, vb_c = 0;  // OR of (value + 1): widths of the packed final-state table
 #pragma unroll
@@ -367,12 +357,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     if (e < sz) {
       bad |= k_r[i] >= SMX_N_KINDS || sym_r[i] >= (u64)P.n_sym;
       const u32 k = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
-      if (TS32) {
-        out_of_range |= ts_r[i] < tmin || ts_r[i] > tmax;
-        sts32[e] = (u32)(ts_r[i] - tmin);
-      } else {
-        sts[e] = ts_r[i];
-      }
+      sts[e] = ts_r[i];
       skind[e] = (u8)k;
       // the payload's first word: sym | the move's has-value bits (msym)
       if (k == KMOVE) {
@@ -400,10 +385,6 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   if (t < SMX_N_KINDS) wck[t] = 0;
   if (t < SMX_N_KINDS + 2) woffk[t] = woff_x + woff_y;
   if (t == 0) wtot[0] = failed != 0;
-  if (TS32 && sz && tmax - tmin > 0xffffffffull) {  // uniform: every thread leaves
-    if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, (unsigned long long)WF_FAIL_TSRANGE);
-    return;
-  }
   __syncthreads();
   if (wtot[0]) return;  // (wtot is written again in step 6)
   WSTAMP(1);
@@ -430,22 +411,16 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   //    branch log is non-decreasing (the pair straddling a window start is checked
   //    here too); it shares the merge's barrier and a window that fails it discards
   //    the merge.
-  bool dec = out_of_range;
+  bool dec = false;
   if (t == 0) {
-    if (TS32)  // (tmin / tmax: the parts' first and last timestamps)
-      dec |= (a0 > 0 && na > 0 && prev_a > P.kts[a0]) || (b0 > 0 && nb > 0 && prev_b > P.kts[bld + na]);
-    else
-      dec |= (a0 > 0 && na > 0 && prev_a > sts[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
+    dec = (a0 > 0 && na > 0 && prev_a > sts[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
     win_publish_widths(P.meta, &vbw[0][0], WF_WAVES, vcur);
   }
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
     if (e >= sz) continue;
-    if (SMX_DIAG && (P.ablate & 1)) continue;
-    if (TS32 ? (e != 0 && e != na && sts32[e - 1] > (u32)(ts_r[i] - tmin))
-             : (e != 0 && e != na && sts[e - 1] > ts_r[i]))
-      dec = true;
+    if (!(SMX_DIAG && (P.ablate & 1)) && e != 0 && e != na && sts[e - 1] > ts_r[i]) dec = true;
   }
   {
     const int d0 = t * WF_ITEMS < sz ? t * WF_ITEMS : sz;
@@ -453,12 +428,12 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     int lo = d0 - nb > 0 ? d0 - nb : 0, hi = d0 < na ? d0 : na;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (TS32 ? sts32[mid] <= sts32[na + d0 - 1 - mid] : sts[mid] <= sts[na + d0 - 1 - mid]) lo = mid + 1;
+      if (sts[mid] <= sts[na + d0 - 1 - mid]) lo = mid + 1;
       else hi = mid;
     }
     int ia = lo, ib = d0 - lo;
     for (int d = d0; d < d1; ++d) {
-      const bool take_a = ia < na && (ib >= nb || (TS32 ? sts32[ia] <= sts32[na + ib] : sts[ia] <= sts[na + ib]));
+      const bool take_a = ia < na && (ib >= nb || sts[ia] <= sts[na + ib]);
       const int e = take_a ? ia++ : na + ib++;
       sord[d] = (u16)e;
       skS[d] = skind[e];
@@ -469,6 +444,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     return;
   }
   WSTAMP(3);
+  WF_EXIT(2);
 
   // 3. stable multisplit of S by rank (wave ballots); element, kind and rank stay in
   //    registers for the scatter (m = t + WF_NT * j is chunk wv + WF_WAVES * j)
@@ -508,6 +484,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
   __syncthreads();
   WSTAMP(4);
+  WF_EXIT(3);
   for (int k = wv; k < SMX_N_KINDS; k += WF_WAVES) {
     const u32 x = lane < nch ? ccnt[lane][k] : 0u;
     const u32 inc = wave_incl_sum(x);
@@ -521,6 +498,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
   __syncthreads();
   WSTAMP(6);
+  WF_EXIT(4);
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) {
     const int m = t + WF_NT * j;
@@ -533,6 +511,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
   __syncthreads();
   WSTAMP(7);
+  WF_EXIT(5);
 
   // 4. group-start bits (a group = equal (rank, timestamp), contiguous in slots),
   //    then the timestamps are dead and their buffer takes the slot-space oid prefix
@@ -542,13 +521,14 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     bool f = false;
     if (p < sz) {
       const int e = fin[p];
-      f = (p == (int)kbase[skind[e]]) || (TS32 ? sts32[fin[p - 1]] != sts32[e] : sts[fin[p - 1]] != sts[e]);
+      f = (p == (int)kbase[skind[e]]) || (sts[fin[p - 1]] != sts[e]);
     }
     const u64 b = __ballot(f);
     if (lane == 0 && (p >> 6) < WF_NCH) gbits[p >> 6] = b;
   }
   __syncthreads();
   WSTAMP(8);
+  WF_EXIT(6);
   // slot-space rank keys: the top 32 bits of oid_hi; sl is reset to "no slot" for
   // the rank phase's collision check
   u32* pkey = (u32*)sts;
@@ -563,6 +543,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
   __syncthreads();
   WSTAMP(9);
+  WF_EXIT(7);
 
   // 5. order each group by (oid, side, index): counting rank over the group on the
   //    32-bit keys, four per LDS read.  Two keys of a group that are equal (about one
@@ -715,6 +696,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
 #endif
   __syncthreads();
   WSTAMP(10);
+  WF_EXIT(8);
   // 6. renames: rank among the window's renames of the same branch (final order).
   //    Computed in the collision-check phase into registers (rown aliases fin, which
   //    the exact re-rank still reads) and stored once no tie is known; redone after a
@@ -803,6 +785,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   if (none_mv) atomicAdd((unsigned long long*)&P.meta->n_move_none, (unsigned long long)none_mv);
   __syncthreads();
   WSTAMP(12);
+  WF_EXIT(9);
 
   // 7. payload by element, round 1: sym (| the move's has-value bits) and v0; the
   //    position of each rename in its branch's list (posl)
@@ -830,6 +813,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
   __syncthreads();
   WSTAMP(13);
+  WF_EXIT(10);
   // 8. natural-head DivergentRename flags -> candidate slots; window exports
   win_rename_flags<WF_NT>(
       P, w, woffk[KREN], RN, cntA, cntB, posl, gbits,
@@ -843,6 +827,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
         return make_uint2(st_a[e] & SYM_MASK, (u32)st_b[e]);
       });
   WSTAMP(14);
+  WF_EXIT(11);
 
   // 9. T-ordered records in final order (consecutive lanes -> consecutive T inside
   //    each kind: coalesced)
@@ -867,6 +852,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
   __syncthreads();
   WSTAMP(15);
+  WF_EXIT(12);
   // round 2: v1 -> the move's newFile, the rename's chain value
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {

@@ -282,23 +282,10 @@ class ShardedCompose:
         return torch.cat(parts + [ok, self._signed])
 
     @staticmethod
-    def _range_plan(g):
-        """From every rank's _range_info (g [W, 9], numpy or a device tensor): (ordered,
-        tau) -- the key ranges' lower bounds tau[1..W-1] (shard r owns keys [tau_r,
-        tau_r+1)), the running maximum of the ranks' first keys."""
-        if not isinstance(g, np.ndarray):  # the same on the device (no host sync)
-            import torch
-            W = g.shape[0]
-            lo = torch.full((1,), I64_MIN, dtype=torch.int64, device=g.device)
-            ordered = g[:, 6].min() == 1
-            for br in range(2):             # slices of a branch must follow each other
-                nz = g[:, br] > 0
-                last = torch.where(nz, g[:, 3 + 2 * br], lo)
-                prev = torch.cat([lo, torch.cummax(last, 0).values[:-1]])
-                ordered = ordered & (~nz | (g[:, 2 + 2 * br] >= prev)).all()
-            cand = torch.where(g[:, 0] > 0, g[:, 2], torch.where(g[:, 1] > 0, g[:, 4], lo))
-            cand[0] = I64_MIN
-            return ordered, torch.cummax(cand, 0).values[1:]
+    def _range_plan(g: np.ndarray):
+        """Host, from every rank's _range_info (g [W, 9]): (ordered, tau) -- the key
+        ranges' lower bounds tau[1..W-1] (shard r owns keys [tau_r, tau_r+1)), the
+        running maximum of the ranks' first keys."""
         W = g.shape[0]
         ordered = bool(g[:, 6].min() == 1)
         for br in range(2):                 # slices of a branch must follow each other
@@ -312,30 +299,27 @@ class ShardedCompose:
 
     def _range_counts(self):
         """allc [W, 2, W] (src, branch, dest) op counts of the key-range split, or None when
-        the logs are not timestamp-ordered.  One host sync: the ranks' slice ends are
-        gathered, the splitters and every rank's cut positions (binary searches) are
-        computed on the device, and the cuts are gathered with the slice ends."""
+        the logs are not timestamp-ordered.  Two small host syncs: the ranks' slice ends,
+        then every rank's cut positions (binary searches on the device).  (Planning on the
+        device instead, to save one sync, measured slower: a dozen tiny torch launches
+        cost more than the sync, profiles/r03_c/shard_probe.txt.)"""
         torch = self.torch
         W = self.world
-        g_dev = self.comm.all_gather(self._range_info())                  # [W, 9]
-        ordered_dev, tau = self._range_plan(g_dev)
+        g = self.comm.all_gather(self._range_info()).cpu().numpy()        # [W, 9]
+        ordered, tau = self._range_plan(g)
+        if not ordered:
+            return None
         cuts = torch.zeros((2, max(W - 1, 1)), dtype=torch.int64, device=self.dev)
         if W > 1:
+            tk = torch.from_numpy(tau).to(self.dev)
             for br, n in ((0, self.na_s), (1, self.nb_s)):
                 if n:
                     ts = self._orig(br, "ts")
                     # every timestamp below 2^63: search the stored words (int64 order =
                     # u64 order); a splitter above 2^63 (key >= 0) is fixed on the host
-                    cuts[br] = torch.searchsorted(ts, _u64_key(tau)) if self._ts_signed[br] else \
-                        torch.searchsorted(_u64_key(ts).contiguous(), tau)
-        both = self.comm.all_gather(torch.cat([cuts.reshape(-1), ordered_dev.to(torch.int64).view(1)]))
-        host = torch.cat([g_dev.reshape(-1), both.reshape(-1)]).cpu().numpy()     # the one host sync
-        g = host[: W * 9].reshape(W, 9)
-        both = host[W * 9:].reshape(W, -1)
-        if not bool(both[0, -1]):
-            return None
-        _, tau = self._range_plan(g)
-        gc = both[:, :-1].reshape(W, 2, max(W - 1, 1))                     # [W, 2, W-1]
+                    cuts[br] = torch.searchsorted(ts, _u64_key(tk)) if self._ts_signed[br] else \
+                        torch.searchsorted(_u64_key(ts).contiguous(), tk)
+        gc = self.comm.all_gather(cuts).cpu().numpy()                      # [W, 2, W-1]
         allc = np.zeros((W, 2, W), np.int64)
         for q in range(W):
             for br in range(2):

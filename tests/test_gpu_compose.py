@@ -128,9 +128,9 @@ def test_gpu_equals_oracle_soa(spec):
 
 @pytest.mark.parametrize("stretch", ["all", "half"])
 def test_gpu_wide_timestamp_range(stretch):
-    """Timestamps whose window span exceeds the 32-bit window keys (k_window_f TS32):
-    the windows flag it and the presorted plan reruns on u64 keys -- every window
-    ("all") or only the windows of the later half of each branch ("half")."""
+    """Timestamps far apart (windows spanning more than 2^32 key units: every window
+    ("all") or the windows across a 2^40 jump ("half")): the presorted plan's u64
+    window keys order them exactly."""
     soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(400_000, 2_000, 71)))
     for lo, m in ((0, soa.n_a), (soa.n_a, soa.n_b)):
         ts = soa.ts[lo:lo + m].copy()

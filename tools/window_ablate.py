@@ -1,7 +1,8 @@
-"""Window-kernel ablation: time k_window_f variants in ONE process, interleaved rounds
-(cdna_hip_programming.md §5.4 rule 24).  SMX_ABLATE bits: 1 skip layout check,
-2 skip group ranking loop, 4 skip the output phases, 16 load only.  Results of ablated
-runs are invalid by design; only the window stage time is read."""
+"""Window-kernel ablation (diagnostic build, SMX_LIB=<-DSMX_DIAG=1 build>): time
+k_window_f variants in ONE process, interleaved rounds (cdna_hip_programming.md §5.4
+rule 24).  SMX_ABLATE = 16: load only; 100 + N: leave after phase N (smx_window.h
+WF_EXIT), so phase N costs exitN - exit(N-1).  Results of ablated runs are invalid by
+design; only the window stage time is read."""
 import os
 import sys
 
@@ -19,10 +20,10 @@ def main():
     soa = synth.lift_soa(synth.lift_logs(spec))
     dc = _lib.DeviceCompose(soa)
     lib = _lib.lib()
-    variants = [("base", {}), ("nocheck", {"SMX_ABLATE": "1"}), ("norank", {"SMX_ABLATE": "2"}),
-                ("nowrite", {"SMX_ABLATE": "4"}), ("loadonly", {"SMX_ABLATE": "16"}),
-                ("tgt1280", {"SMX_WIN_TGT": "1280"}), ("tgt1536", {"SMX_WIN_TGT": "1536"}),
-                ("tgt1792", {"SMX_WIN_TGT": "1792"})]
+    names = {2: "merge", 3: "ksplit", 4: "kscan", 5: "kscatter", 6: "gbits", 7: "pkey", 8: "bucket",
+             9: "renrank", 10: "posl", 11: "flags", 12: "out1"}
+    variants = [("base", {}), ("loadonly", {"SMX_ABLATE": "16"})] + \
+        [(f"exit{k:02d}_{v}", {"SMX_ABLATE": str(100 + k)}) for k, v in names.items()]
     res = {k: [] for k, _ in variants}
     for rnd in range(4):
         for name, env in variants:
