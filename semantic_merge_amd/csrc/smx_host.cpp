@@ -690,10 +690,23 @@ PyObject* ops_from_dicts(PyObject*, PyObject* args) {
 
 // ---------------------------------------------------------------- JSON (ops.py:112-118)
 
+// json.JSONDecodeError(msg, doc, pos) -- what orjson.loads raises (orjson.JSONDecodeError
+// subclasses it, and ValueError).  pos counts characters, as the json module's do.
+void raise_json_error(const char* what, const char* b, const char* e, const char* at) {
+  Ref js(PyImport_ImportModule("json"));
+  Ref cls(js ? PyObject_GetAttrString(js.p, "JSONDecodeError") : nullptr);
+  Ref doc(PyUnicode_DecodeUTF8(b, e - b, "replace"));
+  Ref pre(PyUnicode_DecodeUTF8(b, at - b, "replace"));
+  if (!cls || !doc || !pre) return;
+  Ref exc(PyObject_CallFunction(cls.p, "sOn", what, doc.p, PyUnicode_GET_LENGTH(pre.p)));
+  if (exc) PyErr_SetObject(cls.p, exc.p);
+}
+
 // A strict JSON reader with the standard json module's results (dict / list / str /
 // int / float / True / False / None; duplicate keys: the last wins; big integers
-// exact; float(token) for the rest) and orjson's input rules: NaN / Infinity rejected,
-// no control characters inside strings, nesting up to 1024, nothing after the value.
+// exact; float(token) for the rest) and orjson's input rules: NaN / Infinity and lone
+// surrogate escapes rejected, no control characters inside strings, nesting up to 1024,
+// nothing after the value; errors are json.JSONDecodeError.
 struct JsonReader {
   const char* p;
   const char* b;
@@ -746,8 +759,7 @@ struct JsonReader {
   }
 
   bool fail(const char* what) {
-    if (!PyErr_Occurred())
-      PyErr_Format(PyExc_ValueError, "JSON decode error: %s at offset %zd", what, (Py_ssize_t)(p - b));
+    if (!PyErr_Occurred()) raise_json_error(what, b, e, p < e ? p : e);
     return false;
   }
   void ws() {
@@ -777,7 +789,11 @@ struct JsonReader {
     }
     if (p >= e) return fail("unterminated string"), nullptr;
     const char* s1 = p++;
-    if (!esc) return PyUnicode_DecodeUTF8(s0, s1 - s0, "strict");
+    if (!esc) {
+      PyObject* r = PyUnicode_DecodeUTF8(s0, s1 - s0, "strict");
+      if (!r && PyErr_ExceptionMatches(PyExc_UnicodeDecodeError)) PyErr_Clear(), p = s0, fail("invalid UTF-8");
+      return r;
+    }
     std::vector<Py_UCS4> u;
     u.reserve((size_t)(s1 - s0));
     for (const char* q = s0; q < s1;) {
@@ -800,12 +816,14 @@ struct JsonReader {
             if (cp < 0) return p = q, fail("invalid \\u escape"), nullptr;
             q += 4;
             if (cp >= 0xD800 && cp <= 0xDBFF && s1 - q >= 6 && q[0] == '\\' && q[1] == 'u') {
-              const int lo2 = hex4(q + 2);  // a surrogate pair (json pairs them; a lone one stays)
+              const int lo2 = hex4(q + 2);  // a surrogate pair
               if (lo2 >= 0xDC00 && lo2 <= 0xDFFF) {
                 cp = 0x10000 + ((cp - 0xD800) << 10) + (lo2 - 0xDC00);
                 q += 6;
               }
             }
+            // a lone surrogate is not UTF-8: orjson rejects it (the json module keeps it)
+            if (cp >= 0xD800 && cp <= 0xDFFF) return p = q - 6, fail("lone surrogate in \\u escape"), nullptr;
             u.push_back((Py_UCS4)cp);
             break;
           }
@@ -818,7 +836,10 @@ struct JsonReader {
       int len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
       if (!len || q + len > s1) return p = q, fail("invalid UTF-8"), nullptr;
       Ref one_cp(PyUnicode_DecodeUTF8(q, len, "strict"));
-      if (!one_cp) return nullptr;
+      if (!one_cp) {
+        if (PyErr_ExceptionMatches(PyExc_UnicodeDecodeError)) PyErr_Clear(), p = q, fail("invalid UTF-8");
+        return nullptr;
+      }
       u.push_back(PyUnicode_READ_CHAR(one_cp.p, 0));
       q += len;
     }
@@ -971,6 +992,16 @@ struct JsonReader {
 bool utf8_of(PyObject* x, Ref& hold, const char** s, Py_ssize_t* n) {
   if (PyUnicode_Check(x)) {
     *s = PyUnicode_AsUTF8AndSize(x, n);
+    if (!*s && PyErr_ExceptionMatches(PyExc_UnicodeEncodeError)) {  // lone surrogates: orjson's error
+      PyErr_Clear();
+      Ref js(PyImport_ImportModule("json"));
+      Ref cls(js ? PyObject_GetAttrString(js.p, "JSONDecodeError") : nullptr);
+      if (cls) {
+        Ref exc(PyObject_CallFunction(cls.p, "sOn", "str is not valid UTF-8: surrogates not allowed", x,
+                                      (Py_ssize_t)0));
+        if (exc) PyErr_SetObject(cls.p, exc.p);
+      }
+    }
     return *s != nullptr;
   }
   hold.reset(PyBytes_FromObject(x));
@@ -1008,7 +1039,39 @@ PyObject* decode_oplogs(PyObject*, PyObject* args) {
   GcPause gc_pause;
   Ref one(PyLong_FromLong(1)), lists(PyTuple_New(PyTuple_GET_SIZE(texts)));
   if (!one || !lists) return nullptr;
+  // The reference decodes each text whole (orjson.loads), then builds its ops
+  // (Op.from_dict per item, ops.py:116-118), and compose marshals after both: a JSON
+  // error anywhere in a text comes before an item error of that text, which comes
+  // before any marshalling error.  Items are built while the text is read; the first
+  // item / marshalling error is held back until its turn.
+  struct Held {
+    PyObject *t = nullptr, *v = nullptr, *tb = nullptr;
+    bool set() const { return t != nullptr; }
+    void take() { PyErr_Fetch(&t, &v, &tb); }
+    PyObject* raise() {
+      PyErr_Restore(t, v, tb);
+      t = v = tb = nullptr;
+      return nullptr;
+    }
+    ~Held() {
+      Py_XDECREF(t);
+      Py_XDECREF(v);
+      Py_XDECREF(tb);
+    }
+  } marshal_err;
   for (Py_ssize_t t = 0; t < PyTuple_GET_SIZE(texts); ++t) {
+    Held item_err;
+    auto add_item = [&](PyObject* item, PyObject* out) -> bool {  // false: a real failure
+      if (item_err.set()) return true;  // the reference stopped at the first failing item
+      Ref op(op_from_dict(item, ctor, op_cls, tcls, one.p));
+      if (!op) {
+        item_err.take();
+        return true;
+      }
+      if (PyList_Append(out, op.p) < 0) return false;
+      if (!marshal_err.set() && !M.add(op.p)) marshal_err.take();
+      return true;
+    };
     Ref hold, memo(PyDict_New());
     const char* s;
     Py_ssize_t n;
@@ -1019,6 +1082,7 @@ PyObject* decode_oplogs(PyObject*, PyObject* args) {
     R.ws();
     if (R.p < R.e && *R.p == '[') {  // the usual document: ops decoded as they are read
       ++R.p;
+      R.depth = 1;  // the outer array counts toward the nesting limit
       R.ws();
       bool first = true;
       while (!(R.p < R.e && *R.p == ']')) {
@@ -1029,8 +1093,7 @@ PyObject* decode_oplogs(PyObject*, PyObject* args) {
         first = false;
         Ref item(R.value());
         if (!item) return nullptr;
-        Ref op(op_from_dict(item.p, ctor, op_cls, tcls, one.p));
-        if (!op || !M.add(op.p) || PyList_Append(out.p, op.p) < 0) return nullptr;
+        if (!add_item(item.p, out.p)) return nullptr;
         R.ws();
       }
       ++R.p;
@@ -1043,13 +1106,14 @@ PyObject* decode_oplogs(PyObject*, PyObject* args) {
       if (!it) return nullptr;
       while (PyObject* raw = PyIter_Next(it.p)) {
         Ref item(raw);
-        Ref op(op_from_dict(item.p, ctor, op_cls, tcls, one.p));
-        if (!op || !M.add(op.p) || PyList_Append(out.p, op.p) < 0) return nullptr;
+        if (!add_item(item.p, out.p)) return nullptr;
       }
       if (PyErr_Occurred()) return nullptr;
     }
+    if (item_err.set()) return item_err.raise();
     PyTuple_SET_ITEM(lists.p, t, out.release());
   }
+  if (marshal_err.set()) return marshal_err.raise();
   Ref sum(M.summary());
   if (!sum) return nullptr;
   auto col = [](const void* d, size_t bytes) { return PyByteArray_FromStringAndSize((const char*)d, (Py_ssize_t)bytes); };

@@ -46,12 +46,23 @@ def _orjson():
         return None
 
 
+def _utf8_str(x: str) -> str:
+    """orjson.dumps refuses str with lone surrogates (not UTF-8)."""
+    try:
+        x.encode("utf-8")
+    except UnicodeEncodeError:
+        raise TypeError("str is not valid UTF-8: surrogates not allowed") from None
+    return x
+
+
 def _json_ready(x: Any) -> Any:
     """orjson's output rules on the standard encoder: non-finite floats -> null,
-    string keys only, integers within 64 bits."""
+    string keys only, integers within 64 bits, str without lone surrogates."""
     if isinstance(x, float):
         return x if math.isfinite(x) else None
-    if isinstance(x, bool) or x is None or isinstance(x, str):
+    if isinstance(x, str):
+        return _utf8_str(x)
+    if isinstance(x, bool) or x is None:
         return x
     if isinstance(x, int):
         if not -(2 ** 63) <= x < 2 ** 64:
@@ -62,7 +73,7 @@ def _json_ready(x: Any) -> Any:
         for k, v in x.items():
             if not isinstance(k, str):
                 raise TypeError("Dict key must be str")
-            out[k] = _json_ready(v)
+            out[_utf8_str(k)] = _json_ready(v)
         return out
     if isinstance(x, (list, tuple)):
         return [_json_ready(v) for v in x]
@@ -77,15 +88,11 @@ def dumps(obj: Any) -> str:
     return json.dumps(_json_ready(obj), separators=(",", ":"), ensure_ascii=False)
 
 
-def _reject_constant(name: str):
-    raise json.JSONDecodeError(f"unexpected {name}", name, 0)
-
-
 def loads(data: Any) -> Any:
-    """``orjson.loads(data)`` (ops.py:117): str or bytes, NaN / Infinity rejected.
-    Without orjson: the native strict reader (csrc/smx_host.cpp JsonReader; the json
-    module's results), or the json module for str the reader cannot view as UTF-8
-    (lone surrogates)."""
+    """``orjson.loads(data)`` (ops.py:117): str or bytes; NaN / Infinity, lone
+    surrogates (in the text or as escapes) and invalid UTF-8 rejected with
+    json.JSONDecodeError (orjson.JSONDecodeError subclasses it).  Without orjson: the
+    native strict reader (csrc/smx_host.cpp JsonReader; the json module's results)."""
     oj = _orjson()
     if oj is not None:
         return oj.loads(data)
@@ -93,7 +100,7 @@ def loads(data: Any) -> Any:
         try:
             data.encode("utf-8")
         except UnicodeEncodeError:
-            return json.loads(data, parse_constant=_reject_constant)
+            raise json.JSONDecodeError("str is not valid UTF-8: surrogates not allowed", data, 0) from None
     return host().json_loads(data)
 
 

@@ -35,7 +35,7 @@ def test_reader_matches_json_module():
         for text in (json.dumps(doc), json.dumps(doc, ensure_ascii=False), json.dumps(doc, indent=2)):
             assert host().json_loads(text) == json.loads(text), text
             assert host().json_loads(text.encode()) == json.loads(text)
-    for text in ('"\\ud83d\\ude00"', '"\\ud800"', '"\\udc00x"', '[1e400, -1e400, 1E2, -0, -0.0]',
+    for text in ('"\\ud83d\\ude00"', '[1e400, -1e400, 1E2, -0, -0.0]',
                  '{"a": 1, "a": 2}', ' \n[ ] ', '123456789012345678901234567890'):
         got, want = host().json_loads(text), json.loads(text)
         assert repr(got) == repr(want), text
@@ -43,12 +43,37 @@ def test_reader_matches_json_module():
 
 @pytest.mark.parametrize("bad", ["[NaN]", "[Infinity]", "[-Infinity]", "[1,]", "{\"a\" 1}", "[1] x", "",
                                  "\"a\u0001\"", "[01]", "[1.]", "[.5]", "tru", "{'a': 1}", "[\"\\x\"]",
-                                 "[" * 1100 + "]" * 1100])
+                                 "[" * 1100 + "]" * 1100, '"\\ud800"', '"\\udc00x"', '["\\ud83dx"]',
+                                 b'["\xff"]', b'"\xed\xa0\x80"', "\"\ud800\""])
 def test_reader_rejects(bad):
-    with pytest.raises(ValueError):
-        host().json_loads(bad)
-    with pytest.raises(ValueError):
+    """orjson's input rules (ops.py:117), raised as json.JSONDecodeError as orjson does
+    (orjson.JSONDecodeError subclasses it): NaN / Infinity, lone surrogates (escaped or in
+    the text), invalid UTF-8, nesting beyond 1024, trailing data."""
+    if not isinstance(bad, bytes) and "\ud800" not in bad:
+        with pytest.raises(json.JSONDecodeError):
+            host().json_loads(bad)
+    with pytest.raises(json.JSONDecodeError):
         loads(bad)
+
+
+def test_decode_pair_error_order():
+    """The reference parses a whole text before building any op (orjson.loads, then
+    Op.from_dict per item): a syntax error late in the text wins over a bad item early;
+    a bad item (KeyError) is raised when the text parses; the outer array counts toward
+    the 1024 nesting limit."""
+    good = json.dumps([{"id": "x", "type": "addDecl", "target": {"symbolId": "s"}}])
+    bad_item = '[{"type": "addDecl"}, {"id": "y", "type": "addDecl", "target": {"symbolId": "s"}}'
+    with pytest.raises(json.JSONDecodeError):
+        decode_pair(bad_item + ", tru]", good)
+    with pytest.raises(KeyError):
+        decode_pair(bad_item + "]", good)
+    with pytest.raises(json.JSONDecodeError):       # text b's JSON error after text a's items
+        decode_pair(good, "[1,")
+    deep = "[" + "[" * 1024 + "]" * 1024 + "]"
+    with pytest.raises(json.JSONDecodeError):
+        host().json_loads(deep)
+    with pytest.raises(json.JSONDecodeError):
+        decode_pair(deep, good)
 
 
 def _soa_equal(a, b):
