@@ -5,7 +5,9 @@
 
 One step = one composition (semmerge/compose.py:11-114 restated on the GPU) of
 SURVEY §8(d) config 3: 100M lift-shaped ops (50M per branch), 1M symbols, seed 11.
-Inputs are resident in HBM before timing.  N = 1: one smx_compose call per step.
+Inputs are resident in HBM before timing.  N = 1: one smx_compose call per step (on a
+stream of its own: the library replays the merge's launches as one HIP graph; every
+step still recomputes everything from the inputs and syncs once).
 N > 1 (torchrun, one process per GPU): by default ONE merge of the same 100M ops
 split over the N ranks (strong scaling, BASELINE config 3 "100M ops across 8 GPUs"),
 sharded by timestamp key range (semantic_merge_amd/shard.py); a step is the whole
@@ -47,7 +49,14 @@ sys.path.insert(0, REPO)
 METRIC = "op-log compose+conflict throughput (ops/s), 100M-op logs, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 PIPE_BYTES_PER_OP = 53         # 37 B in + 16 B out per op (+8 B per conflict)
-WINDOW_BYTES_PER_OP = 41       # k_window: 37 B of input read once + 4 B T-order index written
+# The roofline kernel is the plan's dominant one, by the library's stage timers:
+#   stage      kernel                 algorithmic bytes per op of the merge
+#   window     k_window_f             41: the 37 B of input read once + the 4 B T-order index
+#   window_g   k_window_g             45: the 37 B + the 4 B sort permutation + the 4 B index
+#   segsort    k_segsort (2 launches) 52: ts, oid (24 B) read, sorted copies (24 B) + the
+#                                     permutation (4 B) written
+ROOF_STAGES = {"window": ("k_window_f", 41), "window_g": ("k_window_g", 45), "segsort": ("k_segsort", 52)}
+WINDOW_BYTES_PER_OP = ROOF_STAGES["window"][1]
 REF_PY_OPS_S = 47_600          # SURVEY §3.4 / BASELINE.md: reference compose_oplogs, 1 core, 1M ops
 FETCH_FACTOR, WRITE_FACTOR = 2.0, 1.0   # gfx950 FETCH_SIZE reads 1/2 of streamed bytes (guide)
 
@@ -95,12 +104,6 @@ def pmc_traffic(args) -> dict:
     def kbytes(vals, factor):
         return sum(vals) * 1024.0 * factor
 
-    win = [k for k in per if k.startswith("k_window_f") or k.startswith("k_window_g")]
-    if win:
-        k = win[0]
-        f, w = per[k].get("FETCH_SIZE", []), per[k].get("WRITE_SIZE", [])
-        out["kernel"] = k
-        out["traffic"] = round((kbytes(f, FETCH_FACTOR) + kbytes(w, WRITE_FACTOR)) / max(len(f), 1))
     tot = 0.0
     kern = {}
     for k, cs in per.items():
@@ -109,7 +112,8 @@ def pmc_traffic(args) -> dict:
         kern[k] = round(b)
         tot += b
     out["pipeline_traffic"] = round(tot)
-    out["per_kernel"] = dict(sorted(kern.items(), key=lambda x: -x[1])[:12])
+    out["per_kernel"] = dict(sorted(kern.items(), key=lambda x: -x[1])[:12])   # bytes per merge
+    out["per_kernel_all"] = {k.split("<")[0]: v for k, v in kern.items()}
     out["status"] = "ok"
     return out
 
@@ -263,13 +267,18 @@ def main() -> None:
         run = dc.run
         log(f"[rank {rank}] resident on {dev}; workspace {dc.ws_bytes / 2**30:.2f} GiB")
 
-    for _ in range(args.warmup):
+    # a stream of its own (not the null stream): smx_compose replays its asynchronous
+    # part as a HIP graph from the second merge on (smx_compose.hip compose_async_graph)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    lib = _lib.lib()
+    # the stage timers run in the warm-up too, so that the timed steps replay the graph
+    # the warm-up captured (timer events are part of it)
+    lib.smx_set_profiling(1)
+    for _ in range(args.warmup):  # (the second merge captures the graph: W >= 2 keeps it out of the timed steps)
         run()
     torch.cuda.synchronize(dev)
-
-    lib = _lib.lib()
     lib.smx_reset_stage_times()
-    lib.smx_set_profiling(1)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -326,9 +335,14 @@ def main() -> None:
     n = soa.n
     ms_step = elapsed / args.steps * 1e3
     value = job_throughput(n_job, 1, args.steps, elapsed)
-    win_ms, win_calls = stages.get("window", (0.0, 0))
-    win_avg = win_ms / max(win_calls, 1)
-    achieved = WINDOW_BYTES_PER_OP * n / (win_avg * 1e-3) / 1e9 if win_avg > 0 else None
+    # the dominant kernel of the plan that ran: the largest stage time per merge
+    roof_stage = max(ROOF_STAGES, key=lambda k: stages.get(k, (0.0, 0))[0])
+    roof_kernel, roof_bpo = ROOF_STAGES[roof_stage]
+    st_ms, st_calls = stages.get(roof_stage, (0.0, 0))
+    # per launch of the kernel: a failed presorted attempt shares the "window" stage with
+    # nothing else; the segmented sort's stage covers both branch launches of a merge
+    win_avg = st_ms / max(st_calls, 1)
+    achieved = roof_bpo * n / (win_avg * 1e-3) / 1e9 if win_avg > 0 else None
     pipe_gbs = (PIPE_BYTES_PER_OP * n_job + 8 * nconf) / (ms_step * 1e-3) / 1e9
 
     solo = world == 1
@@ -377,13 +391,16 @@ def main() -> None:
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_window_f",
+            "kernel": roof_kernel + (" (both branches)" if roof_stage == "segsort" else ""),
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": pmc.get("traffic") if pmc else None,
-            "bytes_per_op": WINDOW_BYTES_PER_OP,
+            # HBM bytes per merge of that kernel (PMC passes; per launch for the one-launch
+            # kernels, both branch launches for the segmented sort)
+            "traffic": round(pmc.pop("per_kernel_all").get(roof_kernel, 0))
+            if pmc and pmc.get("status") == "ok" else None,
+            "bytes_per_op": roof_bpo,
             "avg_launch_ms": round(win_avg, 4),
         },
         "pipeline_roofline": {

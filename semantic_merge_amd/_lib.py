@@ -142,6 +142,8 @@ class ComposeSession:
         self.device = self.torch.device(device)
         self.cap_n = self.cap_ws = -1
         self.last = {}
+        # its own stream: repeated merges of one size replay the library's HIP graph
+        self.stream = self.torch.cuda.Stream(self.device)
 
     def _ensure(self, n: int, ws_bytes: int) -> None:
         torch = self.torch
@@ -178,8 +180,10 @@ class ComposeSession:
             off += _al(n * w)
         t1 = time.perf_counter()
         torch = self.torch
-        stream = torch.cuda.current_stream(self.device)
-        self.d_in[:off].copy_(self.h_in[:off], non_blocking=True)
+        stream = self.stream
+        stream.wait_stream(torch.cuda.current_stream(self.device))  # buffers (re)allocated on it
+        with torch.cuda.stream(stream):
+            self.d_in[:off].copy_(self.h_in[:off], non_blocking=True)
         ccap = max(min(soa.n_a, soa.n_b), 1)
         o0 = self.d_out.data_ptr()
         q = _al(n * 4)             # outputs laid out for n: one contiguous copy back
@@ -188,7 +192,8 @@ class ComposeSession:
         cnt_off = 4 * q + _al(8 * ccap)
         out = _abi.SmxComposeOut(o0, o0 + q, o0 + 2 * q, o0 + 3 * q, o0 + 4 * q, ccap, o0 + cnt_off)
         check(lib().smx_compose(C.byref(ops), C.byref(out), self.ws.data_ptr(), ws.value, stream.cuda_stream))
-        self.h_out[:cnt_off + 16].copy_(self.d_out[:cnt_off + 16], non_blocking=True)
+        with torch.cuda.stream(stream):
+            self.h_out[:cnt_off + 16].copy_(self.d_out[:cnt_off + 16], non_blocking=True)
         stream.synchronize()
         t2 = time.perf_counter()
         hout = self.h_out.numpy()

@@ -124,6 +124,12 @@ __device__ __forceinline__ u64 lanemask_lt() {
   return (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
 }
 
+__device__ __forceinline__ void wave_lds_sync() {  // LDS writes of this wave visible to its lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Lanes of this wave holding the same `nbits`-bit value `d` (among lanes with `valid`).
 template <int NBITS>
 __device__ __forceinline__ u64 wave_peers(u32 d, bool valid) {

@@ -27,6 +27,7 @@
 //   tables      per-symbol last writers: bucket by symbol range, LDS max-reduce
 //   k_emit      compacted output of every op after the move block: order, addr,
 //               file, ctx
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -51,9 +52,12 @@ int smx_set_error(int code, const char* msg) { return set_err(code, msg ? msg : 
       return set_err(SMX_E_HIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-enum Stage { ST_PLAN, ST_GSORT, ST_WINDOW, ST_WALK, ST_TABLES, ST_MVPREFIX, ST_EMIT, ST_N };
-static const char* kStageNames[ST_N] = {"plan",   "gsort",     "window", "walk",
-                                        "tables", "mvprefix", "emit"};
+// gsort: the generic plan's sort and window planning; segsort: its segmented sort's
+// kernels alone (inside gsort); window_g: the generic window kernel (window: the
+// presorted one, including attempts that fail)
+enum Stage { ST_PLAN, ST_GSORT, ST_WINDOW, ST_WALK, ST_TABLES, ST_MVPREFIX, ST_EMIT, ST_SEGSORT, ST_WINDOW_G, ST_N };
+static const char* kStageNames[ST_N] = {"plan",   "gsort",    "window", "walk",    "tables",
+                                        "mvprefix", "emit", "segsort", "window_g"};
 static std::mutex g_prof_mu;
 static int g_prof = 0;
 static double g_stage_ms[ST_N];
@@ -162,6 +166,22 @@ __global__ void __launch_bounds__(BLOCK) k_keymask(const u64* __restrict__ ts, c
     atomicOr((unsigned long long*)&meta->key_or[s][q], ((unsigned long long)v[1] << 32) | v[0]);
     atomicAnd((unsigned long long*)&meta->key_and[s][q], ~(((unsigned long long)v[3] << 32) | v[2]));
   }
+}
+
+// Zero fill as a kernel: the asynchronous part of a merge, which is captured into a
+// HIP graph, holds kernel nodes only.
+__global__ void k_zero(u32* __restrict__ p, u64 nw) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (u64)gridDim.x * blockDim.x) p[i] = 0u;
+}
+static int zero_async(void* p, size_t bytes, hipStream_t st) {
+  if (bytes % 4) return set_err(SMX_E_ARG, "zero_async: size not a multiple of 4");
+  const u64 nw = bytes / 4;
+  if (nw == 0) return SMX_OK;
+  u64 g = SMX_CEIL_DIV(nw, (u64)BLOCK * 4);
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(k_zero, dim3((u32)g), dim3(BLOCK), 0, st, (u32*)p, nw);
+  HIP_TRY(hipGetLastError());
+  return SMX_OK;
 }
 
 __global__ void k_meta_init(ComposeMeta* meta) {
@@ -1148,7 +1168,10 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
   u64* skipbits = C.ws<u64>(B_SKIPBITS);
   u32* skiplist = C.ws<u32>(B_SKIPLIST);
   u32* part = C.ws<u32>(B_PART);
-  HIP_TRY(hipMemsetAsync(skipbits, 0, (size_t)(SMX_CEIL_DIV(n, (i64)64) + 1) * 8, st));
+  {
+    const int rc = zero_async(skipbits, (size_t)(SMX_CEIL_DIV(n, (i64)64) + 1) * 8, st);
+    if (rc) return rc;
+  }
   const WalkArgs Wk = walk_args(C, sh);
   u32* cslot = C.ws<u32>(B_CSLOT);
   u32* wcand = C.ws<u32>(B_WCAND);
@@ -1257,9 +1280,10 @@ static int launch_tables(const Ctx& C, u64* part_tab, u32 tag, bool* bucketed, b
     u32* tabA = C.ws<u32>(B_TABA);
     u32* tabF = C.ws<u32>(B_TABF);
     u32* tabR = C.ws<u32>(B_TABR);
-    HIP_TRY(hipMemsetAsync(tabA, 0, (size_t)n_sym * 4, st));
-    HIP_TRY(hipMemsetAsync(tabF, 0, (size_t)n_sym * 4, st));
-    HIP_TRY(hipMemsetAsync(tabR, 0, (size_t)n_sym * 4, st));
+    int rc;
+    if ((rc = zero_async(tabA, (size_t)n_sym * 4, st)) || (rc = zero_async(tabF, (size_t)n_sym * 4, st)) ||
+        (rc = zero_async(tabR, (size_t)n_sym * 4, st)))
+      return rc;
     hipLaunchKernelGGL(k_tab_atomic, dim3(grid_for(n)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR);
     hipLaunchKernelGGL(k_finalize, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR, n_sym, fin,
                        part_tab, tag);
@@ -1360,6 +1384,14 @@ static int side_stream(hipStream_t caller, SideStream** out) {
 #ifndef SMX_TB_OVERLAP_MIN
 #define SMX_TB_OVERLAP_MIN (1 << 22)  // ops
 #endif
+// launch_tail forks the table scatter onto the side stream for this merge
+static bool n_side_needed(const smx_ops* ops) {
+  u64 width = SMX_CEIL_DIV((u64)ops->n_sym, (u64)TB_NBK_TGT);
+  if (width < 1) width = 1;
+  if (width > TB_WIDTH) width = TB_WIDTH;
+  return SMX_TB_OVERLAP && SMX_CEIL_DIV((u64)ops->n_sym, width) <= TB_MAXBK &&
+         ops->n_a + ops->n_b >= SMX_TB_OVERLAP_MIN;
+}
 
 // Walk, tables, emit of a single merge.  The bucketed tables' scatter keeps every
 // rename and runs on the side stream while the walk runs; k_tb_unskip then kills
@@ -1433,7 +1465,11 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
   C.tm->begin(ST_PLAN);
-  HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
+  static_assert(sizeof(ComposeMeta) % 4 == 0, "meta is zeroed by words");
+  {
+    const int rc = zero_async(meta, sizeof(ComposeMeta), st);
+    if (rc) return rc;
+  }
   if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
   if (tgt > WF_CAP) tgt = WF_CAP;
   tgt -= tgt % CH;  // chunk-aligned diagonals (k_fpart's sampled first level)
@@ -1800,6 +1836,7 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
   C.tm->begin(ST_GSORT);
   HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
   if (mode == GEN_SEG) {
+    C.tm->begin(ST_SEGSORT);
     for (int side = 0; side < 2; ++side) {
       const i64 off = side ? na : 0, cnt = side ? nb : na;
       if (cnt == 0) continue;
@@ -1807,6 +1844,7 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
                          C.ops->oid_hi + off, C.ops->oid_lo + off, cnt, (u32)off, sts + off, shi + off, slo + off,
                          perm + off, meta);
     }
+    C.tm->end(ST_SEGSORT);
     ComposeMeta hm;
     int rc = read_meta(C, &hm);
     if (rc) return rc;
@@ -1870,10 +1908,10 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
   P.perm = perm;
   P.W = W;
   P.ablate = 0;
-  C.tm->begin(ST_WINDOW);
+  C.tm->begin(ST_WINDOW_G);
   hipLaunchKernelGGL(k_window_g, dim3(W), dim3(WG_NT), 0, st, P);
   HIP_TRY(hipGetLastError());
-  C.tm->end(ST_WINDOW);
+  C.tm->end(ST_WINDOW_G);
   return SMX_OK;
 }
 
@@ -1991,23 +2029,183 @@ static int run_mvprefix(const Ctx& C, const ComposeMeta& hm, const u64* mvpre) {
 // sync (hipGraph-capturable).  counts[0] < -1 afterwards asks for
 // smx_compose_finish: -2 the plan failed, -3 moves with a None value need their
 // prefix fix-up.
+// evs != nullptr (graph capture): the stage events stay with the graph, which records
+// them again on every replay, instead of going to the pending list.
+static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* ws, const Layout& L,
+                         hipStream_t st, bool timed, std::vector<PendingEv>* evs = nullptr) {
+  const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
+  StageTimer tm(st, timed);
+  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
+  int rc;
+  if ((rc = run_presorted(C, knob("SMX_WIN_TGT", WIN_TGT)))) return rc;
+  if (!knob("SMX_ABLATE", 0) && (rc = launch_tail(C))) return rc;  // SMX_ABLATE (diagnostic builds): window only
+  if (evs) {
+    evs->swap(tm.done);
+    return SMX_OK;
+  }
+  tm.flush();
+  return SMX_OK;
+}
+
+// The asynchronous part of a merge is ~25 launches whose arguments depend only on the
+// sizes and the buffers, never on the data: on a (non-null) stream, the second merge
+// with the same (stream, ops, outputs, workspace) captures it into a HIP graph that
+// this and later merges replay -- one launch instead of ~25 (the host launch cost the
+// per-merge sync would otherwise expose; a one-off merge never pays for a capture).
+// Not inside a caller's own capture.  With the stage timers on, the graph records its
+// stage events on every replay and they are read before the next one.
+#ifndef SMX_GRAPH
+#define SMX_GRAPH 1
+#endif
+#define GRAPH_CACHE 8
+struct GraphEntry {
+  hipStream_t st = nullptr;
+  int dev = -1;
+  bool timed = false;
+  smx_ops ops{};
+  smx_compose_out out{};
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  hipGraphExec_t exec = nullptr;
+  hipGraph_t graph = nullptr;  // kept while exec lives: on this ROCm an exec replays
+                               // node parameters its graph owns (destroying the graph
+                               // after instantiation corrupted the later replays)
+  u64 used = 0;
+  std::vector<PendingEv> evs;  // timed graphs: the stage events every replay records
+  bool unresolved = false;     // a replay's stage times are not accumulated yet
+  bool nograph = false;        // capturing this key failed: enqueue directly
+};
+static std::mutex g_graph_mu;  // (taken before g_prof_mu, never the other way)
+static GraphEntry g_graph[GRAPH_CACHE];
+static u64 g_graph_tick = 0;
+
+// Accumulates the stage times of the entry's last replay (waits for it).
+static void graph_resolve_locked(GraphEntry& e) {
+  if (!e.unresolved) return;
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  for (auto& p : e.evs) {
+    (void)hipEventSynchronize(p.b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    g_stage_ms[p.stage] += ms;
+    g_stage_calls[p.stage] += 1;
+  }
+  e.unresolved = false;
+}
+
+static void graph_release_locked(GraphEntry& e) {
+  if (e.exec) {
+    (void)hipStreamSynchronize(e.st);  // its last replay finishes first
+    graph_resolve_locked(e);
+    (void)hipGraphExecDestroy(e.exec);
+    if (e.graph) (void)hipGraphDestroy(e.graph);
+    for (auto& p : e.evs) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+  }
+  e = GraphEntry{};
+}
+
+static void graphs_resolve_all() {
+  std::lock_guard<std::mutex> g(g_graph_mu);
+  for (auto& e : g_graph) graph_resolve_locked(e);
+}
+
+static bool graph_key_eq(const GraphEntry& g, hipStream_t st, int dev, bool timed, const smx_ops* ops,
+                         const smx_compose_out* out, void* ws, size_t ws_bytes) {
+  return g.used && g.st == st && g.dev == dev && g.timed == timed && g.ws == ws && g.ws_bytes == ws_bytes &&
+         std::memcmp(&g.ops, ops, sizeof(smx_ops)) == 0 && std::memcmp(&g.out, out, sizeof(smx_compose_out)) == 0;
+}
+
+static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
+                               const Layout& L, hipStream_t st, bool timed, bool* done) {
+  *done = false;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(st, &cs));
+  if (cs != hipStreamCaptureStatusNone) return SMX_OK;  // the caller is capturing: plain enqueue
+  std::lock_guard<std::mutex> g(g_graph_mu);  // (per-entry state: held through the launch)
+  GraphEntry* ent = nullptr;
+  for (auto& e : g_graph)
+    if (graph_key_eq(e, st, dev, timed, ops, out, ws, ws_bytes)) ent = &e;
+  if (!ent) {  // first sight of this key: remember it, enqueue directly
+    ent = &g_graph[0];
+    for (auto& e : g_graph)
+      if (!e.used || (ent->used && e.used < ent->used)) ent = &e;
+    graph_release_locked(*ent);  // the least recently used one, if the cache is full
+    ent->st = st;
+    ent->dev = dev;
+    ent->timed = timed;
+    ent->ops = *ops;
+    ent->out = *out;
+    ent->ws = ws;
+    ent->ws_bytes = ws_bytes;
+    ent->used = ++g_graph_tick;
+    return SMX_OK;
+  }
+  if (ent->nograph) return SMX_OK;
+  if (!ent->exec) {  // seen before: capture
+    if (n_side_needed(ops)) {  // the table scatter's side stream exists before the capture
+      SideStream* S = nullptr;
+      int rc = side_stream(st, &S);
+      if (rc) return rc;
+    }
+    hipGraph_t graph = nullptr;
+    std::vector<PendingEv> evs;
+    if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+      (void)hipGetLastError();
+      ent->nograph = true;  // a graph is an optimisation only: the plain path runs
+      return SMX_OK;
+    }
+    const int rc = enqueue_async(ops, out, ws, L, st, timed, &evs);
+    const hipError_t ce = hipStreamEndCapture(st, &graph);
+    hipGraphExec_t exec = nullptr;
+    hipError_t ie = hipErrorUnknown;
+    if (!rc && ce == hipSuccess && graph) ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    if (rc || ce != hipSuccess || ie != hipSuccess) {
+      if (exec) (void)hipGraphExecDestroy(exec);
+      if (graph) (void)hipGraphDestroy(graph);
+      for (auto& p : evs) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+      }
+      if (rc) return rc;
+      (void)hipGetLastError();
+      ent->nograph = true;  // a graph is an optimisation only: the plain path runs
+      return SMX_OK;
+    }
+    ent->exec = exec;
+    ent->graph = graph;
+    ent->evs.swap(evs);
+  }
+  graph_resolve_locked(*ent);  // the previous replay's stage times, before they are re-recorded
+  ent->used = ++g_graph_tick;
+  HIP_TRY(hipGraphLaunch(ent->exec, st));
+  ent->unresolved = timed;
+  *done = true;
+  return SMX_OK;
+}
+
 static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
                               hipStream_t st) {
   Layout L{};
   int rc = check_args(ops, out, ws, ws_bytes, &L);
   if (rc) return rc;
-  const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
+  const i64 n = ops->n_a + ops->n_b;
   g_plan = SMX_PLAN_PRESORTED;
   if (n == 0) {
     HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
     return SMX_OK;
   }
-  StageTimer tm(st, profiling_on() != 0);
-  Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
-  if ((rc = run_presorted(C, knob("SMX_WIN_TGT", WIN_TGT)))) return rc;
-  if (!knob("SMX_ABLATE", 0) && (rc = launch_tail(C))) return rc;  // SMX_ABLATE (diagnostic builds): window only
-  tm.flush();
-  return SMX_OK;
+  const bool timed = profiling_on() != 0;
+  if (SMX_GRAPH && st != nullptr && !knob("SMX_NO_GRAPH", 0)) {
+    bool done = false;
+    if ((rc = compose_async_graph(ops, out, ws, ws_bytes, L, st, timed, &done))) return rc;
+    if (done) return SMX_OK;
+  }
+  return enqueue_async(ops, out, ws, L, st, timed);
 }
 
 // smx_compose_finish: one host sync; runs whatever the asynchronous part left
@@ -2249,6 +2447,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
 extern "C" int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const smx_compose_out* out,
                               void* workspace, size_t workspace_bytes, void* stream, int step) {
   if (!ops) return set_err(SMX_E_ARG, "null ops");
+  (void)hipGetLastError();  // an earlier call's error (any library's) is not this call's
   try {
     return shard_impl(ops, shard, out, workspace, workspace_bytes, (hipStream_t)stream, step);
   } catch (const std::exception& e) {
@@ -2259,6 +2458,7 @@ extern "C" int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const 
 extern "C" int smx_compose_async(const smx_ops* ops, const smx_compose_out* out, void* workspace,
                                  size_t workspace_bytes, void* stream) {
   if (!ops) return set_err(SMX_E_ARG, "null ops");
+  (void)hipGetLastError();  // an earlier call's error (any library's) is not this call's
   try {
     return compose_async_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream);
   } catch (const std::exception& e) {
@@ -2269,6 +2469,7 @@ extern "C" int smx_compose_async(const smx_ops* ops, const smx_compose_out* out,
 extern "C" int smx_compose_finish(const smx_ops* ops, const smx_compose_out* out, void* workspace,
                                   size_t workspace_bytes, void* stream) {
   if (!ops) return set_err(SMX_E_ARG, "null ops");
+  (void)hipGetLastError();  // an earlier call's error (any library's) is not this call's
   try {
     return compose_finish_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream);
   } catch (const std::exception& e) {
@@ -2291,6 +2492,7 @@ extern "C" int smx_set_profiling(int enabled) {
 }
 
 extern "C" int smx_reset_stage_times(void) {
+  graphs_resolve_all();
   std::lock_guard<std::mutex> g(g_prof_mu);
   resolve_pending_locked();
   for (int i = 0; i < ST_N; ++i) {
@@ -2301,6 +2503,7 @@ extern "C" int smx_reset_stage_times(void) {
 }
 
 extern "C" int smx_stage_times(double* ms, int64_t* calls, int cap) {
+  graphs_resolve_all();
   std::lock_guard<std::mutex> g(g_prof_mu);
   resolve_pending_locked();
   for (int i = 0; i < ST_N && i < cap; ++i) {

@@ -325,11 +325,6 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
                   // bit2 no key order, bit3 load only
 #endif
 
-__device__ __forceinline__ void wave_lds_sync() {  // LDS writes of this wave visible to its lanes
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // v from lane ^ lm (lm a constant after unrolling): DPP for 1, 2, 3, 7, 15, a swizzle
 // within 32 lanes for 4, 8, 16, 31, a permute otherwise.
@@ -962,5 +957,6 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
 extern "C" int smx_rga_replay(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, size_t wsb,
                               void* stream) {
   if (!ops) return SMX_E_ARG;
+  (void)hipGetLastError();  // an earlier call's error (any library's) is not this call's
   return rga_impl(ops, out, ws, wsb, (hipStream_t)stream);
 }

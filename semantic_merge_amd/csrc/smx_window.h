@@ -230,6 +230,9 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_BUCKET
 #define WF_BUCKET 1  // step 5 by interpolation buckets (0: counting rank over each group)
 #endif
+#ifndef WF_BK16
+#define WF_BK16 1    // bucket-ordered 16-bit key prefixes for the rank loop (window 1.329 -> 1.286 ms, profiles/r03_e/ab.txt)
+#endif
 #ifdef WF_WPE
 #define WF_BOUNDS __launch_bounds__(WF_NT) __attribute__((amdgpu_waves_per_eu(WF_WPE, WF_WPE)))
 #else
@@ -572,10 +575,19 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   };
   const u64 le_mask = lanemask_lt() | (1ull << lane);
 #if WF_BUCKET
+  bool btie = false;  // two equal 32-bit keys in one group (the exact re-rank below)
+#endif
+#if WF_BUCKET
   // interpolation buckets over slot space: slot p of group [gs, ge) goes to bucket
   // gs + (ge - gs) * key / 2^32 (one op per bucket on random ids); 16-bit counters,
   // two per word, in the upper half of sts (free until step 7)
   u32* bcnt = reinterpret_cast<u32*>(sts) + WF_CAP;
+#if WF_BK16
+  // the top 16 bits of each key in bucket order (the last quarter of sts): the rank
+  // loop compares them without the slot -> key chain, the full key only on a tie
+  u16* bk16 = reinterpret_cast<u16*>(reinterpret_cast<u32*>(sts) + WF_CAP + WF_CAP / 2);
+  u32 own_r[WF_ITEMS];
+#endif
   for (int i = t; i < WF_CAP / 2; i += WF_NT) bcnt[i] = 0u;
   __syncthreads();
   u32 bk_r[WF_ITEMS];
@@ -643,7 +655,6 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     sl[r] = (u16)p;  // sl now maps rank -> slot
   }
 #if WF_BUCKET
-  bool btie = false;  // two equal 32-bit keys in one group (the exact re-rank below)
   {
     __syncthreads();
     // exclusive scan of the counters, 4 per thread (2 words)
@@ -663,6 +674,10 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       const u32 sh = 16 * (b & 1);
       const u32 old = atomicAdd(&bcnt[b >> 1], 1u << sh);
       sl[(old >> sh) & 0xffffu] = (u16)((WF_NT * j) / WAVE * WAVE + wv * WAVE + lane);
+#if WF_BK16
+      own_r[j] = (old >> sh) & 0xffffu;
+      bk16[own_r[j]] = (u16)(kp_r[j] >> 16);
+#endif
     }
     __syncthreads();
     // rank inside the bucket on the 32-bit key
@@ -676,11 +691,27 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       const u32 lo = b ? (bcnt[(b - 1) >> 1] >> (16 * ((b - 1) & 1))) & 0xffffu : 0u;
       const u32 kp = kp_r[j];
       u32 c = 0, eq = 0;
+#if WF_BK16
+      const u32 k16 = kp >> 16, own = own_r[j];
+      eq = 1;
+      for (u32 q = lo; q < e; ++q) {
+        const u32 x = bk16[q];
+        if (q == own) continue;
+        if (x != k16) {
+          c += x < k16;
+        } else {  // equal top halves: the full keys (rare)
+          const u32 k = pkey[sl[q]];
+          c += k < kp;
+          eq += k == kp;
+        }
+      }
+#else
       for (u32 q = lo; q < e; ++q) {
         const u32 k = pkey[sl[q]];
         c += k < kp;
         eq += k == kp;
       }
+#endif
       btie |= eq > 1;
       rr[j] = (int)(lo + c);
     }

@@ -138,3 +138,46 @@ def test_two_threads_compose_concurrently():
             ref = oracle.compose(soas[t][k])
             for name, g, r in zip(("order", "addr", "file", "ctx", "conflicts"), results[(t, k)], ref):
                 assert np.array_equal(g, r), f"thread {t} merge {k}: {name}"
+
+
+def test_graph_replay_reads_current_inputs():
+    """smx_compose on a non-null stream replays a HIP graph from the second merge with the
+    same buffers on: every replay recomputes from the inputs as they are at launch --
+    new data in the same buffers (same sizes) gives that data's composition."""
+    import torch
+    spec = synth.LiftSpec(600_000, 4_000, 31)
+    soas = [synth.lift_soa(synth.lift_logs(synth.LiftSpec(**{**spec.__dict__, "seed": sd}))) for sd in (31, 32, 33)]
+    assert all(x.n == soas[0].n and x.n_a == soas[0].n_a for x in soas)
+    dc = _lib.DeviceCompose(soas[0])
+    s = torch.cuda.Stream()
+    for rep, soa in enumerate(soas + soas[:1]):
+        for name, col, dt in (("kind", soa.kind, np.uint8), ("ts", soa.ts, np.int64), ("hi", soa.oid_hi, np.int64),
+                              ("lo", soa.oid_lo, np.int64), ("sym", soa.sym, np.int32), ("v0", soa.v0, np.int32),
+                              ("v1", soa.v1, np.int32)):
+            getattr(dc, name).copy_(torch.from_numpy(np.ascontiguousarray(col).view(dt)))
+        torch.cuda.synchronize()
+        dc.run(s)
+        s.synchronize()
+        _check(dc, soa, f"merge {rep}")
+
+
+def test_graph_replay_with_stage_timers():
+    """With the stage timers on, replays record their stage events and the library reads
+    them before the next replay: one window and one emit time per merge."""
+    import torch
+    soa = _lift(300_000, 3_000, 34)
+    dc = _lib.DeviceCompose(soa)
+    s = torch.cuda.Stream()
+    L = _lib.lib()
+    L.smx_reset_stage_times()
+    L.smx_set_profiling(1)
+    try:
+        for _ in range(4):
+            dc.run(s)
+        s.synchronize()
+    finally:
+        L.smx_set_profiling(0)
+    st = _lib.stage_times()
+    assert st["window"][1] == 4 and st["emit"][1] == 4, st
+    assert all(ms > 0 for ms, c in st.values() if c)
+    _check(dc, soa, "timed replays")
