@@ -2029,20 +2029,14 @@ static int run_mvprefix(const Ctx& C, const ComposeMeta& hm, const u64* mvpre) {
 // sync (hipGraph-capturable).  counts[0] < -1 afterwards asks for
 // smx_compose_finish: -2 the plan failed, -3 moves with a None value need their
 // prefix fix-up.
-// evs != nullptr (graph capture): the stage events stay with the graph, which records
-// them again on every replay, instead of going to the pending list.
 static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* ws, const Layout& L,
-                         hipStream_t st, bool timed, std::vector<PendingEv>* evs = nullptr) {
+                         hipStream_t st, bool timed) {
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
   StageTimer tm(st, timed);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
   int rc;
   if ((rc = run_presorted(C, knob("SMX_WIN_TGT", WIN_TGT)))) return rc;
   if (!knob("SMX_ABLATE", 0) && (rc = launch_tail(C))) return rc;  // SMX_ABLATE (diagnostic builds): window only
-  if (evs) {
-    evs->swap(tm.done);
-    return SMX_OK;
-  }
   tm.flush();
   return SMX_OK;
 }
@@ -2052,8 +2046,9 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
 // with the same (stream, ops, outputs, workspace) captures it into a HIP graph that
 // this and later merges replay -- one launch instead of ~25 (the host launch cost the
 // per-merge sync would otherwise expose; a one-off merge never pays for a capture).
-// Not inside a caller's own capture.  With the stage timers on, the graph records its
-// stage events on every replay and they are read before the next one.
+// Not inside a caller's own capture, and not while the stage timers are on: event
+// timestamps recorded by a replayed graph read back as 0 ms on this ROCm
+// (profiles/r03_i/bench.json: every stage 0.0), so timed merges enqueue directly.
 #ifndef SMX_GRAPH
 #define SMX_GRAPH 1
 #endif
@@ -2061,7 +2056,6 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
 struct GraphEntry {
   hipStream_t st = nullptr;
   int dev = -1;
-  bool timed = false;
   smx_ops ops{};
   smx_compose_out out{};
   void* ws = nullptr;
@@ -2071,55 +2065,29 @@ struct GraphEntry {
                                // node parameters its graph owns (destroying the graph
                                // after instantiation corrupted the later replays)
   u64 used = 0;
-  std::vector<PendingEv> evs;  // timed graphs: the stage events every replay records
-  bool unresolved = false;     // a replay's stage times are not accumulated yet
   bool nograph = false;        // capturing this key failed: enqueue directly
 };
-static std::mutex g_graph_mu;  // (taken before g_prof_mu, never the other way)
+static std::mutex g_graph_mu;
 static GraphEntry g_graph[GRAPH_CACHE];
 static u64 g_graph_tick = 0;
-
-// Accumulates the stage times of the entry's last replay (waits for it).
-static void graph_resolve_locked(GraphEntry& e) {
-  if (!e.unresolved) return;
-  std::lock_guard<std::mutex> g(g_prof_mu);
-  for (auto& p : e.evs) {
-    (void)hipEventSynchronize(p.b);
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, p.a, p.b);
-    g_stage_ms[p.stage] += ms;
-    g_stage_calls[p.stage] += 1;
-  }
-  e.unresolved = false;
-}
 
 static void graph_release_locked(GraphEntry& e) {
   if (e.exec) {
     (void)hipStreamSynchronize(e.st);  // its last replay finishes first
-    graph_resolve_locked(e);
     (void)hipGraphExecDestroy(e.exec);
     if (e.graph) (void)hipGraphDestroy(e.graph);
-    for (auto& p : e.evs) {
-      (void)hipEventDestroy(p.a);
-      (void)hipEventDestroy(p.b);
-    }
   }
   e = GraphEntry{};
 }
 
-static void graphs_resolve_all() {
-  std::lock_guard<std::mutex> g(g_graph_mu);
-  for (auto& e : g_graph) graph_resolve_locked(e);
-}
-
-static bool graph_key_eq(const GraphEntry& g, hipStream_t st, int dev, bool timed, const smx_ops* ops,
+static bool graph_key_eq(const GraphEntry& g, hipStream_t st, int dev, const smx_ops* ops,
                          const smx_compose_out* out, void* ws, size_t ws_bytes) {
-  return g.used && g.st == st && g.dev == dev && g.timed == timed && g.ws == ws && g.ws_bytes == ws_bytes &&
+  return g.used && g.st == st && g.dev == dev && g.ws == ws && g.ws_bytes == ws_bytes &&
          std::memcmp(&g.ops, ops, sizeof(smx_ops)) == 0 && std::memcmp(&g.out, out, sizeof(smx_compose_out)) == 0;
 }
 
 static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
-                               const Layout& L, hipStream_t st, bool timed, bool* done) {
+                               const Layout& L, hipStream_t st, bool* done) {
   *done = false;
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
@@ -2129,7 +2097,7 @@ static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, v
   std::lock_guard<std::mutex> g(g_graph_mu);  // (per-entry state: held through the launch)
   GraphEntry* ent = nullptr;
   for (auto& e : g_graph)
-    if (graph_key_eq(e, st, dev, timed, ops, out, ws, ws_bytes)) ent = &e;
+    if (graph_key_eq(e, st, dev, ops, out, ws, ws_bytes)) ent = &e;
   if (!ent) {  // first sight of this key: remember it, enqueue directly
     ent = &g_graph[0];
     for (auto& e : g_graph)
@@ -2137,7 +2105,6 @@ static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, v
     graph_release_locked(*ent);  // the least recently used one, if the cache is full
     ent->st = st;
     ent->dev = dev;
-    ent->timed = timed;
     ent->ops = *ops;
     ent->out = *out;
     ent->ws = ws;
@@ -2153,13 +2120,12 @@ static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, v
       if (rc) return rc;
     }
     hipGraph_t graph = nullptr;
-    std::vector<PendingEv> evs;
     if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
       (void)hipGetLastError();
       ent->nograph = true;  // a graph is an optimisation only: the plain path runs
       return SMX_OK;
     }
-    const int rc = enqueue_async(ops, out, ws, L, st, timed, &evs);
+    const int rc = enqueue_async(ops, out, ws, L, st, false);
     const hipError_t ce = hipStreamEndCapture(st, &graph);
     hipGraphExec_t exec = nullptr;
     hipError_t ie = hipErrorUnknown;
@@ -2167,10 +2133,6 @@ static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, v
     if (rc || ce != hipSuccess || ie != hipSuccess) {
       if (exec) (void)hipGraphExecDestroy(exec);
       if (graph) (void)hipGraphDestroy(graph);
-      for (auto& p : evs) {
-        (void)hipEventDestroy(p.a);
-        (void)hipEventDestroy(p.b);
-      }
       if (rc) return rc;
       (void)hipGetLastError();
       ent->nograph = true;  // a graph is an optimisation only: the plain path runs
@@ -2178,12 +2140,9 @@ static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, v
     }
     ent->exec = exec;
     ent->graph = graph;
-    ent->evs.swap(evs);
   }
-  graph_resolve_locked(*ent);  // the previous replay's stage times, before they are re-recorded
   ent->used = ++g_graph_tick;
   HIP_TRY(hipGraphLaunch(ent->exec, st));
-  ent->unresolved = timed;
   *done = true;
   return SMX_OK;
 }
@@ -2200,9 +2159,9 @@ static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, vo
     return SMX_OK;
   }
   const bool timed = profiling_on() != 0;
-  if (SMX_GRAPH && st != nullptr && !knob("SMX_NO_GRAPH", 0)) {
+  if (SMX_GRAPH && st != nullptr && !timed && !knob("SMX_NO_GRAPH", 0)) {
     bool done = false;
-    if ((rc = compose_async_graph(ops, out, ws, ws_bytes, L, st, timed, &done))) return rc;
+    if ((rc = compose_async_graph(ops, out, ws, ws_bytes, L, st, &done))) return rc;
     if (done) return SMX_OK;
   }
   return enqueue_async(ops, out, ws, L, st, timed);
@@ -2492,7 +2451,6 @@ extern "C" int smx_set_profiling(int enabled) {
 }
 
 extern "C" int smx_reset_stage_times(void) {
-  graphs_resolve_all();
   std::lock_guard<std::mutex> g(g_prof_mu);
   resolve_pending_locked();
   for (int i = 0; i < ST_N; ++i) {
@@ -2503,7 +2461,6 @@ extern "C" int smx_reset_stage_times(void) {
 }
 
 extern "C" int smx_stage_times(double* ms, int64_t* calls, int cap) {
-  graphs_resolve_all();
   std::lock_guard<std::mutex> g(g_prof_mu);
   resolve_pending_locked();
   for (int i = 0; i < ST_N && i < cap; ++i) {

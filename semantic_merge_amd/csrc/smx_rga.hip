@@ -271,7 +271,14 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
 
 // lstart[l] = first sorted position of list l (an empty list starts where the next
 // one does); one pass over the sorted list ids.
-__global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* __restrict__ lstart) {
+// Also zeroes the survivor sums of 256-list chunks (csum, RGA_CS_MAX words), which the
+// list kernels fill and k_rga_out reads.
+#define RGA_CS_LISTS 256                   // lists per survivor-sum chunk
+#define RGA_CS_MAX 256                     // chunks (k_rga_out: one uint4 per lane)
+#define RGA_FUSED_MAX (RGA_CS_LISTS * RGA_CS_MAX)  // lists up to which k_rga_out finds its own offsets
+__global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* __restrict__ lstart,
+                             u32* __restrict__ csum) {
+  if (blockIdx.x == 0 && threadIdx.x < RGA_CS_MAX) csum[threadIdx.x] = 0u;
   for (i64 j = (i64)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (i64)gridDim.x * BLOCK) {
     const i64 l = keys[j];
     const i64 lp = j ? (i64)keys[j - 1] : -1;
@@ -283,6 +290,13 @@ __global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* _
 
 __device__ __forceinline__ u32 rga_lend(const u32* lstart, u32 l, i64 nl, i64 n) {
   return l + 1 < nl ? lstart[l + 1] : (u32)n;
+}
+
+// A list's survivor count, and its share of its chunk's sum: the RGA_CS_MAX chunk
+// sums sit just before scnt (rga_layout); k_rga_out adds them up to its list's offset.
+__device__ __forceinline__ void rga_put_count(u32* scnt, u32 l, u32 m) {
+  scnt[l] = m;
+  if (l < RGA_FUSED_MAX) atomicAdd(scnt - RGA_CS_MAX + (l / RGA_CS_LISTS), m);  // (more lists: scan_excl)
 }
 
 // Events ia, ib (stream indices) whose record words 0 are equal: the rest of the
@@ -482,7 +496,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
   }
   wave_lds_sync();
   if (RW_ABL & 8) {
-    if (lane == 0) scnt[l] = (u32)S.w0[lane] & 1u;
+    if (lane == 0) rga_put_count(scnt, l, (u32)S.w0[lane] & 1u);
     return;
   }
   const u64 lt = lanemask_lt();
@@ -625,7 +639,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
   } else {
     rw_order<8>(S, src, o, key, pay, m, s0, lane, tmp_v, tmp_s);
   }
-  if (lane == 0) scnt[l] = m;
+  if (lane == 0) rga_put_count(scnt, l, m);
 }
 
 __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave(smx_rga_ops o, const u64* __restrict__ R,
@@ -759,7 +773,7 @@ __device__ void rga_big_list(const smx_rga_ops& o, const u64* __restrict__ R, u3
     tmp_v[s0 + j] = (u32)(w >> 32);
     tmp_s[s0 + j] = ((u32)w & RGA_IDX_MASK) | (G[j] & RGA_TOMB_BIT);
   }
-  if (t == 0) scnt[l] = m;
+  if (t == 0) rga_put_count(scnt, l, m);
 }
 
 __global__ void __launch_bounds__(1024) k_rga_big(smx_rga_ops o, const u64* __restrict__ R,
@@ -771,6 +785,40 @@ __global__ void __launch_bounds__(1024) k_rga_big(smx_rga_ops o, const u64* __re
   for (u32 item = blockIdx.x; item < *ntodo; item += gridDim.x) {
     __syncthreads();
     rga_big_list(o, R, todo[item], lstart, n, nl, bst, gp, tmp_v, tmp_s, scnt, tomb != 0);
+  }
+}
+
+// Per list (one wave each): its output offset = the survivor sums of the earlier chunks
+// + the counts of the chunk's earlier lists (one 16-byte read of each per lane, a wave
+// sum), then its survivors, in list order, to their place in the output.  The last
+// list's wave writes the total.  n_lists <= RGA_FUSED_MAX.
+__global__ void __launch_bounds__(BLOCK) k_rga_out_fused(const u32* __restrict__ tmp_v, const u32* __restrict__ tmp_s,
+                                                        const u32* __restrict__ lstart, const u32* __restrict__ scnt,
+                                                        i64 nl, smx_rga_out out) {
+  const u32 lane = threadIdx.x & (WAVE - 1);
+  const i64 l = (i64)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE;
+  if (l >= nl) return;
+  const u32 c = (u32)l / RGA_CS_LISTS, c0 = c * RGA_CS_LISTS;
+  const uint4 cs = reinterpret_cast<const uint4*>(scnt - RGA_CS_MAX)[lane];
+  const uint4 ls = reinterpret_cast<const uint4*>(scnt + c0)[lane];
+  const u32 q = 4 * lane;
+  u32 part = (q < c ? cs.x : 0u) + (q + 1 < c ? cs.y : 0u) + (q + 2 < c ? cs.z : 0u) + (q + 3 < c ? cs.w : 0u);
+  const u32 r = (u32)l - c0;
+  part += (q < r ? ls.x : 0u) + (q + 1 < r ? ls.y : 0u) + (q + 2 < r ? ls.z : 0u) + (q + 3 < r ? ls.w : 0u);
+  const u32 d = (u32)__builtin_amdgcn_readlane((int)wave_incl_sum_u32(part), WAVE - 1);
+  const u32 s0 = lstart[l], m = scnt[l];
+  for (u32 x = lane; x < m; x += WAVE) {
+    out.out_value[d + x] = __builtin_nontemporal_load(&tmp_v[s0 + x]);
+    const u32 sx = __builtin_nontemporal_load(&tmp_s[s0 + x]);
+    out.out_src[d + x] = (i32)(sx & ~RGA_TOMB_BIT);
+    if (out.out_tomb) out.out_tomb[d + x] = sx & RGA_TOMB_BIT ? 1 : 0;
+  }
+  if (lane == 0) {
+    out.out_offsets[l] = d;
+    if (l == nl - 1) {
+      out.out_offsets[nl] = d + m;
+      out.counts[0] = d + m;
+    }
   }
 }
 
@@ -789,30 +837,6 @@ __global__ void __launch_bounds__(BLOCK) k_rga_out(const u32* __restrict__ tmp_v
     if (out.out_tomb) out.out_tomb[d + x] = sx & RGA_TOMB_BIT ? 1 : 0;
   }
   if (lane == 0) out.out_offsets[l] = d;
-}
-
-// Exclusive scan of the survivor counts in one workgroup (n_lists up to RS_MAX), and
-// the output's total: out_offsets[n_lists] = counts[0] = survivors.
-#define RS_NT 1024
-#define RS_MAX (RS_NT * 64)
-__global__ void __launch_bounds__(RS_NT) k_rga_scnt_scan(const u32* __restrict__ scnt, u32* __restrict__ soff,
-                                                         i64 nl, smx_rga_out out) {
-  __shared__ u32 sh[RS_NT / WAVE + 1];
-  const i64 per = SMX_CEIL_DIV(nl, (i64)RS_NT);
-  const i64 b0 = (i64)threadIdx.x * per, b1 = b0 + per < nl ? b0 + per : nl;
-  u32 sum = 0;
-  for (i64 i = b0; i < b1; ++i) sum += scnt[i];
-  u32 tot;
-  u32 run = block_excl_scan<OpSum, u32, RS_NT / WAVE>(sum, sh, &tot);
-  for (i64 i = b0; i < b1; ++i) {
-    const u32 c = scnt[i];
-    soff[i] = run;
-    run += c;
-  }
-  if (threadIdx.x == 0) {
-    out.out_offsets[nl] = tot;
-    out.counts[0] = tot;
-  }
 }
 
 __global__ void k_rga_fin(const u32* __restrict__ soff_total, i64 n_lists, smx_rga_out out) {
@@ -844,7 +868,9 @@ static RgaLayout rga_layout(i64 n, i64 nl) {
   }
   sz[R_BST] = (size_t)nn;
   sz[R_PART] = SCAN_NB * 8 + 64;  // + error word + totals
-  sz[R_LSTART] = sz[R_SCNT] = sz[R_SOFF] = sz[R_DEF1] = sz[R_DEF2] = (size_t)(nl + 1) * 4;
+  sz[R_LSTART] = sz[R_SOFF] = sz[R_DEF1] = sz[R_DEF2] = (size_t)(nl + 1) * 4;
+  // scnt: RGA_CS_MAX chunk sums, then the counts padded to whole 256-list chunks
+  sz[R_SCNT] = (size_t)(RGA_CS_MAX + SMX_CEIL_DIV(nl + 1, (i64)RGA_CS_LISTS) * RGA_CS_LISTS) * 4;
   RgaLayout L;
   size_t acc = 0;
   for (int i = 0; i < R_N; ++i) {
@@ -890,7 +916,7 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   i32* err = (i32*)(b + L.off[R_PART] + SCAN_NB * 8);
   u32* totals = (u32*)(err + 2);
   u32* lstart = (u32*)(b + L.off[R_LSTART]);
-  u32* scnt = (u32*)(b + L.off[R_SCNT]);
+  u32* scnt = (u32*)(b + L.off[R_SCNT]) + RGA_CS_MAX;  // (the chunk sums before it)
   u32* soff = (u32*)(b + L.off[R_SOFF]);
   u32* def1 = (u32*)(b + L.off[R_DEF1]);
   u32* def2 = (u32*)(b + L.off[R_DEF2]);
@@ -928,7 +954,8 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
         hipLaunchKernelGGL(k_rrec_scatter<false>, dim3(sgrid), dim3(RR_NT), 0, st, o, kbuf[(p - 1) & 1],
                            rbuf[(p - 1) & 1], kbuf[p & 1], rbuf[p & 1], 8 * p, rhist, err, (u32)nblk);
     }
-    hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, kbuf[(npass - 1) & 1], n, nl, lstart);
+    hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, kbuf[(npass - 1) & 1], n, nl, lstart,
+                       scnt - RGA_CS_MAX);
   }
   const int tomb = out->out_tomb != nullptr;
   hipLaunchKernelGGL(k_rga_wave, dim3(SMX_CEIL_DIV(nl, (i64)RW_WAVES)), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n,
@@ -937,14 +964,15 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
                      ndef + 1, tmp_v, tmp_s, scnt, tomb);
   hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
                      tmp_s, scnt, tomb);
-  if (nl <= RS_MAX) {
-    hipLaunchKernelGGL(k_rga_scnt_scan, dim3(1), dim3(RS_NT), 0, st, scnt, soff, nl, *out);
+  if (nl <= RGA_FUSED_MAX) {  // each list's wave finds its own offset
+    hipLaunchKernelGGL(k_rga_out_fused, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE))), dim3(BLOCK), 0, st, tmp_v,
+                       tmp_s, lstart, scnt, nl, *out);
   } else {
     RGA_TRY((scan_excl<OpSum, u32, u32>(scnt, soff, nl, nullptr, part, totals, st)));
+    hipLaunchKernelGGL(k_rga_out, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE))), dim3(BLOCK), 0, st, tmp_v, tmp_s,
+                       lstart, scnt, soff, nl, *out);
+    hipLaunchKernelGGL(k_rga_fin, dim3(1), dim3(1), 0, st, totals, nl, *out);
   }
-  hipLaunchKernelGGL(k_rga_out, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE))), dim3(BLOCK), 0, st, tmp_v, tmp_s, lstart,
-                     scnt, soff, nl, *out);
-  if (nl > RS_MAX) hipLaunchKernelGGL(k_rga_fin, dim3(1), dim3(1), 0, st, totals, nl, *out);
   RGA_TRY(hipGetLastError());
   i32 herr = 0;
   RGA_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));

@@ -60,6 +60,13 @@ __device__ __forceinline__ int rk4(const uint4 x, u32 kp, int m) {
   return (m > 0 && x.x < kp) + (m > 1 && x.y < kp) + (m > 2 && x.z < kp) + (m > 3 && x.w < kp);
 }
 
+// Four consecutive i32 stores as one 16-byte store (4-byte aligned address).
+typedef i32 __attribute__((ext_vector_type(4))) win_v4i;
+typedef win_v4i __attribute__((aligned(4))) win_v4i_a4;
+__device__ __forceinline__ void st4(i32* p, i32 a, i32 b, i32 c, i32 d) {
+  *reinterpret_cast<win_v4i_a4*>(p) = win_v4i{a, b, c, d};
+}
+
 struct WinArgs {
   const u8* kind;
   const u32* sym;
@@ -233,6 +240,12 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_BK16
 #define WF_BK16 1    // bucket-ordered 16-bit key prefixes for the rank loop (window 1.329 -> 1.286 ms, profiles/r03_e/ab.txt)
 #endif
+#ifndef WF_BZ4
+#define WF_BZ4 1     // step 5's bucket counters zeroed in step 4's last phase (one barrier fewer)
+#endif
+#ifndef WF_OUT2
+#define WF_OUT2 0    // steps 7-9: payload staged by final slot (inv), four slots per thread, 16-byte stores
+#endif
 #ifdef WF_WPE
 #define WF_BOUNDS __launch_bounds__(WF_NT) __attribute__((amdgpu_waves_per_eu(WF_WPE, WF_WPE)))
 #else
@@ -241,11 +254,15 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 template <bool DBG, bool MAP>
 __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   __shared__ __attribute__((aligned(16))) u64 sts[WF_CAP];  // element space: timestamps; later slot-space rank keys
-  __shared__ u16 sord[WF_CAP];       // S order (merge), later the final order
+  __shared__ __attribute__((aligned(16))) u16 sord[WF_CAP];  // S order (merge), later the final order
   __shared__ u16 fin[WF_CAP];        // slot -> element, later rename ranks
   __shared__ u16 sl[WF_CAP];         // element -> slot, later rank -> slot, later posl
   __shared__ u8 skind[WF_CAP];
-  __shared__ u8 skS[WF_CAP];         // kinds in S order
+  __shared__ __attribute__((aligned(16))) u8 skS[WF_CAP];  // kinds in S order, later by slot (WF_OUT2)
+#if WF_OUT2
+  __shared__ u16 inv[WF_CAP];        // element -> final slot
+  __shared__ u64 tbase[SMX_N_KINDS]; // T of a kind's slot x = tbase[kind] + x
+#endif
   __shared__ u64 gbits[WF_NCH];       // group-start bits over slots, later candidate ballots
   __shared__ u16 ccnt[WF_NCH][SMX_N_KINDS];
   __shared__ u16 rc[WF_NCH][2];
@@ -510,6 +527,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       const int p = kbase[k] + ccnt[wv + WF_WAVES * j][k] + (mkr[j] >> 8);
       fin[p] = (u16)me[j];
       sl[me[j]] = (u16)p;
+      if (WF_OUT2) skS[p] = (u8)k;  // (skS was read in the prologue, before two barriers)
     }
   }
   __syncthreads();
@@ -524,7 +542,11 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     bool f = false;
     if (p < sz) {
       const int e = fin[p];
+#if WF_OUT2 && !defined(WF_GBS0)
+      f = (p == (int)kbase[skS[p]]) || (sts[fin[p - 1]] != sts[e]);  // (skS: kinds by slot)
+#else
       f = (p == (int)kbase[skind[e]]) || (sts[fin[p - 1]] != sts[e]);
+#endif
     }
     const u64 b = __ballot(f);
     if (lane == 0 && (p >> 6) < WF_NCH) gbits[p >> 6] = b;
@@ -544,6 +566,10 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       sl[e] = 0xffffu;
     }
   }
+#if WF_BUCKET && WF_BZ4
+  // step 5's bucket counters (the upper half of sts: the timestamps are dead)
+  for (int i = t; i < WF_CAP / 2; i += WF_NT) reinterpret_cast<u32*>(sts)[WF_CAP + i] = 0u;
+#endif
   __syncthreads();
   WSTAMP(9);
   WF_EXIT(7);
@@ -588,8 +614,10 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   u16* bk16 = reinterpret_cast<u16*>(reinterpret_cast<u32*>(sts) + WF_CAP + WF_CAP / 2);
   u32 own_r[WF_ITEMS];
 #endif
+#if !WF_BZ4
   for (int i = t; i < WF_CAP / 2; i += WF_NT) bcnt[i] = 0u;
   __syncthreads();
+#endif
   u32 bk_r[WF_ITEMS];
   u32 kp_r[WF_ITEMS];
 #pragma unroll
@@ -653,6 +681,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     }
     sord[r] = fin[p];
     sl[r] = (u16)p;  // sl now maps rank -> slot
+#if WF_OUT2
+    inv[fin[p]] = (u16)r;
+#endif
   }
 #if WF_BUCKET
   {
@@ -720,12 +751,20 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     for (int j = 0; j < WF_ITEMS; ++j) {
       if (rr[j] < 0) continue;
       const int p = (WF_NT * j) / WAVE * WAVE + wv * WAVE + lane;
-      sord[rr[j]] = fin[p];
+      const int e = fin[p];
+      sord[rr[j]] = (u16)e;
       sl[rr[j]] = (u16)p;  // sl now maps rank -> slot
+#if WF_OUT2
+      inv[e] = (u16)rr[j];
+#endif
     }
   }
 #endif
   __syncthreads();
+#if defined(WF_INVPASS) && WF_OUT2
+  for (int r = t; r < sz; r += WF_NT) inv[sord[r]] = (u16)r;
+  __syncthreads();
+#endif
   WSTAMP(10);
   WF_EXIT(8);
   // 6. renames: rank among the window's renames of the same branch (final order).
@@ -788,7 +827,13 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       sl[gs + c] = (u16)p;
     }
     __syncthreads();
-    for (int r = t; r < sz; r += WF_NT) sord[r] = fin[sl[r]];
+    for (int r = t; r < sz; r += WF_NT) {
+      const int e = fin[sl[r]];
+      sord[r] = (u16)e;
+#if WF_OUT2
+      inv[e] = (u16)r;
+#endif
+    }
     __syncthreads();
     rename_ranks(true);
     __syncthreads();
@@ -824,6 +869,20 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   u32* st_a = (u32*)sts;             // [WF_CAP] sym | flags
   i32* st_b = (i32*)sts + WF_CAP;   // [WF_CAP] v0, then v1
   u16* posl = sl;
+#if WF_OUT2
+  // by final slot: each element's owner stores its payload at inv[element]
+  int xi[WF_ITEMS];
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i) {
+    const int e = t + WF_NT * i;
+    xi[i] = e < sz ? inv[e] : WF_CAP;
+    if (e < sz) {
+      st_a[xi[i]] = sym_r[i];
+      st_b[xi[i]] = v0_r[i];
+    }
+  }
+  if (t < SMX_N_KINDS) tbase[t] = base[t] + woffk[t] - kbase[t];
+#else
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
@@ -832,6 +891,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       st_b[e] = v0_r[i];
     }
   }
+#endif
   const int cntA = wtot[0], cntB = wtot[1];
   for (int x = t; x < RN; x += WF_NT) {
     const int e = sord[R0 + x];
@@ -854,8 +914,12 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
         *own = rc[x >> 6][*s] + rown[x];
       },
       [&](int x) -> uint2 {
+#if WF_OUT2
+        return make_uint2(st_a[R0 + x] & SYM_MASK, (u32)st_b[R0 + x]);
+#else
         const int e = sord[R0 + x];
         return make_uint2(st_a[e] & SYM_MASK, (u32)st_b[e]);
+#endif
       });
   WSTAMP(14);
   WF_EXIT(11);
@@ -864,6 +928,92 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   //    each kind: coalesced)
   const u64 nall = (u64)(P.na + P.nb);
   const u64 nmv = base[KREN];
+#if WF_OUT2
+  // four consecutive slots per thread (WF_CAP = 4 * WF_NT): one LDS read of each array,
+  // and when the four share a kind (kinds are contiguous slot ranges) one 16-byte
+  // store per output array
+  static_assert(WF_CAP == 4 * WF_NT, "four slots per thread");
+  const int x0 = 4 * t;
+  const int m4 = sz - x0 < 4 ? sz - x0 : 4;
+  u32 k4[4];
+  u64 T4[4];
+  i32 j4[4];
+  bool uni = false;
+  if (m4 > 0) {
+    const uint2 ew = *reinterpret_cast<const uint2*>(&sord[x0]);
+    const u32 kw = *reinterpret_cast<const u32*>(&skS[x0]);
+    const uint4 av = *reinterpret_cast<const uint4*>(&st_a[x0]);
+    const uint4 bv = *reinterpret_cast<const uint4*>(&st_b[x0]);
+    const u32 ee[4] = {ew.x & 0xffffu, ew.x >> 16, ew.y & 0xffffu, ew.y >> 16};
+    const u32 aa[4] = {av.x, av.y, av.z, av.w};
+    const i32 bb[4] = {(i32)bv.x, (i32)bv.y, (i32)bv.z, (i32)bv.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      k4[u] = (kw >> (8 * u)) & 0xffu;
+      k4[u] = k4[u] < SMX_N_KINDS ? k4[u] : 0u;  // (slots past sz)
+      T4[u] = tbase[k4[u]] + (u64)(x0 + u);
+      j4[u] = (i32)(ee[u] < (u32)na ? a0 + ee[u] : bpos + ee[u]);
+    }
+    uni = m4 == 4 && k4[3] == k4[0] && T4[0] + 3 < nall;
+    auto gsrc = [&](i32 j) -> i32 {
+      return MAP ? P.src_map[j] : (j < P.na ? (i32)(P.src_a + j) : (i32)(P.src_b + (j - P.na)));
+    };
+    if (uni) {
+      const u64 T = T4[0];
+      if (k4[0] == KMOVE) {
+        st4(P.out_order + T, gsrc(j4[0]), gsrc(j4[1]), gsrc(j4[2]), gsrc(j4[3]));
+        st4(P.out_addr + T, bb[0], bb[1], bb[2], bb[3]);
+        st4(P.out_ctx + T, -1, -1, -1, -1);
+        st4((i32*)P.msym + T, (i32)aa[0], (i32)aa[1], (i32)aa[2], (i32)aa[3]);
+      } else {
+        st4(P.tsrc + (T - nmv), j4[0], j4[1], j4[2], j4[3]);
+        st4((i32*)P.tsym + (T - nmv), (i32)(aa[0] & SYM_MASK), (i32)(aa[1] & SYM_MASK), (i32)(aa[2] & SYM_MASK),
+            (i32)(aa[3] & SYM_MASK));
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const u64 T = T4[u];
+        if (u >= m4 || T >= nall) continue;  // (T >= nall: only a failed, discarded plan)
+        if (k4[u] == KMOVE) {
+          P.out_order[T] = gsrc(j4[u]);
+          P.out_addr[T] = bb[u];
+          P.out_ctx[T] = -1;
+          P.msym[T] = aa[u];
+        } else {
+          P.tsrc[T - nmv] = j4[u];
+          P.tsym[T - nmv] = aa[u] & SYM_MASK;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  WSTAMP(15);
+  WF_EXIT(12);
+  // round 2: v1 -> the move's newFile, the rename's chain value
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i)
+    if (xi[i] < WF_CAP) st_b[xi[i]] = v1_r[i];
+  __syncthreads();
+  if (m4 > 0 && (k4[0] <= KREN || k4[m4 - 1] <= KREN)) {
+    const uint4 bv = *reinterpret_cast<const uint4*>(&st_b[x0]);
+    const i32 bb[4] = {(i32)bv.x, (i32)bv.y, (i32)bv.z, (i32)bv.w};
+    if (uni) {
+      const u64 T = T4[0];
+      st4(k4[0] == KMOVE ? P.out_file + T : P.Rstr + (T - nmv), bb[0], bb[1], bb[2], bb[3]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const u64 T = T4[u];
+        if (u >= m4 || T >= nall || k4[u] > KREN) continue;
+        if (k4[u] == KMOVE) P.out_file[T] = bb[u];
+        else P.Rstr[T - nmv] = bb[u];
+      }
+    }
+  }
+#else
+  // 9. T-ordered records in final order (consecutive lanes -> consecutive T inside
+  //    each kind: coalesced)
   for (int x = t; x < sz; x += WF_NT) {
     const int e = sord[x];
     const u32 k = skind[e];
@@ -900,6 +1050,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     if (k == KMOVE) P.out_file[T] = st_b[e];
     else P.Rstr[T - nmv] = st_b[e];
   }
+#endif
   if (DBG) {
     __syncthreads();
     WSTAMP(16);

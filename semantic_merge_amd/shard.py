@@ -48,6 +48,7 @@ S_OPEN, S_AHEAD, S_D, S_NCONF, S_NSKIP, S_OVER, S_WIDTH = 22, 23, 24, 25, 26, 27
 N_KINDS = 18
 SUM = _abi.SHARD_SUMMARY
 I64_MIN = -(2 ** 63)
+RH = 32  # keys from each end of each branch slice in the range info (host-side cuts)
 
 # packed exchange record: ts, hi, lo (8 B each), sym, v0, v1 (4 B), kind (1 B) = 37 B;
 # the sample-sort exchange appends the op's global source index (4 B) = 41 B
@@ -239,6 +240,8 @@ class ShardedCompose:
         self._signed = torch.tensor([int(x) for x in self._ts_signed], dtype=torch.int64, device=dv)
         self._bind_key = None
         self._halo_key = None
+        self._info_key = None
+        self.host_cut_plans = 0  # exchanges planned from the gathered head / tail keys alone
 
     def _alloc(self, hd: int, a, b) -> None:
         """Field buffers [hd | A slice | 2 hd | B slice | hd]; a, b: BranchSlices or the
@@ -263,23 +266,62 @@ class ShardedCompose:
         return self.buf[f][self._oa: self._oa + self.na_s] if br == 0 else \
             self.buf[f][self._ob: self._ob + self.nb_s]
 
+    def _info_index(self):
+        """Buffer positions of the range info's keys: the first and last key of each
+        branch slice, then RH keys from the head and RH from the tail of each (the tail
+        right-aligned; short slices repeat their first position as padding)."""
+        ends, edges = [], []
+        for o, n in ((self._oa, self.na_s), (self._ob, self.nb_s)):
+            ends += [o, o + n - 1] if n else [0, 0]
+            h = min(RH, n)
+            pad = [o if n else 0]
+            edges += [o + i for i in range(h)] + pad * (RH - h)
+            edges += pad * (RH - h) + [o + n - h + i for i in range(h)]
+        return self.torch.tensor(ends + edges, dtype=self.torch.int64, device=self.dev)
+
     def _range_info(self):
-        """Device int64 [9]: this rank's slice sizes, first / last key of each slice
-        (u64 order as int64), whether the slices are ordered, and per branch whether
-        every timestamp is below 2^63 (the cut search below runs on the stored words)."""
+        """Device int64 [9 + 4 RH]: this rank's slice sizes, first / last key of each
+        slice (u64 order as int64), whether the slices are ordered, per branch whether
+        every timestamp is below 2^63 (the device cut search runs on the stored words),
+        then the RH head and RH tail keys of each slice (host-side cuts)."""
         torch = self.torch
-        parts = [self._sizes]
+        if self._info_key != (self._oa, self._ob):
+            self._info_idx = self._info_index()
+            self._info_key = (self._oa, self._ob)
+        keys = _u64_key(self.buf["ts"].index_select(0, self._info_idx))
         ok = self._one
-        for br, n in ((0, self.na_s), (1, self.nb_s)):
-            if n:
-                ts = self._orig(br, "ts")
-                parts.append(_u64_key(torch.stack([ts[0], ts[-1]])))
-                if n > 1 and self.mode == "auto":  # "range": the ORDER plan checks the order itself
-                    k = _u64_key(ts)
+        if self.mode == "auto":  # "range": the ORDER plan checks the order itself
+            for br, n in ((0, self.na_s), (1, self.nb_s)):
+                if n > 1:
+                    k = _u64_key(self._orig(br, "ts"))
                     ok = ok & (k[1:] >= k[:-1]).all().to(torch.int64).view(1)  # both branches
-            else:
-                parts.append(self._zero2)
-        return torch.cat(parts + [ok, self._signed])
+        return torch.cat([self._sizes, keys[:4], ok, self._signed, keys[4:]])
+
+    @staticmethod
+    def _host_cuts(g: np.ndarray, tau: np.ndarray):
+        """allc [W, 2, W] from the gathered range info alone, or None when a splitter
+        falls between a slice's RH head and RH tail keys (then the device searches)."""
+        W = g.shape[0]
+        allc = np.zeros((W, 2, W), np.int64)
+        for q in range(W):
+            for br in range(2):
+                n = int(g[q, br])
+                h = min(RH, n)
+                o = 9 + 2 * RH * br
+                head, tail = g[q, o: o + h], g[q, o + 2 * RH - h: o + 2 * RH]
+                cuts = []
+                for t in tau:
+                    if n == 0:
+                        c = 0
+                    elif n <= RH or t <= head[-1]:  # every key below t lies in the head
+                        c = int(np.searchsorted(head, t, side="left"))
+                    elif t > tail[0]:               # every key before the tail lies below t
+                        c = n - h + int(np.searchsorted(tail, t, side="left"))
+                    else:
+                        return None
+                    cuts.append(c)
+                allc[q, br] = np.diff(np.concatenate([[0], np.clip(cuts, 0, n), [n]]).astype(np.int64))
+        return allc
 
     @staticmethod
     def _range_plan(g: np.ndarray):
@@ -299,16 +341,23 @@ class ShardedCompose:
 
     def _range_counts(self):
         """allc [W, 2, W] (src, branch, dest) op counts of the key-range split, or None when
-        the logs are not timestamp-ordered.  Two small host syncs: the ranks' slice ends,
-        then every rank's cut positions (binary searches on the device).  (Planning on the
-        device instead, to save one sync, measured slower: a dozen tiny torch launches
-        cost more than the sync, profiles/r03_c/shard_probe.txt.)"""
+        the logs are not timestamp-ordered.  One host sync: the gathered range info
+        carries RH keys from each end of every slice, and a splitter (the running maximum
+        of the ranks' first keys) cuts a timestamp-ordered slice near one of its ends
+        unless the slices are badly skewed, so every rank computes every cut on the host.
+        Otherwise a second sync: every rank's cut positions from binary searches on the
+        device.  (Planning on the device, to save the sync, measured slower: a dozen tiny
+        torch launches cost more than the sync, profiles/r03_c/shard_probe.txt.)"""
         torch = self.torch
         W = self.world
-        g = self.comm.all_gather(self._range_info()).cpu().numpy()        # [W, 9]
+        g = self.comm.all_gather(self._range_info()).cpu().numpy()        # [W, 9 + 4 RH]
         ordered, tau = self._range_plan(g)
         if not ordered:
             return None
+        allc = self._host_cuts(g, tau)
+        if allc is not None:  # the common case: one host sync for the whole plan
+            self.host_cut_plans += 1
+            return allc
         cuts = torch.zeros((2, max(W - 1, 1)), dtype=torch.int64, device=self.dev)
         if W > 1:
             tk = torch.from_numpy(tau).to(self.dev)

@@ -161,23 +161,30 @@ def test_graph_replay_reads_current_inputs():
         _check(dc, soa, f"merge {rep}")
 
 
-def test_graph_replay_with_stage_timers():
-    """With the stage timers on, replays record their stage events and the library reads
-    them before the next replay: one window and one emit time per merge."""
+def test_stage_timers_time_every_merge():
+    """With the stage timers on, merges enqueue directly (no graph replay: a replayed
+    graph's event timestamps read back as 0 ms) and every merge's stages get a time;
+    with the timers off again the merge goes back to the graph replay."""
     import torch
     soa = _lift(300_000, 3_000, 34)
     dc = _lib.DeviceCompose(soa)
     s = torch.cuda.Stream()
     L = _lib.lib()
-    L.smx_reset_stage_times()
+    for _ in range(3):  # the key is seen, captured and replayed before the timed merges
+        dc.run(s)
+    s.synchronize()
     L.smx_set_profiling(1)
     try:
-        for _ in range(4):
+        for rep in range(3):
+            L.smx_reset_stage_times()
             dc.run(s)
-        s.synchronize()
+            s.synchronize()
+            st = _lib.stage_times()
+            assert st["window"][1] == 1 and st["emit"][1] == 1, st
+            assert all(ms > 0 for ms, c in st.values() if c), (rep, st)
     finally:
         L.smx_set_profiling(0)
-    st = _lib.stage_times()
-    assert st["window"][1] == 4 and st["emit"][1] == 4, st
-    assert all(ms > 0 for ms, c in st.values() if c)
-    _check(dc, soa, "timed replays")
+    _check(dc, soa, "timed merges")
+    dc.run(s)
+    s.synchronize()
+    _check(dc, soa, "graph replay after the timed merges")

@@ -80,6 +80,7 @@ def _check(batch):
 
 @pytest.mark.parametrize("n_ops,n_lists,seed", [(200_000, 1_000, 13), (1_000_000, 5_000, 14),
                                                 (400_000, 100_000, 16),  # > 65536 lists: multi-block scan
+                                                (300_000, 65_536, 17),   # the most lists k_rga_out_fused takes
                                                 (300_000, 30, 15)])
 def test_rga_batch_equals_oracle(n_ops, n_lists, seed):
     _check(synth.rga_batch(n_ops, n_lists, seed))

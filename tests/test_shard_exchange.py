@@ -254,3 +254,41 @@ def test_exchange_strong_split_slices():
         if r + 1 < world and res[r + 1][5] is not None:
             assert tmax < res[r + 1][5]
     assert ea == na_g and eb == na_g and na_g == world * (n_total // world // 2)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_host_cuts_match_full_searches(seed):
+    """ShardedCompose._host_cuts (the one-sync plan) gives the cuts a binary search over
+    every whole slice gives, or declines (None) when a splitter falls between a slice's
+    head and tail keys; slices of 0..3*RH keys, ties across splitters included."""
+    from semantic_merge_amd.shard import RH, ShardedCompose
+    rng = np.random.default_rng(seed)
+    W = int(rng.integers(2, 6))
+    sl = [[np.sort(rng.integers(-50, 50, size=int(rng.integers(0, 3 * RH)))).astype(np.int64)
+           for _ in range(2)] for _ in range(W)]
+    g = np.zeros((W, 9 + 4 * RH), np.int64)
+    for q in range(W):
+        for br in range(2):
+            k = sl[q][br]
+            n, h = len(k), min(RH, len(k))
+            g[q, br] = n
+            o = 9 + 2 * RH * br
+            g[q, o: o + h] = k[:h]
+            g[q, o + 2 * RH - h: o + 2 * RH] = k[n - h:]
+    declined = 0
+    for _ in range(20):
+        tau = np.sort(rng.integers(-60, 60, size=W - 1)).astype(np.int64)
+        got = ShardedCompose._host_cuts(g, tau)
+        want = np.zeros((W, 2, W), np.int64)
+        for q in range(W):
+            for br in range(2):
+                c = np.searchsorted(sl[q][br], tau, side="left")
+                want[q, br] = np.diff(np.concatenate([[0], c, [len(sl[q][br])]]))
+        if got is None:
+            declined += 1
+            # a decline only when some splitter really falls strictly inside a middle
+            assert any(len(k) > RH and k[RH - 1] < t <= k[len(k) - RH]
+                       for q in range(W) for k in sl[q] for t in tau)
+        else:
+            assert np.array_equal(got, want), (tau, got, want)
+    assert declined < 20
