@@ -334,6 +334,14 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
 #define RW_EMPTY 0xffffffffu
 #define RW_NIL 0xffffu
 #define RW_DEAD 0x400u
+#ifndef RW_H16
+#define RW_H16 1  // 16-bit group counts / bases (a list has at most 2 * RW_CAP events): less LDS per wave
+#endif
+#if RW_H16
+#define RW_HT u16
+#else
+#define RW_HT u32
+#endif
 #ifndef RW_ABL
 #define RW_ABL 0  // timing ablations (wrong results): bit0 no replay, bit1 no grouping / replay,
                   // bit2 no key order, bit3 load only
@@ -403,8 +411,8 @@ struct RwLds {
   union {
     struct {
       u32 hkey[HT];     // the slot's value, RW_EMPTY
-      u32 hcnt[HT];     // members of the slot's group
-      u32 hbase[HT];    // first member position (exclusive scan of hcnt)
+      RW_HT hcnt[HT];   // members of the slot's group
+      RW_HT hbase[HT];  // first member position (exclusive scan of hcnt)
     } h;
     u64 gs[CAP];        // step 3: survivors' word 0, sorted
   };
@@ -539,7 +547,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
       const u32 base = valid ? S.h.hcnt[slot[k]] : 0u;
       rk[k] = base + (u32)__popcll(peers & lt);
       wave_lds_sync();
-      if (valid && (peers & lt) == 0) S.h.hcnt[slot[k]] = base + (u32)__popcll(peers);
+      if (valid && (peers & lt) == 0) S.h.hcnt[slot[k]] = (RW_HT)(base + (u32)__popcll(peers));
       wave_lds_sync();
     }
     {  // exclusive scan of the group sizes, HT / 64 slots per lane
@@ -553,7 +561,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
       u32 run = wave_incl_sum(tot) - tot;
 #pragma unroll
       for (int i = 0; i < PL; ++i) {
-        S.h.hbase[lane * PL + i] = run;
+        S.h.hbase[lane * PL + i] = (RW_HT)run;
         run += c[i];
       }
     }

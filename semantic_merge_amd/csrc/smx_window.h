@@ -542,7 +542,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     bool f = false;
     if (p < sz) {
       const int e = fin[p];
-#if WF_OUT2 && !defined(WF_GBS0)
+#if WF_OUT2
       f = (p == (int)kbase[skS[p]]) || (sts[fin[p - 1]] != sts[e]);  // (skS: kinds by slot)
 #else
       f = (p == (int)kbase[skind[e]]) || (sts[fin[p - 1]] != sts[e]);
@@ -628,27 +628,22 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     const int wi = __builtin_amdgcn_readfirstlane((WF_NT * j) / WAVE + wv);  // this wave's slot chunk
     if (wi >= nch) break;  // wave-uniform
     const int p = wi * WAVE + lane;
+    // Group bounds, branch-free: every lane broadcast (v_readlane) runs with the whole
+    // wave active.  (Lane reads inside the lanes' divergent branches mis-ordered groups
+    // in some builds: a register's value in lanes outside the branch is not defined.)
+    // The last group start before the chunk and the first one after it are scalar.
     const u64 W = bcast64(gw, wi);
-    int gs, ge;
-    {
-      const u64 below = W & le_mask;
-      if (below) {
-        gs = wi * WAVE + 63 - __clzll(below);
-      } else {  // the group began in an earlier chunk (slot 0 always starts one)
-        const u64 prev = gnz & ((1ull << wi) - 1);
-        const int wp = prev ? 63 - __clzll(prev) : 0;
-        gs = wp * WAVE + 63 - __clzll(bcast64(gw, wp) | 1ull);
-      }
-      const u64 above = W & ~le_mask;
-      if (above) {
-        ge = wi * WAVE + __ffsll((unsigned long long)above) - 1;
-      } else {
-        const u64 nxt = wi + 1 < WAVE ? gnz & ~((2ull << wi) - 1) : 0ull;
-        const int wn = nxt ? __ffsll((unsigned long long)nxt) - 1 : 0;
-        ge = nxt ? wn * WAVE + __ffsll((unsigned long long)bcast64(gw, wn)) - 1 : sz;
-      }
-      ge = ge < sz ? ge : sz;
-    }
+    const u64 prevm = gnz & ((1ull << wi) - 1);  // (slot 0 always starts a group)
+    const int wp = prevm ? 63 - __clzll(prevm) : 0;
+    const int prevS = wp * WAVE + 63 - __clzll(bcast64(gw, wp) | 1ull);
+    const u64 nxtm = wi + 1 < WAVE ? gnz & ~((2ull << wi) - 1) : 0ull;
+    const int wn = nxtm ? __ffsll((unsigned long long)nxtm) - 1 : 0;
+    const u64 Wn = bcast64(gw, wn);
+    const int nextS = nxtm ? wn * WAVE + __ffsll((unsigned long long)(Wn | (1ull << 63))) - 1 : sz;
+    const u64 below = W & le_mask, above = W & ~le_mask;
+    const int gs = below ? wi * WAVE + 63 - __clzll(below | 1ull) : prevS;
+    int ge = above ? wi * WAVE + __ffsll((unsigned long long)(above | (1ull << 63))) - 1 : nextS;
+    ge = ge < sz ? ge : sz;
     if (p >= sz) continue;
 #if WF_BUCKET
     {
@@ -761,10 +756,18 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
 #endif
   __syncthreads();
-#if defined(WF_INVPASS) && WF_OUT2
-  for (int r = t; r < sz; r += WF_NT) inv[sord[r]] = (u16)r;
-  __syncthreads();
-#endif
+  if (DBG) {  // diagnostics: the group order against the slot-space keys (dbg words 5, 17, 18)
+    for (int r = t + 1; r < sz; r += WF_NT) {
+      const bool start = (gbits[r >> 6] >> (r & 63)) & 1ull;
+      if (!start && pkey[sl[r - 1]] > pkey[sl[r]]) atomicAdd((unsigned long long*)&P.dbg[w * WF_NSTAMP + 5], 1ull);
+      if (!start && sts[0] == 0x12345ull) P.meta->dup_key = 3;  // (keeps sts live)
+    }
+    for (int r = t; r < sz; r += WF_NT) {
+      const int p0 = sl[r];
+      if (p0 >= sz) atomicAdd((unsigned long long*)&P.dbg[w * WF_NSTAMP + 17], 1ull);
+      else if (fin[p0] != sord[r]) atomicAdd((unsigned long long*)&P.dbg[w * WF_NSTAMP + 18], 1ull);
+    }
+  }
   WSTAMP(10);
   WF_EXIT(8);
   // 6. renames: rank among the window's renames of the same branch (final order).
