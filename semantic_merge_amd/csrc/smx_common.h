@@ -119,6 +119,15 @@ __device__ __forceinline__ int4 fin_decode(const FinPack& P, u64 x) {
   return make_int4(a, f, c, 0);
 }
 
+// Workgroup b of a grid of n -> the work item it processes, so that the workgroups
+// the dispatcher deals to one XCD (b % 8 labels them; cdna_hip_programming.md T1)
+// take consecutive items: neighbouring windows share their input lines in that XCD's
+// L2.  Bijective for any n.  A speed choice only: any placement gives the same result.
+__device__ __forceinline__ i64 xcd_item(i64 b, i64 n) {
+  const i64 q = n / 8, r = n % 8, x = b % 8, i = b / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 __device__ __forceinline__ u64 lanemask_lt() {
   const int lane = threadIdx.x & (WAVE - 1);
   return (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));

@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, c
                                                   const i64* __restrict__ bnd, i64 na, i64 W,
                                                   u32* __restrict__ wcnt, ComposeMeta* meta) {
   __shared__ u32 c[NCNT];
-  const i64 w = blockIdx.x;
+  const i64 w = SMX_XCD_WIN ? xcd_item(blockIdx.x, W) : (i64)blockIdx.x;  // (the window's gathers stay in one L2)
   if (threadIdx.x < NCNT) c[threadIdx.x] = 0;
   __syncthreads();
   const i64 a0 = bnd[2 * w], b0 = bnd[2 * w + 1], a1 = bnd[2 * w + 2], b1 = bnd[2 * w + 3];

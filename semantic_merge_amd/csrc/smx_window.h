@@ -36,6 +36,9 @@
 #include "smx_common.h"
 
 #define WIN_CAP 2048               // max ops per window held in LDS
+#ifndef SMX_XCD_WIN
+#define SMX_XCD_WIN 1              // generic-plan windows dealt to XCDs in consecutive runs
+#endif
 #ifndef WIN_TGT
 #define WIN_TGT 1792               // default target window size, presorted path (SMX_WIN_TGT)
 #endif
@@ -244,7 +247,7 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #define WF_BZ4 1     // step 5's bucket counters zeroed in step 4's last phase (one barrier fewer)
 #endif
 #ifndef WF_OUT2
-#define WF_OUT2 0    // steps 7-9: payload staged by final slot (inv), four slots per thread, 16-byte stores
+#define WF_OUT2 1    // steps 7-9 staged by final slot (inv), four slots per thread, 16-byte stores: window 1.271 -> 1.233 ms (profiles/r03_m/ab.txt)
 #endif
 #ifdef WF_WPE
 #define WF_BOUNDS __launch_bounds__(WF_NT) __attribute__((amdgpu_waves_per_eu(WF_WPE, WF_WPE)))
@@ -1107,7 +1110,9 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   const int t = threadIdx.x;
   const int lane = t & (WAVE - 1);
   const int wv = t / WAVE;
-  const i64 w = blockIdx.x;
+  // consecutive windows on one XCD: a timestamp group spans several windows, whose
+  // gathers through the permutation then hit the same L2
+  const i64 w = SMX_XCD_WIN ? xcd_item(blockIdx.x, P.W) : (i64)blockIdx.x;
   const i64 a0 = P.bnd[2 * w], b0 = P.bnd[2 * w + 1];
   const int na = (int)(P.bnd[2 * w + 2] - a0);
   const int nb = (int)(P.bnd[2 * w + 3] - b0);

@@ -1,7 +1,7 @@
 # Round-end measurement pass: full GPU suite, smoke, default bench (PMC + CPU legs),
 # rocprof kernel stats, config 5 / config 2 / RGA bench lines.
 set -o pipefail
-TAG=${TAG:-r02k_end}; R=$PWD; O=$R/gpurun_out/$TAG; mkdir -p $O
+TAG=${TAG:-r03_end}; R=$PWD; O=$R/gpurun_out/$TAG; mkdir -p $O
 bash tools/gpu_check.sh $TAG tests bench prof || exit 1
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
 timeout -k 10 300 python -u bench.py --config c5 --steps 10 --no-cpu-baseline --no-e2e > $O/bench_c5.json 2> $O/bench_c5.err || { tail -5 $O/bench_c5.err; exit 1; }

@@ -13,7 +13,7 @@ for s in $STEPS; do
            cat "$O/bench.json";;
     benchq) timeout -k 10 200 python -u bench.py --no-cpu-baseline > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
            cat "$O/bench.json";;
-    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o p -- python3 "$R/bench.py" --steps 8 --warmup 2 --no-cpu-baseline > "$O/prof.log" 2>&1) || { tail -20 "$O/prof.log"; exit 1; }
+    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o p -- python3 "$R/bench.py" --steps 8 --warmup 2 --no-cpu-baseline --no-pmc --no-e2e > "$O/prof.log" 2>&1) || { tail -20 "$O/prof.log"; exit 1; }
           python3 tools/prof_export.py "$O/prof" "$O/kernel_stats.csv" && head -12 "$O/kernel_stats.csv";;
     pmc) timeout -k 10 900 bash tools/pmc_passes.sh "$O/pmc" || exit 1;;
   esac
