@@ -222,6 +222,9 @@ __global__ void k_tb_unskip(TbArgs A0, const u32* __restrict__ lst, u32* __restr
 }
 
 #define TBR_NT 1024
+#ifndef SMX_XCD_TB
+#define SMX_XCD_TB 1
+#endif
 #ifndef TBR_TK
 #define TBR_TK 16
 #endif
@@ -238,7 +241,9 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
   const FinPack FP = fin_pack_of(A0.meta->vbits, true);
   __shared__ u32 tA[TB_WIDTH], tF[TB_WIDTH], tC[TB_WIDTH];
   const TbArgs A = tb_load(A0);
-  const u32 b = blockIdx.x;
+  // neighbouring buckets on one XCD: a tile's runs of buckets b and b + 1 share their
+  // boundary lines, which are then fetched into one L2 only
+  const u32 b = SMX_XCD_TB ? (u32)xcd_item(blockIdx.x, gridDim.x) : blockIdx.x;
   for (u32 i = threadIdx.x; i < A.width; i += TBR_NT) tA[i] = tF[i] = tC[i] = 0;
   __syncthreads();
   auto put = [&](u32 q, u64 rb) {

@@ -280,7 +280,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   const int t = threadIdx.x;
   const int lane = t & (WAVE - 1);
   const int wv = t / WAVE;
-  const i64 w = blockIdx.x;
+  const i64 w = blockIdx.x;  // (XCD-ordered presorted windows measured slower: 1.241 -> 1.269 ms, profiles/r03_p)
   const i64 a0 = P.bnd[2 * w], b0 = P.bnd[2 * w + 1];
   const int na = (int)(P.bnd[2 * w + 2] - a0);
   const int nb = (int)(P.bnd[2 * w + 3] - b0);
