@@ -306,20 +306,20 @@ class ShardedCompose:
         for q in range(W):
             for br in range(2):
                 n = int(g[q, br])
+                if n == 0:
+                    continue
                 h = min(RH, n)
                 o = 9 + 2 * RH * br
                 head, tail = g[q, o: o + h], g[q, o + 2 * RH - h: o + 2 * RH]
-                cuts = []
-                for t in tau:
-                    if n == 0:
-                        c = 0
-                    elif n <= RH or t <= head[-1]:  # every key below t lies in the head
-                        c = int(np.searchsorted(head, t, side="left"))
-                    elif t > tail[0]:               # every key before the tail lies below t
-                        c = n - h + int(np.searchsorted(tail, t, side="left"))
-                    else:
+                if n <= RH:                    # the head is the whole slice
+                    cuts = np.searchsorted(head, tau, side="left")
+                else:
+                    in_head = tau <= head[-1]  # every key below tau lies in the head
+                    in_tail = tau > tail[0]    # every key before the tail lies below tau
+                    if not np.all(in_head | in_tail):
                         return None
-                    cuts.append(c)
+                    cuts = np.where(in_head, np.searchsorted(head, tau, side="left"),
+                                    n - h + np.searchsorted(tail, tau, side="left"))
                 allc[q, br] = np.diff(np.concatenate([[0], np.clip(cuts, 0, n), [n]]).astype(np.int64))
         return allc
 
