@@ -115,6 +115,10 @@ def pmc_traffic(args) -> dict:
     out["pipeline_traffic"] = round(tot)
     out["per_kernel"] = dict(sorted(kern.items(), key=lambda x: -x[1])[:12])   # bytes per merge
     out["per_kernel_all"] = {k.split("<")[0]: v for k, v in kern.items()}
+    out["factors"] = {"FETCH_SIZE": FETCH_FACTOR, "WRITE_SIZE": WRITE_FACTOR,
+                      "note": "FETCH_SIZE x2 is calibrated on streaming reads (DESIGN.md §5); for "
+                              "gather-dominated kernels (k_emit4) the x2 figure is an upper bound "
+                              "and x1 the lower bound"}
     out["status"] = "ok"
     return out
 

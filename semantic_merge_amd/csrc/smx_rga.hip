@@ -334,6 +334,9 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
 #define RW_EMPTY 0xffffffffu
 #define RW_NIL 0xffffu
 #define RW_DEAD 0x400u
+#ifndef RW_HT1
+#define RW_HT1 1
+#endif
 #ifndef RW_H16
 #define RW_H16 1  // 16-bit group counts / bases (a list has at most 2 * RW_CAP events): less LDS per wave
 #endif
@@ -405,7 +408,10 @@ __device__ __forceinline__ void wave_bitonic(u64 (&key)[8], u32 (&pay)[8], u32 l
 
 template <int CAP>
 struct RwLds {
-  static constexpr int HT = 2 * CAP;  // hash slots
+  // hash slots: one per event for k_rga_wave's lists (RW_HT1: 7.4 KB of LDS per list, five
+  // waves per SIMD; a full table still terminates, every value finds its slot), two
+  // per event otherwise
+  static constexpr int HT = (RW_HT1 && CAP == RW_CAP) ? CAP : 2 * CAP;
   u64 w0[CAP];          // key word 0 of each event (words 1-3 stay in global memory / L2)
   u64 wv[CAP];          // value << 32 | op << 30 | index (record word RGA_WV)
   union {
@@ -508,7 +514,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
     return;
   }
   const u64 lt = lanemask_lt();
-  constexpr int HB = CAP == 256 ? 9 : 10;  // log2 of the hash slots
+  constexpr int HB = RwLds<CAP>::HT == 256 ? 8 : RwLds<CAP>::HT == 512 ? 9 : 10;  // log2 of the hash slots
   static_assert(RwLds<CAP>::HT == 1 << HB, "hash slots");
   u32 slot[8], rk[8];
 #pragma unroll

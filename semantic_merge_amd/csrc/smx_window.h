@@ -244,10 +244,7 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #define WF_BK16 1    // bucket-ordered 16-bit key prefixes for the rank loop (window 1.329 -> 1.286 ms, profiles/r03_e/ab.txt)
 #endif
 #ifndef WF_FUSEFIN
-#define WF_FUSEFIN 0  // step 5's final order written by the rank loop itself (one barrier and loop fewer)
-#endif
-#ifndef WF_SCAN1
-#define WF_SCAN1 0   // step 5's counter scan with one barrier (block_excl_scan takes three)
+#define WF_FUSEFIN 1  // step 5's final order written by the rank loop itself: window 1.248 -> 1.227 ms (profiles/r03_q)
 #endif
 #ifndef WF_BZ4
 #define WF_BZ4 1     // step 5's bucket counters zeroed in step 4's last phase (one barrier fewer)
@@ -695,21 +692,8 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     // exclusive scan of the counters, 4 per thread (2 words)
     const u32 w0 = bcnt[2 * t], w1 = bcnt[2 * t + 1];
     const u32 c0 = w0 & 0xffffu, c1 = w0 >> 16, c2 = w1 & 0xffffu, c3 = w1 >> 16;
-#if WF_SCAN1
-    // one barrier: each wave's total to LDS, then every wave adds up those before it
-    // (vbw is dead after step 2)
-    const u32 s4 = c0 + c1 + c2 + c3;
-    const u32 inc = wave_incl_sum(s4);
-    u32* wsum = &vbw[0][0];
-    if (lane == WAVE - 1) wsum[wv] = inc;
-    __syncthreads();
-    u32 pre = 0;
-    for (int i = 0; i < wv; ++i) pre += wsum[i];  // (wave-uniform)
-    const u32 e0 = pre + inc - s4;
-#else
     u32 tot;
     const u32 e0 = block_excl_scan<OpSum, u32, WF_WAVES>(c0 + c1 + c2 + c3, &vbw[0][0], &tot);  // (vbw is dead after step 2)
-#endif
     bcnt[2 * t] = e0 | ((e0 + c0) << 16);
     bcnt[2 * t + 1] = (e0 + c0 + c1) | ((e0 + c0 + c1 + c2) << 16);
     __syncthreads();

@@ -117,3 +117,16 @@ def test_rga_hot_list_and_invalid_input():
     b.list_id[5] = 50
     with pytest.raises(Exception, match="n_lists"):
         rga_replay_device(b)
+
+
+def test_rga_lists_at_capacity_all_values_distinct():
+    """Lists of exactly 256 events (k_rga_wave's capacity) whose values are all distinct:
+    the list kernel's value hash table (one slot per event) fills completely; and lists
+    of 257 events (the deferred kernel)."""
+    b = synth.rga_batch(400 * 256 + 300 * 257, 700, 19)
+    rng = np.random.default_rng(19)
+    lid = np.concatenate([np.repeat(np.arange(400), 256), np.repeat(np.arange(400, 700), 257)])
+    rng.shuffle(lid)
+    b.list_id = lid.astype(np.uint32)
+    b.value = np.arange(lid.size, dtype=np.uint32)  # distinct everywhere (first-seen order)
+    _check(b)
