@@ -8,3 +8,5 @@ timeout -k 10 300 python -u bench.py --config c5 --steps 10 --no-cpu-baseline --
 timeout -k 10 300 python -u bench.py --config c2 --steps 50 --no-pmc --no-e2e > $O/bench_c2.json 2> $O/bench_c2.err || { tail -5 $O/bench_c2.err; exit 1; }
 timeout -k 10 300 python -u tools/bench_rga.py > $O/bench_rga.json 2> $O/bench_rga.err || { tail -5 $O/bench_rga.err; exit 1; }
 cut -c1-300 $O/bench_c5.json $O/bench_rga.json
+(cd /tmp && export TMPDIR=/tmp && RGA_NO_CPU=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/prof_rga" -o r -- python3 "$R/tools/bench_rga.py" > "$O/prof_rga.log" 2>&1) || { tail -5 "$O/prof_rga.log"; exit 1; }
+python3 tools/prof_export.py "$O/prof_rga" "$O/rga_kernel_stats.csv" && head -8 "$O/rga_kernel_stats.csv"
