@@ -16,6 +16,10 @@
  * stream).  smx_compose performs one stream synchronisation (in smx_compose_finish)
  * to check its plan; read device-side counts only after synchronising the stream.
  *
+ * Reentrant: host threads may compose concurrently, each on its own stream and
+ * workspace (the library's side stream and fork/join events are kept per caller
+ * stream; tests/test_gpu_async.py runs two threads on one GPU).
+ *
  * Return value: 0 on success, a negative SMX_E* code otherwise; the message is
  * available from smx_last_error() (thread-local).  Nothing aborts the process.
  */

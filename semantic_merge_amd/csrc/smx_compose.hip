@@ -27,6 +27,7 @@
 //   tables      per-symbol last writers: bucket by symbol range, LDS max-reduce
 //   k_emit      compacted output of every op after the move block: order, addr,
 //               file, ctx
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -71,6 +72,27 @@ struct PendingEv {
 };
 static std::vector<PendingEv> g_pending;
 
+// Timing events are reused: creating and destroying a dozen per merge sat on the host
+// path between one merge's sync and the next merge's first launch.  (g_prof_mu guards
+// the pool.)
+static std::vector<hipEvent_t> g_ev_pool;
+static hipEvent_t ev_acquire() {
+  {
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    if (!g_ev_pool.empty()) {
+      hipEvent_t e = g_ev_pool.back();
+      g_ev_pool.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+static void ev_release_locked(hipEvent_t e) {  // (caller holds g_prof_mu)
+  if (e) g_ev_pool.push_back(e);
+}
+
 struct StageTimer {
   hipStream_t st;
   bool on;
@@ -80,15 +102,13 @@ struct StageTimer {
   StageTimer(hipStream_t s, bool enabled) : st(s), on(enabled) {}
   void begin(int i) {
     if (!on) return;
-    if (is_open[i]) (void)hipEventDestroy(open[i]);  // a stage restarted (plan retries)
-    (void)hipEventCreate(&open[i]);
+    if (!is_open[i]) open[i] = ev_acquire();  // (a restarted stage re-records its open event)
     (void)hipEventRecord(open[i], st);
     is_open[i] = true;
   }
   void end(int i) {
     if (!on || !is_open[i]) return;
-    hipEvent_t b;
-    (void)hipEventCreate(&b);
+    hipEvent_t b = ev_acquire();
     (void)hipEventRecord(b, st);
     done.push_back({i, open[i], b});
     is_open[i] = false;
@@ -99,13 +119,16 @@ struct StageTimer {
     for (auto& p : done) g_pending.push_back(p);
     done.clear();
   }
-  ~StageTimer() {
-    for (auto& p : done) {  // an error path left events unpublished
-      (void)hipEventDestroy(p.a);
-      (void)hipEventDestroy(p.b);
+  ~StageTimer() {  // an error path left events unpublished: back to the pool
+    if (done.empty() && !std::any_of(is_open, is_open + ST_N, [](bool b) { return b; })) return;
+    (void)hipStreamSynchronize(st);  // (recorded events may still be pending)
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    for (auto& p : done) {
+      ev_release_locked(p.a);
+      ev_release_locked(p.b);
     }
     for (int i = 0; i < ST_N; ++i)
-      if (is_open[i]) (void)hipEventDestroy(open[i]);
+      if (is_open[i]) ev_release_locked(open[i]);
   }
 };
 
@@ -116,8 +139,8 @@ static void resolve_pending_locked() {
     (void)hipEventElapsedTime(&ms, p.a, p.b);
     g_stage_ms[p.stage] += ms;
     g_stage_calls[p.stage] += 1;
-    (void)hipEventDestroy(p.a);
-    (void)hipEventDestroy(p.b);
+    ev_release_locked(p.a);
+    ev_release_locked(p.b);
   }
   g_pending.clear();
 }
@@ -1915,9 +1938,14 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
   return SMX_OK;
 }
 
+// The meta block comes back through a pinned staging buffer (one per host thread): a
+// DMA, not the runtime's staged copy into pageable memory.
 static int read_meta(const Ctx& C, ComposeMeta* hm) {
-  HIP_TRY(hipMemcpyAsync(hm, C.ws<ComposeMeta>(B_META), sizeof(ComposeMeta), hipMemcpyDeviceToHost, C.st));
+  static thread_local ComposeMeta* pinned = nullptr;
+  if (!pinned) HIP_TRY(hipHostMalloc((void**)&pinned, sizeof(ComposeMeta), hipHostMallocDefault));
+  HIP_TRY(hipMemcpyAsync(pinned, C.ws<ComposeMeta>(B_META), sizeof(ComposeMeta), hipMemcpyDeviceToHost, C.st));
   HIP_TRY(hipStreamSynchronize(C.st));
+  std::memcpy(hm, pinned, sizeof(ComposeMeta));
   return SMX_OK;
 }
 
