@@ -307,7 +307,11 @@ def main() -> None:
     # smx_compose_finish after the last: what a caller pipelining merges gets (no host
     # sync between merges).  Reported beside the headline, outside its timed region.
     async_api = None
-    if not sharded and world == 1 and not args.no_async:
+    if not sharded and world == 1 and not args.no_async and plan != "presorted":
+        # only the presorted plan completes inside smx_compose_async: any other plan
+        # returns -2 there and runs in smx_compose_finish, one merge per finish
+        async_api = {"status": f"plan {plan}: each merge needs its own smx_compose_finish (not pipelined)"}
+    elif not sharded and world == 1 and not args.no_async:
         for _ in range(2):  # (the merge's key is seen, then captured as a graph, untimed)
             dc.run_async()
         dc.finish()
@@ -319,7 +323,7 @@ def main() -> None:
         torch.cuda.synchronize(dev)
         el_async = time.perf_counter() - t1
         k2, _ = (int(x) for x in dc.counts.cpu().tolist())
-        if k2 == k:  # the presorted plan held: every enqueued merge was complete
+        if k2 == k and _lib.DeviceCompose.last_plan() == "presorted":  # every enqueued merge was complete
             async_api = {"ms_per_step": round(el_async / args.steps * 1e3, 4),
                          "value": round(n_job * args.steps / el_async, 1),
                          "note": "smx_compose_async per merge, one smx_compose_finish after the last"}

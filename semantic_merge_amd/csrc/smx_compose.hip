@@ -212,6 +212,16 @@ __global__ void k_meta_init(ComposeMeta* meta) {
     for (int q = 0; q < 3; ++q) meta->key_and[s][q] = ~0ull;
 }
 
+#ifndef SMX_KHIST_LONG
+#define SMX_KHIST_LONG 1     // k_khist flags timestamp groups longer than a window
+#endif
+#ifndef SMX_FPART_FAILCHK
+#define SMX_FPART_FAILCHK 1  // k_fpart skips its snap and writes on a failed plan
+#endif
+#ifndef SMX_CSCAN_FAILCHK
+#define SMX_CSCAN_FAILCHK 1  // the chunk scans leave on a failed plan
+#endif
+
 // Presorted windows: boundary k sits at the merge-path split of diagonal k*tgt
 // (timestamps, A first on ties), snapped down to the first op of that timestamp on
 // both branches, so every (timestamp) group lands whole in one window.
@@ -221,9 +231,11 @@ __global__ void k_meta_init(ComposeMeta* meta) {
 // search runs on them, the second inside one chunk.  The snap gallops back over
 // the (short) run of equal timestamps.
 __global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB, const u64* __restrict__ sA,
-                        const u64* __restrict__ sB, i64 na, i64 nb, i64 W, i64 tgt, i64* __restrict__ bnd) {
+                        const u64* __restrict__ sB, i64 na, i64 nb, i64 W, i64 tgt, i64* __restrict__ bnd,
+                        const ComposeMeta* meta) {
   const i64 k = (i64)blockIdx.x * BLOCK + threadIdx.x;
   if (k > W) return;
+  const u64 failed = SMX_FPART_FAILCHK ? meta->f_fail : 0ull;  // (k_khist saw a group no window holds; used after the search)
   const i64 n = na + nb;
   const u64* A = ts;
   const u64* B = tsB;
@@ -255,6 +267,7 @@ __global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB,
       else hi = mid;
     }
   }
+  if (failed) return;
   const i64 a = lo, b = d - lo;
   const u64 tau = (a < na && (b >= nb || A[a] <= B[b])) ? A[a] : B[b];
   // first index of each branch with ts >= tau: at or before the split
@@ -286,9 +299,10 @@ __global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB,
 
 // Generic windows over branch logs sorted by (ts, oid): fixed diagonals of WIN_CAP.
 __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi,
-                        const u64* __restrict__ slo, i64 na, i64 nb, i64 W, i64* __restrict__ bnd) {
+                        const u64* __restrict__ slo, i64 na, i64 nb, i64 W, i64* __restrict__ bnd,
+                        const ComposeMeta* meta) {
   const i64 k = (i64)blockIdx.x * BLOCK + threadIdx.x;
-  if (k > W) return;
+  if (k > W || meta->f_fail) return;  // (the segmented sort failed: nothing to cut)
   const i64 n = na + nb;
   const i64 d = k * WG_CAP;
   if (k == 0) { bnd[0] = 0; bnd[1] = 0; return; }
@@ -324,7 +338,8 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 // the row adds them up with DPP shifts; the row's last lane holds the chunk's counts.
 __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, const u64* __restrict__ ts,
                                                  i64 na, i64 nb, i64 bgap, i64 CM, u32* __restrict__ cnt,
-                                                 u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta) {
+                                                 u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta,
+                                                 u32* long_host) {
   __shared__ u32 c[CH_PER_BLOCK * KH_R][SMX_N_KINDS];
   __shared__ u32 km[2];
   const i64 CA = SMX_CEIL_DIV(na, (i64)CH), CB = SMX_CEIL_DIV(nb, (i64)CH);
@@ -333,6 +348,7 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
   // KH_R rounds of CH_PER_BLOCK chunks per block; every round's loads are issued first
   u32 w[KH_R][4];
   int nvr[KH_R];
+  bool long_group = false;  // a timestamp run longer than a presorted window
 #pragma unroll
   for (int rd = 0; rd < KH_R; ++rd) {
     const i64 g = ((i64)blockIdx.x * KH_R + rd) * CH_PER_BLOCK + j;
@@ -345,8 +361,20 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
     const u8* src = kind + (side ? na + bgap : 0) + r0;
     // timestamp samples for k_fpart: first op of each A chunk, last op of each full B chunk
     if (g < CA + CB) {
-      if (!side && q == 0) sA[cc] = ts[cc * CH];
-      if (side && q == 15 && nv == 16) sB[cc] = ts[na + bgap + cc * CH + CH - 1];
+      // ... and whether the sample and the op WF_CAP later (another chunk's sample: no
+      // extra line) share a timestamp: that group alone overflows a window, so the
+      // presorted plan cannot hold (config 5's groups)
+      if (!side && q == 0) {
+        const u64 v = ts[cc * CH];
+        sA[cc] = v;
+        if (SMX_KHIST_LONG && cc * CH + WF_CAP < na) long_group = v == ts[cc * CH + WF_CAP];
+      }
+      if (side && q == 15 && nv == 16) {
+        const i64 x = cc * CH + CH - 1;
+        const u64 v = ts[na + bgap + x];
+        sB[cc] = v;
+        if (SMX_KHIST_LONG && x + WF_CAP < nb) long_group = v == ts[na + bgap + x + WF_CAP];
+      }
     }
     w[rd][0] = w[rd][1] = w[rd][2] = w[rd][3] = 0u;
     if (nv == 16 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
@@ -397,6 +425,15 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
     }
   }
   if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) meta->bad_sym = 1;
+  // flagged before the windows run: k_fpart, the chunk scans and k_window_f then leave
+  // at once (6: a window too large, and smaller windows cannot help)
+  if (__ballot(long_group) && (threadIdx.x & (WAVE - 1)) == 0 &&
+      __hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 6ull) {
+    atomicOr((unsigned long long*)&meta->f_fail, 6ull);
+    // ... and, on the synchronous path, to the host (pinned, coherent), which then
+    // launches no tail behind this failed plan
+    if (long_host) __hip_atomic_store(long_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   __syncthreads();
   // column-major output: consecutive threads write consecutive chunks of one column;
   // the kinds present per branch (the scans skip the all-zero columns)
@@ -438,7 +475,7 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_up(const u32* __restrict__ cnt,
                                                     i64 NT, u32* __restrict__ tsum, const ComposeMeta* meta) {
   __shared__ u32 s[NWAVES + 1];
   const int col = blockIdx.y;
-  if (!cs_present(meta, col)) return;  // all-zero column: its prefixes are its counts
+  if (!cs_present(meta, col) || (SMX_CSCAN_FAILCHK && meta->f_fail)) return;  // all-zero column: its prefixes are its counts
   const i64 C = SMX_CEIL_DIV(col >= SMX_N_KINDS ? nb : na, (i64)CH);
   const i64 t0 = (i64)blockIdx.x * CS_TILE;
   if (t0 >= C) return;
@@ -456,6 +493,7 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_mid(u32* __restrict__ tsum, i64
                                                      u32* __restrict__ cnt, ComposeMeta* meta) {
   __shared__ u32 s[NWAVES + 1];
   const int col = blockIdx.x;
+  if (SMX_CSCAN_FAILCHK && meta->f_fail) return;  // (k_khist saw a group no window holds)
   const int side = col / SMX_N_KINDS, k = col % SMX_N_KINDS;
   const i64 C = SMX_CEIL_DIV(side ? nb : na, (i64)CH);
   const i64 nt = cs_present(meta, col) ? SMX_CEIL_DIV(C, (i64)CS_TILE) : 0;  // (absent: total 0)
@@ -479,7 +517,7 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_down(u32* __restrict__ cnt, i64
                                                       const u32* __restrict__ tsum, const ComposeMeta* meta) {
   __shared__ u32 s[NWAVES + 1];
   const int col = blockIdx.y;
-  if (!cs_present(meta, col)) return;
+  if (!cs_present(meta, col) || (SMX_CSCAN_FAILCHK && meta->f_fail)) return;
   const i64 C = SMX_CEIL_DIV(col >= SMX_N_KINDS ? nb : na, (i64)CH);
   const i64 t0 = (i64)blockIdx.x * CS_TILE;
   if (t0 >= C) return;
@@ -522,6 +560,7 @@ __global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, c
                                                   const i64* __restrict__ bnd, i64 na, i64 W,
                                                   u32* __restrict__ wcnt, ComposeMeta* meta) {
   __shared__ u32 c[NCNT];
+  if (perm != nullptr && meta->f_fail) return;  // the segmented sort failed: perm is not written
   const i64 w = SMX_XCD_WIN ? xcd_item(blockIdx.x, W) : (i64)blockIdx.x;  // (the window's gathers stay in one L2)
   if (threadIdx.x < NCNT) c[threadIdx.x] = 0;
   __syncthreads();
@@ -1218,6 +1257,7 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
     hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d,
                        (const i64*)sh->in_state_dev, meta, C.out->conflicts, (u64)C.out->conflict_cap, skiplist,
                        skipbits);
+  // (one k_scan1 block over the window counts measured slower: walk 0.165 -> 0.185 ms, profiles/r03_w)
   HIP_TRY((scan_excl<OpSum, u32, u32>(wtot, wcoff, Wmax, &meta->n_win, part, ncand32, st)));
   hipLaunchKernelGGL(k_cand_compact, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, cslot, wcoff, ncand_dev, cand);
   hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
@@ -1483,7 +1523,15 @@ static int launch_tail(const Ctx& C) {
 // Presorted plan: branch logs with non-decreasing timestamps (what lift.ts
 // emits).  Speculative: k_window_f verifies the layout and flags f_fail.
 
-static int run_presorted(const Ctx& C, i64 tgt) {
+// early (optional, not inside a graph capture): k_khist raises early->flag when a timestamp
+// group is longer than a window (the plan then fails for sure); early->ev is recorded
+// right behind k_khist, so the host knows before the windows are done.
+struct EarlyFail {
+  u32* flag_host = nullptr;
+  u32* flag_dev = nullptr;
+  hipEvent_t ev = nullptr;
+};
+static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
@@ -1503,10 +1551,12 @@ static int run_presorted(const Ctx& C, i64 tgt) {
   u64* sA = C.ws<u64>(B_SMP);
   u64* sB = sA + SMX_CEIL_DIV(C.na, (i64)CH) + 1;
   hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK * KH_R)), dim3(KH_NT), 0, st, C.ops->kind,
-                     C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta);
+                     C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta,
+                     early ? early->flag_dev : nullptr);
+  if (early) HIP_TRY(hipEventRecord(early->ev, st));
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
                      C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na,
-                     C.nb, W, tgt, bnd);
+                     C.nb, W, tgt, bnd, meta);
   {
     const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);
     u32* tsum = C.ws<u32>(B_TSUM);
@@ -1612,6 +1662,17 @@ __device__ __forceinline__ void seg_pass(u64 (&v)[8], u32 base, u32 b, u32 k, in
 // every duplicate id) are re-sorted exactly afterwards.  Each thread holds 8 keys whose
 // indices differ in three consecutive bits b .. b+2, so three stages of the network run
 // in registers per LDS round trip (33 round trips for 8192 keys instead of 91 stages).
+// The segmented sort cannot order this log: seg_over for the host, and f_fail bit 3 so
+// that every kernel queued behind the sort (k_gpart, k_wcount, k_window_g, the tail)
+// leaves at once -- the host learns it from the merge's one meta read and runs the
+// radix plan then (no host round trip between the sort and the windows).
+__device__ __forceinline__ void seg_fail(ComposeMeta* meta) {
+  meta->seg_over = 1;
+  atomicOr((unsigned long long*)&meta->f_fail, (unsigned long long)SEG_FAIL_BIT);
+}
+
+// One launch per branch (both in one grid measured slower: segsort 0.52 -> 0.60 ms on
+// config 5, profiles/r03_v).
 __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, const u64* __restrict__ hi,
                                                     const u64* __restrict__ lo, i64 cnt, u32 off,
                                                     u64* __restrict__ sts, u64* __restrict__ shi,
@@ -1660,13 +1721,13 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
   if (t == 0 && p0 - W > 0 && ts[p0 - W - 1] == v0) bad = true;
   if (t == 1 && has_end && a1 > 0 && ts[a1 - 1] == v1) bad = true;
   if (__syncthreads_or(bad)) {
-    if (t == 0) meta->seg_over = 1;
+    if (t == 0) seg_fail(meta);
     return;
   }
   const i64 s = a0 + se[0], size = (has_end ? a1 + se[1] : cnt) - s;
   if (size <= 0) return;
   if (size > SEG_CAP) {
-    if (t == 0) meta->seg_over = 1;
+    if (t == 0) seg_fail(meta);
     return;
   }
   u32 P = 8, lgP = 3;
@@ -1842,9 +1903,10 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
 
 static int read_meta(const Ctx& C, ComposeMeta* hm);
 
-// *fallback: the segmented sort could not order this log (mode GEN_SEG only); nothing
-// after the sort was launched.
-static int run_generic(const Ctx& C, int mode, bool* fallback) {
+// GEN_SEG: when the segmented sort cannot order this log it flags seg_over and f_fail
+// bit 3; every kernel after it leaves at once, and the caller reads seg_over from the
+// meta after the tail.
+static int run_generic(const Ctx& C, int mode) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
@@ -1855,7 +1917,6 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
   u64* shi = C.ws<u64>(B_SHI);
   u64* slo = C.ws<u64>(B_SLO);
   u32* perm = C.ws<u32>(B_PERM);
-  *fallback = false;
   C.tm->begin(ST_GSORT);
   HIP_TRY(hipMemsetAsync(meta, 0, sizeof(ComposeMeta), st));
   if (mode == GEN_SEG) {
@@ -1868,14 +1929,6 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
                          perm + off, meta);
     }
     C.tm->end(ST_SEGSORT);
-    ComposeMeta hm;
-    int rc = read_meta(C, &hm);
-    if (rc) return rc;
-    if (hm.seg_over) {
-      C.tm->end(ST_GSORT);
-      *fallback = true;
-      return SMX_OK;
-    }
   } else {
     const bool with_lo = mode == GEN_RADIX_LO;
     hipLaunchKernelGGL(k_meta_init, dim3(1), dim3(1), 0, st, meta);
@@ -1917,7 +1970,7 @@ static int run_generic(const Ctx& C, int mode, bool* fallback) {
   }
   const i64 W = SMX_CEIL_DIV(n, (i64)WG_CAP);
   hipLaunchKernelGGL(k_gpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, sts, shi, slo, na, nb,
-                     W, bnd);
+                     W, bnd, meta);
   hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, C.ops->kind, C.ops->v0, C.ops->v1, perm, bnd, na, W,
                      wcnt, meta);
   hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, W, meta);
@@ -1996,17 +2049,19 @@ static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeM
   if (hm->f_fail && !hm->bad_sym && allow_generic) {
     if (C.ops->b_gap != 0)
       return set_err(SMX_E_ARG, "branch logs not timestamp-ordered: the generic plan needs b_gap = 0");
-    bool fallback = true;
-    g_plan = SMX_PLAN_SEGMENTED;
-    if (!(hm->f_fail & 1) && (rc = run_generic(C, GEN_SEG, &fallback))) return rc;  // ordered, long groups
-    if (fallback) {
-      g_plan = SMX_PLAN_RADIX;
-      if ((rc = run_generic(C, GEN_RADIX, &fallback))) return rc;
+    if (!(hm->f_fail & 1)) {  // ordered, long groups: the segmented sort, tail behind it
+      g_plan = SMX_PLAN_SEGMENTED;
+      if ((rc = run_generic(C, GEN_SEG))) return rc;
+      if (tail && (rc = launch_tail(C))) return rc;
       if ((rc = read_meta(C, hm))) return rc;
-      if (hm->dup_key) {
-        g_plan = SMX_PLAN_RADIX_LO;
-        if ((rc = run_generic(C, GEN_RADIX_LO, &fallback))) return rc;
-      }
+      if (!hm->seg_over) return SMX_OK;
+    }
+    g_plan = SMX_PLAN_RADIX;
+    if ((rc = run_generic(C, GEN_RADIX))) return rc;
+    if ((rc = read_meta(C, hm))) return rc;
+    if (hm->dup_key) {
+      g_plan = SMX_PLAN_RADIX_LO;
+      if ((rc = run_generic(C, GEN_RADIX_LO))) return rc;
     }
     if (tail && (rc = launch_tail(C))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
@@ -2057,13 +2112,70 @@ static int run_mvprefix(const Ctx& C, const ComposeMeta& hm, const u64* mvpre) {
 // sync (hipGraph-capturable).  counts[0] < -1 afterwards asks for
 // smx_compose_finish: -2 the plan failed, -3 moves with a None value need their
 // prefix fix-up.
+// Plan-failed counts without the tail: what k_emit4's first thread writes on a failed plan.
+__global__ void k_counts_failed(const ComposeMeta* meta, i64* counts) {
+  counts[0] = meta->bad_sym ? -1 : -2;
+  counts[1] = meta->bad_sym ? -1 : (i64)meta->n_conf;
+}
+
+// The early-failure flag of this host thread on device dev (pinned, coherent).
+static int early_fail_of(int dev, EarlyFail* e) {
+  struct Slot {
+    int dev = -1;
+    EarlyFail e;
+  };
+  static thread_local Slot slots[4];
+  for (auto& s : slots)
+    if (s.dev == dev) {
+      *e = s.e;
+      return SMX_OK;
+    }
+  for (auto& s : slots)
+    if (s.dev < 0) {
+      HIP_TRY(hipHostMalloc((void**)&s.e.flag_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
+      HIP_TRY(hipHostGetDevicePointer((void**)&s.e.flag_dev, s.e.flag_host, 0));
+      HIP_TRY(hipEventCreateWithFlags(&s.e.ev, hipEventDisableTiming));
+      s.dev = dev;
+      *e = s.e;
+      return SMX_OK;
+    }
+  return SMX_E_HIP;  // (more than four devices per host thread: no early flag)
+}
+
+#ifndef SMX_EARLY_MIN
+#define SMX_EARLY_MIN (1ll << 22)  // ops from which a synchronous merge waits for k_khist's verdict
+#endif
+
 static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* ws, const Layout& L,
-                         hipStream_t st, bool timed) {
+                         hipStream_t st, bool timed, bool early_ok = false, bool* early_failed = nullptr) {
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
   StageTimer tm(st, timed);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
   int rc;
-  if ((rc = run_presorted(C, knob("SMX_WIN_TGT", WIN_TGT)))) return rc;
+  // A large synchronous merge (not captured): the host waits for k_khist's verdict while
+  // the windows run, and launches no tail (~20 launches that would only see the failure)
+  // behind a plan that fails for sure -- smx_compose_finish then runs the fallback plan.
+  EarlyFail early;
+  bool use_early = false;
+  if (early_ok && n >= SMX_EARLY_MIN) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    int dev = 0;
+    HIP_TRY(hipStreamIsCapturing(st, &cs));
+    HIP_TRY(hipGetDevice(&dev));
+    use_early = cs == hipStreamCaptureStatusNone && early_fail_of(dev, &early) == SMX_OK;
+    if (use_early) *(volatile u32*)early.flag_host = 0u;  // (the previous merge on this thread has synced)
+  }
+  if ((rc = run_presorted(C, knob("SMX_WIN_TGT", WIN_TGT), use_early ? &early : nullptr))) return rc;
+  if (use_early) {
+    HIP_TRY(hipEventSynchronize(early.ev));
+    if (*(volatile u32*)early.flag_host) {
+      if (early_failed) *early_failed = true;
+      hipLaunchKernelGGL(k_counts_failed, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), out->counts);
+      HIP_TRY(hipGetLastError());
+      tm.flush();
+      return SMX_OK;
+    }
+  }
   if (!knob("SMX_ABLATE", 0) && (rc = launch_tail(C))) return rc;  // SMX_ABLATE (diagnostic builds): window only
   tm.flush();
   return SMX_OK;
@@ -2175,8 +2287,9 @@ static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, v
   return SMX_OK;
 }
 
+// early_ok: the synchronous smx_compose (a host wait for k_khist's verdict is allowed)
 static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
-                              hipStream_t st) {
+                              hipStream_t st, bool early_ok) {
   Layout L{};
   int rc = check_args(ops, out, ws, ws_bytes, &L);
   if (rc) return rc;
@@ -2192,7 +2305,16 @@ static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, vo
     if ((rc = compose_async_graph(ops, out, ws, ws_bytes, L, st, &done))) return rc;
     if (done) return SMX_OK;
   }
-  return enqueue_async(ops, out, ws, L, st, timed);
+  bool early_failed = false;
+  if ((rc = enqueue_async(ops, out, ws, L, st, timed, early_ok, &early_failed))) return rc;
+  if (early_failed && SMX_GRAPH && st != nullptr) {  // a graph of a plan that fails is not worth capturing
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(g_graph_mu);
+    for (auto& e : g_graph)
+      if (graph_key_eq(e, st, dev, ops, out, ws, ws_bytes) && !e.exec) e.nograph = true;
+  }
+  return SMX_OK;
 }
 
 // smx_compose_finish: one host sync; runs whatever the asynchronous part left
@@ -2447,7 +2569,7 @@ extern "C" int smx_compose_async(const smx_ops* ops, const smx_compose_out* out,
   if (!ops) return set_err(SMX_E_ARG, "null ops");
   (void)hipGetLastError();  // an earlier call's error (any library's) is not this call's
   try {
-    return compose_async_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream);
+    return compose_async_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream, false);
   } catch (const std::exception& e) {
     return set_err(SMX_E_HIP, e.what());
   }
@@ -2466,7 +2588,14 @@ extern "C" int smx_compose_finish(const smx_ops* ops, const smx_compose_out* out
 
 extern "C" int smx_compose(const smx_ops* ops, const smx_compose_out* out, void* workspace,
                            size_t workspace_bytes, void* stream) {
-  const int rc = smx_compose_async(ops, out, workspace, workspace_bytes, stream);
+  if (!ops) return set_err(SMX_E_ARG, "null ops");
+  (void)hipGetLastError();  // an earlier call's error (any library's) is not this call's
+  int rc;
+  try {
+    rc = compose_async_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream, true);
+  } catch (const std::exception& e) {
+    return set_err(SMX_E_HIP, e.what());
+  }
   return rc ? rc : smx_compose_finish(ops, out, workspace, workspace_bytes, stream);
 }
 

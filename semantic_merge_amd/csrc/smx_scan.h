@@ -32,20 +32,24 @@ __global__ void __launch_bounds__(BLOCK) k_scan_reduce(const TI* __restrict__ in
 // Exclusive scan of the SCAN_NB partials in place; optionally stores the grand total.
 template <typename Op, typename TO>
 __global__ void __launch_bounds__(BLOCK) k_scan_partials(TO* partials, TO* total_out) {
-  __shared__ TO s[SCAN_NB];
-  for (int i = threadIdx.x; i < SCAN_NB; i += BLOCK) s[i] = partials[i];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    TO acc = Op::template identity<TO>();
-    for (int i = 0; i < SCAN_NB; ++i) {
-      TO x = s[i];
-      s[i] = acc;
-      acc = Op::apply(acc, x);
-    }
-    if (total_out) *total_out = acc;
+  static_assert(SCAN_NB % BLOCK == 0, "whole partials per thread");
+  constexpr int PER = SCAN_NB / BLOCK;
+  __shared__ TO s[NWAVES + 1];
+  TO v[PER];
+  TO acc = Op::template identity<TO>();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {  // consecutive partials per thread
+    v[j] = partials[threadIdx.x * PER + j];
+    acc = Op::apply(acc, v[j]);
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < SCAN_NB; i += BLOCK) partials[i] = s[i];
+  TO total;
+  TO run = block_excl_scan<Op, TO>(acc, s, &total);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    partials[threadIdx.x * PER + j] = run;
+    run = Op::apply(run, v[j]);
+  }
+  if (total_out && threadIdx.x == 0) *total_out = total;
 }
 
 template <typename Op, typename TI, typename TO>

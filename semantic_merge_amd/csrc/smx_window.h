@@ -284,6 +284,10 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   const int lane = t & (WAVE - 1);
   const int wv = t / WAVE;
   const i64 w = blockIdx.x;  // (XCD-ordered presorted windows measured slower: 1.241 -> 1.269 ms, profiles/r03_p)
+  // the plan already failed (k_khist saw a timestamp group no window holds, or an
+  // earlier window overflowed): leave before any load; a scalar read, in flight with
+  // the window bounds' (a stale 0 only defers the exit to the check after the loads)
+  if (P.meta->f_fail) return;
   const i64 a0 = P.bnd[2 * w], b0 = P.bnd[2 * w + 1];
   const int na = (int)(P.bnd[2 * w + 2] - a0);
   const int nb = (int)(P.bnd[2 * w + 3] - b0);
@@ -1127,6 +1131,7 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
   // consecutive windows on one XCD: a timestamp group spans several windows, whose
   // gathers through the permutation then hit the same L2
   const i64 w = SMX_XCD_WIN ? xcd_item(blockIdx.x, P.W) : (i64)blockIdx.x;
+  if (P.meta->f_fail) return;  // the segmented sort failed: no permutation to gather through
   const i64 a0 = P.bnd[2 * w], b0 = P.bnd[2 * w + 1];
   const int na = (int)(P.bnd[2 * w + 2] - a0);
   const int nb = (int)(P.bnd[2 * w + 3] - b0);

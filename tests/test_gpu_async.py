@@ -75,6 +75,29 @@ def test_async_reports_pending_work():
     _check(dc, soa, "none moves")
 
 
+def test_long_groups_fail_before_the_tail():
+    """>= 4M ops whose timestamp groups (8192 ops) no presorted window holds: k_khist flags
+    the plan; the synchronous merge launches no tail behind it and takes the segmented
+    plan, the asynchronous one reports -2 and finish runs it.  Both equal the oracle,
+    and so do repeated merges of the same buffers (no graph is captured for them)."""
+    soa = _lift(4_300_000, 3_000, 19, ops_per_ms=4096, mix=synth.ADVERSARIAL_MIX)
+    dc = _lib.DeviceCompose(soa)
+    s = dc.torch.cuda.Stream()  # a non-null stream: the library's graph cache sees the key
+    for rep in range(3):  # first sight of the key, then the calls a graph would serve
+        dc.order.fill_(-7)
+        dc.torch.cuda.synchronize()
+        dc.run(stream=s)
+        _check(dc, soa, f"sync, long groups ({rep})")
+        assert dc.last_plan() == "segmented"
+    dc.counts.fill_(-7)
+    dc.run_async()
+    dc.torch.cuda.synchronize()
+    assert int(dc.counts[0].item()) == -2
+    dc.finish()
+    _check(dc, soa, "async, long groups")
+    assert dc.last_plan() == "segmented"
+
+
 def test_async_captured_in_a_graph_forked_tail():
     # >= 4M ops: the table scatter runs on the caller's side stream (event fork/join),
     # so the capture holds both streams

@@ -177,6 +177,17 @@ def test_gpu_segmented_plan_clustered_ids():
     assert DeviceCompose.last_plan() == "segmented"
 
 
+def test_gpu_segmented_sort_fails_then_radix():
+    """Ordered logs whose timestamp groups (10k ops) exceed the segmented sort's tiles:
+    the sort flags the plan failed, the kernels queued behind it (windows, walk, tables,
+    emit) leave at once, and the merge's meta read sends it to the radix plan."""
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(300_000, 500, 59, ops_per_ms=10_000)))
+    dc = DeviceCompose(soa)
+    dc.run()
+    _eq_soa(dc.results(), oracle.compose(soa), "segmented sort fails, radix plan")
+    assert dc.last_plan().startswith("radix")
+
+
 @pytest.mark.parametrize("bits", [15, 20, 31], ids=["packed48", "packed64", "wide"])
 def test_gpu_value_widths(bits):
     """Value ids of `bits` bits: 3 x 15 fits the 6-byte final-state table entries,
