@@ -216,10 +216,10 @@ __global__ void k_meta_init(ComposeMeta* meta) {
 #define SMX_KHIST_LONG 1     // k_khist flags timestamp groups longer than a window
 #endif
 #ifndef SMX_FPART_FAILCHK
-#define SMX_FPART_FAILCHK 1  // k_fpart skips its snap and writes on a failed plan
+#define SMX_FPART_FAILCHK 0  // k_fpart skips its snap and writes on a failed plan (off: plan 0.135 -> 0.14 ms on config 3, profiles/r03_x/ab_plan_checks.txt)
 #endif
 #ifndef SMX_CSCAN_FAILCHK
-#define SMX_CSCAN_FAILCHK 1  // the chunk scans leave on a failed plan
+#define SMX_CSCAN_FAILCHK 0  // the chunk scans leave on a failed plan (off, as k_fpart)
 #endif
 
 // Presorted windows: boundary k sits at the merge-path split of diagonal k*tgt
