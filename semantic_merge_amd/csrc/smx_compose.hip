@@ -213,7 +213,7 @@ __global__ void k_meta_init(ComposeMeta* meta) {
 }
 
 #ifndef SMX_KHIST_LONG
-#define SMX_KHIST_LONG 1     // k_khist flags timestamp groups longer than a window
+#define SMX_KHIST_LONG 1     // k_fpart flags timestamp groups longer than a window (from k_khist's samples)
 #endif
 #ifndef SMX_FPART_FAILCHK
 #define SMX_FPART_FAILCHK 0  // k_fpart skips its snap and writes on a failed plan (off: plan 0.135 -> 0.14 ms on config 3, profiles/r03_x/ab_plan_checks.txt)
@@ -232,8 +232,27 @@ __global__ void k_meta_init(ComposeMeta* meta) {
 // the (short) run of equal timestamps.
 __global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB, const u64* __restrict__ sA,
                         const u64* __restrict__ sB, i64 na, i64 nb, i64 W, i64 tgt, i64* __restrict__ bnd,
-                        const ComposeMeta* meta) {
+                        ComposeMeta* meta, u32* long_host) {
   const i64 k = (i64)blockIdx.x * BLOCK + threadIdx.x;
+  if (SMX_KHIST_LONG) {
+    // A chunk sample equal to the sample WF_CAP ops later (A: first ops of chunks c and
+    // c + WF_CAP / CH; B: last ops of full chunks): that timestamp group alone overflows a
+    // window, so the presorted plan cannot hold (config 5's groups).  Flagged before the
+    // windows run: k_window_f then leaves before its loads (6: a window too large, and
+    // smaller windows cannot help).  Grid-stride over the samples, off the search's path.
+    constexpr i64 D = WF_CAP / CH;
+    const i64 nt = (i64)gridDim.x * BLOCK, ca = SMX_CEIL_DIV(na, (i64)CH), cb = nb / CH;
+    bool lg = false;
+    for (i64 c = k; c + D < ca; c += nt) lg |= sA[c] == sA[c + D];
+    for (i64 c = k; c + D < cb; c += nt) lg |= sB[c] == sB[c + D];
+    if (__ballot(lg) && (threadIdx.x & (WAVE - 1)) == 0 &&
+        __hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 6ull) {
+      atomicOr((unsigned long long*)&meta->f_fail, 6ull);
+      // ... and, on the synchronous path, to the host (pinned, coherent), which then
+      // launches no tail behind this failed plan
+      if (long_host) __hip_atomic_store(long_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
   if (k > W) return;
   const u64 failed = SMX_FPART_FAILCHK ? meta->f_fail : 0ull;  // (k_khist saw a group no window holds; used after the search)
   const i64 n = na + nb;
@@ -348,7 +367,6 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
   // KH_R rounds of CH_PER_BLOCK chunks per block; every round's loads are issued first
   u32 w[KH_R][4];
   int nvr[KH_R];
-  bool long_group = false;  // a timestamp run longer than a presorted window
 #pragma unroll
   for (int rd = 0; rd < KH_R; ++rd) {
     const i64 g = ((i64)blockIdx.x * KH_R + rd) * CH_PER_BLOCK + j;
@@ -361,20 +379,8 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
     const u8* src = kind + (side ? na + bgap : 0) + r0;
     // timestamp samples for k_fpart: first op of each A chunk, last op of each full B chunk
     if (g < CA + CB) {
-      // ... and whether the sample and the op WF_CAP later (another chunk's sample: no
-      // extra line) share a timestamp: that group alone overflows a window, so the
-      // presorted plan cannot hold (config 5's groups)
-      if (!side && q == 0) {
-        const u64 v = ts[cc * CH];
-        sA[cc] = v;
-        if (SMX_KHIST_LONG && cc * CH + WF_CAP < na) long_group = v == ts[cc * CH + WF_CAP];
-      }
-      if (side && q == 15 && nv == 16) {
-        const i64 x = cc * CH + CH - 1;
-        const u64 v = ts[na + bgap + x];
-        sB[cc] = v;
-        if (SMX_KHIST_LONG && x + WF_CAP < nb) long_group = v == ts[na + bgap + x + WF_CAP];
-      }
+      if (!side && q == 0) sA[cc] = ts[cc * CH];
+      if (side && q == 15 && nv == 16) sB[cc] = ts[na + bgap + cc * CH + CH - 1];
     }
     w[rd][0] = w[rd][1] = w[rd][2] = w[rd][3] = 0u;
     if (nv == 16 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
@@ -424,15 +430,9 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
       for (int k = 0; k < SMX_N_KINDS; ++k) c[rd * CH_PER_BLOCK + j][k] = (f[k / 3] >> (10 * (k % 3))) & 1023u;
     }
   }
-  if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) meta->bad_sym = 1;
-  // flagged before the windows run: k_fpart, the chunk scans and k_window_f then leave
-  // at once (6: a window too large, and smaller windows cannot help)
-  if (__ballot(long_group) && (threadIdx.x & (WAVE - 1)) == 0 &&
-      __hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 6ull) {
-    atomicOr((unsigned long long*)&meta->f_fail, 6ull);
-    // ... and, on the synchronous path, to the host (pinned, coherent), which then
-    // launches no tail behind this failed plan
-    if (long_host) __hip_atomic_store(long_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) {
+    meta->bad_sym = 1;
+    if (long_host) __hip_atomic_store(long_host + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
   // column-major output: consecutive threads write consecutive chunks of one column;
@@ -1523,9 +1523,10 @@ static int launch_tail(const Ctx& C) {
 // Presorted plan: branch logs with non-decreasing timestamps (what lift.ts
 // emits).  Speculative: k_window_f verifies the layout and flags f_fail.
 
-// early (optional, not inside a graph capture): k_khist raises early->flag when a timestamp
-// group is longer than a window (the plan then fails for sure); early->ev is recorded
-// right behind k_khist, so the host knows before the windows are done.
+// early (optional, not inside a graph capture): k_khist raises early->flag[0] when a
+// timestamp group is longer than a window (the plan then fails for sure) and flag[1] on
+// an invalid kind; early->ev is recorded right behind k_khist, so the host knows before
+// the windows are done.
 struct EarlyFail {
   u32* flag_host = nullptr;
   u32* flag_dev = nullptr;
@@ -1553,10 +1554,10 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
   hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK * KH_R)), dim3(KH_NT), 0, st, C.ops->kind,
                      C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta,
                      early ? early->flag_dev : nullptr);
-  if (early) HIP_TRY(hipEventRecord(early->ev, st));
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
                      C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na,
-                     C.nb, W, tgt, bnd, meta);
+                     C.nb, W, tgt, bnd, meta, early ? early->flag_dev : nullptr);
+  if (early) HIP_TRY(hipEventRecord(early->ev, st));
   {
     const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);
     u32* tsum = C.ws<u32>(B_TSUM);
@@ -2146,8 +2147,14 @@ static int early_fail_of(int dev, EarlyFail* e) {
 #define SMX_EARLY_MIN (1ll << 22)  // ops from which a synchronous merge waits for k_khist's verdict
 #endif
 
+// What the synchronous merge's host learned from k_khist before the windows ran.
+struct EarlyVerdict {
+  bool failed = false;  // the presorted plan fails for sure (f_fail 6)
+  bool bad = false;     // ... and k_khist saw an invalid kind
+};
+
 static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* ws, const Layout& L,
-                         hipStream_t st, bool timed, bool early_ok = false, bool* early_failed = nullptr) {
+                         hipStream_t st, bool timed, bool early_ok = false, EarlyVerdict* verdict = nullptr) {
   const i64 na = ops->n_a, nb = ops->n_b, n = na + nb, n_sym = ops->n_sym;
   StageTimer tm(st, timed);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
@@ -2163,13 +2170,16 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
     HIP_TRY(hipStreamIsCapturing(st, &cs));
     HIP_TRY(hipGetDevice(&dev));
     use_early = cs == hipStreamCaptureStatusNone && early_fail_of(dev, &early) == SMX_OK;
-    if (use_early) *(volatile u32*)early.flag_host = 0u;  // (the previous merge on this thread has synced)
+    if (use_early) early.flag_host[0] = early.flag_host[1] = 0u;  // (the previous merge on this thread has synced)
   }
   if ((rc = run_presorted(C, knob("SMX_WIN_TGT", WIN_TGT), use_early ? &early : nullptr))) return rc;
   if (use_early) {
     HIP_TRY(hipEventSynchronize(early.ev));
-    if (*(volatile u32*)early.flag_host) {
-      if (early_failed) *early_failed = true;
+    if (((volatile u32*)early.flag_host)[0]) {
+      if (verdict) {
+        verdict->failed = true;
+        verdict->bad = ((volatile u32*)early.flag_host)[1] != 0;
+      }
       hipLaunchKernelGGL(k_counts_failed, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), out->counts);
       HIP_TRY(hipGetLastError());
       tm.flush();
@@ -2289,7 +2299,7 @@ static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, v
 
 // early_ok: the synchronous smx_compose (a host wait for k_khist's verdict is allowed)
 static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
-                              hipStream_t st, bool early_ok) {
+                              hipStream_t st, bool early_ok, EarlyVerdict* verdict = nullptr) {
   Layout L{};
   int rc = check_args(ops, out, ws, ws_bytes, &L);
   if (rc) return rc;
@@ -2305,9 +2315,10 @@ static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, vo
     if ((rc = compose_async_graph(ops, out, ws, ws_bytes, L, st, &done))) return rc;
     if (done) return SMX_OK;
   }
-  bool early_failed = false;
-  if ((rc = enqueue_async(ops, out, ws, L, st, timed, early_ok, &early_failed))) return rc;
-  if (early_failed && SMX_GRAPH && st != nullptr) {  // a graph of a plan that fails is not worth capturing
+  EarlyVerdict ev;
+  if ((rc = enqueue_async(ops, out, ws, L, st, timed, early_ok, &ev))) return rc;
+  if (verdict) *verdict = ev;
+  if (ev.failed && SMX_GRAPH && st != nullptr) {  // a graph of a plan that fails is not worth capturing
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     std::lock_guard<std::mutex> g(g_graph_mu);
@@ -2319,8 +2330,10 @@ static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, vo
 
 // smx_compose_finish: one host sync; runs whatever the asynchronous part left
 // (the fallback plans, the None-value move prefix) and the final counts.
+// known: the synchronous merge's early verdict (the plan failed): no meta read needed
+// before the fallback plan -- k_khist was the last kernel to write the meta's flags
 static int compose_finish_impl(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
-                               hipStream_t st) {
+                               hipStream_t st, const EarlyVerdict* known = nullptr) {
   Layout L{};
   int rc = check_args(ops, out, ws, ws_bytes, &L);
   if (rc) return rc;
@@ -2329,7 +2342,13 @@ static int compose_finish_impl(const smx_ops* ops, const smx_compose_out* out, v
   StageTimer tm(st, profiling_on() != 0);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
   ComposeMeta hm;
-  if ((rc = read_meta(C, &hm))) return rc;
+  if (known && known->failed) {
+    std::memset(&hm, 0, sizeof(hm));
+    hm.f_fail = 6;
+    hm.bad_sym = known->bad ? 1 : 0;
+  } else if ((rc = read_meta(C, &hm))) {
+    return rc;
+  }
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
   if (hm.f_fail && (rc = order_fallbacks(C, true, true, &hm, knob("SMX_WIN_TGT", WIN_TGT)))) return rc;
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
@@ -2592,11 +2611,13 @@ extern "C" int smx_compose(const smx_ops* ops, const smx_compose_out* out, void*
   (void)hipGetLastError();  // an earlier call's error (any library's) is not this call's
   int rc;
   try {
-    rc = compose_async_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream, true);
+    EarlyVerdict ev;
+    rc = compose_async_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream, true, &ev);
+    if (!rc) rc = compose_finish_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream, &ev);
   } catch (const std::exception& e) {
     return set_err(SMX_E_HIP, e.what());
   }
-  return rc ? rc : smx_compose_finish(ops, out, workspace, workspace_bytes, stream);
+  return rc;
 }
 
 extern "C" int smx_last_plan(void) { return g_plan; }

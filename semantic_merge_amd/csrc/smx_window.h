@@ -456,6 +456,8 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     const int d0 = t * WF_ITEMS < sz ? t * WF_ITEMS : sz;
     const int d1 = d0 + WF_ITEMS < sz ? d0 + WF_ITEMS : sz;
     int lo = d0 - nb > 0 ? d0 - nb : 0, hi = d0 < na ? d0 : na;
+    // (a fixed count of predicated halving steps measured slower: window 1.225 -> 1.270 ms,
+    //  profiles/r03_x/ab_merge_search_fixed_steps.txt)
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (sts[mid] <= sts[na + d0 - 1 - mid]) lo = mid + 1;

@@ -10,3 +10,5 @@ timeout -k 10 300 python -u tools/bench_rga.py > $O/bench_rga.json 2> $O/bench_r
 cut -c1-300 $O/bench_c5.json $O/bench_rga.json
 (cd /tmp && export TMPDIR=/tmp && RGA_NO_CPU=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/prof_rga" -o r -- python3 "$R/tools/bench_rga.py" > "$O/prof_rga.log" 2>&1) || { tail -5 "$O/prof_rga.log"; exit 1; }
 python3 tools/prof_export.py "$O/prof_rga" "$O/rga_kernel_stats.csv" && head -8 "$O/rga_kernel_stats.csv"
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/prof_c5" -o c5 -- python3 "$R/bench.py" --config c5 --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-pmc > "$O/prof_c5.log" 2>&1) || { tail -5 "$O/prof_c5.log"; exit 1; }
+python3 tools/prof_export.py "$O/prof_c5" "$O/c5_kernel_stats.csv" && python3 tools/prof_timeline.py "$O/prof_c5" 60 > "$O/c5_timeline.txt" && tail -3 "$O/c5_timeline.txt"
