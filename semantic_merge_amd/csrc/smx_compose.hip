@@ -555,7 +555,10 @@ __device__ __forceinline__ void wc_add_bytes(u32 x, u32 (&c)[SMX_N_KINDS], bool&
   for (int q = 0; q < 4; ++q) wc_add_one((x >> (8 * q)) & 0xffu, c, bad);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, const i32* __restrict__ v0,
+#ifndef WC_NT
+#define WC_NT BLOCK  // threads per generic window in k_wcount
+#endif
+__global__ void __launch_bounds__(WC_NT) k_wcount(const u8* __restrict__ kind, const i32* __restrict__ v0,
                                                   const i32* __restrict__ v1, const u32* __restrict__ perm,
                                                   const i64* __restrict__ bnd, i64 na, i64 W,
                                                   u32* __restrict__ wcnt, ComposeMeta* meta) {
@@ -576,12 +579,12 @@ __global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, c
       for (int kk = 0; kk < SMX_N_KINDS; ++kk) cnt[kk] = 0;
       const i64 alo = (lo + 15) & ~(i64)15, ahi = hi & ~(i64)15;
       if (alo >= ahi) {  // short range: bytes
-        for (i64 j = lo + threadIdx.x; j < hi; j += BLOCK) wc_add_one(kind[j], cnt, bad);
+        for (i64 j = lo + threadIdx.x; j < hi; j += WC_NT) wc_add_one(kind[j], cnt, bad);
       } else {
-        for (i64 j = lo + threadIdx.x; j < alo; j += BLOCK) wc_add_one(kind[j], cnt, bad);
-        for (i64 j = ahi + threadIdx.x; j < hi; j += BLOCK) wc_add_one(kind[j], cnt, bad);
+        for (i64 j = lo + threadIdx.x; j < alo; j += WC_NT) wc_add_one(kind[j], cnt, bad);
+        for (i64 j = ahi + threadIdx.x; j < hi; j += WC_NT) wc_add_one(kind[j], cnt, bad);
         const uint4* v = (const uint4*)(kind + alo);
-        for (i64 q = threadIdx.x; q < (ahi - alo) / 16; q += BLOCK) {
+        for (i64 q = threadIdx.x; q < (ahi - alo) / 16; q += WC_NT) {
           const uint4 x = v[q];
           wc_add_bytes(x.x, cnt, bad);
           wc_add_bytes(x.y, cnt, bad);
@@ -602,7 +605,7 @@ __global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, c
     // a window holds at most WG_CAP ops: WC_ITEMS per thread, every load issued before
     // any is used (the perm -> kind -> value chain is one round trip per level, not one
     // per item); the item count is fixed, so the ballots stay wave-uniform
-    constexpr int WC_ITEMS = (WG_CAP + BLOCK - 1) / BLOCK;
+    constexpr int WC_ITEMS = (WG_CAP + WC_NT - 1) / WC_NT;
     const u64 lt = lanemask_lt();
     const i64 nA = a1 - a0, nW = nA + (b1 - b0);
     u32 src[WC_ITEMS], kv[WC_ITEMS];
@@ -610,7 +613,7 @@ __global__ void __launch_bounds__(BLOCK) k_wcount(const u8* __restrict__ kind, c
     bool val[WC_ITEMS], sd[WC_ITEMS];
 #pragma unroll
     for (int i = 0; i < WC_ITEMS; ++i) {
-      const i64 e = (i64)i * BLOCK + threadIdx.x;
+      const i64 e = (i64)i * WC_NT + threadIdx.x;
       val[i] = e < nW && e < WG_CAP;
       sd[i] = e >= nA;
       src[i] = val[i] ? perm[sd[i] ? na + b0 + (e - nA) : a0 + e] : 0u;
@@ -1972,7 +1975,7 @@ static int run_generic(const Ctx& C, int mode) {
   const i64 W = SMX_CEIL_DIV(n, (i64)WG_CAP);
   hipLaunchKernelGGL(k_gpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, sts, shi, slo, na, nb,
                      W, bnd, meta);
-  hipLaunchKernelGGL(k_wcount, dim3(W), dim3(BLOCK), 0, st, C.ops->kind, C.ops->v0, C.ops->v1, perm, bnd, na, W,
+  hipLaunchKernelGGL(k_wcount, dim3(W), dim3(WC_NT), 0, st, C.ops->kind, C.ops->v0, C.ops->v1, perm, bnd, na, W,
                      wcnt, meta);
   hipLaunchKernelGGL(k_wscan, dim3(NCNT), dim3(BLOCK), 0, st, wcnt, woff, W, meta);
   hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta, (u64)W);

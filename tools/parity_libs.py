@@ -15,8 +15,10 @@ def main():
     import torch  # noqa: F401
     from oracle import oracle
     from semantic_merge_amd import _abi, _lib, synth
-    cases = [synth.lift_soa(synth.lift_logs(synth.LiftSpec(n, s, seed)))
-             for n, s, seed in ((5000, 50, 1), (20_000, 200, 3), (300_000, 3000, 5))]
+    specs = [synth.LiftSpec(n, s, seed) for n, s, seed in ((5000, 50, 1), (20_000, 200, 3), (300_000, 3000, 5))]
+    specs += [synth.LiftSpec(600_000, 2_000, 17, ops_per_ms=4096, mix=synth.ADVERSARIAL_MIX),  # segmented plan
+              synth.LiftSpec(300_000, 3_000, 7, shuffle=True)]                                 # radix plan
+    cases = [synth.lift_soa(synth.lift_logs(sp)) for sp in specs]
     refs = [oracle.compose(c) for c in cases]
     for item in sys.argv[1:]:
         name, path = item.split("=", 1)
