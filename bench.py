@@ -277,8 +277,12 @@ def main() -> None:
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     lib = _lib.lib()
-    # the stage timers (HIP events on the call's stream) run in the timed steps; timed
-    # merges enqueue their launches directly (the graph replay is the graph_api leg)
+    # the timed steps carry HIP events around the roofline kernels' stages only (an event
+    # pair around every stage of every merge cost ~2% of config 3's step); timed merges
+    # enqueue their launches directly (the graph replay is the graph_api leg).  The full
+    # per-stage breakdown comes from an untimed leg after them.
+    names = [lib.smx_stage_name(i).decode() for i in range(32)]
+    lib.smx_set_profiling_stages(sum(1 << i for i, nm in enumerate(names) if nm in ROOF_STAGES))
     lib.smx_set_profiling(1)
     for _ in range(args.warmup):
         run()
@@ -297,6 +301,16 @@ def main() -> None:
     lib.smx_set_profiling(0)
     plan = _lib.DeviceCompose.last_plan()
     stages = _lib.stage_times()
+    # per-stage breakdown (every stage timed), outside the timed region
+    lib.smx_set_profiling_stages(0xFFFFFFFF)
+    lib.smx_reset_stage_times()
+    lib.smx_set_profiling(1)
+    for _ in range(min(args.steps, 5)):
+        run()
+    torch.cuda.synchronize(dev)
+    lib.smx_set_profiling(0)
+    stages_all = _lib.stage_times()
+    lib.smx_reset_stage_times()
     if sharded:
         k, nconf = sc.totals()
     else:
@@ -440,7 +454,7 @@ def main() -> None:
             "pipeline_traffic": pmc.get("pipeline_traffic") if pmc else None,
         },
         "pmc": pmc,
-        "stages_ms_per_step": {k2: round(v[0] / max(v[1], 1), 4) for k2, v in stages.items()
+        "stages_ms_per_step": {k2: round(v[0] / max(v[1], 1), 4) for k2, v in stages_all.items()
                                if v[1]},
         "cpu_baseline": cpu,
         "end_to_end": e2e,

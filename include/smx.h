@@ -226,9 +226,12 @@ int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const smx_compose
  * benchmark: when enabled, each stage is bracketed by hipEvents on the call's
  * stream and the elapsed milliseconds are accumulated per stage.
  * smx_stage_times copies up to `cap` entries and returns the number of stages;
- * smx_stage_name(i) names stage i.
+ * smx_stage_name(i) names stage i.  smx_set_profiling_stages limits the timing to the
+ * stages whose bit (1 << i) is set (default: all), so that a benchmark can time one
+ * kernel without an event pair around every stage of every merge.
  */
 int smx_set_profiling(int enabled);
+int smx_set_profiling_stages(uint32_t mask);
 int smx_stage_times(double* ms, int64_t* calls, int cap);
 const char* smx_stage_name(int i);
 int smx_reset_stage_times(void);

@@ -109,6 +109,7 @@ EXPORTS = (
     "smx_last_plan",
     "smx_shard_step",
     "smx_set_profiling",
+    "smx_set_profiling_stages",
     "smx_stage_times",
     "smx_stage_name",
     "smx_reset_stage_times",
@@ -137,6 +138,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.smx_shard_step.restype = C.c_int
     lib.smx_set_profiling.argtypes = [C.c_int]
     lib.smx_set_profiling.restype = C.c_int
+    lib.smx_set_profiling_stages.argtypes = [C.c_uint32]
+    lib.smx_set_profiling_stages.restype = C.c_int
     lib.smx_stage_times.argtypes = [C.POINTER(C.c_double), c_i64p, C.c_int]
     lib.smx_stage_times.restype = C.c_int
     lib.smx_stage_name.argtypes = [C.c_int]

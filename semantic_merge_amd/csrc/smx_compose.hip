@@ -61,6 +61,7 @@ static const char* kStageNames[ST_N] = {"plan",   "gsort",    "window", "walk", 
                                         "mvprefix", "emit", "segsort", "window_g"};
 static std::mutex g_prof_mu;
 static int g_prof = 0;
+static u32 g_prof_mask = ~0u;  // the stages timed while profiling is on (smx_set_profiling_stages)
 static double g_stage_ms[ST_N];
 static int64_t g_stage_calls[ST_N];
 
@@ -96,12 +97,18 @@ static void ev_release_locked(hipEvent_t e) {  // (caller holds g_prof_mu)
 struct StageTimer {
   hipStream_t st;
   bool on;
+  u32 mask = ~0u;
   hipEvent_t open[ST_N];
   std::vector<PendingEv> done;
   bool is_open[ST_N] = {};
-  StageTimer(hipStream_t s, bool enabled) : st(s), on(enabled) {}
+  StageTimer(hipStream_t s, bool enabled) : st(s), on(enabled) {
+    if (on) {
+      std::lock_guard<std::mutex> g(g_prof_mu);
+      mask = g_prof_mask;
+    }
+  }
   void begin(int i) {
-    if (!on) return;
+    if (!on || !((mask >> i) & 1u)) return;
     if (!is_open[i]) open[i] = ev_acquire();  // (a restarted stage re-records its open event)
     (void)hipEventRecord(open[i], st);
     is_open[i] = true;
@@ -2628,6 +2635,12 @@ extern "C" int smx_last_plan(void) { return g_plan; }
 extern "C" int smx_set_profiling(int enabled) {
   std::lock_guard<std::mutex> g(g_prof_mu);
   g_prof = enabled;
+  return SMX_OK;
+}
+
+extern "C" int smx_set_profiling_stages(uint32_t mask) {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  g_prof_mask = mask;
   return SMX_OK;
 }
 
