@@ -1,7 +1,7 @@
 """Benchmark: op-log compose+conflict throughput on device-resident synthetic logs.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--n-ops N]
-                    [--weak | --independent] [--no-pmc] [--no-cpu-baseline] [--no-e2e] [--no-async]
+                    [--weak | --independent] [--no-pmc] [--no-cpu-baseline] [--no-e2e] [--no-async] [--no-breakdown]
 
 One step = one composition (semmerge/compose.py:11-114 restated on the GPU) of
 SURVEY §8(d) config 3: 100M lift-shaped ops (50M per branch), 1M symbols, seed 11.
@@ -79,7 +79,7 @@ def pmc_traffic(args) -> dict:
         cmd = [exe, "--pmc", counter, "--kernel-include-regex", "k_", "-d", d, "-o", "p",
                "--output-format", "csv", "--", sys.executable, os.path.join(REPO, "bench.py"),
                "--steps", "2", "--warmup", "1", "--config", args.config, "--no-cpu-baseline",
-               "--no-pmc", "--no-e2e", "--no-async"]
+               "--no-pmc", "--no-e2e", "--no-async", "--no-breakdown"]
         if args.n_ops:
             cmd += ["--n-ops", str(args.n_ops)]
         if args.n_sym:
@@ -213,6 +213,8 @@ def main() -> None:
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
     ap.add_argument("--no-e2e", action="store_true", help="skip the drop-in end-to-end leg")
     ap.add_argument("--no-async", action="store_true", help="skip the smx_compose_async pipeline leg")
+    ap.add_argument("--no-breakdown", action="store_true",
+                    help="skip the untimed per-stage breakdown leg (the PMC child: exactly 3 merges)")
     ap.add_argument("--e2e-ops", type=int, default=100_000)
     ap.add_argument("--verify", action="store_true", help="check GPU == oracle (slow, N = 1)")
     ap.add_argument("--weak", action="store_true", help="N > 1: N x the config's ops (weak scaling)")
@@ -303,14 +305,16 @@ def main() -> None:
     stages = _lib.stage_times()
     # per-stage breakdown (every stage timed), outside the timed region
     lib.smx_set_profiling_stages(0xFFFFFFFF)
-    lib.smx_reset_stage_times()
-    lib.smx_set_profiling(1)
-    for _ in range(min(args.steps, 5)):
-        run()
-    torch.cuda.synchronize(dev)
-    lib.smx_set_profiling(0)
-    stages_all = _lib.stage_times()
-    lib.smx_reset_stage_times()
+    stages_all = stages
+    if not args.no_breakdown:
+        lib.smx_reset_stage_times()
+        lib.smx_set_profiling(1)
+        for _ in range(min(args.steps, 5)):
+            run()
+        torch.cuda.synchronize(dev)
+        lib.smx_set_profiling(0)
+        stages_all = _lib.stage_times()
+        lib.smx_reset_stage_times()
     if sharded:
         k, nconf = sc.totals()
     else:
