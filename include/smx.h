@@ -20,6 +20,14 @@
  * workspace (the library's side stream and fork/join events are kept per caller
  * stream; tests/test_gpu_async.py runs two threads on one GPU).
  *
+ * Graph cache: the second smx_compose / smx_compose_async with the same (stream,
+ * inputs, outputs, workspace) captures the merge's launches into a HIP graph that
+ * later calls replay.  The library keeps the stream handle only as part of that key:
+ * it never synchronizes the caller's stream after a call returns (eviction waits on
+ * an event of its own), so the stream may be destroyed at any time.
+ * smx_release_graphs(stream) (NULL: every stream) drops the cached graphs, e.g.
+ * before freeing the buffers they were captured with.
+ *
  * Return value: 0 on success, a negative SMX_E* code otherwise; the message is
  * available from smx_last_error() (thread-local).  Nothing aborts the process.
  */
@@ -116,6 +124,9 @@ int smx_compose_async(const smx_ops* ops, const smx_compose_out* out, void* work
 int smx_compose_finish(const smx_ops* ops, const smx_compose_out* out, void* workspace,
                        size_t workspace_bytes, void* stream);
 
+/* Drop the library's cached merge graphs of `stream` (NULL: of every stream). */
+int smx_release_graphs(void* stream);
+
 /* The order plan the last composition on this thread ran (bench reporting). */
 #define SMX_PLAN_PRESORTED 0 /* timestamp-ordered logs: presorted windows */
 #define SMX_PLAN_SEGMENTED 1 /* ordered logs with long equal-timestamp groups */
@@ -142,7 +153,9 @@ int smx_last_plan(void);
  *                     (bit 0 not ordered, bit 1 invalid input, bit 2 a window
  *                     overflowed on dense timestamp ties) and is repaired by
  *   SMX_SHARD_ORDER_FIX  the plan fallbacks (smaller windows; with b_gap = 0 the
- *                     generic plan); rewrites summary[0..21] and the exports
+ *                     segmented or radix plan, never for a slice whose timestamps
+ *                     decrease: that returns SMX_E_ARG); rewrites summary[0..21]
+ *                     and the exports
  *   SMX_SHARD_WALK    DivergentRename walk with the halo (the next shards'
  *                     exports) and an incoming open region (in_ahead, in_d);
  *                     may be re-run when the incoming region changes;
@@ -151,7 +164,8 @@ int smx_last_plan(void);
  *                     over shards next); writes summary[28..30].  ORDER and
  *                     ORDER_FIX already bucket the table records (beside the
  *                     walk); TABLES applies the walk's skips to them, which it can
- *                     do once:
+ *                     do once (a second TABLES without ORDER / ORDER_FIX / SCATTER
+ *                     in between returns SMX_E_ARG):
  *   SMX_SHARD_SCATTER re-buckets the records, for a TABLES after a WALK re-run
  *   SMX_SHARD_EMIT    composed output from the reduced tables (fin_tab) and
  *                     the global value widths (glob[0..2]); mv_prefix (or NULL

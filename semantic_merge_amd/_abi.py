@@ -106,6 +106,7 @@ EXPORTS = (
     "smx_compose",
     "smx_compose_async",
     "smx_compose_finish",
+    "smx_release_graphs",
     "smx_last_plan",
     "smx_shard_step",
     "smx_set_profiling",
@@ -131,6 +132,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     for f in ("smx_compose_async", "smx_compose_finish"):
         getattr(lib, f).argtypes = lib.smx_compose.argtypes
         getattr(lib, f).restype = C.c_int
+    lib.smx_release_graphs.argtypes = [C.c_void_p]
+    lib.smx_release_graphs.restype = C.c_int
     lib.smx_last_plan.argtypes = []
     lib.smx_last_plan.restype = C.c_int
     lib.smx_shard_step.argtypes = [C.POINTER(SmxOps), C.POINTER(SmxShard), C.POINTER(SmxComposeOut),

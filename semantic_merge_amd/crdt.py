@@ -124,17 +124,73 @@ def replay_lists(streams: Sequence[Sequence[Event]]) -> List[List[Elem]]:
 
 
 class RGA:
-    """Drop-in for crdt.py:23-46: same methods; state is the recorded stream.  ``list``
-    is the reference's ``List[Elem]`` state, computed on the GPU from the stream when it
-    is read (a fresh list of fresh ``Elem`` objects each time: mutating it does not
-    change the RGA, which is why it is read-only here)."""
+    """Drop-in for crdt.py:23-46: same methods, and ``list`` (crdt.py:26-27) is the
+    reference's mutable ``List[Elem]`` state.
+
+    Events are recorded and replayed on the GPU (``smx_rga_replay``) when the state is
+    needed.  Reading ``list`` folds the pending events into the state and returns the
+    SAME list object on every read until new events arrive, so ``rga.list.append(e)`` or
+    ``rga.list[0].tombstone = True`` change the RGA as they do in the reference;
+    assigning ``rga.list = [...]`` replaces the state.  A later fold replays the state as
+    a prefix of the stream (each live element as its insert; each tombstoned one as an
+    insert of a private value that is then deleted, so no later event can touch it) and
+    keeps the existing ``Elem`` objects: a later ``delete`` sets ``tombstone`` on them in
+    place, as crdt.py:40-43 does.  The device replay relies on the list being in key
+    order (what ``insert`` and ``move`` maintain, crdt.py:48-57); a state the caller put
+    out of key order raises ``ValueError`` instead of being replayed differently."""
 
     def __init__(self) -> None:
         self._events: List[Event] = []
+        self._list: "List[Elem] | None" = None  # the state, once read or assigned
 
     @property
     def list(self) -> List[Elem]:
-        return replay_lists([self._events])[0]
+        if self._list is None or self._events:
+            self._list = self._fold()
+            self._events = []
+        return self._list
+
+    @list.setter
+    def list(self, value: List[Elem]) -> None:
+        self._list = value
+        self._events = []
+
+    def _fold(self) -> List[Elem]:
+        base = self._list or []
+        if not base:
+            return replay_lists([self._events])[0]
+        prev = None
+        stream: List[Event] = []
+        origin: List[int] = []  # stream index -> base index (-1: a later event)
+        for i, e in enumerate(base):
+            k = (e.key.anchor, e.key.t, e.key.author, e.key.opid)
+            if prev is not None and k < prev:
+                raise ValueError("RGA.list is not in key order (element %d): the GPU replay needs the "
+                                 "order insert() and move() keep" % i)
+            prev = k
+            if e.tombstone:
+                tag = object()  # equal to nothing else: no later move/delete reaches it
+                stream.append((INSERT, e.key, tag))
+                stream.append((DELETE, None, tag))
+                origin += [i, -1]
+            else:
+                stream.append((INSERT, e.key, e.value))
+                origin.append(i)
+        nb = len(stream)
+        stream += self._events
+        origin += [-1] * len(self._events)
+        src, tomb = _replay_list_src(stream)
+        out: List[Elem] = []
+        for s, tb in zip(src, tomb):
+            if s < nb:
+                e = base[origin[s]]
+                if tb:
+                    e.tombstone = True
+            else:
+                _, key, value = stream[s]
+                e = Elem(key, value, bool(tb))
+            out.append(e)
+        return out
 
     def insert(self, key: Key, value: str) -> None:
         self._events.append((INSERT, key, value))
@@ -146,4 +202,16 @@ class RGA:
         self._events.append((DELETE, None, value))
 
     def materialize(self) -> List[str]:
-        return replay([self._events])[0]
+        if self._list is None:
+            return replay([self._events])[0]
+        return [e.value for e in self.list if not e.tombstone]
+
+
+def _replay_list_src(stream: Sequence[Event]) -> Tuple[List[int], List[int]]:
+    """One stream in list mode on the GPU: (creating event index, tombstone) per element
+    of the final list, in list order."""
+    from ._lib import rga_replay_device  # the HIP library; raises if missing
+    batch = marshal_streams([stream])
+    _, src, offsets, tomb = rga_replay_device(batch, tombstones=True)
+    n = int(offsets[1])
+    return src[:n].tolist(), tomb[:n].tolist()

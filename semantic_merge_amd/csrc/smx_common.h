@@ -26,6 +26,7 @@ typedef uint8_t u8;
 // Device-side state of one smx_compose call (lives at the start of the workspace).
 // Counters written by kernels; read by later kernels and (once) by the host.
 #define SEG_FAIL_BIT 8ull
+#define SEG_DECREASE 2ull  // meta->seg_over: a timestamp decreases (the segmented sort)
 struct ComposeMeta {
   u64 kcnt[SMX_N_KINDS];     // ops per precedence rank (stats kernel)
   u64 base[SMX_N_KINDS + 1]; // exclusive prefix of kcnt: T-order segment starts
@@ -49,7 +50,7 @@ struct ComposeMeta {
   u64 n_conf_loc;            // conflicts of this shard's own regions (scan total)
   u64 nskip_in;              // skipped renames of the incoming region (head of the skip list)
   u64 dup_key;               // generic plan: equal (ts, oid_hi) pair seen -> sort with oid_lo
-  u64 seg_over;              // segmented plan: a timestamp group too long, or a branch not ordered
+  u64 seg_over;              // segmented plan: bit 0 a timestamp group too long, bit 1 a branch not ordered
   u64 n_win;                 // windows of the plan that ran
   u32 kmask[2];              // presorted plan: kinds present per branch (k_khist)
 };

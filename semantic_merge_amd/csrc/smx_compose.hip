@@ -128,6 +128,11 @@ struct StageTimer {
   }
   ~StageTimer() {  // an error path left events unpublished: back to the pool
     if (done.empty() && !std::any_of(is_open, is_open + ST_N, [](bool b) { return b; })) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+      (void)hipGetLastError();
+      return;  // a capturing stream must not be synchronized: these events are left to leak
+    }
     (void)hipStreamSynchronize(st);  // (recorded events may still be pending)
     std::lock_guard<std::mutex> g(g_prof_mu);
     for (auto& p : done) {
@@ -1677,8 +1682,11 @@ __device__ __forceinline__ void seg_pass(u64 (&v)[8], u32 base, u32 b, u32 k, in
 // that every kernel queued behind the sort (k_gpart, k_wcount, k_window_g, the tail)
 // leaves at once -- the host learns it from the merge's one meta read and runs the
 // radix plan then (no host round trip between the sort and the windows).
-__device__ __forceinline__ void seg_fail(ComposeMeta* meta) {
-  meta->seg_over = 1;
+// seg_over bit 0: a timestamp group longer than a tile holds (the branch is ordered: the
+// radix plan orders it); bit 1 (SEG_DECREASE): a timestamp decreases (a sharded range
+// slice must then fail, not be radix-sorted locally: smx_shard_step ORDER_FIX).
+__device__ __forceinline__ void seg_fail(ComposeMeta* meta, bool decrease) {
+  atomicOr((unsigned long long*)&meta->seg_over, decrease ? (unsigned long long)SEG_DECREASE : 1ull);
   atomicOr((unsigned long long*)&meta->f_fail, (unsigned long long)SEG_FAIL_BIT);
 }
 
@@ -1706,12 +1714,12 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
   const u64 v0 = ts[p0];
   const bool has_end = p0 + SEG_H < cnt;
   const u64 v1 = has_end ? ts[p0 + SEG_H] : 0;
-  bool bad = false;
+  bool dec = false, bad = false;
   u32 c0 = 0, c1 = 0;
 #pragma unroll
   for (int r = 0; r < SEG_H / SEG_NT; ++r) {
     const i64 i = p0 + r * SEG_NT + t;
-    if (i + 1 < cnt) bad |= ts[i + 1] < ts[i];
+    if (i + 1 < cnt) dec |= ts[i + 1] < ts[i];
   }
 #pragma unroll
   for (int r = 0; r < W / SEG_NT; ++r) {
@@ -1731,14 +1739,15 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
   // a group reaching below its window: longer than the tile scheme allows
   if (t == 0 && p0 - W > 0 && ts[p0 - W - 1] == v0) bad = true;
   if (t == 1 && has_end && a1 > 0 && ts[a1 - 1] == v1) bad = true;
-  if (__syncthreads_or(bad)) {
-    if (t == 0) seg_fail(meta);
+  const bool any_dec = __syncthreads_or(dec);
+  if (any_dec | __syncthreads_or(bad)) {
+    if (t == 0) seg_fail(meta, any_dec);
     return;
   }
   const i64 s = a0 + se[0], size = (has_end ? a1 + se[1] : cnt) - s;
   if (size <= 0) return;
   if (size > SEG_CAP) {
-    if (t == 0) seg_fail(meta);
+    if (t == 0) seg_fail(meta, false);
     return;
   }
   u32 P = 8, lgP = 3;
@@ -2004,8 +2013,15 @@ static int run_generic(const Ctx& C, int mode) {
 
 // The meta block comes back through a pinned staging buffer (one per host thread): a
 // DMA, not the runtime's staged copy into pageable memory.
+struct PinnedMeta {  // freed when its host thread exits (thread-pool callers)
+  ComposeMeta* p = nullptr;
+  ~PinnedMeta() {
+    if (p) (void)hipHostFree(p);
+  }
+};
 static int read_meta(const Ctx& C, ComposeMeta* hm) {
-  static thread_local ComposeMeta* pinned = nullptr;
+  static thread_local PinnedMeta holder;
+  ComposeMeta*& pinned = holder.p;
   if (!pinned) HIP_TRY(hipHostMalloc((void**)&pinned, sizeof(ComposeMeta), hipHostMallocDefault));
   HIP_TRY(hipMemcpyAsync(pinned, C.ws<ComposeMeta>(B_META), sizeof(ComposeMeta), hipMemcpyDeviceToHost, C.st));
   HIP_TRY(hipStreamSynchronize(C.st));
@@ -2048,8 +2064,17 @@ static thread_local int g_plan = SMX_PLAN_PRESORTED;
 // a window that overflows LDS (dense timestamp ties) retries with smaller windows;
 // a log that is not timestamp-ordered goes to the generic plan when allowed.  The
 // tail (walk, tables, emit) is launched behind each plan when `tail`.
-static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm, i64 tgt) {
+// require_ordered (a sharded range slice): a slice whose timestamps decrease must fail
+// loudly -- the radix plan would order it locally, not across the shards -- so it is
+// refused when the window kernel (f_fail bit 0) or the segmented sort (SEG_DECREASE)
+// saw a decrease.  (k_fpart's early verdict, f_fail 6, can hide bit 0: then the
+// segmented sort runs and reports the decrease itself.)
+static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm, i64 tgt,
+                           bool require_ordered = false) {
   int rc;
+  auto unordered = [&]() {
+    return set_err(SMX_E_ARG, "sharded merge needs timestamp-ordered branch logs in every shard");
+  };
   g_plan = SMX_PLAN_PRESORTED;
   while (hm->f_fail == 2 && !hm->bad_sym && tgt > WIN_TGT_MIN) {  // dense groups: smaller windows
     tgt = (tgt / 2) / CH * CH;
@@ -2060,12 +2085,14 @@ static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeM
   if (hm->f_fail && !hm->bad_sym && allow_generic) {
     if (C.ops->b_gap != 0)
       return set_err(SMX_E_ARG, "branch logs not timestamp-ordered: the generic plan needs b_gap = 0");
+    if (require_ordered && (hm->f_fail & 1)) return unordered();
     if (!(hm->f_fail & 1)) {  // ordered, long groups: the segmented sort, tail behind it
       g_plan = SMX_PLAN_SEGMENTED;
       if ((rc = run_generic(C, GEN_SEG))) return rc;
       if (tail && (rc = launch_tail(C))) return rc;
       if ((rc = read_meta(C, hm))) return rc;
       if (!hm->seg_over) return SMX_OK;
+      if (require_ordered && (hm->seg_over & SEG_DECREASE)) return unordered();
     }
     g_plan = SMX_PLAN_RADIX;
     if ((rc = run_generic(C, GEN_RADIX))) return rc;
@@ -2135,14 +2162,28 @@ static int early_fail_of(int dev, EarlyFail* e) {
     int dev = -1;
     EarlyFail e;
   };
-  static thread_local Slot slots[4];
-  for (auto& s : slots)
-    if (s.dev == dev) {
+  struct Slots {  // the pinned flags and events, freed when the host thread exits
+    Slot s[4];
+    ~Slots() {
+      for (auto& x : s) {
+        if (x.dev < 0) continue;
+        int cur = 0;
+        if (hipGetDevice(&cur) == hipSuccess && cur != x.dev) (void)hipSetDevice(x.dev);
+        if (x.e.ev) (void)hipEventDestroy(x.e.ev);
+        if (x.e.flag_host) (void)hipHostFree(x.e.flag_host);
+        if (cur != x.dev) (void)hipSetDevice(cur);
+      }
+    }
+  };
+  static thread_local Slots holder;
+  Slot* slots = holder.s;
+  for (int i = 0; i < 4; ++i)
+    if (Slot& s = slots[i]; s.dev == dev) {
       *e = s.e;
       return SMX_OK;
     }
-  for (auto& s : slots)
-    if (s.dev < 0) {
+  for (int i = 0; i < 4; ++i)
+    if (Slot& s = slots[i]; s.dev < 0) {
       HIP_TRY(hipHostMalloc((void**)&s.e.flag_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
       HIP_TRY(hipHostGetDevicePointer((void**)&s.e.flag_dev, s.e.flag_host, 0));
       HIP_TRY(hipEventCreateWithFlags(&s.e.ev, hipEventDisableTiming));
@@ -2224,6 +2265,9 @@ struct GraphEntry {
   hipGraph_t graph = nullptr;  // kept while exec lives: on this ROCm an exec replays
                                // node parameters its graph owns (destroying the graph
                                // after instantiation corrupted the later replays)
+  hipEvent_t done = nullptr;   // recorded behind every replay: eviction waits on it, never
+                               // on the caller's stream (which may be gone by then, or in
+                               // the middle of the caller's own capture)
   u64 used = 0;
   bool nograph = false;        // capturing this key failed: enqueue directly
 };
@@ -2233,10 +2277,11 @@ static u64 g_graph_tick = 0;
 
 static void graph_release_locked(GraphEntry& e) {
   if (e.exec) {
-    (void)hipStreamSynchronize(e.st);  // its last replay finishes first
+    if (e.done) (void)hipEventSynchronize(e.done);  // its last replay finishes first
     (void)hipGraphExecDestroy(e.exec);
     if (e.graph) (void)hipGraphDestroy(e.graph);
   }
+  if (e.done) (void)hipEventDestroy(e.done);
   e = GraphEntry{};
 }
 
@@ -2298,12 +2343,30 @@ static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, v
       ent->nograph = true;  // a graph is an optimisation only: the plain path runs
       return SMX_OK;
     }
+    if (hipEventCreateWithFlags(&ent->done, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGraphExecDestroy(exec);
+      (void)hipGraphDestroy(graph);
+      (void)hipGetLastError();
+      ent->done = nullptr;
+      ent->nograph = true;
+      return SMX_OK;
+    }
     ent->exec = exec;
     ent->graph = graph;
   }
   ent->used = ++g_graph_tick;
   HIP_TRY(hipGraphLaunch(ent->exec, st));
+  HIP_TRY(hipEventRecord(ent->done, st));
   *done = true;
+  return SMX_OK;
+}
+
+// Drop the cached graphs of one stream (all of them for a null stream): each waits
+// for its last replay through the library's own event.
+extern "C" int smx_release_graphs(void* stream) {
+  std::lock_guard<std::mutex> g(g_graph_mu);
+  for (auto& e : g_graph)
+    if (e.used && (stream == nullptr || e.st == (hipStream_t)stream)) graph_release_locked(e);
   return SMX_OK;
 }
 
@@ -2486,6 +2549,24 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
     if (step == SMX_SHARD_EMIT) HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
     return SMX_OK;
   }
+  // The bucketed table records are consumed by SMX_SHARD_TABLES (k_tb_unskip kills the
+  // walk's skipped renames in place): a second TABLES needs a SCATTER (or ORDER) first.
+  // Tracked per workspace on the host, where the steps are issued in stream order.
+  auto records_state = [&](int set) -> int {  // set: 1 scattered, 2 consumed; -1 query
+    static std::mutex mu;
+    static std::vector<std::pair<void*, int>> st_of;
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& e : st_of)
+      if (e.first == ws) {
+        if (set >= 0) e.second = set;
+        return e.second;
+      }
+    if (set >= 0) {
+      if (st_of.size() >= 64) st_of.erase(st_of.begin());
+      st_of.push_back({ws, set});
+    }
+    return set >= 0 ? set : 0;
+  };
   auto order_outputs = [&]() -> int {
     hipLaunchKernelGGL(k_shard_summary, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary);
     if (sh->halo_cap > 0)
@@ -2493,6 +2574,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
                          sh->export_cls, sh->export_src, (u64)sh->halo_cap);
     HIP_TRY(hipGetLastError());
     // the table records, bucketed while the host exchanges the summaries and walks
+    records_state(1);
     return launch_tb_prescatter(C);
   };
   switch (step) {
@@ -2513,7 +2595,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       } else {
         if ((rc = read_meta(C, &hm))) return rc;
         // a compacted shard (b_gap = 0) may take the generic plan
-        if (hm.f_fail && (rc = order_fallbacks(C, ops->b_gap == 0, false, &hm, tgt))) return rc;
+        if (hm.f_fail && (rc = order_fallbacks(C, ops->b_gap == 0, false, &hm, tgt, true))) return rc;
       }
       if ((rc = order_outputs())) return rc;
       if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
@@ -2542,6 +2624,10 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
     }
     case SMX_SHARD_TABLES: {
       if (!sh->part_tab) return set_err(SMX_E_ARG, "null part_tab");
+      if (records_state(-1) != 1)
+        return set_err(SMX_E_ARG, "SMX_SHARD_TABLES needs the records bucketed by SMX_SHARD_ORDER / "
+                                  "ORDER_FIX / SCATTER since the last TABLES");
+      records_state(2);
       tm.begin(ST_TABLES);
       bool bucketed = false;
       // (ORDER / ORDER_FIX / SCATTER bucketed the records)
@@ -2553,6 +2639,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       break;
     }
     case SMX_SHARD_SCATTER: {
+      records_state(1);
       if ((rc = launch_tb_prescatter(C))) return rc;
       break;
     }

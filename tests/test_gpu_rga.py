@@ -53,6 +53,58 @@ def test_rga_class_list_property():
     assert [e.value for e in r.list if not e.tombstone] == r.materialize() == ["a"]
 
 
+def _run_mutation_script(steps):
+    r, held, rec = RGA(), None, []
+
+    def snap():
+        return [[[e.key.anchor, e.key.t, e.key.author, e.key.opid], e.value, e.tombstone] for e in r.list]
+
+    for st in steps:
+        op = st[0]
+        if op == "insert":
+            r.insert(Key(*st[2]), st[1])
+        elif op == "move":
+            r.move(st[1], Key(*st[2]))
+        elif op == "delete":
+            r.delete(st[1])
+        elif op == "read":
+            rec.append(snap())
+        elif op == "materialize":
+            rec.append(r.materialize())
+        elif op == "append":
+            r.list.append(Elem(Key(*st[1]), st[2], st[3]))
+        elif op == "pop":
+            r.list.pop(st[1])
+        elif op == "set_tomb":
+            r.list[st[1]].tombstone = st[2]
+        elif op == "assign":
+            r.list = [Elem(Key(*k), v, tb) for k, v, tb in st[1]]
+        elif op == "hold":
+            held = r.list[st[1]]
+        elif op == "held":
+            rec.append(None if held is None else held.tombstone)
+    return rec
+
+
+def test_rga_list_mutable_state_golden_gpu():
+    """RGA.list is the reference's mutable attribute (crdt.py:26-27): reads return the
+    state object itself, appends / pops / tombstone flips / assignments change the RGA,
+    and an element held across a later delete() is tombstoned in place (crdt.py:40-43).
+    300 scripts, the reference's own results (tools/make_golden.py --only rga_mut)."""
+    cases = load("rga_mutation_cases.json")
+    assert sum(1 for c in cases for s in c["steps"] if s[0] in ("append", "pop", "set_tomb", "assign")) > 100
+    for i, case in enumerate(cases):
+        assert _run_mutation_script(case["steps"]) == case["out"], f"rga mutation script {i}"
+
+
+def test_rga_list_out_of_key_order_fails_loudly():
+    r = RGA()
+    r.list = [Elem(Key("b", 0, "u", "o"), "x"), Elem(Key("a", 0, "u", "o"), "y")]
+    r.insert(Key("c", 0, "u", "o"), "z")
+    with pytest.raises(ValueError, match="key order"):
+        r.list
+
+
 @pytest.mark.parametrize("n_ops,n_lists,seed", [(1_000_000, 5_000, 14), (300_000, 30, 15)])
 def test_rga_list_mode_live_elements_match(n_ops, n_lists, seed):
     """At scale (the oracle has no list mode): the list state's live elements are exactly

@@ -5,7 +5,6 @@ must equal the CPU oracle's composition of the whole merge, bit for bit."""
 import os
 import queue
 import shutil
-import socket
 import tempfile
 
 import numpy as np
@@ -13,16 +12,6 @@ import pytest
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
-
-
-def _free_port():
-    # only for torch.distributed.run's --master-port (test_bench_two_ranks_sharded);
-    # the spawned workers below rendezvous through a FileStore instead
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _init(rank, world, store_path, backend="gloo"):
@@ -283,8 +272,10 @@ def test_bench_two_ranks_sharded():
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, SMX_BENCH_BACKEND="gloo")
     for extra, total, scaling in (([], 2_000_000, "strong"), (["--weak"], 4_000_000, "weak")):
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+        # --standalone: the launcher binds its own rendezvous store on an OS-chosen port
+        # (no port picked here and handed over, which another process could take first)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+               "--nproc-per-node", "2", "bench.py",
                "--gpus", "2", "--steps", "2", "--warmup", "1", "--n-ops", "2000000", "--n-sym",
                "20000"] + extra
         r = subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=240)

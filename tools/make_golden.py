@@ -270,6 +270,79 @@ def make_rga_list_cases(crdt):
     return out
 
 
+def make_rga_mutation_cases(crdt, n_cases: int, seed: int):
+    """Scripts that mix RGA events with reads and in-place changes of the reference's
+    mutable state RGA.list (crdt.py:26-27): appends, pops, tombstone flips, whole-list
+    assignments, and an element held across later events (delete() sets its tombstone in
+    place, crdt.py:40-43).  Each script keeps the list in key order (what insert() and
+    move() maintain).  Recorded: the list after every "read", materialize() after every
+    "materialize", the held element's tombstone after every "held"."""
+    rng = random.Random(seed)
+
+    def key():
+        return [rng.choice(["", "a", "b"]), rng.choice([0, 1, 2, 7, -3]), rng.choice(["u1", "u2"]),
+                rng.choice(["o1", "o2", "o3"])]
+
+    def snap(rga):
+        return [[[e.key.anchor, e.key.t, e.key.author, e.key.opid], e.value, e.tombstone] for e in rga.list]
+
+    def tup(k):
+        return (k.anchor, k.t, k.author, k.opid)
+
+    cases = []
+    for _ in range(n_cases):
+        vals = ["v%d" % i for i in range(rng.choice([1, 2, 4]))]
+        rga = crdt.RGA()
+        held = None
+        steps, rec = [], []
+        for _ in range(rng.choice([4, 10, 25])):
+            r = rng.random()
+            if r < 0.35:
+                step = ["insert", rng.choice(vals), key()]
+                rga.insert(crdt.Key(*step[2]), step[1])
+            elif r < 0.5:
+                step = ["move", rng.choice(vals), key()]
+                rga.move(step[1], crdt.Key(*step[2]))
+            elif r < 0.6:
+                step = ["delete", rng.choice(vals)]
+                rga.delete(step[1])
+            elif r < 0.68:
+                step = ["read"]
+                rec.append(snap(rga))
+            elif r < 0.74:
+                step = ["materialize"]
+                rec.append(rga.materialize())
+            elif r < 0.8:  # append past the last key (the list stays in key order)
+                last = tup(rga.list[-1].key) if rga.list else None
+                k = key()
+                if last is not None and tuple(k) < last:
+                    k = [last[0], last[1] + 1, last[2], last[3]]
+                step = ["append", k, rng.choice(vals), rng.random() < 0.3]
+                rga.list.append(crdt.Elem(crdt.Key(*step[1]), step[2], step[3]))
+            elif r < 0.85 and rga.list:
+                step = ["pop", rng.randrange(len(rga.list))]
+                rga.list.pop(step[1])
+            elif r < 0.9 and rga.list:
+                step = ["set_tomb", rng.randrange(len(rga.list)), rng.random() < 0.5]
+                rga.list[step[1]].tombstone = step[2]
+            elif r < 0.93:
+                items = sorted([(tuple(key()), rng.choice(vals), rng.random() < 0.3)
+                                for _ in range(rng.choice([0, 1, 3]))], key=lambda x: x[0])
+                step = ["assign", [[list(k), v, tb] for k, v, tb in items]]
+                rga.list = [crdt.Elem(crdt.Key(*k), v, tb) for k, v, tb in items]
+            elif r < 0.97 and rga.list:
+                step = ["hold", rng.randrange(len(rga.list))]
+                held = rga.list[step[1]]
+            else:
+                step = ["held"]
+                rec.append(None if held is None else held.tombstone)
+            steps.append(step)
+        steps.append(["read"])
+        rec.append(snap(rga))
+        cases.append({"steps": steps, "out": rec})
+    return cases
+
+
 # ---------------------------------------------------------------------------
 # OpLog.from_json cases (ops.py:106-121): JSON texts of op dicts with the coercions
 # Op.from_dict applies (ops.py:89-100), and the reference's decoded ops -- or the
@@ -436,7 +509,7 @@ def make_applier_cases(applier_mod, ops_mod, n_cases: int, seed: int):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
-    ap.add_argument("--only", choices=["oplog", "applier", "big", "e2e", "rga_list"],
+    ap.add_argument("--only", choices=["oplog", "applier", "big", "e2e", "rga_list", "rga_mut"],
                     help="regenerate one fixture only")
     args = ap.parse_args()
     compose, crdt, ops_mod = _import_reference()
@@ -452,6 +525,9 @@ def main() -> None:
     if args.only == "rga_list":
         with open(os.path.join(GOLD, "rga_list_cases.json"), "w") as fh:
             json.dump(make_rga_list_cases(crdt), fh, separators=(",", ":"))
+    if args.only == "rga_mut":
+        with open(os.path.join(GOLD, "rga_mutation_cases.json"), "w") as fh:
+            json.dump(make_rga_mutation_cases(crdt, 300, seed=31), fh, separators=(",", ":"))
     if args.only == "e2e":
         from semmerge import applier as applier_mod
         with open(os.path.join(GOLD, "e2e_tree.json"), "w") as fh:
