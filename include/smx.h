@@ -180,6 +180,7 @@ int smx_last_plan(void);
  *   [22] outgoing region open  [23] its ahead branch  [24] its d
  *   [25] conflicts  [26] skipped renames  [27] halo too short
  *   [28..30] bit widths of (value + 1) for addr, file, ctx
+ *   [31] a value too wide for the tab32 entries (TABLES with tab32 > 0)
  */
 #define SMX_SHARD_ORDER 0
 #define SMX_SHARD_WALK 1
@@ -230,6 +231,13 @@ typedef struct smx_shard {
    * device: halo_sym / halo_cls / halo_src ([halo_cap] each, writable) and halo_dev
    * (writable) are then outputs, so the host needs no read of the summaries. */
   const int64_t* order_gather;
+  /* 0: part_tab / fin_tab are uint64 [3][n_sym] (+ glob, int64 [3]), entries
+   * (rank + 1) << 32 | (value + 1).  tab32 > 0: half the MAX all-reduce -- they are
+   * int32 [3 * n_sym + 3], entries (rank + 1) << (31 - tab32) | (value + 1) (a tag of
+   * tab32 bits under a clear sign bit, so an int32 MAX keeps the last writer), the
+   * three value widths after them (glob unused); a value too wide for the 31 - tab32
+   * bits sets summary[31] and the caller redoes the step with tab32 = 0. */
+  int32_t tab32;
 } smx_shard;
 
 int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const smx_compose_out* out,

@@ -65,6 +65,7 @@ class SmxShard(C.Structure):
         ("src_map", C.c_void_p),
         ("summary_host", C.c_void_p),
         ("order_gather", C.c_void_p),
+        ("tab32", C.c_int32),
     ]
 
 

@@ -47,6 +47,7 @@ struct ComposeMeta {
   u64 q_in, nconf_in;
   u64 out_open, out_ahead, out_d;
   u64 halo_overflow;
+  u64 tab_over;              // sharded TABLES, 32-bit entries: a value too wide for them
   u64 n_conf_loc;            // conflicts of this shard's own regions (scan total)
   u64 nskip_in;              // skipped renames of the incoming region (head of the skip list)
   u64 dup_key;               // generic plan: equal (ts, oid_hi) pair seen -> sort with oid_lo

@@ -1331,7 +1331,8 @@ static int launch_tb_prescatter(const Ctx& C) {
 // when the value widths allow); otherwise this shard's partial tables.  prescattered:
 // launch_tb_prescatter already bucketed the records (then only the skips and the
 // reduce run here).
-static int launch_tables(const Ctx& C, u64* part_tab, u32 tag, bool* bucketed, bool prescattered = false) {
+static int launch_tables(const Ctx& C, void* part_tab, u32 tag, int tagbits, bool* bucketed,
+                         bool prescattered = false) {
   hipStream_t st = C.st;
   const i64 n = C.n;
   int4* fin = C.ws<int4>(B_FIN);
@@ -1352,7 +1353,8 @@ static int launch_tables(const Ctx& C, u64* part_tab, u32 tag, bool* bucketed, b
     } else {
       hipLaunchKernelGGL(k_tb_scatter, dim3(nblk), dim3(TB_NT), 0, st, A, lst, rec);
     }
-    hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, lst, rec, n_sym, fin, part_tab, tag);
+    hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, lst, rec, n_sym, fin,
+                       PartTab{part_tab, tag, tagbits, C.ws<ComposeMeta>(B_META)});
   } else {
     // very large symbol spaces: device-scope atomics on the packed keys
     u32* tabA = C.ws<u32>(B_TABA);
@@ -1364,7 +1366,7 @@ static int launch_tables(const Ctx& C, u64* part_tab, u32 tag, bool* bucketed, b
       return rc;
     hipLaunchKernelGGL(k_tab_atomic, dim3(grid_for(n)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR);
     hipLaunchKernelGGL(k_finalize, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, A, tabA, tabF, tabR, n_sym, fin,
-                       part_tab, tag);
+                       PartTab{part_tab, tag, tagbits, C.ws<ComposeMeta>(B_META)});
   }
   HIP_TRY(hipGetLastError());
   return SMX_OK;
@@ -1494,7 +1496,7 @@ static int launch_tail(const Ctx& C) {
     C.tm->end(ST_WALK);
     C.tm->begin(ST_TABLES);
     bool bucketed = false;
-    if ((rc = launch_tables(C, nullptr, 0, &bucketed))) return rc;
+    if ((rc = launch_tables(C, nullptr, 0, 0, &bucketed))) return rc;
     C.tm->end(ST_TABLES);
     C.tm->begin(ST_EMIT);
     if ((rc = launch_emit(C, bucketed, nullptr))) return rc;
@@ -1526,7 +1528,7 @@ static int launch_tail(const Ctx& C) {
   C.tm->begin(ST_TABLES);
   hipLaunchKernelGGL(k_tb_unskip, dim3(1024), dim3(BLOCK), 0, st, A, lst, rec, C.ws<u32>(B_SKIPLIST));
   hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, lst, rec, n_sym, C.ws<int4>(B_FIN),
-                     (u64*)nullptr, 0u);
+                     PartTab{nullptr, 0u, 0, nullptr});
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_TABLES);
   C.tm->begin(ST_EMIT);
@@ -2471,20 +2473,32 @@ __global__ void k_shard_walk_sum(const ComposeMeta* meta, i64* summary) {
 
 __global__ void k_shard_tab_sum(const ComposeMeta* meta, i64* summary, int bucketed) {
   for (int i = 0; i < 3; ++i) summary[28 + i] = bucketed ? (i64)bit_width32(meta->vbits[i]) : 32;
+  summary[31] = (i64)meta->tab_over;
 }
+__global__ void k_tab_over_reset(ComposeMeta* meta) { meta->tab_over = 0; }
 
 // fin from the reduced partial tables: packed with the global widths when they
 // fit in 64 bits (meta->vbits takes the global widths, for k_emit).
-__global__ void k_fin_from_tab(const u64* __restrict__ tab, const i64* __restrict__ glob, i64 n_sym,
-                               ComposeMeta* meta, int4* __restrict__ fin) {
+__global__ void k_fin_from_tab(const void* __restrict__ tabv, const i64* __restrict__ glob, i64 n_sym,
+                               int tagbits, ComposeMeta* meta, int4* __restrict__ fin) {
   u32 w[3];
-  for (int i = 0; i < 3; ++i) w[i] = (u32)min(max(glob[i], (i64)0), (i64)32);
+  const u64* tab = (const u64*)tabv;
+  const u32* tab32 = (const u32*)tabv;
+  for (int i = 0; i < 3; ++i)
+    w[i] = (u32)min(max(tagbits ? (i64)(i32)tab32[3 * n_sym + i] : glob[i], (i64)0), (i64)32);
   const FinPack FP = fin_pack_make(w[0], w[1], w[2], true);
   if (blockIdx.x == 0 && threadIdx.x < 3)
     meta->vbits[threadIdx.x] = w[threadIdx.x] >= 32 ? ~0u : ((1u << w[threadIdx.x]) - 1u);
   for (i64 s = (i64)blockIdx.x * BLOCK + threadIdx.x; s < n_sym; s += (i64)gridDim.x * BLOCK) {
-    const u64 a = tab[s], f = tab[n_sym + s], c = tab[2 * n_sym + s];
-    const int va = a ? (int)(u32)a - 1 : -1, vf = f ? (int)(u32)f - 1 : -1, vc = c ? (int)(u32)c - 1 : -1;
+    int va, vf, vc;
+    if (tagbits) {
+      const u32 m = (1u << (31 - tagbits)) - 1u;
+      const u32 a = tab32[s], f = tab32[n_sym + s], c = tab32[2 * n_sym + s];
+      va = a ? (int)(a & m) - 1 : -1, vf = f ? (int)(f & m) - 1 : -1, vc = c ? (int)(c & m) - 1 : -1;
+    } else {
+      const u64 a = tab[s], f = tab[n_sym + s], c = tab[2 * n_sym + s];
+      va = a ? (int)(u32)a - 1 : -1, vf = f ? (int)(u32)f - 1 : -1, vc = c ? (int)(u32)c - 1 : -1;
+    }
     fin_put(FP, fin, (u32)s, va, vf, vc);
   }
 }
@@ -2545,7 +2559,7 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       HIP_TRY(hipGetLastError());
     }
     if (step == SMX_SHARD_TABLES && sh->part_tab)
-      HIP_TRY(hipMemsetAsync(sh->part_tab, 0, (size_t)3 * n_sym * 8, st));
+      HIP_TRY(hipMemsetAsync(sh->part_tab, 0, (size_t)3 * n_sym * (sh->tab32 > 0 ? 4 : 8), st));
     if (step == SMX_SHARD_EMIT) HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
     return SMX_OK;
   }
@@ -2631,7 +2645,10 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       tm.begin(ST_TABLES);
       bool bucketed = false;
       // (ORDER / ORDER_FIX / SCATTER bucketed the records)
-      if ((rc = launch_tables(C, sh->part_tab, (u32)sh->rank + 1u, &bucketed, true))) return rc;
+      if (sh->tab32 < 0 || sh->tab32 > 8 || (sh->tab32 > 0 && ((u64)sh->rank + 1u) >> sh->tab32))
+        return set_err(SMX_E_ARG, "tab32: the tag (rank + 1) must fit tab32 <= 8 bits");
+      hipLaunchKernelGGL(k_tab_over_reset, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META));
+      if ((rc = launch_tables(C, sh->part_tab, (u32)sh->rank + 1u, sh->tab32, &bucketed, true))) return rc;
       hipLaunchKernelGGL(k_shard_tab_sum, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), sh->summary,
                          bucketed ? 1 : 0);
       HIP_TRY(hipGetLastError());
@@ -2644,10 +2661,11 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
       break;
     }
     case SMX_SHARD_EMIT: {
-      if (!sh->fin_tab || !sh->glob) return set_err(SMX_E_ARG, "null fin_tab / glob");
+      if (!sh->fin_tab || (!sh->glob && sh->tab32 == 0)) return set_err(SMX_E_ARG, "null fin_tab / glob");
+      if (sh->tab32 < 0 || sh->tab32 > 8) return set_err(SMX_E_ARG, "tab32 must be 0..8");
       tm.begin(ST_EMIT);
-      hipLaunchKernelGGL(k_fin_from_tab, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, sh->fin_tab, sh->glob, n_sym,
-                         C.ws<ComposeMeta>(B_META), C.ws<int4>(B_FIN));
+      hipLaunchKernelGGL(k_fin_from_tab, dim3(grid_for(n_sym)), dim3(BLOCK), 0, st, (const void*)sh->fin_tab,
+                         sh->glob, n_sym, (int)sh->tab32, C.ws<ComposeMeta>(B_META), C.ws<int4>(B_FIN));
       if ((rc = launch_emit(C, true, sh))) return rc;
       tm.end(ST_EMIT);
       ComposeMeta hm;

@@ -234,10 +234,35 @@ __global__ void k_tb_unskip(TbArgs A0, const u32* __restrict__ lst, u32* __restr
 // values are fetched once: fin[sym] = (addr, file, ctx).
 // part != nullptr (sharded merge): instead of fin, write this shard's partial
 // tables part[3][n_sym] = (tag << 32) | (value + 1), 0 = no record; the MAX
-// all-reduce over shards then keeps the last writer (highest shard).
+// all-reduce over shards then keeps the last writer (highest shard).  tagbits > 0:
+// 32-bit entries tag << (31 - tagbits) | (value + 1) instead (smx_shard.tab32).
+struct PartTab {
+  void* p;
+  u32 tag;
+  int tagbits;  // 0: u64 entries
+  ComposeMeta* meta;
+  __device__ __forceinline__ void put(i64 n_sym, i64 s, int va, int vf, int vc) const {
+    if (tagbits == 0) {
+      u64* part = (u64*)p;
+      const u64 tg = (u64)tag << 32;
+      part[s] = va >= 0 ? tg | (u32)(va + 1) : 0ull;
+      part[n_sym + s] = vf >= 0 ? tg | (u32)(vf + 1) : 0ull;
+      part[2 * n_sym + s] = vc >= 0 ? tg | (u32)(vc + 1) : 0ull;
+      return;
+    }
+    u32* part = (u32*)p;
+    const u32 vb = 31u - (u32)tagbits, tg = tag << vb, lim = 1u << vb;
+    const u32 a1 = (u32)(va + 1), f1 = (u32)(vf + 1), c1 = (u32)(vc + 1);
+    if ((a1 | f1 | c1) >= lim) meta->tab_over = 1;  // the caller redoes the step with u64 entries
+    part[s] = va >= 0 ? tg | (a1 & (lim - 1)) : 0u;
+    part[n_sym + s] = vf >= 0 ? tg | (f1 & (lim - 1)) : 0u;
+    part[2 * n_sym + s] = vc >= 0 ? tg | (c1 & (lim - 1)) : 0u;
+  }
+};
+
 __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __restrict__ lst,
                                                       const u32* __restrict__ rec, i64 n_sym,
-                                                      int4* __restrict__ fin, u64* __restrict__ part, u32 tag) {
+                                                      int4* __restrict__ fin, PartTab part) {
   const FinPack FP = fin_pack_of(A0.meta->vbits, true);
   __shared__ u32 tA[TB_WIDTH], tF[TB_WIDTH], tC[TB_WIDTH];
   const TbArgs A = tb_load(A0);
@@ -302,14 +327,8 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
     const u32 a = tA[i], f = tF[i], c = tC[i];
     const int va = a ? A.mv_addr[a - 1] : -1, vf = f ? A.mv_file[f - 1] : -1;
     const int vc = c ? A.Rstr[(u64)(c - 1) - A.nMv] : -1;
-    if (part) {
-      const u64 tg = (u64)tag << 32;
-      part[s0 + i] = a ? tg | (u32)(va + 1) : 0ull;
-      part[n_sym + s0 + i] = f ? tg | (u32)(vf + 1) : 0ull;
-      part[2 * n_sym + s0 + i] = c ? tg | (u32)(vc + 1) : 0ull;
-    } else {
-      fin_put(FP, fin, s0 + i, va, vf, vc);
-    }
+    if (part.p) part.put(n_sym, s0 + i, va, vf, vc);
+    else fin_put(FP, fin, s0 + i, va, vf, vc);
   }
 }
 
@@ -331,20 +350,13 @@ __global__ void k_tab_atomic(TbArgs A0, u32* __restrict__ tabA, u32* __restrict_
 }
 
 __global__ void k_finalize(TbArgs A0, const u32* __restrict__ tabA, const u32* __restrict__ tabF,
-                           const u32* __restrict__ tabR, i64 n_sym, int4* __restrict__ fin,
-                           u64* __restrict__ part, u32 tag) {
+                           const u32* __restrict__ tabR, i64 n_sym, int4* __restrict__ fin, PartTab part) {
   const TbArgs A = tb_load(A0);
   for (i64 s = (i64)blockIdx.x * BLOCK + threadIdx.x; s < n_sym; s += (i64)gridDim.x * BLOCK) {
     const u32 a = tabA[s], f = tabF[s], c = tabR[s];
     const int va = a ? A.mv_addr[a - 1] : -1, vf = f ? A.mv_file[f - 1] : -1;
     const int vc = c ? A.Rstr[(u64)(c - 1) - A.nMv] : -1;
-    if (part) {
-      const u64 tg = (u64)tag << 32;
-      part[s] = a ? tg | (u32)(va + 1) : 0ull;
-      part[n_sym + s] = f ? tg | (u32)(vf + 1) : 0ull;
-      part[2 * n_sym + s] = c ? tg | (u32)(vc + 1) : 0ull;
-    } else {
-      fin[s] = make_int4(va, vf, vc, 0);
-    }
+    if (part.p) part.put(n_sym, s, va, vf, vc);
+    else fin[s] = make_int4(va, vf, vc, 0);
   }
 }

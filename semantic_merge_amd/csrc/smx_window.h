@@ -240,6 +240,15 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_BUCKET
 #define WF_BUCKET 1  // step 5 by interpolation buckets (0: counting rank over each group)
 #endif
+#ifndef WF_BF
+#define WF_BF 1      // branch-free per-item code in the load and merge phases
+#endif
+#ifndef WF_ONEATOM
+#define WF_ONEATOM 1 // step 5 places each slot at start + arrival rank (one LDS atomic per element, not two)
+#endif
+#ifndef WF_RANK8
+#define WF_RANK8 1   // step 5's bucket rank: 8 predicated compares, the loop only for larger buckets / equal halves
+#endif
 #ifndef WF_BK16
 #define WF_BK16 1    // bucket-ordered 16-bit key prefixes for the rank loop (window 1.329 -> 1.286 ms, profiles/r03_e/ab.txt)
 #endif
@@ -251,6 +260,9 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #endif
 #ifndef WF_OUT2
 #define WF_OUT2 1    // steps 7-9 staged by final slot (inv), four slots per thread, 16-byte stores: window 1.271 -> 1.233 ms (profiles/r03_m/ab.txt)
+#endif
+#ifndef WF_STB_KIND
+#define WF_STB_KIND 1  // v0 / v1 staged for moves and renames only (the other kinds output neither)
 #endif
 #ifdef WF_WPE
 #define WF_BOUNDS __launch_bounds__(WF_NT) __attribute__((amdgpu_waves_per_eu(WF_WPE, WF_WPE)))
@@ -381,6 +393,28 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
   u32 none_mv = 0;  // moves with a None value (prefix fix-up)
   u32 vb_a = 0, vb_f = 0, vb_c = 0;  // OR of (value + 1): widths of the packed final-state table
+#if WF_BF
+  // branch-free: the LDS slots past sz take harmless values (every later phase reads
+  // slots < sz only), the rest is selects -- no exec-mask bookkeeping per item
+  static_assert(WF_NT * WF_ITEMS <= WF_CAP, "item slots inside the LDS arrays");
+#pragma unroll
+  for (int i = 0; i < WF_ITEMS; ++i) {
+    const int e = t + WF_NT * i;
+    const bool ok = e < sz;
+    const u32 kr = k_r[i];
+    bad |= ok & ((kr >= SMX_N_KINDS) | (sym_r[i] >= (u64)P.n_sym));
+    const u32 k = kr < SMX_N_KINDS ? kr : SMX_N_KINDS - 1;
+    sts[e] = ts_r[i];
+    skind[e] = (u8)k;
+    const bool mv = ok & (k == KMOVE), rn = ok & (k == KREN);
+    const bool ha = v0_r[i] >= 0, hf = v1_r[i] >= 0;
+    sym_r[i] = (sym_r[i] & SYM_MASK) | ((mv & ha) ? MS_HAS_A : 0u) | ((mv & hf) ? MS_HAS_F : 0u);
+    none_mv += (mv & !(ha & hf)) ? 1u : 0u;
+    vb_a |= mv ? (u32)(v0_r[i] + 1) : 0u;
+    vb_f |= mv ? (u32)(v1_r[i] + 1) : 0u;
+    vb_c |= rn ? (u32)(v1_r[i] + 1) : 0u;
+  }
+#else
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i) {
     const int e = t + WF_NT * i;
@@ -401,6 +435,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       }
     }
   }
+#endif
   vb_a = wave_or_to_last(vb_a);
   vb_f = wave_or_to_last(vb_f);
   vb_c = wave_or_to_last(vb_c);
@@ -464,12 +499,29 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       else hi = mid;
     }
     int ia = lo, ib = d0 - lo;
+#if WF_BF
+    // WF_ITEMS outputs, predicated (a thread past sz stores nothing)
+#pragma unroll
+    for (int u = 0; u < WF_ITEMS; ++u) {
+      const int d = d0 + u;
+      const u64 ta = sts[ia < na ? ia : 0], tb = sts[na + (ib < nb ? ib : 0)];
+      const bool take_a = ia < na && (ib >= nb || ta <= tb);
+      const int e = take_a ? ia : na + ib;
+      ia += take_a ? 1 : 0;
+      ib += take_a ? 0 : 1;
+      if (d < d1) {
+        sord[d] = (u16)e;
+        skS[d] = skind[e];
+      }
+    }
+#else
     for (int d = d0; d < d1; ++d) {
       const bool take_a = ia < na && (ib >= nb || sts[ia] <= sts[na + ib]);
       const int e = take_a ? ia++ : na + ib++;
       sord[d] = (u16)e;
       skS[d] = skind[e];
     }
+#endif
   }
   if (__syncthreads_or(dec)) {
     if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
@@ -632,6 +684,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
 #endif
   u32 bk_r[WF_ITEMS];
   u32 kp_r[WF_ITEMS];
+#if WF_ONEATOM
+  u32 ar_r[WF_ITEMS];  // arrival rank inside the bucket (the count atomic's return value)
+#endif
 #pragma unroll
   for (int j = 0; j < WF_ITEMS; ++j) bk_r[j] = 0xffffffffu, kp_r[j] = 0u;
 #endif
@@ -663,7 +718,11 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       const u32 b = (u32)gs + (u32)(((u64)(u32)(ge - gs) * kp) >> 32);
       kp_r[j] = kp;
       bk_r[j] = b;
+#if WF_ONEATOM
+      ar_r[j] = (atomicAdd(&bcnt[b >> 1], 1u << (16 * (b & 1))) >> (16 * (b & 1))) & 0xffffu;
+#else
       atomicAdd(&bcnt[b >> 1], 1u << (16 * (b & 1)));
+#endif
       continue;
     }
 #endif
@@ -704,17 +763,26 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     bcnt[2 * t + 1] = (e0 + c0 + c1) | ((e0 + c0 + c1 + c2) << 16);
     __syncthreads();
     // scatter the slots into their buckets (sl: bucket position -> slot); the counters
-    // become the bucket ends
+    // become the bucket ends (WF_ONEATOM: they stay the starts; position = start +
+    // arrival rank, no second atomic)
+    u32 lo_r[WF_ITEMS];
 #pragma unroll
     for (int j = 0; j < WF_ITEMS; ++j) {
       const u32 b = bk_r[j];
+      lo_r[j] = 0;
       if (b == 0xffffffffu) continue;
       const u32 sh = 16 * (b & 1);
+#if WF_ONEATOM
+      lo_r[j] = (bcnt[b >> 1] >> sh) & 0xffffu;
+      const u32 pos = lo_r[j] + ar_r[j];
+#else
       const u32 old = atomicAdd(&bcnt[b >> 1], 1u << sh);
-      sl[(old >> sh) & 0xffffu] = (u16)((WF_NT * j) / WAVE * WAVE + wv * WAVE + lane);
+      const u32 pos = (old >> sh) & 0xffffu;
+#endif
+      sl[pos] = (u16)((WF_NT * j) / WAVE * WAVE + wv * WAVE + lane);
 #if WF_BK16
-      own_r[j] = (old >> sh) & 0xffffu;
-      bk16[own_r[j]] = (u16)(kp_r[j] >> 16);
+      own_r[j] = pos;
+      bk16[pos] = (u16)(kp_r[j] >> 16);
 #endif
     }
     __syncthreads();
@@ -725,14 +793,42 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       const u32 b = bk_r[j];
       rr[j] = -1;
       if (b == 0xffffffffu) continue;
+#if WF_ONEATOM
+      // bucket [start(b), start(b + 1)); the starts are an exclusive scan over every
+      // bucket of the window (buckets past the last slot start at the total)
+      const u32 lo = lo_r[j];
+      const u32 e = b + 1 < (u32)WF_CAP ? (bcnt[(b + 1) >> 1] >> (16 * ((b + 1) & 1))) & 0xffffu : (u32)sz;
+#else
       const u32 e = (bcnt[b >> 1] >> (16 * (b & 1))) & 0xffffu;
       const u32 lo = b ? (bcnt[(b - 1) >> 1] >> (16 * ((b - 1) & 1))) & 0xffffu : 0u;
+#endif
       const u32 kp = kp_r[j];
       u32 c = 0, eq = 0;
 #if WF_BK16
       const u32 k16 = kp >> 16, own = own_r[j];
       eq = 1;
+#if WF_RANK8
+      // buckets of at most 8 (all but ~1e-5 of the elements on random ids): eight
+      // predicated compares, no lane-divergent loop (whose exec-mask bookkeeping is
+      // scalar work, the window's scarcest issue slot); larger buckets and equal top
+      // halves take the general loop below
+      {
+        const u32 nb = e - lo;
+        bool gen = nb > 8;
+#pragma unroll
+        for (u32 i = 0; i < 8; ++i) {
+          const u32 q = lo + i;
+          const u32 x = bk16[q];  // (past the bucket: masked; LDS reads never fault)
+          const bool in = i < nb && q != own;
+          c += (in && x < k16) ? 1u : 0u;
+          gen |= in && x == k16;
+        }
+        if (gen) c = 0;
+        for (u32 q = gen ? lo : e; q < e; ++q) {
+#else
+      {
       for (u32 q = lo; q < e; ++q) {
+#endif
         const u32 x = bk16[q];
         if (q == own) continue;
         if (x != k16) {
@@ -742,6 +838,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
           c += k < kp;
           eq += k == kp;
         }
+      }
       }
 #else
       for (u32 q = lo; q < e; ++q) {
@@ -904,7 +1001,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     xi[i] = e < sz ? inv[e] : WF_CAP;
     if (e < sz) {
       st_a[xi[i]] = sym_r[i];
-      st_b[xi[i]] = v0_r[i];
+      if (!WF_STB_KIND || k_r[i] <= KREN) st_b[xi[i]] = v0_r[i];
     }
   }
   if (t < SMX_N_KINDS) tbase[t] = base[t] + woffk[t] - kbase[t];
@@ -1019,7 +1116,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   // round 2: v1 -> the move's newFile, the rename's chain value
 #pragma unroll
   for (int i = 0; i < WF_ITEMS; ++i)
-    if (xi[i] < WF_CAP) st_b[xi[i]] = v1_r[i];
+    if (xi[i] < WF_CAP && (!WF_STB_KIND || k_r[i] <= KREN)) st_b[xi[i]] = v1_r[i];
   __syncthreads();
   if (m4 > 0 && (k4[0] <= KREN || k4[m4 - 1] <= KREN)) {
     const uint4 bv = *reinterpret_cast<const uint4*>(&st_b[x0]);

@@ -45,6 +45,7 @@ from ._lib import _ptr, check, lib
 FIELDS = ("kind", "ts", "hi", "lo", "sym", "v0", "v1")
 S_KINDS, S_REN, S_MVNONE, S_FAIL = 0, 18, 20, 21
 S_OPEN, S_AHEAD, S_D, S_NCONF, S_NSKIP, S_OVER, S_WIDTH = 22, 23, 24, 25, 26, 27, 28
+S_TABOVER = 31   # a value too wide for the 32-bit partial tables (smx_shard.tab32)
 N_KINDS = 18
 SUM = _abi.SHARD_SUMMARY
 I64_MIN = -(2 ** 63)
@@ -229,6 +230,13 @@ class ShardedCompose:
         # partial tables [3][n_sym] then the 3 value widths: one MAX all_reduce for both
         self.part = torch.zeros(3 * max(n_sym, 1) + 3, dtype=torch.int64, device=dv)
         self.glob = self.part[3 * max(n_sym, 1):]
+        # the same tables with 32-bit entries: the rank tag in the top bits under a clear
+        # sign bit (an int32 MAX keeps the last writer) -- half the all-reduce's bytes
+        # whenever every value fits the rest (include/smx.h smx_shard.tab32)
+        self.tab_bits = int(self.world).bit_length()
+        self.part32 = torch.zeros(3 * max(n_sym, 1) + 3, dtype=torch.int32, device=dv) \
+            if 31 - self.tab_bits >= 16 else None
+        self.tab32_used = 0  # tables steps that ran with 32-bit entries (tests, probes)
         self.n_xchg = 0      # ops this rank received from other ranks in the last exchange
         self.order_fixes = 0  # ORDER_FIX runs (dense timestamp ties) on this rank
         # every timestamp below 2^63 (ISO keys, dense ranks): the signed int64 order of
@@ -606,16 +614,30 @@ class ShardedCompose:
                                    _ptr(self._ws), self._ws_bytes, s, step))
 
     # -- 2..5 -------------------------------------------------------------------------
-    def _tables(self, summ: Optional[np.ndarray], rescatter: bool) -> None:
+    def _tables(self, summ: Optional[np.ndarray], rescatter: bool, wide: bool = True) -> None:
         """TABLES (+ the lower shards' move tables when a move has a None value, which
         needs the gathered summaries `summ`) and the MAX all_reduce of the partial
         tables and value widths (collective).  rescatter: the records were consumed by
-        an earlier TABLES of this step (a WALK re-run) and are bucketed again."""
+        an earlier TABLES of this step (a WALK re-run) and are bucketed again.  wide:
+        64-bit entries; otherwise 32-bit ones (half the all-reduce), which a value too
+        wide for them flags in summary[S_TABOVER] (the caller then redoes it wide)."""
         torch = self.torch
         if rescatter:
             self._step(_abi.SHARD_SCATTER)
-        self._step(_abi.SHARD_TABLES)
         n3 = 3 * max(self.n_sym, 1)
+        if not wide and self.part32 is not None and summ is None:
+            self._sh.tab32 = self.tab_bits
+            self._sh.part_tab = self._sh.fin_tab = _ptr(self.part32)
+            self._step(_abi.SHARD_TABLES)
+            self.part32[n3:].copy_(self.summary[S_WIDTH:S_WIDTH + 3])
+            self._mvpre = None
+            self._sh.mv_prefix = None
+            self.tab32_used += 1
+            self.comm.all_reduce_max(self.part32)  # last writers and value widths together
+            return
+        self._sh.tab32 = 0
+        self._sh.part_tab = self._sh.fin_tab = _ptr(self.part)
+        self._step(_abi.SHARD_TABLES)
         self.part[n3:].copy_(self.summary[S_WIDTH:S_WIDTH + 3])
         mvpre = None
         if summ is not None and summ[:, S_MVNONE].sum() > 0:
@@ -636,9 +658,10 @@ class ShardedCompose:
         self._order_exchange()
         self.in_dev.zero_()
         self._step(_abi.SHARD_WALK)
-        self._tables(None, rescatter=False)
+        self._tables(None, rescatter=False, wide=False)
         summ, reran = self._walk(first_done=True)
-        final = not reran and not summ[:, S_FAIL].any() and summ[:, S_MVNONE].sum() == 0
+        final = (not reran and not summ[:, S_FAIL].any() and summ[:, S_MVNONE].sum() == 0
+                 and not summ[:, S_TABOVER].any())
         if summ[:, S_FAIL].any():          # an asynchronous ORDER failed somewhere
             if int(np.bitwise_or.reduce(summ[:, S_FAIL])) & 3:
                 self._fail(summ)

@@ -78,6 +78,14 @@ def _make(case):
     if kind == "dense":  # long equal-timestamp groups: windows overflow, ORDER_FIX repairs
         spec = synth.LiftSpec(n, n_sym, seed, ops_per_ms=4096)
         return synth.lift_soa(synth.lift_logs(spec))
+    if kind == "dense_unordered":  # ... and two ops of A's first quarter swapped across ms groups
+        soa = _make(("dense", n, n_sym, seed))
+        i, j = 100, soa.n_a // 4
+        assert soa.ts[i] < soa.ts[j]
+        for f in ("kind", "ts", "oid_hi", "oid_lo", "sym", "v0", "v1"):
+            a = getattr(soa, f)
+            a[i], a[j] = a[j].copy(), a[i].copy()
+        return soa
     if kind == "lift":
         spec = synth.LiftSpec(n, n_sym, seed, ops_per_ms=64)
     elif kind == "adv":  # rename-heavy, 30% of symbols renamed on both sides: many conflicts
@@ -163,7 +171,8 @@ def _worker(rank, world, store_path, q, case, halo, mode="auto", backend="gloo")
         res2 = sc.results()
         same = all(np.array_equal(x, y) for x, y in zip(first[0][:5], res2[:5]))
         _phase(q, rank, "destroy_process_group")
-        q.put(("done", rank, (res, sc.in_state, (sc.exchange_mode, same, first[1], sc.order_fixes))))
+        q.put(("done", rank, (res, sc.in_state, (sc.exchange_mode, same, first[1], sc.order_fixes,
+                                                 sc.tab32_used))))
     except Exception as e:  # report to the parent instead of hanging the collective
         q.put(("done", rank, (repr(e), None, None)))
         raise
@@ -189,7 +198,7 @@ def _check(case, world, halo=4096, mode="auto", want_mode=None, backend="gloo"):
         assert g.shape == r.shape, f"{case} x{world}: {name} shape {g.shape} vs {r.shape}"
         assert np.array_equal(g, r), f"{case} x{world}: {name} differs"
     for r in range(world):
-        emode, same, totals, _ = got[r][2]
+        emode, same, totals, _, _ = got[r][2]
         assert same, f"rank {r}: a second run differs"
         assert totals == (len(ref[0]), len(ref[4])), totals
         if want_mode:
@@ -260,6 +269,67 @@ def test_shard_dense_ties_order_fix():
     # ORDER; ORDER_FIX retries with smaller windows
     got, _ = _check(("dense", 200_000, 2_000, 6), 2, want_mode="range")
     assert any(got[r][2][3] for r in range(2)), "ORDER_FIX did not run"
+
+
+def test_shard_eight_ranks_range_config2_shape():
+    """The 8-GPU node's geometry on one GPU (8 gloo ranks): 7 splitters, halos and open
+    regions across 7 boundaries, an 8-way MAX all-reduce; config 2's shape (1M ops, 10k
+    symbols) with None-valued moves whose prefix crosses shards, timestamp ranges."""
+    _check(("lift", 1_000_000, 10_000, 7), 8, want_mode="range")
+
+
+def test_shard_eight_ranks_32bit_tables():
+    """Eight ranks without None-valued moves: the speculative tables go through the
+    32-bit all-reduce (rank tag in the top 4 bits) and are final -- no 64-bit redo."""
+    got, _ = _check(("lift", 800_000, 10_000, 8), 8, want_mode="range")
+    assert all(got[r][2][4] == 2 for r in range(8)), [got[r][2][4] for r in range(8)]  # (two runs)
+
+
+def test_shard_eight_ranks_sample_sort_shuffled():
+    _check(("c2s", 400_000, 4_000, 7), 8, want_mode="sample")
+
+
+def test_shard_eight_ranks_open_region_across_shards():
+    """One DivergentRename region from the first shard holding B's renames to the last:
+    it is open at several shard ends and handed on, shard by shard."""
+    got, ref = _check(("chain", 3000, 0, 3), 8)  # (depth <= 3000: inside the 4096-rename halo)
+    assert len(ref[4]) == 3000
+    handed = [r for r in range(8) if got[r][1] != (0, 0)]
+    assert len(handed) >= 2, handed
+
+
+def test_shard_range_unordered_dense_slice_fails_loudly():
+    """mode "range" trusts the ORDER step to reject a slice whose timestamps decrease.
+    With dense ties the presorted plan's early verdict (a group no window holds) hides the
+    window kernel's order check, so ORDER_FIX runs the segmented sort, which reports the
+    decrease itself: the step must fail on every rank, never radix-sort the slice locally
+    (that orders it within the shard but not across the shards)."""
+    with pytest.raises(AssertionError, match="timestamp-ordered"):
+        _check(("dense_unordered", 200_000, 2_000, 6), 2, mode="range")
+
+
+def test_shard_tables_twice_without_scatter_rejected():
+    """SMX_SHARD_TABLES consumes the bucketed records (the walk's skips are applied in
+    place): a second TABLES without SCATTER in between is an argument error."""
+    import ctypes as C
+    import torch
+    import torch.distributed as dist
+    from semantic_merge_amd import _abi, _lib, shard, synth
+    store = tempfile.mkdtemp(prefix="smx_store_")
+    dist.init_process_group("gloo", store=dist.FileStore(os.path.join(store, "s"), 1), rank=0, world_size=1)
+    try:
+        soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(20_000, 200, 3)))
+        a, b, na, nb = shard.slices_from_soa(soa, 0, 1, "cuda:0")
+        sc = shard.ShardedCompose(a, b, na, nb, soa.n_sym, shard.Comm(), "cuda:0", mode="range")
+        sc.run()
+        sc._step(_abi.SHARD_SCATTER)
+        sc._step(_abi.SHARD_TABLES)
+        with pytest.raises(_lib.SmxError, match="TABLES"):
+            sc._step(_abi.SHARD_TABLES)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+        shutil.rmtree(store, ignore_errors=True)
 
 
 def test_bench_two_ranks_sharded():

@@ -64,7 +64,10 @@ def _worker(rank, world, port, args, q):  # port: the FileStore path
 @pytest.mark.parametrize("world,n,opm,headroom,high", [(2, 20_000, 64, None, False),
                                                        (3, 30_000, 7, None, False),
                                                        (3, 9_000, 1000, 0, False),
-                                                       (4, 24_000, 64, None, True)])
+                                                       (4, 24_000, 64, None, True),
+                                                       # the 8-GPU node's geometry: 7 splitters
+                                                       (8, 48_000, 64, None, False),
+                                                       (8, 16_000, 333, 0, True)])
 def test_exchange_key_ranges(world, n, opm, headroom, high):
     from semantic_merge_amd import shard
     ctx = mp.get_context("spawn")
@@ -164,7 +167,7 @@ def _sample_worker(rank, world, port, args, q):
 
 
 @pytest.mark.parametrize("world,n,mode,only_a", [(2, 6_000, "sample", False), (3, 9_001, "auto", False),
-                                                (2, 6_000, "auto", True)])
+                                                (2, 6_000, "auto", True), (8, 24_000, "sample", False)])
 def test_exchange_sample_sort(world, n, mode, only_a):
     """Unordered branch logs: every op lands exactly once on the shard owning its full T
     key (kind, ts, oid, side, index), A' and B' in global index order, shards balanced.
@@ -239,11 +242,12 @@ def _strong_worker(rank, world, port, args, q):
         dist.destroy_process_group()
 
 
-def test_exchange_strong_split_slices():
+@pytest.mark.parametrize("world", [3, 8])
+def test_exchange_strong_split_slices(world):
     """bench.py --gpus N (strong scaling): each rank generates its own index slice of the
     config's ops (synth.lift_slice_soa); the key-range exchange tiles both branches in
     shard order, moving only the ops at the slice edges."""
-    world, n_total = 3, 60_000
+    n_total = 20_000 * world
     res = _spawn(_strong_worker, world, (n_total,))
     ea = eb = 0
     for r in range(world):
