@@ -132,6 +132,7 @@ int smx_release_graphs(void* stream);
 #define SMX_PLAN_SEGMENTED 1 /* ordered logs with long equal-timestamp groups */
 #define SMX_PLAN_RADIX 2     /* unordered logs: radix sort on (ts, oid_hi) */
 #define SMX_PLAN_RADIX_LO 3  /* ... and oid_lo (duplicate (ts, oid_hi) pairs) */
+#define SMX_PLAN_PRESORTED_WIDE 4 /* ordered logs, groups up to 8192 ops: wide presorted windows */
 int smx_last_plan(void);
 
 /*

@@ -72,7 +72,7 @@ class SmxShard(C.Structure):
 SHARD_ORDER, SHARD_WALK, SHARD_TABLES, SHARD_EMIT = 0, 1, 2, 3
 SHARD_ORDER_FIX = 4
 SHARD_SCATTER = 5
-PLAN_NAMES = ("presorted", "segmented", "radix", "radix+oid_lo")  # smx_last_plan()
+PLAN_NAMES = ("presorted", "segmented", "radix", "radix+oid_lo", "presorted-wide")  # smx_last_plan()
 SHARD_SUMMARY = 32
 
 

@@ -243,16 +243,15 @@ __global__ void k_meta_init(ComposeMeta* meta) {
 // search runs on them, the second inside one chunk.  The snap gallops back over
 // the (short) run of equal timestamps.
 __global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB, const u64* __restrict__ sA,
-                        const u64* __restrict__ sB, i64 na, i64 nb, i64 W, i64 tgt, i64* __restrict__ bnd,
+                        const u64* __restrict__ sB, i64 na, i64 nb, i64 W, i64 tgt, i64 D, i64* __restrict__ bnd,
                         ComposeMeta* meta, u32* long_host) {
   const i64 k = (i64)blockIdx.x * BLOCK + threadIdx.x;
   if (SMX_KHIST_LONG) {
-    // A chunk sample equal to the sample WF_CAP ops later (A: first ops of chunks c and
-    // c + WF_CAP / CH; B: last ops of full chunks): that timestamp group alone overflows a
-    // window, so the presorted plan cannot hold (config 5's groups).  Flagged before the
-    // windows run: k_window_f then leaves before its loads (6: a window too large, and
-    // smaller windows cannot help).  Grid-stride over the samples, off the search's path.
-    constexpr i64 D = WF_CAP / CH;
+    // A chunk sample equal to the sample D chunks (one window capacity) later (A: first
+    // ops of chunks c and c + D; B: last ops of full chunks): that timestamp group alone
+    // overflows a window, so the presorted plan cannot hold.  Flagged before the windows
+    // run: k_window_f then leaves before its loads (6: a window too large, and smaller
+    // windows cannot help).  Grid-stride over the samples, off the search's path.
     const i64 nt = (i64)gridDim.x * BLOCK, ca = SMX_CEIL_DIV(na, (i64)CH), cb = nb / CH;
     bool lg = false;
     for (i64 c = k; c + D < ca; c += nt) lg |= sA[c] == sA[c + D];
@@ -1549,7 +1548,9 @@ struct EarlyFail {
   u32* flag_dev = nullptr;
   hipEvent_t ev = nullptr;
 };
-static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr) {
+// wide: WF_WIDE_CAP-op windows on WF_WIDE_NT threads (one per CU) for logs whose
+// equal-timestamp groups no WF_CAP window holds (config 5: 8192-op groups).
+static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr, bool wide = false) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
@@ -1560,7 +1561,8 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
     if (rc) return rc;
   }
   if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
-  if (tgt > WF_CAP) tgt = WF_CAP;
+  const i64 cap = wide ? WF_WIDE_CAP : WF_CAP;
+  if (tgt > cap) tgt = cap;
   tgt -= tgt % CH;  // chunk-aligned diagonals (k_fpart's sampled first level)
   const i64 W = SMX_CEIL_DIV(C.n, tgt);
   const i64 CM = SMX_CEIL_DIV(C.na > C.nb ? C.na : C.nb, (i64)CH) + 1;
@@ -1573,7 +1575,7 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
                      early ? early->flag_dev : nullptr);
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
                      C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na,
-                     C.nb, W, tgt, bnd, meta, early ? early->flag_dev : nullptr);
+                     C.nb, W, tgt, cap / CH, bnd, meta, early ? early->flag_dev : nullptr);
   if (early) HIP_TRY(hipEventRecord(early->ev, st));
   {
     const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);
@@ -1599,13 +1601,19 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
   P.ablate = knob("SMX_ABLATE", 0);
   C.tm->begin(ST_WINDOW);
 #if SMX_DIAG
-  if (g_phase_dbg && !P.src_map && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
+  if (g_phase_dbg && !wide && !P.src_map && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
     P.dbg = (u64*)g_phase_dbg;
-    hipLaunchKernelGGL((k_window_f<true, false>), dim3(W), dim3(WF_NT), 0, st, P);
+    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, true, false>), dim3(W), dim3(WF_NT), 0, st, P);
   } else
 #endif
-  if (P.src_map) hipLaunchKernelGGL((k_window_f<false, true>), dim3(W), dim3(WF_NT), 0, st, P);
-  else hipLaunchKernelGGL((k_window_f<false, false>), dim3(W), dim3(WF_NT), 0, st, P);
+  if (wide) {
+    if (P.src_map) hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, true>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
+    else hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, false>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
+  } else if (P.src_map) {
+    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, true>), dim3(W), dim3(WF_NT), 0, st, P);
+  } else {
+    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, false>), dim3(W), dim3(WF_NT), 0, st, P);
+  }
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_WINDOW);
   return SMX_OK;
@@ -2083,6 +2091,16 @@ static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeM
     if ((rc = run_presorted(C, tgt))) return rc;
     if (tail && (rc = launch_tail(C))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
+  }
+  // ordered logs whose equal-timestamp groups no WF_CAP window holds (f_fail 6, or 2 at
+  // the smallest windows): the wide windows, from half their capacity down (a window
+  // holds its target plus the group its end snaps back over)
+  for (i64 wt = WF_WIDE_CAP / 2; hm->f_fail && !(hm->f_fail & 1) && !hm->bad_sym && wt >= WIN_TGT_MIN; wt /= 2) {
+    g_plan = SMX_PLAN_PRESORTED_WIDE;
+    if ((rc = run_presorted(C, wt, nullptr, true))) return rc;
+    if (tail && (rc = launch_tail(C))) return rc;
+    if ((rc = read_meta(C, hm))) return rc;
+    if (hm->f_fail != 2) break;  // held, or groups longer than a wide window (6), or unordered (1)
   }
   if (hm->f_fail && !hm->bad_sym && allow_generic) {
     if (C.ops->b_gap != 0)

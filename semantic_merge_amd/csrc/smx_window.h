@@ -141,7 +141,7 @@ __device__ __forceinline__ i32 win_gsrc(const WinArgs& P, i64 j) {
 // Flags -> candidate slots in M order; thread 0 writes where the boundary renames
 // (after the other branch's last rename of the window) start.
 // SymCls(x) -> (symbol, newName class) of rename x.
-template <int NT, typename SideOwn, typename SymCls>
+template <int NT, int NCHK, typename SideOwn, typename SymCls>
 __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mbase, int RN, int cntA,
                                                  int cntB, const u16* posl, u64* cb, SideOwn side_own,
                                                  SymCls sym_cls) {
@@ -181,7 +181,8 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
   for (int c = wv; c < nrc; c += NW) {
     const u64 b = cb[c];
     if (!b) continue;
-    u32 before = lane < c ? (u32)__popcll(cb[lane]) : 0u;  // c < NCHUNK <= WAVE
+    u32 before = lane < c ? (u32)__popcll(cb[lane]) : 0u;  // chunks before c
+    if (NCHK > WAVE) before += WAVE + lane < c ? (u32)__popcll(cb[WAVE + lane]) : 0u;
     before = wave_incl_sum(before);
     before = __builtin_amdgcn_readlane(before, WAVE - 1);
     if ((b >> lane) & 1ull) {
@@ -205,6 +206,10 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_CAP
 #define WF_CAP WIN_CAP              // max ops per presorted window
 #endif
+#ifndef WF_WIDE_CAP
+#define WF_WIDE_CAP 8192  // the wide presorted window (run_presorted(wide)): one per CU
+#endif
+#define WF_WIDE_NT 1024
 #define WF_NCH (WF_CAP / WAVE)
 #define WF_WAVES (WF_NT / WAVE)
 #define WF_ITEMS (WF_CAP / WF_NT)
@@ -246,8 +251,11 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_ONEATOM
 #define WF_ONEATOM 1 // step 5 places each slot at start + arrival rank (one LDS atomic per element, not two)
 #endif
+#ifndef WF_TIEFIX
+#define WF_TIEFIX 1  // wide windows: equal 32-bit keys in a bucket ranked on the full ids right there (no window re-rank)
+#endif
 #ifndef WF_RANK8
-#define WF_RANK8 1   // step 5's bucket rank: 8 predicated compares, the loop only for larger buckets / equal halves
+#define WF_RANK8 0   // step 5's bucket rank by 8 predicated compares (the loop only for larger buckets): window 1.223 -> 1.260 ms, off (profiles/r04_d)
 #endif
 #ifndef WF_BK16
 #define WF_BK16 1    // bucket-ordered 16-bit key prefixes for the rank loop (window 1.329 -> 1.286 ms, profiles/r03_e/ab.txt)
@@ -269,27 +277,35 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #else
 #define WF_BOUNDS __launch_bounds__(WF_NT, WF_MINB)
 #endif
-template <bool DBG, bool MAP>
-__global__ void WF_BOUNDS k_window_f(WinArgs P) {
-  __shared__ __attribute__((aligned(16))) u64 sts[WF_CAP];  // element space: timestamps; later slot-space rank keys
-  __shared__ __attribute__((aligned(16))) u16 sord[WF_CAP];  // S order (merge), later the final order
-  __shared__ u16 fin[WF_CAP];        // slot -> element, later rename ranks
-  __shared__ u16 sl[WF_CAP];         // element -> slot, later rank -> slot, later posl
-  __shared__ u8 skind[WF_CAP];
-  __shared__ __attribute__((aligned(16))) u8 skS[WF_CAP];  // kinds in S order, later by slot (WF_OUT2)
+template <int CAP, int NT, bool DBG, bool MAP>
+__global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinArgs P) {
+  // CAP ops per window on NT threads: (2048, 512) four windows per CU; (8192, 1024) one
+  // window per CU for logs whose equal-timestamp groups need it (config 5)
+  constexpr int ITEMS = CAP / NT, NCH = CAP / WAVE, WAVES = NT / WAVE, KP = (2 * CH + NT - 1) / NT;
+  // equal 32-bit rank keys resolved in the rank loop itself (the wide window, whose
+  // 8192-op groups see ~1 such pair in 128 and whose exact re-rank would be quadratic);
+  // the small windows flag them for the window re-rank (fewer registers in the loop)
+  constexpr bool TIEFIX = WF_TIEFIX && CAP > WF_CAP;
+  static_assert(CAP % NT == 0 && NCH <= 2 * WAVE && CAP <= 65536, "window geometry");
+  __shared__ __attribute__((aligned(16))) u64 sts[CAP];  // element space: timestamps; later slot-space rank keys
+  __shared__ __attribute__((aligned(16))) u16 sord[CAP];  // S order (merge), later the final order
+  __shared__ u16 fin[CAP];        // slot -> element, later rename ranks
+  __shared__ u16 sl[CAP];         // element -> slot, later rank -> slot, later posl
+  __shared__ u8 skind[CAP];
+  __shared__ __attribute__((aligned(16))) u8 skS[CAP];  // kinds in S order, later by slot (WF_OUT2)
 #if WF_OUT2
-  __shared__ u16 inv[WF_CAP];        // element -> final slot
+  __shared__ u16 inv[CAP];        // element -> final slot
   __shared__ u64 tbase[SMX_N_KINDS]; // T of a kind's slot x = tbase[kind] + x
 #endif
-  __shared__ u64 gbits[WF_NCH];       // group-start bits over slots, later candidate ballots
-  __shared__ u16 ccnt[WF_NCH][SMX_N_KINDS];
-  __shared__ u16 rc[WF_NCH][2];
+  __shared__ u64 gbits[NCH];       // group-start bits over slots, later candidate ballots
+  __shared__ u16 ccnt[NCH][SMX_N_KINDS];
+  __shared__ u16 rc[NCH][2];
   __shared__ u32 kbase[SMX_N_KINDS + 1];
   __shared__ u32 wck[SMX_N_KINDS];
   __shared__ u64 base[SMX_N_KINDS + 1];
   __shared__ u32 woffk[SMX_N_KINDS + 2];  // this window's offsets: kinds, renames of A, of B
   __shared__ u32 wtot[2];                 // the window's renames of A, of B
-  __shared__ u32 vbw[WF_WAVES][3];        // per wave: value widths (addr, file, name)
+  __shared__ u32 vbw[WAVES][3];        // per wave: value widths (addr, file, name)
   u16* rown = fin;                    // rename rank within its branch (after step 5)
 
   const int t = threadIdx.x;
@@ -304,7 +320,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   const int na = (int)(P.bnd[2 * w + 2] - a0);
   const int nb = (int)(P.bnd[2 * w + 3] - b0);
   const int sz = na + nb;
-  if (na < 0 || nb < 0 || sz > WF_CAP) {  // the presorted plan does not hold
+  if (na < 0 || nb < 0 || sz > CAP) {  // the presorted plan does not hold
     // bit 0: branch logs not timestamp-ordered; bit 1: window too large for LDS;
     // bit 2: ... and it holds one timestamp only, so smaller windows cannot help
     if (threadIdx.x == 0) {
@@ -325,10 +341,10 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   WSTAMP(0);
 
   // 1. load the sort keys (kind, timestamp, top of the id) and the payload
-  u32 hi_r[WF_ITEMS];  // the top 32 bits of oid_hi: the rank key (only they are loaded)
-  u32 sym_r[WF_ITEMS];
-  i32 v0_r[WF_ITEMS], v1_r[WF_ITEMS];
-  u32 k_r[WF_ITEMS];
+  u32 hi_r[ITEMS];  // the top 32 bits of oid_hi: the rank key (only they are loaded)
+  u32 sym_r[ITEMS];
+  i32 v0_r[ITEMS], v1_r[ITEMS];
+  u32 k_r[ITEMS];
   bool bad = false;
   // every global read of the window is issued here, before any loaded value is used:
   // the load phase is one round trip to memory, and the later phases find their
@@ -336,10 +352,10 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   // reads go first, so that their address arithmetic never waits on the bulk loads.
   // kinds of the <= 255 ops between each branch's chunk start and the window start
   // (window offsets below); entries 0..255 branch A, 256..511 branch B
-  u32 kpart[WF_KP];
+  u32 kpart[KP];
 #pragma unroll
-  for (int u = 0; u < WF_KP; ++u) {
-    const int x = t + WF_NT * u;
+  for (int u = 0; u < KP; ++u) {
+    const int x = t + NT * u;
     const int pa = (int)(a0 % CH), pb = (int)(b0 % CH);
     const int side = x >= CH;
     const int q = x - side * CH;
@@ -376,14 +392,14 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
   // all loads are issued unconditionally (clamped to a valid op) so that the
   // loads of a lane are in flight together; the guards apply to the LDS stores only
-  u64 ts_r[WF_ITEMS];
+  u64 ts_r[ITEMS];
   auto op_index = [&](int e) -> i64 {  // (an empty window still writes its exports)
     const int ec = e < sz ? e : 0;
     return sz == 0 ? 0 : (ec < na ? a0 + ec : bld + ec);
   };
 #pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i) {
-    const i64 j = op_index(t + WF_NT * i);
+  for (int i = 0; i < ITEMS; ++i) {
+    const i64 j = op_index(t + NT * i);
     k_r[i] = P.kind[j];
     ts_r[i] = P.kts[j];
     hi_r[i] = reinterpret_cast<const u32*>(P.khi)[2 * j + 1];
@@ -396,10 +412,10 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
 #if WF_BF
   // branch-free: the LDS slots past sz take harmless values (every later phase reads
   // slots < sz only), the rest is selects -- no exec-mask bookkeeping per item
-  static_assert(WF_NT * WF_ITEMS <= WF_CAP, "item slots inside the LDS arrays");
+  static_assert(NT * ITEMS <= CAP, "item slots inside the LDS arrays");
 #pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i) {
-    const int e = t + WF_NT * i;
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e = t + NT * i;
     const bool ok = e < sz;
     const u32 kr = k_r[i];
     bad |= ok & ((kr >= SMX_N_KINDS) | (sym_r[i] >= (u64)P.n_sym));
@@ -416,8 +432,8 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
 #else
 #pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i) {
-    const int e = t + WF_NT * i;
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e = t + NT * i;
     if (e < sz) {
       bad |= k_r[i] >= SMX_N_KINDS || sym_r[i] >= (u64)P.n_sym;
       const u32 k = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
@@ -445,7 +461,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     vbw[wv][2] = vb_c;
   }
   if (bad) P.meta->bad_sym = 1;
-  for (int i = t; i < WF_NCH * SMX_N_KINDS; i += WF_NT) (&ccnt[0][0])[i] = 0;
+  for (int i = t; i < NCH * SMX_N_KINDS; i += NT) (&ccnt[0][0])[i] = 0;
   if (t <= SMX_N_KINDS) base[t] = base_v;
   if (t < SMX_N_KINDS) wck[t] = 0;
   if (t < SMX_N_KINDS + 2) woffk[t] = woff_x + woff_y;
@@ -456,22 +472,22 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   if (SMX_DIAG && (P.ablate & 16)) {  // diagnostics: load only (keeps every load live)
     u32 x = 0;
 #pragma unroll
-    for (int i = 0; i < WF_ITEMS; ++i) x += sym_r[i] + (u32)v0_r[i] + (u32)v1_r[i] + (u32)hi_r[i];
+    for (int i = 0; i < ITEMS; ++i) x += sym_r[i] + (u32)v0_r[i] + (u32)v1_r[i] + (u32)hi_r[i];
     if (x == 0x9e3779b9u) P.meta->dup_key = 1;
     return;
   }
   // window offsets: the partial-chunk kinds
 #pragma unroll
-  for (int u = 0; u < WF_KP; ++u) {
+  for (int u = 0; u < KP; ++u) {
     if (kpart[u] != 0xffffffffu) {
       const u32 k = kpart[u] < SMX_N_KINDS ? kpart[u] : SMX_N_KINDS - 1;
       atomicAdd(&woffk[k], 1u);
-      if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + (t + WF_NT * u >= CH)], 1u);
+      if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + (t + NT * u >= CH)], 1u);
     }
   }
 
   // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties
-  //    (compose.py:54): merge path, WF_ITEMS outputs per lane, with the kinds
+  //    (compose.py:54): merge path, ITEMS outputs per lane, with the kinds
   //    copied into S order.  Presorted-layout check: every adjacent pair of each
   //    branch log is non-decreasing (the pair straddling a window start is checked
   //    here too); it shares the merge's barrier and a window that fails it discards
@@ -479,17 +495,17 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   bool dec = false;
   if (t == 0) {
     dec = (a0 > 0 && na > 0 && prev_a > sts[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
-    win_publish_widths(P.meta, &vbw[0][0], WF_WAVES, vcur);
+    win_publish_widths(P.meta, &vbw[0][0], WAVES, vcur);
   }
 #pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i) {
-    const int e = t + WF_NT * i;
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e = t + NT * i;
     if (e >= sz) continue;
     if (!(SMX_DIAG && (P.ablate & 1)) && e != 0 && e != na && sts[e - 1] > ts_r[i]) dec = true;
   }
   {
-    const int d0 = t * WF_ITEMS < sz ? t * WF_ITEMS : sz;
-    const int d1 = d0 + WF_ITEMS < sz ? d0 + WF_ITEMS : sz;
+    const int d0 = t * ITEMS < sz ? t * ITEMS : sz;
+    const int d1 = d0 + ITEMS < sz ? d0 + ITEMS : sz;
     int lo = d0 - nb > 0 ? d0 - nb : 0, hi = d0 < na ? d0 : na;
     // (a fixed count of predicated halving steps measured slower: window 1.225 -> 1.270 ms,
     //  profiles/r03_x/ab_merge_search_fixed_steps.txt)
@@ -500,9 +516,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     }
     int ia = lo, ib = d0 - lo;
 #if WF_BF
-    // WF_ITEMS outputs, predicated (a thread past sz stores nothing)
+    // ITEMS outputs, predicated (a thread past sz stores nothing)
 #pragma unroll
-    for (int u = 0; u < WF_ITEMS; ++u) {
+    for (int u = 0; u < ITEMS; ++u) {
       const int d = d0 + u;
       const u64 ta = sts[ia < na ? ia : 0], tb = sts[na + (ib < nb ? ib : 0)];
       const bool take_a = ia < na && (ib >= nb || ta <= tb);
@@ -531,13 +547,13 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   WF_EXIT(2);
 
   // 3. stable multisplit of S by rank (wave ballots); element, kind and rank stay in
-  //    registers for the scatter (m = t + WF_NT * j is chunk wv + WF_WAVES * j)
+  //    registers for the scatter (m = t + NT * j is chunk wv + WAVES * j)
   const int nch = (sz + WAVE - 1) / WAVE;
-  int me[WF_ITEMS];
-  u32 mkr[WF_ITEMS];  // kind | rank << 8
+  int me[ITEMS];
+  u32 mkr[ITEMS];  // kind | rank << 8
 #pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) {
-    const int m = t + WF_NT * j;
+  for (int j = 0; j < ITEMS; ++j) {
+    const int m = t + NT * j;
     me[j] = m < sz ? sord[m] : 0;
     mkr[j] = m < sz ? skS[m] : 0u;
   }
@@ -549,9 +565,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   const int kbits = 32 - __clz((int)(max(__popc(kpres), 1u) - 1u));
 #endif
 #pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) {
-    const int m = t + WF_NT * j;
-    const int c = wv + WF_WAVES * j;
+  for (int j = 0; j < ITEMS; ++j) {
+    const int m = t + NT * j;
+    const int c = wv + WAVES * j;
     const bool valid = m < sz;
     const u32 k = mkr[j];
 #if WF_DENSE_KINDS
@@ -569,12 +585,18 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   __syncthreads();
   WSTAMP(4);
   WF_EXIT(3);
-  for (int k = wv; k < SMX_N_KINDS; k += WF_WAVES) {
-    const u32 x = lane < nch ? ccnt[lane][k] : 0u;
-    const u32 inc = wave_incl_sum(x);
-    if (lane < nch) ccnt[lane][k] = (u16)(inc - x);
+  for (int k = wv; k < SMX_N_KINDS; k += WAVES) {
+    u32 carry = 0;
+#pragma unroll
+    for (int c0 = 0; c0 < NCH; c0 += WAVE) {  // (one pass when NCH <= 64)
+      const int c = c0 + lane;
+      const u32 x = c < nch ? ccnt[c][k] : 0u;
+      const u32 inc = wave_incl_sum(x);
+      if (c < nch) ccnt[c][k] = (u16)(carry + inc - x);
+      if (NCH > WAVE) carry += (u32)__builtin_amdgcn_readlane((int)inc, WAVE - 1);
+    }
   }
-  if (wv == WF_WAVES - 1) {  // (kinds 7 and 15 only on this wave)
+  if (wv == WAVES - 1) {  // (kinds 7 and 15 only on this wave)
     const u32 x = lane < SMX_N_KINDS ? wck[lane] : 0u;
     const u32 inc = wave_incl_sum(x);
     if (lane < SMX_N_KINDS) kbase[lane] = inc - x;
@@ -584,11 +606,11 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   WSTAMP(6);
   WF_EXIT(4);
 #pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) {
-    const int m = t + WF_NT * j;
+  for (int j = 0; j < ITEMS; ++j) {
+    const int m = t + NT * j;
     if (m < sz) {
       const u32 k = mkr[j] & 0xffu;
-      const int p = kbase[k] + ccnt[wv + WF_WAVES * j][k] + (mkr[j] >> 8);
+      const int p = kbase[k] + ccnt[wv + WAVES * j][k] + (mkr[j] >> 8);
       fin[p] = (u16)me[j];
       sl[me[j]] = (u16)p;
       if (WF_OUT2) skS[p] = (u8)k;  // (skS was read in the prologue, before two barriers)
@@ -601,8 +623,8 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   // 4. group-start bits (a group = equal (rank, timestamp), contiguous in slots),
   //    then the timestamps are dead and their buffer takes the slot-space oid prefix
 #pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) {
-    const int p = t + WF_NT * j;
+  for (int j = 0; j < ITEMS; ++j) {
+    const int p = t + NT * j;
     bool f = false;
     if (p < sz) {
       const int e = fin[p];
@@ -613,7 +635,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
 #endif
     }
     const u64 b = __ballot(f);
-    if (lane == 0 && (p >> 6) < WF_NCH) gbits[p >> 6] = b;
+    if (lane == 0 && (p >> 6) < NCH) gbits[p >> 6] = b;
   }
   __syncthreads();
   WSTAMP(8);
@@ -622,8 +644,8 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   // the rank phase's collision check
   u32* pkey = (u32*)sts;
 #pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i) {
-    const int e = t + WF_NT * i;
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e = t + NT * i;
     if (e < sz) {
       const int p = sl[e];
       pkey[p] = hi_r[i];
@@ -632,7 +654,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
 #if WF_BUCKET && WF_BZ4
   // step 5's bucket counters (the upper half of sts: the timestamps are dead)
-  for (int i = t; i < WF_CAP / 2; i += WF_NT) reinterpret_cast<u32*>(sts)[WF_CAP + i] = 0u;
+  for (int i = t; i < CAP / 2; i += NT) reinterpret_cast<u32*>(sts)[CAP + i] = 0u;
 #endif
   __syncthreads();
   WSTAMP(9);
@@ -657,11 +679,20 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   };
   // the group bounds of a wave's 64 consecutive slots from one read of every
   // group-start word (nch <= 32) and lane broadcasts: no dependent LDS chain
+  // (NCH > 64: a second word per lane, gw1 / gnz1 for chunks 64..127)
   const u64 gw = lane < nch ? gbits[lane] : 0ull;
   const u64 gnz = __ballot(gw != 0);
+  const u64 gw1 = NCH > WAVE && WAVE + lane < nch ? gbits[(WAVE + lane) % NCH] : 0ull;
+  const u64 gnz1 = NCH > WAVE ? __ballot(gw1 != 0) : 0ull;
   auto bcast64 = [](u64 v, int l) -> u64 {
     return (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, l) |
            ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), l) << 32);
+  };
+  // group-start word i (wave-uniform i < NCH), with the whole wave active
+  auto gword = [&](int i) -> u64 {
+    if (NCH <= WAVE) return bcast64(gw, i);
+    const u64 a = bcast64(gw, i & (WAVE - 1)), b = bcast64(gw1, i & (WAVE - 1));
+    return i < WAVE ? a : b;
   };
   const u64 le_mask = lanemask_lt() | (1ull << lane);
 #if WF_BUCKET
@@ -671,42 +702,58 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   // interpolation buckets over slot space: slot p of group [gs, ge) goes to bucket
   // gs + (ge - gs) * key / 2^32 (one op per bucket on random ids); 16-bit counters,
   // two per word, in the upper half of sts (free until step 7)
-  u32* bcnt = reinterpret_cast<u32*>(sts) + WF_CAP;
+  u32* bcnt = reinterpret_cast<u32*>(sts) + CAP;
 #if WF_BK16
   // the top 16 bits of each key in bucket order (the last quarter of sts): the rank
   // loop compares them without the slot -> key chain, the full key only on a tie
-  u16* bk16 = reinterpret_cast<u16*>(reinterpret_cast<u32*>(sts) + WF_CAP + WF_CAP / 2);
-  u32 own_r[WF_ITEMS];
+  u16* bk16 = reinterpret_cast<u16*>(reinterpret_cast<u32*>(sts) + CAP + CAP / 2);
+  u32 own_r[ITEMS];
 #endif
 #if !WF_BZ4
-  for (int i = t; i < WF_CAP / 2; i += WF_NT) bcnt[i] = 0u;
+  for (int i = t; i < CAP / 2; i += NT) bcnt[i] = 0u;
   __syncthreads();
 #endif
-  u32 bk_r[WF_ITEMS];
-  u32 kp_r[WF_ITEMS];
+  u32 bk_r[ITEMS];
+  u32 kp_r[ITEMS];
 #if WF_ONEATOM
-  u32 ar_r[WF_ITEMS];  // arrival rank inside the bucket (the count atomic's return value)
+  u32 ar_r[ITEMS];  // arrival rank inside the bucket (the count atomic's return value)
 #endif
 #pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) bk_r[j] = 0xffffffffu, kp_r[j] = 0u;
+  for (int j = 0; j < ITEMS; ++j) bk_r[j] = 0xffffffffu, kp_r[j] = 0u;
 #endif
 #pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) {
-    const int wi = __builtin_amdgcn_readfirstlane((WF_NT * j) / WAVE + wv);  // this wave's slot chunk
+  for (int j = 0; j < ITEMS; ++j) {
+    const int wi = __builtin_amdgcn_readfirstlane((NT * j) / WAVE + wv);  // this wave's slot chunk
     if (wi >= nch) break;  // wave-uniform
     const int p = wi * WAVE + lane;
     // Group bounds, branch-free: every lane broadcast (v_readlane) runs with the whole
     // wave active.  (Lane reads inside the lanes' divergent branches mis-ordered groups
     // in some builds: a register's value in lanes outside the branch is not defined.)
     // The last group start before the chunk and the first one after it are scalar.
-    const u64 W = bcast64(gw, wi);
-    const u64 prevm = gnz & ((1ull << wi) - 1);  // (slot 0 always starts a group)
-    const int wp = prevm ? 63 - __clzll(prevm) : 0;
-    const int prevS = wp * WAVE + 63 - __clzll(bcast64(gw, wp) | 1ull);
-    const u64 nxtm = wi + 1 < WAVE ? gnz & ~((2ull << wi) - 1) : 0ull;
-    const int wn = nxtm ? __ffsll((unsigned long long)nxtm) - 1 : 0;
-    const u64 Wn = bcast64(gw, wn);
-    const int nextS = nxtm ? wn * WAVE + __ffsll((unsigned long long)(Wn | (1ull << 63))) - 1 : sz;
+    const u64 W = gword(wi);
+    int wp, wn;
+    bool has_next;
+    if (NCH <= WAVE) {
+      const u64 prevm = gnz & ((1ull << wi) - 1);  // (slot 0 always starts a group)
+      wp = prevm ? 63 - __clzll(prevm) : 0;
+      const u64 nxtm = wi + 1 < WAVE ? gnz & ~((2ull << wi) - 1) : 0ull;
+      has_next = nxtm != 0;
+      wn = nxtm ? __ffsll((unsigned long long)nxtm) - 1 : 0;
+    } else {
+      // the last non-empty word before wi and the first after it, over 128 words
+      const int wl = wi & (WAVE - 1);
+      const u64 below0 = wi < WAVE ? gnz & ((1ull << wl) - 1) : gnz;
+      const u64 below1 = wi < WAVE ? 0ull : gnz1 & ((1ull << wl) - 1);
+      wp = below1 ? WAVE + 63 - __clzll(below1) : (below0 ? 63 - __clzll(below0) : 0);
+      const u64 above0 = wi < WAVE ? (wl + 1 < WAVE ? gnz & ~((2ull << wl) - 1) : 0ull) : 0ull;
+      const u64 above1 = wi < WAVE ? gnz1 : (wl + 1 < WAVE ? gnz1 & ~((2ull << wl) - 1) : 0ull);
+      has_next = (above0 | above1) != 0;
+      wn = above0 ? __ffsll((unsigned long long)above0) - 1
+                  : (above1 ? WAVE + __ffsll((unsigned long long)above1) - 1 : 0);
+    }
+    const int prevS = wp * WAVE + 63 - __clzll(gword(wp) | 1ull);
+    const u64 Wn = gword(wn);
+    const int nextS = has_next ? wn * WAVE + __ffsll((unsigned long long)(Wn | (1ull << 63))) - 1 : sz;
     const u64 below = W & le_mask, above = W & ~le_mask;
     const int gs = below ? wi * WAVE + 63 - __clzll(below | 1ull) : prevS;
     int ge = above ? wi * WAVE + __ffsll((unsigned long long)(above | (1ull << 63))) - 1 : nextS;
@@ -754,20 +801,29 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
 #if WF_BUCKET
   {
     __syncthreads();
-    // exclusive scan of the counters, 4 per thread (2 words)
-    const u32 w0 = bcnt[2 * t], w1 = bcnt[2 * t + 1];
-    const u32 c0 = w0 & 0xffffu, c1 = w0 >> 16, c2 = w1 & 0xffffu, c3 = w1 >> 16;
+    // exclusive scan of the CAP counters: CAP / NT per thread (two 16-bit ones per word)
+    constexpr int WPT = CAP / (2 * NT);
+    u32 cw[WPT], sum = 0;
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      cw[i] = bcnt[WPT * t + i];
+      sum += (cw[i] & 0xffffu) + (cw[i] >> 16);
+    }
     u32 tot;
-    const u32 e0 = block_excl_scan<OpSum, u32, WF_WAVES>(c0 + c1 + c2 + c3, &vbw[0][0], &tot);  // (vbw is dead after step 2)
-    bcnt[2 * t] = e0 | ((e0 + c0) << 16);
-    bcnt[2 * t + 1] = (e0 + c0 + c1) | ((e0 + c0 + c1 + c2) << 16);
+    u32 run = block_excl_scan<OpSum, u32, WAVES>(sum, &vbw[0][0], &tot);  // (vbw is dead after step 2)
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const u32 c0 = cw[i] & 0xffffu, c1 = cw[i] >> 16;
+      bcnt[WPT * t + i] = run | ((run + c0) << 16);
+      run += c0 + c1;
+    }
     __syncthreads();
     // scatter the slots into their buckets (sl: bucket position -> slot); the counters
     // become the bucket ends (WF_ONEATOM: they stay the starts; position = start +
     // arrival rank, no second atomic)
-    u32 lo_r[WF_ITEMS];
+    u32 lo_r[ITEMS];
 #pragma unroll
-    for (int j = 0; j < WF_ITEMS; ++j) {
+    for (int j = 0; j < ITEMS; ++j) {
       const u32 b = bk_r[j];
       lo_r[j] = 0;
       if (b == 0xffffffffu) continue;
@@ -779,7 +835,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       const u32 old = atomicAdd(&bcnt[b >> 1], 1u << sh);
       const u32 pos = (old >> sh) & 0xffffu;
 #endif
-      sl[pos] = (u16)((WF_NT * j) / WAVE * WAVE + wv * WAVE + lane);
+      sl[pos] = (u16)((NT * j) / WAVE * WAVE + wv * WAVE + lane);
 #if WF_BK16
       own_r[j] = pos;
       bk16[pos] = (u16)(kp_r[j] >> 16);
@@ -787,9 +843,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     }
     __syncthreads();
     // rank inside the bucket on the 32-bit key
-    int rr[WF_ITEMS];
+    int rr[ITEMS];
 #pragma unroll
-    for (int j = 0; j < WF_ITEMS; ++j) {
+    for (int j = 0; j < ITEMS; ++j) {
       const u32 b = bk_r[j];
       rr[j] = -1;
       if (b == 0xffffffffu) continue;
@@ -797,7 +853,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       // bucket [start(b), start(b + 1)); the starts are an exclusive scan over every
       // bucket of the window (buckets past the last slot start at the total)
       const u32 lo = lo_r[j];
-      const u32 e = b + 1 < (u32)WF_CAP ? (bcnt[(b + 1) >> 1] >> (16 * ((b + 1) & 1))) & 0xffffu : (u32)sz;
+      const u32 e = b + 1 < (u32)CAP ? (bcnt[(b + 1) >> 1] >> (16 * ((b + 1) & 1))) & 0xffffu : (u32)sz;
 #else
       const u32 e = (bcnt[b >> 1] >> (16 * (b & 1))) & 0xffffu;
       const u32 lo = b ? (bcnt[(b - 1) >> 1] >> (16 * ((b - 1) & 1))) & 0xffffu : 0u;
@@ -835,8 +891,18 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
           c += x < k16;
         } else {  // equal top halves: the full keys (rare)
           const u32 k = pkey[sl[q]];
-          c += k < kp;
-          eq += k == kp;
+          if (!TIEFIX || k != kp) {
+            c += k < kp;
+            eq += k == kp;
+          } else {
+            // equal 32-bit keys (duplicate ids; ~1 pair in 2^33 per group on random
+            // ids): the full ids, then slot order -- (side, index) order in a group
+            const int pm = (NT * j) / WAVE * WAVE + wv * WAVE + lane, po = sl[q];
+            const int em = fin[pm], eo = fin[po];
+            const i64 jm = em < na ? a0 + em : bld + em, jo = eo < na ? a0 + eo : bld + eo;
+            const u64 hm = P.khi[jm], ho = P.khi[jo], lm = P.klo[jm], lo2 = P.klo[jo];
+            c += ho < hm || (ho == hm && (lo2 < lm || (lo2 == lm && po < pm)));
+          }
         }
       }
       }
@@ -852,7 +918,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       if (WF_FUSEFIN && !DBG) {
         // the final order at once: nothing in this loop reads sord or inv, and the
         // rank -> slot map is not needed after step 5 (the exact re-rank rebuilds it)
-        const int e = fin[(WF_NT * j) / WAVE * WAVE + wv * WAVE + lane];
+        const int e = fin[(NT * j) / WAVE * WAVE + wv * WAVE + lane];
         sord[rr[j]] = (u16)e;
 #if WF_OUT2
         inv[e] = (u16)rr[j];
@@ -862,9 +928,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     if (!(WF_FUSEFIN && !DBG)) {
       __syncthreads();
 #pragma unroll
-      for (int j = 0; j < WF_ITEMS; ++j) {
+      for (int j = 0; j < ITEMS; ++j) {
         if (rr[j] < 0) continue;
-        const int p = (WF_NT * j) / WAVE * WAVE + wv * WAVE + lane;
+        const int p = (NT * j) / WAVE * WAVE + wv * WAVE + lane;
         const int e = fin[p];
         sord[rr[j]] = (u16)e;
         sl[rr[j]] = (u16)p;  // sl maps rank -> slot (the diagnostic order check)
@@ -877,12 +943,12 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
 #endif
   __syncthreads();
   if (DBG) {  // diagnostics: the group order against the slot-space keys (dbg words 5, 17, 18)
-    for (int r = t + 1; r < sz; r += WF_NT) {
+    for (int r = t + 1; r < sz; r += NT) {
       const bool start = (gbits[r >> 6] >> (r & 63)) & 1ull;
       if (!start && pkey[sl[r - 1]] > pkey[sl[r]]) atomicAdd((unsigned long long*)&P.dbg[w * WF_NSTAMP + 5], 1ull);
       if (!start && sts[0] == 0x12345ull) P.meta->dup_key = 3;  // (keeps sts live)
     }
-    for (int r = t; r < sz; r += WF_NT) {
+    for (int r = t; r < sz; r += NT) {
       const int p0 = sl[r];
       if (p0 >= sz) atomicAdd((unsigned long long*)&P.dbg[w * WF_NSTAMP + 17], 1ull);
       else if (fin[p0] != sord[r]) atomicAdd((unsigned long long*)&P.dbg[w * WF_NSTAMP + 18], 1ull);
@@ -896,12 +962,12 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   //    (rare) exact re-rank.
   const int R0 = kbase[KREN], RN = wck[KREN];
   const int nrc = (RN + WAVE - 1) / WAVE;
-  constexpr int RQ = (WF_NCH + WF_WAVES - 1) / WF_WAVES;  // rename chunks per wave
+  constexpr int RQ = (NCH + WAVES - 1) / WAVES;  // rename chunks per wave
   u32 rown_r[RQ];
   auto rename_ranks = [&](bool store) {
 #pragma unroll
     for (int q = 0; q < RQ; ++q) {
-      const int c = wv + q * WF_WAVES;
+      const int c = wv + q * WAVES;
       rown_r[q] = 0;
       if (c >= nrc) continue;  // wave-uniform
       const int x = c * WAVE + lane;
@@ -923,8 +989,8 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   tie = btie;
 #else
 #pragma unroll
-  for (int j = 0; j < WF_ITEMS; ++j) {
-    const int r = t + WF_NT * j;
+  for (int j = 0; j < ITEMS; ++j) {
+    const int r = t + NT * j;
     if (r < sz) tie |= sl[r] == 0xffffu;
   }
 #endif
@@ -933,7 +999,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   WSTAMP(21);
   if (any_tie) {
     // exact ranks from the full ids (global memory; rare)
-    for (int p = t; p < sz; p += WF_NT) {
+    for (int p = t; p < sz; p += NT) {
       int gs, ge;
       group_of(p, &gs, &ge);
       const int ex = fin[p];
@@ -950,7 +1016,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
       sl[gs + c] = (u16)p;
     }
     __syncthreads();
-    for (int r = t; r < sz; r += WF_NT) {
+    for (int r = t; r < sz; r += NT) {
       const int e = fin[sl[r]];
       sord[r] = (u16)e;
 #if WF_OUT2
@@ -963,22 +1029,29 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   } else {
 #pragma unroll
     for (int q = 0; q < RQ; ++q) {  // fin is dead now: the ranks go to rown
-      const int x = (wv + q * WF_WAVES) * WAVE + lane;
-      if (wv + q * WF_WAVES < nrc && x < RN) rown[x] = (u16)rown_r[q];
+      const int x = (wv + q * WAVES) * WAVE + lane;
+      if (wv + q * WAVES < nrc && x < RN) rown[x] = (u16)rown_r[q];
     }
   }
   WSTAMP(11);
   if (wv == 0) {
-    const u32 x0 = lane < nrc ? rc[lane][0] : 0u;
-    const u32 x1 = lane < nrc ? rc[lane][1] : 0u;
-    const u32 i0 = wave_incl_sum(x0), i1 = wave_incl_sum(x1);
-    if (lane < nrc) {
-      rc[lane][0] = (u16)(i0 - x0);
-      rc[lane][1] = (u16)(i1 - x1);
+    u32 c0s = 0, c1s = 0;  // carries over 64-chunk passes
+#pragma unroll
+    for (int cb0 = 0; cb0 < NCH; cb0 += WAVE) {
+      const int c = cb0 + lane;
+      const u32 x0 = c < nrc ? rc[c][0] : 0u;
+      const u32 x1 = c < nrc ? rc[c][1] : 0u;
+      const u32 i0 = wave_incl_sum(x0), i1 = wave_incl_sum(x1);
+      if (c < nrc) {
+        rc[c][0] = (u16)(c0s + i0 - x0);
+        rc[c][1] = (u16)(c1s + i1 - x1);
+      }
+      c0s += (u32)__builtin_amdgcn_readlane((int)i0, WAVE - 1);
+      c1s += (u32)__builtin_amdgcn_readlane((int)i1, WAVE - 1);
     }
     if (lane == WAVE - 1) {
-      wtot[0] = i0;
-      wtot[1] = i1;
+      wtot[0] = c0s;
+      wtot[1] = c1s;
     }
   }
   if (none_mv) atomicAdd((unsigned long long*)&P.meta->n_move_none, (unsigned long long)none_mv);
@@ -989,16 +1062,16 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   // 7. payload by element, round 1: sym (| the move's has-value bits) and v0; the
   //    position of each rename in its branch's list (posl)
   if (SMX_DIAG && (P.ablate & 4)) return;
-  u32* st_a = (u32*)sts;             // [WF_CAP] sym | flags
-  i32* st_b = (i32*)sts + WF_CAP;   // [WF_CAP] v0, then v1
+  u32* st_a = (u32*)sts;             // [CAP] sym | flags
+  i32* st_b = (i32*)sts + CAP;   // [CAP] v0, then v1
   u16* posl = sl;
 #if WF_OUT2
   // by final slot: each element's owner stores its payload at inv[element]
-  int xi[WF_ITEMS];
+  int xi[ITEMS];
 #pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i) {
-    const int e = t + WF_NT * i;
-    xi[i] = e < sz ? inv[e] : WF_CAP;
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e = t + NT * i;
+    xi[i] = e < sz ? inv[e] : CAP;
     if (e < sz) {
       st_a[xi[i]] = sym_r[i];
       if (!WF_STB_KIND || k_r[i] <= KREN) st_b[xi[i]] = v0_r[i];
@@ -1007,8 +1080,8 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   if (t < SMX_N_KINDS) tbase[t] = base[t] + woffk[t] - kbase[t];
 #else
 #pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i) {
-    const int e = t + WF_NT * i;
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e = t + NT * i;
     if (e < sz) {
       st_a[e] = sym_r[i];
       st_b[e] = v0_r[i];
@@ -1016,7 +1089,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   }
 #endif
   const int cntA = wtot[0], cntB = wtot[1];
-  for (int x = t; x < RN; x += WF_NT) {
+  for (int x = t; x < RN; x += NT) {
     const int e = sord[R0 + x];
     const int s = e >= na;
     posl[(s ? cntA : 0) + rc[x >> 6][s] + rown[x]] = (u16)x;
@@ -1029,7 +1102,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   WSTAMP(13);
   WF_EXIT(10);
   // 8. natural-head DivergentRename flags -> candidate slots; window exports
-  win_rename_flags<WF_NT>(
+  win_rename_flags<NT, NCH>(
       P, w, woffk[KREN], RN, cntA, cntB, posl, gbits,
       [&](int x, int* s, int* own) {
         const int e = sord[R0 + x];
@@ -1052,17 +1125,24 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   const u64 nall = (u64)(P.na + P.nb);
   const u64 nmv = base[KREN];
 #if WF_OUT2
-  // four consecutive slots per thread (WF_CAP = 4 * WF_NT): one LDS read of each array,
+  // four consecutive slots per thread (CAP = 4 * NT): one LDS read of each array,
   // and when the four share a kind (kinds are contiguous slot ranges) one 16-byte
   // store per output array
-  static_assert(WF_CAP == 4 * WF_NT, "four slots per thread");
-  const int x0 = 4 * t;
-  const int m4 = sz - x0 < 4 ? sz - x0 : 4;
-  u32 k4[4];
-  u64 T4[4];
-  i32 j4[4];
-  bool uni = false;
-  if (m4 > 0) {
+  // (CAP = 4 * NT * OP: OP passes of four slots per thread)
+  constexpr int OP = CAP / (4 * NT);
+  static_assert(CAP == 4 * NT * OP, "four slots per thread and pass");
+  auto gsrc = [&](i32 j) -> i32 {
+    return MAP ? P.src_map[j] : (j < P.na ? (i32)(P.src_a + j) : (i32)(P.src_b + (j - P.na)));
+  };
+  u32 k4[OP][4];
+  u64 T4[OP][4];
+  bool uni[OP];
+#pragma unroll
+  for (int ps = 0; ps < OP; ++ps) {
+    const int x0 = 4 * (t + NT * ps);
+    const int m4 = sz - x0 < 4 ? sz - x0 : 4;
+    uni[ps] = false;
+    if (m4 <= 0) continue;
     const uint2 ew = *reinterpret_cast<const uint2*>(&sord[x0]);
     const u32 kw = *reinterpret_cast<const u32*>(&skS[x0]);
     const uint4 av = *reinterpret_cast<const uint4*>(&st_a[x0]);
@@ -1070,20 +1150,19 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     const u32 ee[4] = {ew.x & 0xffffu, ew.x >> 16, ew.y & 0xffffu, ew.y >> 16};
     const u32 aa[4] = {av.x, av.y, av.z, av.w};
     const i32 bb[4] = {(i32)bv.x, (i32)bv.y, (i32)bv.z, (i32)bv.w};
+    i32 j4[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      k4[u] = (kw >> (8 * u)) & 0xffu;
-      k4[u] = k4[u] < SMX_N_KINDS ? k4[u] : 0u;  // (slots past sz)
-      T4[u] = tbase[k4[u]] + (u64)(x0 + u);
+      u32 k = (kw >> (8 * u)) & 0xffu;
+      k = k < SMX_N_KINDS ? k : 0u;  // (slots past sz)
+      k4[ps][u] = k;
+      T4[ps][u] = tbase[k] + (u64)(x0 + u);
       j4[u] = (i32)(ee[u] < (u32)na ? a0 + ee[u] : bpos + ee[u]);
     }
-    uni = m4 == 4 && k4[3] == k4[0] && T4[0] + 3 < nall;
-    auto gsrc = [&](i32 j) -> i32 {
-      return MAP ? P.src_map[j] : (j < P.na ? (i32)(P.src_a + j) : (i32)(P.src_b + (j - P.na)));
-    };
-    if (uni) {
-      const u64 T = T4[0];
-      if (k4[0] == KMOVE) {
+    uni[ps] = m4 == 4 && k4[ps][3] == k4[ps][0] && T4[ps][0] + 3 < nall;
+    if (uni[ps]) {
+      const u64 T = T4[ps][0];
+      if (k4[ps][0] == KMOVE) {
         st4(P.out_order + T, gsrc(j4[0]), gsrc(j4[1]), gsrc(j4[2]), gsrc(j4[3]));
         st4(P.out_addr + T, bb[0], bb[1], bb[2], bb[3]);
         st4(P.out_ctx + T, -1, -1, -1, -1);
@@ -1096,9 +1175,9 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
     } else {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const u64 T = T4[u];
+        const u64 T = T4[ps][u];
         if (u >= m4 || T >= nall) continue;  // (T >= nall: only a failed, discarded plan)
-        if (k4[u] == KMOVE) {
+        if (k4[ps][u] == KMOVE) {
           P.out_order[T] = gsrc(j4[u]);
           P.out_addr[T] = bb[u];
           P.out_ctx[T] = -1;
@@ -1115,21 +1194,25 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   WF_EXIT(12);
   // round 2: v1 -> the move's newFile, the rename's chain value
 #pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i)
-    if (xi[i] < WF_CAP && (!WF_STB_KIND || k_r[i] <= KREN)) st_b[xi[i]] = v1_r[i];
+  for (int i = 0; i < ITEMS; ++i)
+    if (xi[i] < CAP && (!WF_STB_KIND || k_r[i] <= KREN)) st_b[xi[i]] = v1_r[i];
   __syncthreads();
-  if (m4 > 0 && (k4[0] <= KREN || k4[m4 - 1] <= KREN)) {
+#pragma unroll
+  for (int ps = 0; ps < OP; ++ps) {
+    const int x0 = 4 * (t + NT * ps);
+    const int m4 = sz - x0 < 4 ? sz - x0 : 4;
+    if (m4 <= 0 || (k4[ps][0] > KREN && k4[ps][m4 - 1] > KREN)) continue;
     const uint4 bv = *reinterpret_cast<const uint4*>(&st_b[x0]);
     const i32 bb[4] = {(i32)bv.x, (i32)bv.y, (i32)bv.z, (i32)bv.w};
-    if (uni) {
-      const u64 T = T4[0];
-      st4(k4[0] == KMOVE ? P.out_file + T : P.Rstr + (T - nmv), bb[0], bb[1], bb[2], bb[3]);
+    if (uni[ps]) {
+      const u64 T = T4[ps][0];
+      st4(k4[ps][0] == KMOVE ? P.out_file + T : P.Rstr + (T - nmv), bb[0], bb[1], bb[2], bb[3]);
     } else {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const u64 T = T4[u];
-        if (u >= m4 || T >= nall || k4[u] > KREN) continue;
-        if (k4[u] == KMOVE) P.out_file[T] = bb[u];
+        const u64 T = T4[ps][u];
+        if (u >= m4 || T >= nall || k4[ps][u] > KREN) continue;
+        if (k4[ps][u] == KMOVE) P.out_file[T] = bb[u];
         else P.Rstr[T - nmv] = bb[u];
       }
     }
@@ -1137,7 +1220,7 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
 #else
   // 9. T-ordered records in final order (consecutive lanes -> consecutive T inside
   //    each kind: coalesced)
-  for (int x = t; x < sz; x += WF_NT) {
+  for (int x = t; x < sz; x += NT) {
     const int e = sord[x];
     const u32 k = skind[e];
     const u64 T = base[k] + woffk[k] + (u32)(x - kbase[k]);
@@ -1159,12 +1242,12 @@ __global__ void WF_BOUNDS k_window_f(WinArgs P) {
   WF_EXIT(12);
   // round 2: v1 -> the move's newFile, the rename's chain value
 #pragma unroll
-  for (int i = 0; i < WF_ITEMS; ++i) {
-    const int e = t + WF_NT * i;
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e = t + NT * i;
     if (e < sz) st_b[e] = v1_r[i];
   }
   __syncthreads();
-  for (int x = t; x < sz; x += WF_NT) {
+  for (int x = t; x < sz; x += NT) {
     const int e = sord[x];
     const u32 k = skind[e];
     if (k != KMOVE && k != KREN) continue;
@@ -1405,7 +1488,7 @@ __global__ void __launch_bounds__(WG_NT) k_window_g(WinArgs P) {
     P.wren[2 * w + 1] = woffk[CNT_REN_A];
   }
   __syncthreads();
-  win_rename_flags<WG_NT>(
+  win_rename_flags<WG_NT, WG_NCH>(
       P, w, woffk[KREN], RN, cntA, cntB, posl, cb,
       [&](int x, int* s, int* own) {
         const int e = fin[R0 + x];

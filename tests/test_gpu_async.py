@@ -76,9 +76,9 @@ def test_async_reports_pending_work():
 
 
 def test_long_groups_fail_before_the_tail():
-    """>= 4M ops whose timestamp groups (8192 ops) no presorted window holds: k_khist flags
-    the plan; the synchronous merge launches no tail behind it and takes the segmented
-    plan, the asynchronous one reports -2 and finish runs it.  Both equal the oracle,
+    """>= 4M ops whose timestamp groups (8192 ops) no 2048-op presorted window holds:
+    k_khist flags the plan; the synchronous merge launches no tail behind it and takes
+    the wide presorted windows, the asynchronous one reports -2 and finish runs them.  Both equal the oracle,
     and so do repeated merges of the same buffers (no graph is captured for them)."""
     soa = _lift(4_300_000, 3_000, 19, ops_per_ms=4096, mix=synth.ADVERSARIAL_MIX)
     dc = _lib.DeviceCompose(soa)
@@ -88,14 +88,14 @@ def test_long_groups_fail_before_the_tail():
         dc.torch.cuda.synchronize()
         dc.run(stream=s)
         _check(dc, soa, f"sync, long groups ({rep})")
-        assert dc.last_plan() == "segmented"
+        assert dc.last_plan() == "presorted-wide"
     dc.counts.fill_(-7)
     dc.run_async()
     dc.torch.cuda.synchronize()
     assert int(dc.counts[0].item()) == -2
     dc.finish()
     _check(dc, soa, "async, long groups")
-    assert dc.last_plan() == "segmented"
+    assert dc.last_plan() == "presorted-wide"
 
 
 def test_async_captured_in_a_graph_forked_tail():

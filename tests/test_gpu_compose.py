@@ -117,9 +117,9 @@ def test_synthetic_digests_gpu(name):
     synth.LiftSpec(333_333, 1, 29, ops_per_ms=1),               # one symbol, every head collides
     synth.LiftSpec(1_000_000, 1_000, 41, ops_per_ms=160),       # windows overflow -> smaller windows
     synth.LiftSpec(400_000, 5_000_000, 43),                     # > 4M symbols: atomic tables
-    synth.LiftSpec(600_000, 2_000, 61, ops_per_ms=3000, mix=synth.ADVERSARIAL_MIX),  # segmented plan
+    synth.LiftSpec(600_000, 2_000, 61, ops_per_ms=3000, mix=synth.ADVERSARIAL_MIX),  # wide windows
     synth.LiftSpec(300_000, 500, 59, ops_per_ms=10_000),        # groups too long: radix plan
-], ids=["c2_1M", "c2_1M_shuffled", "c5_2M", "hot64_1M", "onesym", "dense160", "sym5M", "seg3000",
+], ids=["c2_1M", "c2_1M_shuffled", "c5_2M", "hot64_1M", "onesym", "dense160", "sym5M", "wide3000",
         "groups10k"])
 def test_gpu_equals_oracle_soa(spec):
     soa = synth.lift_soa(synth.lift_logs(spec))
@@ -146,12 +146,59 @@ def test_gpu_wide_timestamp_range(stretch):
     assert dc.last_plan() == "presorted"
 
 
+def test_gpu_wide_plan_config5_shape():
+    """Config-5-shaped log (ordered, 8192-op timestamp groups over both branches): no
+    2048-op window holds a group, the wide (8192-op) presorted windows do."""
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(1_000_000, 3_000, 17, ops_per_ms=4096,
+                                                         mix=synth.ADVERSARIAL_MIX, rename_overlap=0.30)))
+    dc = DeviceCompose(soa)
+    dc.run()
+    _eq_soa(dc.results(), oracle.compose(soa), "config 5 shape, wide windows")
+    assert dc.last_plan() == "presorted-wide"
+
+
+def _alternating_groups(spec, big, small):
+    """spec's logs with timestamp groups of alternately `big` and `small` ops per branch
+    (the same on both branches)."""
+    soa = synth.lift_soa(synth.lift_logs(spec))
+    for lo, m in ((0, soa.n_a), (soa.n_a, soa.n_b)):
+        period = big + small
+        k = np.arange(m)
+        grp = 2 * (k // period) + ((k % period) >= big)
+        soa.ts[lo:lo + m] = soa.ts[0] + grp.astype(np.uint64) * np.uint64(2)
+    return soa
+
+
+def test_gpu_segmented_plan_when_wide_windows_overflow():
+    """Groups of 8100 and 200 ops (4050 + 4050, 100 + 100) in turn: a window that holds
+    a large group and the small one after it overflows even the wide window at every
+    target size, so the segmented sort (each branch's groups <= 4096) orders the log."""
+    soa = _alternating_groups(synth.LiftSpec(500_000, 2_000, 73, mix=synth.ADVERSARIAL_MIX), 4050, 100)
+    dc = DeviceCompose(soa)
+    dc.run()
+    _eq_soa(dc.results(), oracle.compose(soa), "alternating 8100 / 200 groups")
+    assert dc.last_plan() == "segmented"
+
+
 def test_gpu_segmented_plan_duplicate_ids():
-    """Config-5-shaped log (ordered, 4096-op timestamp groups: the segmented plan) with
-    duplicate ids and ids equal in their top bits inside groups: the tie runs are
-    re-sorted on the full id, then by index."""
-    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(400_000, 1_000, 67, ops_per_ms=4096,
-                                                         mix=synth.ADVERSARIAL_MIX)))
+    """Config-5-shaped log (ordered, 4096-op timestamp groups per branch: the wide
+    windows) with duplicate ids and ids equal in their top bits inside groups: equal
+    32-bit rank keys are ranked on the full id, then by index, in the rank loop; and the
+    same ids under the segmented sort (groups of 4050 and 100 ops per branch in turn),
+    whose tie runs are re-sorted on the full id, then by index."""
+    for label, soa in (
+            ("wide", synth.lift_soa(synth.lift_logs(synth.LiftSpec(400_000, 1_000, 67, ops_per_ms=4096,
+                                                                    mix=synth.ADVERSARIAL_MIX)))),
+            ("segmented", _alternating_groups(synth.LiftSpec(400_000, 1_000, 67, mix=synth.ADVERSARIAL_MIX),
+                                              4050, 100))):
+        _dup_ids(soa)
+        dc = DeviceCompose(soa)
+        dc.run()
+        _eq_soa(dc.results(), oracle.compose(soa), f"{label} plan, duplicate ids")
+        assert dc.last_plan() == ("presorted-wide" if label == "wide" else "segmented")
+
+
+def _dup_ids(soa):
     rng = np.random.default_rng(67)
     n = soa.n
     dup = rng.choice(n - 1, 3000, replace=False)
@@ -160,21 +207,23 @@ def test_gpu_segmented_plan_duplicate_ids():
     soa.oid_lo[both + 1] = soa.oid_lo[both]          # duplicate ids
     near = rng.choice(n, 2000, replace=False)
     soa.oid_hi[near] = (soa.oid_hi[near] & ~np.uint64(0x1fff)) | np.uint64(7)  # equal above bit 13
-    _eq_soa(compose_soa(soa), oracle.compose(soa), "segmented plan, duplicate ids")
 
 
-def test_gpu_segmented_plan_clustered_ids():
-    """Segmented plan with ids whose top bits cluster (sequential ids in the first half of
-    each branch, as short string ids give; distinct in the 38 sorted bits, so no tie
-    runs): those tiles' interpolation buckets overflow and take the bitonic network; the
-    random-id tiles keep the buckets."""
-    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(400_000, 1_000, 71, ops_per_ms=4096,
-                                                         mix=synth.ADVERSARIAL_MIX)))
+@pytest.mark.parametrize("plan", ["presorted-wide", "segmented"])
+def test_gpu_long_groups_clustered_ids(plan):
+    """Ids whose top bits cluster (sequential ids in the first half of each branch, as
+    short string ids give; distinct in the 38 sorted bits, so no tie runs), in long
+    timestamp groups: the wide windows' interpolation buckets crowd; the segmented
+    sort's tiles overflow their buckets and take the bitonic network, the random-id
+    tiles keep the buckets."""
+    spec = synth.LiftSpec(400_000, 1_000, 71, ops_per_ms=4096, mix=synth.ADVERSARIAL_MIX)
+    soa = (synth.lift_soa(synth.lift_logs(spec)) if plan == "presorted-wide"
+           else _alternating_groups(spec, 4050, 100))
     for lo, hi in ((0, soa.n_a // 2), (soa.n_a, soa.n_a + soa.n_b // 2)):
         seq = np.arange(hi - lo, dtype=np.uint64)
         soa.oid_hi[lo:hi] = ((seq * np.uint64(2654435761)) & np.uint64(0xFFFFF)) << np.uint64(26)
-    _eq_soa(compose_soa(soa), oracle.compose(soa), "segmented plan, clustered ids")
-    assert DeviceCompose.last_plan() == "segmented"
+    _eq_soa(compose_soa(soa), oracle.compose(soa), f"{plan} plan, clustered ids")
+    assert DeviceCompose.last_plan() == plan
 
 
 def test_gpu_segmented_sort_fails_then_radix():
