@@ -26,6 +26,7 @@ typedef uint8_t u8;
 // Device-side state of one smx_compose call (lives at the start of the workspace).
 // Counters written by kernels; read by later kernels and (once) by the host.
 #define SEG_FAIL_BIT 8ull
+#define F_LONG 22ull  // f_fail from k_fpart's long-group check (bits 1, 2 and 4), before any window ran
 #define SEG_DECREASE 2ull  // meta->seg_over: a timestamp decreases (the segmented sort)
 struct ComposeMeta {
   u64 kcnt[SMX_N_KINDS];     // ops per precedence rank (stats kernel)
@@ -33,7 +34,8 @@ struct ComposeMeta {
   u64 nonmono[2];            // per side: 1 if timestamps decrease somewhere
   u64 n_move_none;           // moves with a None newAddress or newFile
   u64 f_fail;                // the plan failed: bit 0 logs not ordered, 1 a window too large, 2 one
-                             // timestamp per window; bit 3 (SEG_FAIL_BIT) the segmented sort
+                             // timestamp per window; bit 3 (SEG_FAIL_BIT) the segmented sort;
+                             // F_LONG: k_fpart's verdict, before any window ran
   u64 bad_sym;               // sym >= n_sym seen
   u64 n_ren_side[2];         // renames per side
   u64 key_or[2][3];          // per side OR / AND of (ts, hi, lo): constant radix digits

@@ -257,8 +257,8 @@ __global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB,
     for (i64 c = k; c + D < ca; c += nt) lg |= sA[c] == sA[c + D];
     for (i64 c = k; c + D < cb; c += nt) lg |= sB[c] == sB[c + D];
     if (__ballot(lg) && (threadIdx.x & (WAVE - 1)) == 0 &&
-        __hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 6ull) {
-      atomicOr((unsigned long long*)&meta->f_fail, 6ull);
+        __hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != F_LONG) {
+      atomicOr((unsigned long long*)&meta->f_fail, F_LONG);
       // ... and, on the synchronous path, to the host (pinned, coherent), which then
       // launches no tail behind this failed plan
       if (long_host) __hip_atomic_store(long_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1548,6 +1548,43 @@ struct EarlyFail {
   u32* flag_dev = nullptr;
   hipEvent_t ev = nullptr;
 };
+// The presorted windows over the boundaries k_fpart left (W windows).
+static int launch_presorted_windows(const Ctx& C, i64 W, i64 CM, bool wide) {
+  hipStream_t st = C.st;
+  WinArgs P = win_args(C);
+  P.cpre = C.ws<u32>(B_CCNT);
+  P.CM = CM;
+  P.kts = C.ops->ts;
+  P.khi = C.ops->oid_hi;
+  P.klo = C.ops->oid_lo;
+  P.perm = nullptr;
+  P.W = W;
+  P.ablate = knob("SMX_ABLATE", 0);
+  C.tm->begin(ST_WINDOW);
+#if SMX_DIAG
+  if (g_phase_dbg && !P.src_map && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
+    P.dbg = (u64*)g_phase_dbg;
+    if (wide)
+      hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, true, false>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
+    else
+      hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, true, false>), dim3(W), dim3(WF_NT), 0, st, P);
+  } else
+#endif
+  if (wide) {
+    if (P.src_map) hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, true>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
+    else hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, false>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
+  } else if (P.src_map) {
+    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, true>), dim3(W), dim3(WF_NT), 0, st, P);
+  } else {
+    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, false>), dim3(W), dim3(WF_NT), 0, st, P);
+  }
+  HIP_TRY(hipGetLastError());
+  C.tm->end(ST_WINDOW);
+  return SMX_OK;
+}
+
+
+
 // wide: WF_WIDE_CAP-op windows on WF_WIDE_NT threads (one per CU) for logs whose
 // equal-timestamp groups no WF_CAP window holds (config 5: 8192-op groups).
 static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr, bool wide = false) {
@@ -1590,35 +1627,35 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
   hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta, (u64)W);
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_PLAN);
-  WinArgs P = win_args(C);
-  P.cpre = ccnt;
-  P.CM = CM;
-  P.kts = C.ops->ts;
-  P.khi = C.ops->oid_hi;
-  P.klo = C.ops->oid_lo;
-  P.perm = nullptr;
-  P.W = W;
-  P.ablate = knob("SMX_ABLATE", 0);
-  C.tm->begin(ST_WINDOW);
-#if SMX_DIAG
-  if (g_phase_dbg && !wide && !P.src_map && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
-    P.dbg = (u64*)g_phase_dbg;
-    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, true, false>), dim3(W), dim3(WF_NT), 0, st, P);
-  } else
-#endif
-  if (wide) {
-    if (P.src_map) hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, true>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
-    else hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, false>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
-  } else if (P.src_map) {
-    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, true>), dim3(W), dim3(WF_NT), 0, st, P);
-  } else {
-    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, false>), dim3(W), dim3(WF_NT), 0, st, P);
-  }
-  HIP_TRY(hipGetLastError());
-  C.tm->end(ST_WINDOW);
-  return SMX_OK;
+  return launch_presorted_windows(C, W, CM, wide);
 }
 
+// k_fpart's long-group verdict (f_fail == F_LONG) is given before any window runs, so
+// the plan's chunk counts, prefixes and bases stand: only the boundaries and the windows
+// are redone, at the wide capacity.
+__global__ void k_plan_rearm(ComposeMeta* meta, u64 nwin) {
+  if (meta->f_fail == F_LONG) meta->f_fail = 0;
+  meta->n_win = nwin;
+}
+static int run_presorted_rewide(const Ctx& C, i64 tgt) {
+  hipStream_t st = C.st;
+  ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
+  if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
+  if (tgt > WF_WIDE_CAP) tgt = WF_WIDE_CAP;
+  tgt -= tgt % CH;
+  const i64 W = SMX_CEIL_DIV(C.n, tgt);
+  const i64 CM = SMX_CEIL_DIV(C.na > C.nb ? C.na : C.nb, (i64)CH) + 1;
+  u64* sA = C.ws<u64>(B_SMP);
+  u64* sB = sA + SMX_CEIL_DIV(C.na, (i64)CH) + 1;
+  C.tm->begin(ST_PLAN);
+  hipLaunchKernelGGL(k_plan_rearm, dim3(1), dim3(1), 0, st, meta, (u64)W);
+  hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
+                     C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na, C.nb, W, tgt, (i64)(WF_WIDE_CAP / CH),
+                     C.ws<i64>(B_BND), meta, (u32*)nullptr);
+  HIP_TRY(hipGetLastError());
+  C.tm->end(ST_PLAN);
+  return launch_presorted_windows(C, W, CM, true);
+}
 
 // Generic plan: each branch sorted by (ts, oid_hi, oid_lo, index), then fixed windows
 // over the sorted logs (k_window_g).  Used when the presorted plan fails.  Two ways to
@@ -2077,8 +2114,8 @@ static thread_local int g_plan = SMX_PLAN_PRESORTED;
 // require_ordered (a sharded range slice): a slice whose timestamps decrease must fail
 // loudly -- the radix plan would order it locally, not across the shards -- so it is
 // refused when the window kernel (f_fail bit 0) or the segmented sort (SEG_DECREASE)
-// saw a decrease.  (k_fpart's early verdict, f_fail 6, can hide bit 0: then the
-// segmented sort runs and reports the decrease itself.)
+// saw a decrease.  (k_fpart's early verdict, F_LONG, can hide bit 0: then the wide
+// windows or the segmented sort report the decrease themselves.)
 static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm, i64 tgt,
                            bool require_ordered = false) {
   int rc;
@@ -2092,12 +2129,12 @@ static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeM
     if (tail && (rc = launch_tail(C))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
   }
-  // ordered logs whose equal-timestamp groups no WF_CAP window holds (f_fail 6, or 2 at
+  // ordered logs whose equal-timestamp groups no WF_CAP window holds (F_LONG or 6, or 2 at
   // the smallest windows): the wide windows, from half their capacity down (a window
   // holds its target plus the group its end snaps back over)
   for (i64 wt = WF_WIDE_CAP / 2; hm->f_fail && !(hm->f_fail & 1) && !hm->bad_sym && wt >= WIN_TGT_MIN; wt /= 2) {
     g_plan = SMX_PLAN_PRESORTED_WIDE;
-    if ((rc = run_presorted(C, wt, nullptr, true))) return rc;
+    if ((rc = hm->f_fail == F_LONG ? run_presorted_rewide(C, wt) : run_presorted(C, wt, nullptr, true))) return rc;
     if (tail && (rc = launch_tail(C))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
     if (hm->f_fail != 2) break;  // held, or groups longer than a wide window (6), or unordered (1)
@@ -2220,7 +2257,7 @@ static int early_fail_of(int dev, EarlyFail* e) {
 
 // What the synchronous merge's host learned from k_khist before the windows ran.
 struct EarlyVerdict {
-  bool failed = false;  // the presorted plan fails for sure (f_fail 6)
+  bool failed = false;  // the presorted plan fails for sure (f_fail F_LONG)
   bool bad = false;     // ... and k_khist saw an invalid kind
 };
 
@@ -2437,7 +2474,7 @@ static int compose_finish_impl(const smx_ops* ops, const smx_compose_out* out, v
   ComposeMeta hm;
   if (known && known->failed) {
     std::memset(&hm, 0, sizeof(hm));
-    hm.f_fail = 6;
+    hm.f_fail = F_LONG;
     hm.bad_sym = known->bad ? 1 : 0;
   } else if ((rc = read_meta(C, &hm))) {
     return rc;

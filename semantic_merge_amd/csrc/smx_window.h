@@ -254,6 +254,12 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_TIEFIX
 #define WF_TIEFIX 1  // wide windows: equal 32-bit keys in a bucket ranked on the full ids right there (no window re-rank)
 #endif
+#ifndef WF_RUNMERGE
+#define WF_RUNMERGE 1  // step 2 by timestamp-run heads (a search per run, not a merge path per thread)
+#endif
+#ifndef WF_KPBAL
+#define WF_KPBAL 1   // partial-chunk kinds counted by peers ballots: one LDS atomic per (wave, kind)
+#endif
 #ifndef WF_RANK8
 #define WF_RANK8 0   // step 5's bucket rank by 8 predicated compares (the loop only for larger buckets): window 1.223 -> 1.260 ms, off (profiles/r04_d)
 #endif
@@ -477,6 +483,25 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     return;
   }
   // window offsets: the partial-chunk kinds
+#if WF_KPBAL && WF_DENSE_KINDS
+  {
+    // one LDS atomic per (wave, kind) from the peers ballots over the dense index of the
+    // present kinds (per-lane atomics on a few hot counters serialise in the LDS);
+    // a wave's slots x = t + NT * u lie on one side of CH (WAVE divides CH)
+    static_assert(CH % WAVE == 0, "one side per wave");
+    const u32 kp0 = __builtin_amdgcn_readfirstlane(kmask_r);
+    const int kb0 = 32 - __clz((int)(max(__popc(kp0), 1u) - 1u));
+#pragma unroll
+    for (int u = 0; u < KP; ++u) {
+      const bool v = kpart[u] != 0xffffffffu;
+      const u32 k = v ? (kpart[u] < SMX_N_KINDS ? kpart[u] : SMX_N_KINDS - 1) : 0u;
+      const u64 peers = wave_peers_n((u32)__popc(kp0 & ((1u << k) - 1u)), v, kb0);
+      if (v && (peers & lanemask_lt()) == 0) atomicAdd(&woffk[k], (u32)__popcll(peers));
+      const u64 rb = __ballot(v && k == KREN);
+      if (lane == 0 && rb) atomicAdd(&woffk[SMX_N_KINDS + (t + NT * u >= CH)], (u32)__popcll(rb));
+    }
+  }
+#else
 #pragma unroll
   for (int u = 0; u < KP; ++u) {
     if (kpart[u] != 0xffffffffu) {
@@ -485,6 +510,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
       if (k == KREN) atomicAdd(&woffk[SMX_N_KINDS + (t + NT * u >= CH)], 1u);
     }
   }
+#endif
 
   // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties
   //    (compose.py:54): merge path, ITEMS outputs per lane, with the kinds
@@ -497,6 +523,54 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     dec = (a0 > 0 && na > 0 && prev_a > sts[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
     win_publish_widths(P.meta, &vbw[0][0], WAVES, vcur);
   }
+#if WF_RUNMERGE
+  // Run-head merge.  Inside a branch the timestamps never decrease, so an op's merged
+  // position is its branch index plus the other branch's ops before its timestamp run
+  // (A first on ties: for an A op the B ops with a smaller timestamp, for a B op the A
+  // ops with a smaller or equal one).  Only the first op of each run (a head) searches
+  // the other branch; the rest read their head's count.  (Config 2 / 3 windows hold ~14
+  // runs per branch, config 5's wide windows one: a few searches instead of a merge-path
+  // search and a merge step chain per thread.)
+  u64* rbits = gbits;  // [NCH] head bits over elements (gbits is next written in step 4)
+  u16* hl = fin;       // per wave: its heads' elements (fin is next written in step 3)
+  u16* roff = sl;      // per head element: the other branch's ops before its run (sl: step 3)
+  u64 hb[ITEMS];
+  int nh = 0;  // this wave's heads (wave-uniform)
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e = t + NT * i;
+    const bool valid = e < sz;
+    const u64 pv = sts[valid && e > 0 ? e - 1 : 0];
+    const bool head = valid && (e == 0 || e == na || pv != ts_r[i]);
+    if (!(SMX_DIAG && (P.ablate & 1))) dec |= valid && e != 0 && e != na && pv > ts_r[i];
+    hb[i] = __ballot(head);
+    if (lane == 0) rbits[(NT * i) / WAVE + wv] = hb[i];
+    if (head) hl[wv * (ITEMS * WAVE) + nh + (int)__popcll(hb[i] & lanemask_lt())] = (u16)e;
+    nh += (int)__popcll(hb[i]);
+  }
+  wave_lds_sync();  // this wave's head list, for its own lanes
+  for (int r = 0; r < nh; r += WAVE) {
+    if (r + lane < nh) {
+      const int e = hl[wv * (ITEMS * WAVE) + r + lane];
+      const u64 x = sts[e];
+      int lo = 0, hi = e < na ? nb : na;
+      if (e < na) {  // B ops with a smaller timestamp
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (sts[na + mid] < x) lo = mid + 1;
+          else hi = mid;
+        }
+      } else {  // A ops with a smaller or equal timestamp
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (sts[mid] <= x) lo = mid + 1;
+          else hi = mid;
+        }
+      }
+      roff[e] = (u16)lo;
+    }
+  }
+#else
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i) {
     const int e = t + NT * i;
@@ -539,10 +613,50 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     }
 #endif
   }
+#endif
   if (__syncthreads_or(dec)) {
     if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
     return;
   }
+#if WF_RUNMERGE
+  {
+    // each op's head: the last head at or before it -- in its own 64-op chunk (the
+    // ballot), else the last head of the nearest earlier chunk that has one (every
+    // chunk's head word read once per wave; lane broadcasts with the whole wave active)
+    const int nchw = (sz + WAVE - 1) / WAVE;
+    const u64 rw0 = lane < nchw ? rbits[lane] : 0ull;
+    const u64 rnz0 = __ballot(rw0 != 0);
+    const u64 rw1 = NCH > WAVE && WAVE + lane < nchw ? rbits[(WAVE + lane) % NCH] : 0ull;
+    const u64 rnz1 = NCH > WAVE ? __ballot(rw1 != 0) : 0ull;
+    auto bc64 = [](u64 v, int l) -> u64 {
+      return (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, l) |
+             ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), l) << 32);
+    };
+    const u64 lem = lanemask_lt() | (1ull << lane);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int c = (NT * i) / WAVE + wv;  // this wave's chunk (uniform)
+      if (c * WAVE >= sz) break;          // (uniform)
+      // the last non-empty chunk before c (chunk 0 starts with a head, so c > 0 has one)
+      const int cl = c & (WAVE - 1);
+      const u64 b0 = c < WAVE ? rnz0 & ((1ull << cl) - 1) : rnz0;
+      const u64 b1 = c < WAVE ? 0ull : rnz1 & ((1ull << cl) - 1);
+      const int wp = b1 ? WAVE + 63 - __clzll(b1) : (b0 ? 63 - __clzll(b0) : 0);
+      const u64 wpw = wp < WAVE ? bc64(rw0, wp & (WAVE - 1)) : bc64(rw1, wp & (WAVE - 1));
+      const int hprev = wp * WAVE + 63 - __clzll(wpw | 1ull);
+      const u64 below = hb[i] & lem;
+      const int e = t + NT * i;
+      if (e < sz) {
+        const int h = below ? c * WAVE + 63 - __clzll(below) : hprev;
+        const int pos = (e < na ? e : e - na) + (int)roff[h];
+        const u32 kr = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
+        sord[pos] = (u16)e;
+        skS[pos] = (u8)kr;
+      }
+    }
+  }
+  __syncthreads();
+#endif
   WSTAMP(3);
   WF_EXIT(2);
 
