@@ -139,6 +139,20 @@ __device__ __forceinline__ u64 lanemask_lt() {
   return (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
 }
 
+// The kernel's argument block read through an opaque pointer: field loads are issued
+// where the pointer is taken, not hoisted to the kernel's start (where long-lived
+// scalars end up spilled to VGPR lanes in large kernels).
+template <class T>
+__device__ __forceinline__ const T* kernarg_late() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const T* p = (const T*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+#else
+  return nullptr;
+#endif
+}
+
 __device__ __forceinline__ void wave_lds_sync() {  // LDS writes of this wave visible to its lanes
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

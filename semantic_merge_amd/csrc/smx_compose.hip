@@ -1232,6 +1232,11 @@ static WalkArgs walk_args(const Ctx& C, const smx_shard* sh) {
     Wk.halo_n[b] = sh && sh->halo_sym[b] ? (u64)sh->halo_n[b] : 0;
     Wk.halo_more[b] = sh ? sh->halo_more[b] : 0;
   }
+  // staging for k_replay_q's short regions: buffers of the sorting plans and of the
+  // None-value move prefix, free while the walk runs
+  Wk.stage = C.ws<u32>(B_RK2);
+  Wk.sok = C.ws<u32>(B_RV2);
+  Wk.stage_cap = RS_CONF ? (u64)(C.n > 0 ? C.n : 1) * 2 / (RS_CONF ? RS_W : 1) : 0;  // B_RK2: 8 bytes per op
   return Wk;
 }
 
@@ -2130,9 +2135,10 @@ static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeM
     if ((rc = read_meta(C, hm))) return rc;
   }
   // ordered logs whose equal-timestamp groups no WF_CAP window holds (F_LONG or 6, or 2 at
-  // the smallest windows): the wide windows, from half their capacity down (a window
-  // holds its target plus the group its end snaps back over)
-  for (i64 wt = WF_WIDE_CAP / 2; hm->f_fail && !(hm->f_fail & 1) && !hm->bad_sym && wt >= WIN_TGT_MIN; wt /= 2) {
+  // the smallest windows): the wide windows, from their full capacity down (a window
+  // holds its target plus the group its end snaps back over; at full capacity each of
+  // config 5's windows is one 8192-op group, and no window is empty)
+  for (i64 wt = WF_WIDE_CAP; hm->f_fail && !(hm->f_fail & 1) && !hm->bad_sym && wt >= WIN_TGT_MIN; wt /= 2) {
     g_plan = SMX_PLAN_PRESORTED_WIDE;
     if ((rc = hm->f_fail == F_LONG ? run_presorted_rewide(C, wt) : run_presorted(C, wt, nullptr, true))) return rc;
     if (tail && (rc = launch_tail(C))) return rc;

@@ -50,7 +50,17 @@ struct WalkArgs {
   const i64* halo_dev;  // device-held halo_n / halo_more (smx_shard.halo_dev), or null
   i64 src_a, src_b;
   const i32* src_map;   // sample-sorted shard: global source of local op j, or null
+  // k_replay_q's staged outputs (candidates c < stage_cap): a region that closes with at
+  // most RS_CONF conflicts leaves its conflict pairs and skip positions at
+  // stage[c * RS_W ..], sok[c] = 1, and k_replay_write copies them instead of replaying
+  u32* stage;
+  u32* sok;
+  u64 stage_cap;
 };
+#ifndef RS_CONF
+#define RS_CONF 2                 // conflicts of a staged region (0: no staging)
+#endif
+#define RS_W (4 * RS_CONF)        // words per candidate: 2 per conflict pair, 2 skips per conflict
 
 __device__ __forceinline__ i32 walk_gsrc(const WalkArgs& W, i32 j) {
   if (W.src_map) return W.src_map[j];
@@ -169,9 +179,11 @@ __device__ __forceinline__ ReplayState replay_fresh() { return ReplayState{-1, 0
 // state is left in st), or Q_LONG when CAP and the region is longer than
 // REPLAY_CAP steps.  WRITE: conflict pairs (global source indices) at pair_off..,
 // skipped positions in increasing order at skip_out.., and their skip bits.
-template <bool WRITE, bool CAP>
+// STAGE: the first RS_CONF conflicts' pairs and their skip positions go to stg (no
+// other side effects).
+template <bool WRITE, bool CAP, bool STAGE = false>
 __device__ u32 replay_region(const WalkArgs& W, u32 p, ReplayState& st, u32* nconf, i32* pairs, u64 pair_cap,
-                             u64 pair_off, u32* skip_out, u64* skipbits, u32* nskip) {
+                             u64 pair_off, u32* skip_out, u64* skipbits, u32* nskip, u32* stg = nullptr) {
   u32 m = p;
   u32 nc = 0, ns = 0, steps = 0;
   while (m < W.nR) {
@@ -183,6 +195,7 @@ __device__ u32 replay_region(const WalkArgs& W, u32 p, ReplayState& st, u32* nco
         skip_out[ns] = m;
         atomicOr((unsigned long long*)&skipbits[m >> 6], 1ull << (m & 63));
       }
+      if (STAGE && ns < 2 * RS_CONF) stg[2 * RS_CONF + ns] = m;
       ++ns;
     } else {
       const int o = 1 - s;
@@ -200,6 +213,12 @@ __device__ u32 replay_region(const WalkArgs& W, u32 p, ReplayState& st, u32* nco
             }
             skip_out[ns] = m;
             atomicOr((unsigned long long*)&skipbits[m >> 6], 1ull << (m & 63));
+          }
+          if (STAGE && nc < RS_CONF) {
+            const i32 mu = walk_gsrc(W, j), hu = walk_src_at(W, o, hc);
+            stg[2 * nc] = (u32)(s ? hu : mu);
+            stg[2 * nc + 1] = (u32)(s ? mu : hu);
+            stg[2 * RS_CONF + ns] = m;
           }
           ++ns;
           ++nc;
@@ -356,7 +375,15 @@ __global__ void k_replay_q(WalkArgs W0, const u32* __restrict__ cand, const Comp
   for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
     u32 k = 0;
     ReplayState st = replay_fresh();
-    q[c] = replay_region<false, true>(W, cand[c], st, &k, nullptr, 0, 0, nullptr, nullptr, nullptr);
+    if (c < W.stage_cap) {
+      const u32 qq = replay_region<false, true, true>(W, cand[c], st, &k, nullptr, 0, 0, nullptr, nullptr, nullptr,
+                                                      W.stage + c * RS_W);
+      q[c] = qq;
+      // staged: closed (d back to 0) within the step cap, with few enough conflicts
+      W.sok[c] = qq != Q_LONG && st.d == 0 && k <= RS_CONF;
+    } else {
+      q[c] = replay_region<false, true>(W, cand[c], st, &k, nullptr, 0, 0, nullptr, nullptr, nullptr);
+    }
     nconf[c] = k;
   }
 }
@@ -408,6 +435,24 @@ __global__ void k_replay_write(WalkArgs W0, const u32* __restrict__ cand, const 
   const u64 off0 = meta->nconf_in, soff0 = meta->nskip_in;
   for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
     if (nreal[c] == 0) continue;
+    if (c < W.stage_cap && W.sok[c]) {  // k_replay_q's staged outputs: copies, no replay
+      const u32 k = nreal[c];
+      const u32* g = W.stage + c * RS_W;
+      const u64 off = off0 + coff[c];
+      u32* sk = skiplist + soff0 + 2 * (u64)coff[c];
+      for (u32 i = 0; i < k; ++i)
+        if (off + i < pair_cap) {
+          pairs[2 * (off + i)] = (i32)g[2 * i];
+          pairs[2 * (off + i) + 1] = (i32)g[2 * i + 1];
+        }
+      for (u32 i = 0; i < 2 * k; ++i) {
+        const u32 m = g[2 * RS_CONF + i];
+        sk[i] = m;
+        atomicOr((unsigned long long*)&skipbits[m >> 6], 1ull << (m & 63));
+      }
+      atomicAdd((unsigned long long*)&meta->n_skip, (unsigned long long)(2 * k));
+      continue;
+    }
     u32 k = 0, ns = 0;
     ReplayState st = replay_fresh();
     replay_region<true, false>(W, cand[c], st, &k, pairs, pair_cap, off0 + coff[c],

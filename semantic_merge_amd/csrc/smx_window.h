@@ -254,11 +254,16 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_TIEFIX
 #define WF_TIEFIX 1  // wide windows: equal 32-bit keys in a bucket ranked on the full ids right there (no window re-rank)
 #endif
+#ifndef WF_LATEARGS
+#define WF_LATEARGS 0  // step 9 re-reads its kernel arguments: 63 -> 17 SGPR spills, but 28 B/lane of VGPR scratch spills (off)
+#endif
 #ifndef WF_RUNMERGE
-#define WF_RUNMERGE 1  // step 2 by timestamp-run heads (a search per run, not a merge path per thread)
+#define WF_RUNMERGE 0  // step 2 by timestamp-run heads (a search per run, not a merge path per thread):
+                       // config 3 window 1.225 -> 1.230 ms, config 5 wide 0.907 -> 0.960 ms; off (profiles/r04_e, r04_f)
 #endif
 #ifndef WF_KPBAL
-#define WF_KPBAL 1   // partial-chunk kinds counted by peers ballots: one LDS atomic per (wave, kind)
+#define WF_KPBAL 0   // partial-chunk kinds counted by peers ballots (one LDS atomic per (wave, kind)): 1.225 -> 1.235 ms,
+                     // and 1.395 ms together with WF_RUNMERGE (+21% VALU in that build); off (profiles/r04_f)
 #endif
 #ifndef WF_RANK8
 #define WF_RANK8 0   // step 5's bucket rank by 8 predicated compares (the loop only for larger buckets): window 1.223 -> 1.260 ms, off (profiles/r04_d)
@@ -1234,9 +1239,13 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
   WSTAMP(14);
   WF_EXIT(11);
 
+  // The output phases' kernel arguments are read again here from the kernarg segment
+  // (scalar loads through an opaque pointer): held from the kernel's start they were
+  // spilled to VGPR lanes and reloaded one v_readlane each in these phases.
+  const WinArgs& Q = WF_LATEARGS ? *kernarg_late<WinArgs>() : P;
   // 9. T-ordered records in final order (consecutive lanes -> consecutive T inside
   //    each kind: coalesced)
-  const u64 nall = (u64)(P.na + P.nb);
+  const u64 nall = (u64)(Q.na + Q.nb);
   const u64 nmv = base[KREN];
 #if WF_OUT2
   // four consecutive slots per thread (CAP = 4 * NT): one LDS read of each array,
@@ -1246,7 +1255,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
   constexpr int OP = CAP / (4 * NT);
   static_assert(CAP == 4 * NT * OP, "four slots per thread and pass");
   auto gsrc = [&](i32 j) -> i32 {
-    return MAP ? P.src_map[j] : (j < P.na ? (i32)(P.src_a + j) : (i32)(P.src_b + (j - P.na)));
+    return MAP ? Q.src_map[j] : (j < Q.na ? (i32)(Q.src_a + j) : (i32)(Q.src_b + (j - Q.na)));
   };
   u32 k4[OP][4];
   u64 T4[OP][4];
@@ -1277,13 +1286,13 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     if (uni[ps]) {
       const u64 T = T4[ps][0];
       if (k4[ps][0] == KMOVE) {
-        st4(P.out_order + T, gsrc(j4[0]), gsrc(j4[1]), gsrc(j4[2]), gsrc(j4[3]));
-        st4(P.out_addr + T, bb[0], bb[1], bb[2], bb[3]);
-        st4(P.out_ctx + T, -1, -1, -1, -1);
-        st4((i32*)P.msym + T, (i32)aa[0], (i32)aa[1], (i32)aa[2], (i32)aa[3]);
+        st4(Q.out_order + T, gsrc(j4[0]), gsrc(j4[1]), gsrc(j4[2]), gsrc(j4[3]));
+        st4(Q.out_addr + T, bb[0], bb[1], bb[2], bb[3]);
+        st4(Q.out_ctx + T, -1, -1, -1, -1);
+        st4((i32*)Q.msym + T, (i32)aa[0], (i32)aa[1], (i32)aa[2], (i32)aa[3]);
       } else {
-        st4(P.tsrc + (T - nmv), j4[0], j4[1], j4[2], j4[3]);
-        st4((i32*)P.tsym + (T - nmv), (i32)(aa[0] & SYM_MASK), (i32)(aa[1] & SYM_MASK), (i32)(aa[2] & SYM_MASK),
+        st4(Q.tsrc + (T - nmv), j4[0], j4[1], j4[2], j4[3]);
+        st4((i32*)Q.tsym + (T - nmv), (i32)(aa[0] & SYM_MASK), (i32)(aa[1] & SYM_MASK), (i32)(aa[2] & SYM_MASK),
             (i32)(aa[3] & SYM_MASK));
       }
     } else {
@@ -1292,13 +1301,13 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
         const u64 T = T4[ps][u];
         if (u >= m4 || T >= nall) continue;  // (T >= nall: only a failed, discarded plan)
         if (k4[ps][u] == KMOVE) {
-          P.out_order[T] = gsrc(j4[u]);
-          P.out_addr[T] = bb[u];
-          P.out_ctx[T] = -1;
-          P.msym[T] = aa[u];
+          Q.out_order[T] = gsrc(j4[u]);
+          Q.out_addr[T] = bb[u];
+          Q.out_ctx[T] = -1;
+          Q.msym[T] = aa[u];
         } else {
-          P.tsrc[T - nmv] = j4[u];
-          P.tsym[T - nmv] = aa[u] & SYM_MASK;
+          Q.tsrc[T - nmv] = j4[u];
+          Q.tsym[T - nmv] = aa[u] & SYM_MASK;
         }
       }
     }
@@ -1320,14 +1329,14 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     const i32 bb[4] = {(i32)bv.x, (i32)bv.y, (i32)bv.z, (i32)bv.w};
     if (uni[ps]) {
       const u64 T = T4[ps][0];
-      st4(k4[ps][0] == KMOVE ? P.out_file + T : P.Rstr + (T - nmv), bb[0], bb[1], bb[2], bb[3]);
+      st4(k4[ps][0] == KMOVE ? Q.out_file + T : Q.Rstr + (T - nmv), bb[0], bb[1], bb[2], bb[3]);
     } else {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const u64 T = T4[ps][u];
         if (u >= m4 || T >= nall || k4[ps][u] > KREN) continue;
-        if (k4[ps][u] == KMOVE) P.out_file[T] = bb[u];
-        else P.Rstr[T - nmv] = bb[u];
+        if (k4[ps][u] == KMOVE) Q.out_file[T] = bb[u];
+        else Q.Rstr[T - nmv] = bb[u];
       }
     }
   }
@@ -1342,13 +1351,13 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     const i64 j = e < na ? a0 + e : bpos + e;
     const u32 sa = st_a[e];
     if (k == KMOVE) {
-      P.out_order[T] = MAP ? P.src_map[j] : (j < P.na ? (i32)(P.src_a + j) : (i32)(P.src_b + (j - P.na)));
-      P.out_addr[T] = st_b[e];
-      P.out_ctx[T] = -1;
-      P.msym[T] = sa;
+      Q.out_order[T] = MAP ? Q.src_map[j] : (j < Q.na ? (i32)(Q.src_a + j) : (i32)(Q.src_b + (j - Q.na)));
+      Q.out_addr[T] = st_b[e];
+      Q.out_ctx[T] = -1;
+      Q.msym[T] = sa;
     } else {
-      P.tsrc[T - nmv] = (i32)j;
-      P.tsym[T - nmv] = sa & SYM_MASK;
+      Q.tsrc[T - nmv] = (i32)j;
+      Q.tsym[T - nmv] = sa & SYM_MASK;
     }
   }
   __syncthreads();
@@ -1367,8 +1376,8 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     if (k != KMOVE && k != KREN) continue;
     const u64 T = base[k] + woffk[k] + (u32)(x - kbase[k]);
     if (T >= nall) continue;
-    if (k == KMOVE) P.out_file[T] = st_b[e];
-    else P.Rstr[T - nmv] = st_b[e];
+    if (k == KMOVE) Q.out_file[T] = st_b[e];
+    else Q.Rstr[T - nmv] = st_b[e];
   }
 #endif
   if (DBG) {
