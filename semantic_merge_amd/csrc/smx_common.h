@@ -56,6 +56,7 @@ struct ComposeMeta {
   u64 seg_over;              // segmented plan: bit 0 a timestamp group too long, bit 1 a branch not ordered
   u64 n_win;                 // windows of the plan that ran
   u32 kmask[2];              // presorted plan: kinds present per branch (k_khist)
+  u64 cs_done;               // k_cscan_mid blocks done (the last one writes base[])
 };
 
 // Per-symbol final states (addr, file, ctx).  When the bit widths of (value + 1)

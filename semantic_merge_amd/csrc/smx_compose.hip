@@ -501,7 +501,7 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_up(const u32* __restrict__ cnt,
 }
 
 __global__ void __launch_bounds__(BLOCK) k_cscan_mid(u32* __restrict__ tsum, i64 na, i64 nb, i64 CM, i64 NT,
-                                                     u32* __restrict__ cnt, ComposeMeta* meta) {
+                                                     u32* __restrict__ cnt, ComposeMeta* meta, u64 nwin) {
   __shared__ u32 s[NWAVES + 1];
   const int col = blockIdx.x;
   if (SMX_CSCAN_FAILCHK && meta->f_fail) return;  // (k_khist saw a group no window holds)
@@ -521,6 +521,18 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_mid(u32* __restrict__ tsum, i64
     cnt[(i64)col * CM + C] = carry;  // prefix at the end of the branch (a window may start there)
     atomicAdd((unsigned long long*)&meta->kcnt[k], (unsigned long long)carry);
     if (k == KREN) meta->n_ren_side[side] = carry;
+    // the last column's block: the T-order segment starts (k_bases), from every total
+    __threadfence();
+    if (atomicAdd((unsigned long long*)&meta->cs_done, 1ull) == (unsigned long long)gridDim.x - 1) {
+      __threadfence();
+      meta->n_win = nwin;
+      u64 acc = 0;
+      for (int kk = 0; kk < SMX_N_KINDS; ++kk) {
+        meta->base[kk] = acc;
+        acc += __hip_atomic_load(&meta->kcnt[kk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      meta->base[SMX_N_KINDS] = acc;
+    }
   }
 }
 
@@ -1276,13 +1288,23 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
     hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d,
                        (const i64*)sh->in_state_dev, meta, C.out->conflicts, (u64)C.out->conflict_cap, skiplist,
                        skipbits);
-  // (one k_scan1 block over the window counts measured slower: walk 0.165 -> 0.185 ms, profiles/r03_w)
-  HIP_TRY((scan_excl<OpSum, u32, u32>(wtot, wcoff, Wmax, &meta->n_win, part, ncand32, st)));
+  // (one k_scan1 block over the window counts measured slower on config 3: walk 0.165 ->
+  // 0.185 ms, profiles/r03_w; small merges are launch-bound: one block)
+  if (Wmax <= WALK_SCAN1_MAXW)
+    hipLaunchKernelGGL(k_scan1<OpSum>, dim3(1), dim3(S1_NT), 0, st, wtot, wcoff, (const u64*)&meta->n_win,
+                       (u64)Wmax, ncand32);
+  else
+    HIP_TRY((scan_excl<OpSum, u32, u32>(wtot, wcoff, Wmax, &meta->n_win, part, ncand32, st)));
   hipLaunchKernelGGL(k_cand_compact, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, cslot, wcoff, ncand_dev, cand);
   hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
-  hipLaunchKernelGGL(k_scan1<OpMax>, dim3(1), dim3(S1_NT), 0, st, q, pm, ncand_dev, (u64)n, (u32*)nullptr);
-  hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, q, pm, nconf, meta, nreal);
-  hipLaunchKernelGGL(k_scan1<OpSum>, dim3(1), dim3(S1_NT), 0, st, nreal, coff, ncand_dev, (u64)n, nconf32);
+  if (n <= WALK_FUSED_MAXN) {  // small merges: max scan, clusters and sum scan in one block
+    hipLaunchKernelGGL(k_cluster_fused, dim3(1), dim3(S1_NT), 0, st, Wk, cand, q, pm, nconf, meta, nreal, coff,
+                       (u64)n, nconf32);
+  } else {
+    hipLaunchKernelGGL(k_scan1<OpMax>, dim3(1), dim3(S1_NT), 0, st, q, pm, ncand_dev, (u64)n, (u32*)nullptr);
+    hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, q, pm, nconf, meta, nreal);
+    hipLaunchKernelGGL(k_scan1<OpSum>, dim3(1), dim3(S1_NT), 0, st, nreal, coff, ncand_dev, (u64)n, nconf32);
+  }
   hipLaunchKernelGGL(k_replay_write, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, nreal, coff, meta,
                      C.out->conflicts, (u64)C.out->conflict_cap, skiplist, skipbits);
   HIP_TRY(hipGetLastError());
@@ -1553,8 +1575,18 @@ struct EarlyFail {
   u32* flag_dev = nullptr;
   hipEvent_t ev = nullptr;
 };
+// Presorted window sizes: small (merges up to WF_SMALL_MAXN ops, latency-bound: more,
+// shorter windows per CU), normal, wide (timestamp groups no normal window holds).
+enum WinLevel { WL_SMALL, WL_NORMAL, WL_WIDE };
+static i64 level_cap(int lv) { return lv == WL_SMALL ? WF_SMALL_CAP : lv == WL_WIDE ? WF_WIDE_CAP : WF_CAP; }
+static int first_level(const Ctx& C) { return C.n <= WF_SMALL_MAXN ? WL_SMALL : WL_NORMAL; }
+static i64 first_tgt(const Ctx& C) {
+  return first_level(C) == WL_SMALL ? knob("SMX_WIN_TGT", WF_SMALL_TGT) : knob("SMX_WIN_TGT", WIN_TGT);
+}
+
 // The presorted windows over the boundaries k_fpart left (W windows).
-static int launch_presorted_windows(const Ctx& C, i64 W, i64 CM, bool wide) {
+static int launch_presorted_windows(const Ctx& C, i64 W, i64 CM, int level) {
+  const bool wide = level == WL_WIDE;
   hipStream_t st = C.st;
   WinArgs P = win_args(C);
   P.cpre = C.ws<u32>(B_CCNT);
@@ -1578,6 +1610,9 @@ static int launch_presorted_windows(const Ctx& C, i64 W, i64 CM, bool wide) {
   if (wide) {
     if (P.src_map) hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, true>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
     else hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, false>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
+  } else if (level == WL_SMALL) {
+    if (P.src_map) hipLaunchKernelGGL((k_window_f<WF_SMALL_CAP, WF_SMALL_NT, false, true>), dim3(W), dim3(WF_SMALL_NT), 0, st, P);
+    else hipLaunchKernelGGL((k_window_f<WF_SMALL_CAP, WF_SMALL_NT, false, false>), dim3(W), dim3(WF_SMALL_NT), 0, st, P);
   } else if (P.src_map) {
     hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, true>), dim3(W), dim3(WF_NT), 0, st, P);
   } else {
@@ -1592,7 +1627,7 @@ static int launch_presorted_windows(const Ctx& C, i64 W, i64 CM, bool wide) {
 
 // wide: WF_WIDE_CAP-op windows on WF_WIDE_NT threads (one per CU) for logs whose
 // equal-timestamp groups no WF_CAP window holds (config 5: 8192-op groups).
-static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr, bool wide = false) {
+static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr, int level = WL_NORMAL) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
@@ -1603,7 +1638,7 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
     if (rc) return rc;
   }
   if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
-  const i64 cap = wide ? WF_WIDE_CAP : WF_CAP;
+  const i64 cap = level_cap(level);
   if (tgt > cap) tgt = cap;
   tgt -= tgt % CH;  // chunk-aligned diagonals (k_fpart's sampled first level)
   const i64 W = SMX_CEIL_DIV(C.n, tgt);
@@ -1625,14 +1660,13 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
     hipLaunchKernelGGL(k_cscan_up, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT, tsum,
                        meta);
     hipLaunchKernelGGL(k_cscan_mid, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, tsum, C.na, C.nb, CM, NT, ccnt,
-                       meta);
+                       meta, (u64)W);
     hipLaunchKernelGGL(k_cscan_down, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT,
                        tsum, meta);
   }
-  hipLaunchKernelGGL(k_bases, dim3(1), dim3(1), 0, st, meta, (u64)W);
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_PLAN);
-  return launch_presorted_windows(C, W, CM, wide);
+  return launch_presorted_windows(C, W, CM, level);
 }
 
 // k_fpart's long-group verdict (f_fail == F_LONG) is given before any window runs, so
@@ -1642,11 +1676,11 @@ __global__ void k_plan_rearm(ComposeMeta* meta, u64 nwin) {
   if (meta->f_fail == F_LONG) meta->f_fail = 0;
   meta->n_win = nwin;
 }
-static int run_presorted_rewide(const Ctx& C, i64 tgt) {
+static int run_presorted_rewide(const Ctx& C, i64 tgt, int level = WL_WIDE) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
-  if (tgt > WF_WIDE_CAP) tgt = WF_WIDE_CAP;
+  if (tgt > level_cap(level)) tgt = level_cap(level);
   tgt -= tgt % CH;
   const i64 W = SMX_CEIL_DIV(C.n, tgt);
   const i64 CM = SMX_CEIL_DIV(C.na > C.nb ? C.na : C.nb, (i64)CH) + 1;
@@ -1655,11 +1689,11 @@ static int run_presorted_rewide(const Ctx& C, i64 tgt) {
   C.tm->begin(ST_PLAN);
   hipLaunchKernelGGL(k_plan_rearm, dim3(1), dim3(1), 0, st, meta, (u64)W);
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
-                     C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na, C.nb, W, tgt, (i64)(WF_WIDE_CAP / CH),
+                     C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na, C.nb, W, tgt, level_cap(level) / CH,
                      C.ws<i64>(B_BND), meta, (u32*)nullptr);
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_PLAN);
-  return launch_presorted_windows(C, W, CM, true);
+  return launch_presorted_windows(C, W, CM, level);
 }
 
 // Generic plan: each branch sorted by (ts, oid_hi, oid_lo, index), then fixed windows
@@ -2122,12 +2156,19 @@ static thread_local int g_plan = SMX_PLAN_PRESORTED;
 // saw a decrease.  (k_fpart's early verdict, F_LONG, can hide bit 0: then the wide
 // windows or the segmented sort report the decrease themselves.)
 static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeMeta* hm, i64 tgt,
-                           bool require_ordered = false) {
+                           bool require_ordered = false, int level = WL_NORMAL) {
   int rc;
   auto unordered = [&]() {
     return set_err(SMX_E_ARG, "sharded merge needs timestamp-ordered branch logs in every shard");
   };
   g_plan = SMX_PLAN_PRESORTED;
+  if (level == WL_SMALL && hm->f_fail && !(hm->f_fail & 1) && !hm->bad_sym) {
+    // small windows that do not hold the log's timestamp groups: the normal ones
+    tgt = knob("SMX_WIN_TGT", WIN_TGT);
+    if ((rc = hm->f_fail == F_LONG ? run_presorted_rewide(C, tgt, WL_NORMAL) : run_presorted(C, tgt))) return rc;
+    if (tail && (rc = launch_tail(C))) return rc;
+    if ((rc = read_meta(C, hm))) return rc;
+  }
   while (hm->f_fail == 2 && !hm->bad_sym && tgt > WIN_TGT_MIN) {  // dense groups: smaller windows
     tgt = (tgt / 2) / CH * CH;
     if ((rc = run_presorted(C, tgt))) return rc;
@@ -2140,7 +2181,7 @@ static int order_fallbacks(const Ctx& C, bool allow_generic, bool tail, ComposeM
   // config 5's windows is one 8192-op group, and no window is empty)
   for (i64 wt = WF_WIDE_CAP; hm->f_fail && !(hm->f_fail & 1) && !hm->bad_sym && wt >= WIN_TGT_MIN; wt /= 2) {
     g_plan = SMX_PLAN_PRESORTED_WIDE;
-    if ((rc = hm->f_fail == F_LONG ? run_presorted_rewide(C, wt) : run_presorted(C, wt, nullptr, true))) return rc;
+    if ((rc = hm->f_fail == F_LONG ? run_presorted_rewide(C, wt) : run_presorted(C, wt, nullptr, WL_WIDE))) return rc;
     if (tail && (rc = launch_tail(C))) return rc;
     if ((rc = read_meta(C, hm))) return rc;
     if (hm->f_fail != 2) break;  // held, or groups longer than a wide window (6), or unordered (1)
@@ -2286,7 +2327,7 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
     use_early = cs == hipStreamCaptureStatusNone && early_fail_of(dev, &early) == SMX_OK;
     if (use_early) early.flag_host[0] = early.flag_host[1] = 0u;  // (the previous merge on this thread has synced)
   }
-  if ((rc = run_presorted(C, knob("SMX_WIN_TGT", WIN_TGT), use_early ? &early : nullptr))) return rc;
+  if ((rc = run_presorted(C, first_tgt(C), use_early ? &early : nullptr, first_level(C)))) return rc;
   if (use_early) {
     HIP_TRY(hipEventSynchronize(early.ev));
     if (((volatile u32*)early.flag_host)[0]) {
@@ -2486,7 +2527,7 @@ static int compose_finish_impl(const smx_ops* ops, const smx_compose_out* out, v
     return rc;
   }
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
-  if (hm.f_fail && (rc = order_fallbacks(C, true, true, &hm, knob("SMX_WIN_TGT", WIN_TGT)))) return rc;
+  if (hm.f_fail && (rc = order_fallbacks(C, true, true, &hm, first_tgt(C), false, first_level(C)))) return rc;
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
   if (hm.n_move_none && hm.kcnt[KMOVE]) {
     tm.begin(ST_MVPREFIX);

@@ -307,11 +307,15 @@ __global__ void __launch_bounds__(BLOCK) k_cand_compact(WalkArgs W0, const u32* 
 // word of a zeroed u64) = the total.  For the candidate arrays, which are short on
 // real logs (one block, no extra launches); long ones loop.
 #define S1_NT 1024
+#ifndef WALK_SCAN1_MAXW
+#define WALK_SCAN1_MAXW 65536        // window-count scan in one block up to this many windows
+#endif
+#ifndef WALK_FUSED_MAXN
+#define WALK_FUSED_MAXN (1ll << 22)  // k_cluster_fused up to this many ops
+#endif
 template <typename Op>
-__global__ void __launch_bounds__(S1_NT) k_scan1(const u32* __restrict__ in, u32* __restrict__ out,
-                                                 const u64* n_dev, u64 cap, u32* total_lo) {
-  __shared__ u32 s[S1_NT / WAVE + 1];
-  const u64 n = min(*n_dev, cap);  // cap: the arrays' capacity
+__device__ __forceinline__ void scan1_block(const u32* __restrict__ in, u32* __restrict__ out, u64 n,
+                                            u32* total_lo, u32* s) {
   u32 carry = Op::template identity<u32>();
   for (u64 r0 = 0; r0 < n; r0 += S1_NT * 8) {
     const u64 b = r0 + threadIdx.x * 8;
@@ -332,6 +336,12 @@ __global__ void __launch_bounds__(S1_NT) k_scan1(const u32* __restrict__ in, u32
     carry = Op::apply(carry, tot);
   }
   if (total_lo && threadIdx.x == 0) *total_lo = carry;
+}
+template <typename Op>
+__global__ void __launch_bounds__(S1_NT) k_scan1(const u32* __restrict__ in, u32* __restrict__ out,
+                                                 const u64* n_dev, u64 cap, u32* total_lo) {
+  __shared__ u32 s[S1_NT / WAVE + 1];
+  scan1_block<Op>(in, out, min(*n_dev, cap), total_lo, s);  // cap: the arrays' capacity
 }
 
 // Incoming open region (sharded merge): the previous shards' walk ended with
@@ -392,13 +402,11 @@ __global__ void k_replay_q(WalkArgs W0, const u32* __restrict__ cand, const Comp
 // region reaches it) is real; inside a cluster, walk sequentially.  A long region
 // (Q_LONG; it joins every later candidate to its cluster) is replayed in full here,
 // once, by the cluster's thread.
-__global__ void k_cluster(WalkArgs W0, const u32* __restrict__ cand, u32* __restrict__ q,
-                          const u32* __restrict__ pm, u32* __restrict__ nconf, const ComposeMeta* meta,
-                          u32* __restrict__ nreal) {
-  const WalkArgs W = walk_load(W0);
-  if (W.fail) return;
+__device__ __forceinline__ void cluster_walk(const WalkArgs& W, const u32* __restrict__ cand, u32* __restrict__ q,
+                                             const u32* __restrict__ pm, u32* __restrict__ nconf,
+                                             const ComposeMeta* meta, u32* __restrict__ nreal, u64 c0, u64 cstep) {
   const u64 nc = meta->n_cand;
-  for (u64 c = (u64)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (u64)gridDim.x * BLOCK) {
+  for (u64 c = c0; c < nc; c += cstep) {
     if (pm[c] > cand[c]) continue;  // not a cluster start
     u32 last_q = (u32)meta->q_in;   // an incoming region (sharded merge) covers [0, q_in)
     for (u64 j = c; j < nc && (j == c || pm[j] > cand[j]); ++j) {
@@ -416,6 +424,30 @@ __global__ void k_cluster(WalkArgs W0, const u32* __restrict__ cand, u32* __rest
       }
     }
   }
+}
+__global__ void k_cluster(WalkArgs W0, const u32* __restrict__ cand, u32* __restrict__ q,
+                          const u32* __restrict__ pm, u32* __restrict__ nconf, const ComposeMeta* meta,
+                          u32* __restrict__ nreal) {
+  const WalkArgs W = walk_load(W0);
+  if (W.fail) return;
+  cluster_walk(W, cand, q, pm, nconf, meta, nreal, (u64)blockIdx.x * blockDim.x + threadIdx.x,
+               (u64)gridDim.x * blockDim.x);
+}
+// Small merges (launch-bound): k_scan1<OpMax> (pm), k_cluster and k_scan1<OpSum> (coff,
+// the conflict total) in one block, barriers between the phases.
+__global__ void __launch_bounds__(S1_NT) k_cluster_fused(WalkArgs W0, const u32* __restrict__ cand,
+                                                         u32* __restrict__ q, u32* __restrict__ pm,
+                                                         u32* __restrict__ nconf, const ComposeMeta* meta,
+                                                         u32* __restrict__ nreal, u32* __restrict__ coff, u64 cap,
+                                                         u32* total_lo) {
+  __shared__ u32 s[S1_NT / WAVE + 1];
+  const WalkArgs W = walk_load(W0);
+  const u64 nc = min(meta->n_cand, cap);
+  scan1_block<OpMax>(q, pm, nc, nullptr, s);
+  __syncthreads();  // (global writes of this block: visible to it after the barrier)
+  if (!W.fail) cluster_walk(W, cand, q, pm, nconf, meta, nreal, threadIdx.x, S1_NT);
+  __syncthreads();
+  scan1_block<OpSum>(nreal, coff, W.fail ? 0 : nc, total_lo, s);
 }
 
 // Writes the conflict pairs, skip-list entries and skip bits of every real

@@ -210,6 +210,16 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #define WF_WIDE_CAP 8192  // the wide presorted window (run_presorted(wide)): one per CU
 #endif
 #define WF_WIDE_NT 1024
+#ifndef WF_SMALL_CAP
+#define WF_SMALL_CAP 512  // small merges' windows (latency-bound: more windows in flight per CU)
+#endif
+#define WF_SMALL_NT 128
+#ifndef WF_SMALL_TGT
+#define WF_SMALL_TGT 256
+#endif
+#ifndef WF_SMALL_MAXN
+#define WF_SMALL_MAXN (1ll << 21)  // merges up to this many ops start with the small windows
+#endif
 #define WF_NCH (WF_CAP / WAVE)
 #define WF_WAVES (WF_NT / WAVE)
 #define WF_ITEMS (WF_CAP / WF_NT)
