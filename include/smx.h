@@ -245,6 +245,20 @@ int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const smx_compose
                    void* workspace, size_t workspace_bytes, void* stream, int step);
 
 /*
+ * The range plan's per-rank info for the sharded exchange (shard.py _range_info), in
+ * two launches instead of a dozen tensor operations.  ts: the rank's timestamp buffer;
+ * its A slice is ts[off_a, off_a + n_a), its B slice ts[off_b, off_b + n_b).  out
+ * (int64, 9 + 4 * rh, device): n_a, n_b; the first and last key of the A slice, of the B
+ * slice (keys: the u64 timestamp with its top bit flipped, so that int64 order is u64
+ * order; 0 for an empty slice); 1 if both slices are non-decreasing (check_order = 0:
+ * not checked, 1); signed_a, signed_b; then rh keys from the head of the A slice and rh
+ * from its tail (right-aligned), the same for B (a slice shorter than rh pads with its
+ * first key).
+ */
+int smx_shard_range_info(const uint64_t* ts, int64_t off_a, int64_t n_a, int64_t off_b, int64_t n_b, int32_t rh,
+                         int32_t check_order, int32_t signed_a, int32_t signed_b, int64_t* out, void* stream);
+
+/*
  * Per-stage device timing of the last smx_compose calls on this thread, for the
  * benchmark: when enabled, each stage is bracketed by hipEvents on the call's
  * stream and the elapsed milliseconds are accumulated per stage.

@@ -110,6 +110,7 @@ EXPORTS = (
     "smx_release_graphs",
     "smx_last_plan",
     "smx_shard_step",
+    "smx_shard_range_info",
     "smx_set_profiling",
     "smx_set_profiling_stages",
     "smx_stage_times",
@@ -140,6 +141,10 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.smx_shard_step.argtypes = [C.POINTER(SmxOps), C.POINTER(SmxShard), C.POINTER(SmxComposeOut),
                                    C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]
     lib.smx_shard_step.restype = C.c_int
+    if hasattr(lib, "smx_shard_range_info"):  # (older builds, e.g. A/B baselines, lack it)
+        lib.smx_shard_range_info.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int32,
+                                             C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        lib.smx_shard_range_info.restype = C.c_int
     lib.smx_set_profiling.argtypes = [C.c_int]
     lib.smx_set_profiling.restype = C.c_int
     lib.smx_set_profiling_stages.argtypes = [C.c_uint32]

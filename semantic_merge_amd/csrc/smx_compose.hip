@@ -2789,6 +2789,61 @@ static int shard_impl(const smx_ops* ops, const smx_shard* sh, const smx_compose
   return SMX_OK;
 }
 
+// smx_shard_range_info (include/smx.h): one block for the keys, then a grid over both
+// slices for the order check (a violation stores 0; every writer stores the same).
+__device__ __forceinline__ i64 rinfo_key(u64 v) { return (i64)(v ^ 0x8000000000000000ull); }
+__global__ void k_range_info(const u64* __restrict__ ts, i64 off_a, i64 n_a, i64 off_b, i64 n_b, int rh,
+                             int sa, int sb, i64* __restrict__ out) {
+  const int t = threadIdx.x;
+  if (t == 0) {
+    out[0] = n_a;
+    out[1] = n_b;
+    out[2] = n_a ? rinfo_key(ts[off_a]) : 0;
+    out[3] = n_a ? rinfo_key(ts[off_a + n_a - 1]) : 0;
+    out[4] = n_b ? rinfo_key(ts[off_b]) : 0;
+    out[5] = n_b ? rinfo_key(ts[off_b + n_b - 1]) : 0;
+    out[6] = 1;
+    out[7] = sa;
+    out[8] = sb;
+  }
+  for (int i = t; i < 4 * rh; i += blockDim.x) {
+    const int br = i / (2 * rh), j = i % (2 * rh);
+    const i64 o = br ? off_b : off_a, n = br ? n_b : n_a;
+    const i64 h = n < rh ? n : rh;
+    i64 pos;
+    if (n == 0) pos = -1;
+    else if (j < rh) pos = j < h ? o + j : o;                         // head, padded
+    else pos = j - rh < rh - h ? o : o + n - h + (j - rh - (rh - h));  // tail, right-aligned
+    out[9 + i] = pos < 0 ? 0 : rinfo_key(ts[pos]);
+  }
+}
+__global__ void k_range_order(const u64* __restrict__ ts, i64 off_a, i64 n_a, i64 off_b, i64 n_b,
+                              i64* __restrict__ out) {
+  bool bad = false;
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n_a + n_b; i += (i64)gridDim.x * blockDim.x) {
+    const bool b = i >= n_a;
+    const i64 k = b ? i - n_a : i;
+    if (k == 0) continue;
+    const i64 o = b ? off_b : off_a;
+    bad |= ts[o + k] < ts[o + k - 1];
+  }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) out[6] = 0;
+}
+extern "C" int smx_shard_range_info(const uint64_t* ts, int64_t off_a, int64_t n_a, int64_t off_b, int64_t n_b,
+                                    int32_t rh, int32_t check_order, int32_t signed_a, int32_t signed_b, int64_t* out,
+                                    void* stream) {
+  if (!ts || !out || n_a < 0 || n_b < 0 || rh < 1 || off_a < 0 || off_b < 0)
+    return set_err(SMX_E_ARG, "smx_shard_range_info: bad argument");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_range_info, dim3(1), dim3(BLOCK), 0, st, (const u64*)ts, off_a, n_a, off_b, n_b, rh,
+                     signed_a, signed_b, (i64*)out);
+  if (check_order && n_a + n_b > 1)
+    hipLaunchKernelGGL(k_range_order, dim3(grid_for(n_a + n_b, BLOCK * 16)), dim3(BLOCK), 0, st, (const u64*)ts,
+                       off_a, n_a, off_b, n_b, (i64*)out);
+  HIP_TRY(hipGetLastError());
+  return SMX_OK;
+}
+
 extern "C" int smx_shard_step(const smx_ops* ops, const smx_shard* shard, const smx_compose_out* out,
                               void* workspace, size_t workspace_bytes, void* stream, int step) {
   if (!ops) return set_err(SMX_E_ARG, "null ops");

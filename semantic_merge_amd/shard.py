@@ -249,6 +249,7 @@ class ShardedCompose:
         self._bind_key = None
         self._halo_key = None
         self._info_key = None
+        self._info_out = None  # smx_shard_range_info's output (int64 [9 + 4 RH])
         self.host_cut_plans = 0  # exchanges planned from the gathered head / tail keys alone
 
     def _alloc(self, hd: int, a, b) -> None:
@@ -293,12 +294,22 @@ class ShardedCompose:
         every timestamp is below 2^63 (the device cut search runs on the stored words),
         then the RH head and RH tail keys of each slice (host-side cuts)."""
         torch = self.torch
+        check_order = self.mode == "auto"  # "range": the ORDER plan checks the order itself
+        if self.dev.type == "cuda":  # two launches (smx_shard_range_info)
+            if self._info_out is None:
+                self._info_out = torch.empty(9 + 4 * RH, dtype=torch.int64, device=self.dev)
+            s = torch.cuda.current_stream(self.dev).cuda_stream
+            check(lib().smx_shard_range_info(self.buf["ts"].data_ptr(), self._oa, self.na_s, self._ob, self.nb_s,
+                                             RH, int(check_order), int(self._ts_signed[0]),
+                                             int(self._ts_signed[1]), self._info_out.data_ptr(), s))
+            return self._info_out
+        # the exchange protocol's CPU tests (gloo, host tensors): the same vector in torch
         if self._info_key != (self._oa, self._ob):
             self._info_idx = self._info_index()
             self._info_key = (self._oa, self._ob)
         keys = _u64_key(self.buf["ts"].index_select(0, self._info_idx))
         ok = self._one
-        if self.mode == "auto":  # "range": the ORDER plan checks the order itself
+        if check_order:
             for br, n in ((0, self.na_s), (1, self.nb_s)):
                 if n > 1:
                     k = _u64_key(self._orig(br, "ts"))

@@ -412,3 +412,45 @@ def test_shard_full_size_c3_two_ranks():
     n_out, n_conf, digest = got[0]
     assert (n_out, n_conf) == (rec["n_out"], rec["n_conflicts"])
     assert digest == rec["sha256"]
+
+
+@pytest.mark.parametrize("na,nb,offb,order", [(1000, 777, 1200, True), (5, 40, 10, True), (0, 50, 3, True),
+                                             (300, 0, 0, True), (300, 200, 400, False)])
+def test_range_info_native_matches_reference_layout(na, nb, offb, order):
+    """smx_shard_range_info (the range plan's per-rank vector in two launches) against
+    the same vector built on the host: sizes, end keys, order flag, signed flags and the
+    RH head / tail keys (right-aligned tail, short slices padded with their first key);
+    timestamps with the top bit set included."""
+    import ctypes as C
+    import torch
+    from semantic_merge_amd._lib import lib
+    from semantic_merge_amd.shard import RH
+    rng = np.random.default_rng(na + nb + offb)
+    buf = np.zeros(offb + nb + 64, dtype=np.uint64)
+    a = np.sort(rng.integers(0, 2**64 - 1, na, dtype=np.uint64))
+    b = np.sort(rng.integers(0, 2**64 - 1, nb, dtype=np.uint64))
+    if not order and nb > 3:
+        b[[1, 2]] = b[[2, 1]]  # a decrease inside the B slice
+    buf[5:5 + na] = a
+    buf[offb:offb + nb] = b
+    dev = torch.device("cuda:0")
+    t = torch.from_numpy(buf.view(np.int64)).to(dev)
+    out = torch.zeros(9 + 4 * RH, dtype=torch.int64, device=dev)
+    rc = lib().smx_shard_range_info(t.data_ptr(), 5, na, offb, nb, RH, 1, 1, 0, out.data_ptr(),
+                                    torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    got = out.cpu().numpy()
+
+    def key(v):
+        return np.int64(np.uint64(v) ^ np.uint64(1 << 63))
+
+    want = [na, nb, key(a[0]) if na else 0, key(a[-1]) if na else 0, key(b[0]) if nb else 0,
+            key(b[-1]) if nb else 0, int(bool(np.all(np.diff(a.astype(object)) >= 0)) and
+                                         bool(np.all(np.diff(b.astype(object)) >= 0))), 1, 0]
+    for x in (a, b):
+        n = len(x)
+        h = min(RH, n)
+        pad = [key(x[0])] if n else [0]
+        want += [key(v) for v in x[:h]] + pad * (RH - h)
+        want += pad * (RH - h) + [key(v) for v in x[n - h:]]
+    assert got.tolist() == [int(w) for w in want]
