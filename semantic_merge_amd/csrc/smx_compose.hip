@@ -473,6 +473,120 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
   }
 }
 
+// k_khist as a persistent grid (KH_PERSIST): each block walks groups of CH_PER_BLOCK
+// chunks with the next group's kind bytes loaded before the current group is counted,
+// counts branch-free, and publishes the kinds present once at its end.
+#ifndef KH_PERSIST
+#define KH_PERSIST 1
+#endif
+#define KH_BLOCKS_PER_CU 4
+__device__ __forceinline__ void kh_load(const u8* __restrict__ kind, const u64* __restrict__ ts, i64 na, i64 nb,
+                                        i64 bgap, i64 CA, i64 CB, i64 g, int q, u64* __restrict__ sA,
+                                        u64* __restrict__ sB, uint4* w, int* nv_o) {
+  const int side = g >= CA;
+  const i64 cc = side ? g - CA : g;
+  const i64 len = side ? nb : na;
+  const i64 r0 = cc * CH + q * 16;
+  const int nv = g < CA + CB ? (int)(len - r0 < 0 ? 0 : (len - r0 < 16 ? len - r0 : 16)) : 0;
+  *nv_o = nv;
+  const u8* src = kind + (side ? na + bgap : 0) + r0;
+  if (g < CA + CB) {
+    if (!side && q == 0) sA[cc] = ts[cc * CH];
+    if (side && q == 15 && nv == 16) sB[cc] = ts[na + bgap + cc * CH + CH - 1];
+  }
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (nv == 16 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    v = *reinterpret_cast<const uint4*>(src);
+  } else {
+    u32 x[4] = {0u, 0u, 0u, 0u};
+    for (int y = 0; y < nv; ++y) x[y >> 2] |= (u32)src[y] << (8 * (y & 3));
+    v = make_uint4(x[0], x[1], x[2], x[3]);
+  }
+  *w = v;
+}
+__global__ void __launch_bounds__(KH_NT) k_khist2(const u8* __restrict__ kind, const u64* __restrict__ ts,
+                                                  i64 na, i64 nb, i64 bgap, i64 CM, u32* __restrict__ cnt,
+                                                  u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta,
+                                                  u32* long_host) {
+  __shared__ u32 c[CH_PER_BLOCK][SMX_N_KINDS];
+  __shared__ u32 km[2];
+  const i64 CA = SMX_CEIL_DIV(na, (i64)CH), CB = SMX_CEIL_DIV(nb, (i64)CH);
+  const i64 ngrp = SMX_CEIL_DIV(CA + CB, (i64)CH_PER_BLOCK);
+  const int j = threadIdx.x / 16, q = threadIdx.x % 16;
+  if (threadIdx.x < 2) km[threadIdx.x] = 0;
+  u32 m0 = 0, m1 = 0;
+  bool bad = false;
+  i64 blk = blockIdx.x;
+  uint4 w;
+  int nv = 0;
+  if (blk < ngrp) kh_load(kind, ts, na, nb, bgap, CA, CB, blk * CH_PER_BLOCK + j, q, sA, sB, &w, &nv);
+  for (; blk < ngrp; blk += gridDim.x) {
+    const uint4 cw = w;
+    const int cnv = nv;
+    if (blk + gridDim.x < ngrp)  // the next group's bytes, in flight while this one is counted
+      kh_load(kind, ts, na, nb, bgap, CA, CB, (blk + gridDim.x) * CH_PER_BLOCK + j, q, sA, sB, &w, &nv);
+    const u32 ww[4] = {cw.x, cw.y, cw.z, cw.w};
+    u32 pk[3] = {0u, 0u, 0u};  // kind k: bits 5 * (k % 6) of word k / 6
+#pragma unroll
+    for (int y = 0; y < 16; ++y) {
+      const bool ok = y < cnv;
+      u32 k = (ww[y >> 2] >> (8 * (y & 3))) & 0xffu;
+      bad |= ok & (k >= SMX_N_KINDS);
+      k = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
+      const u32 wd = (k * 43u) >> 8;  // k / 6 for k < 18
+      const u32 inc = ok ? 1u << (5u * (k - 6u * wd)) : 0u;
+      pk[0] += wd == 0 ? inc : 0u;
+      pk[1] += wd == 1 ? inc : 0u;
+      pk[2] += wd == 2 ? inc : 0u;
+    }
+    u32 f[6];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      f[2 * i] = (pk[i] & 31u) | ((pk[i] >> 5) & 31u) << 10 | ((pk[i] >> 10) & 31u) << 20;
+      f[2 * i + 1] = ((pk[i] >> 15) & 31u) | ((pk[i] >> 20) & 31u) << 10 | ((pk[i] >> 25) & 31u) << 20;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      u32 v = f[i];
+      v += dpp_u32<0x111, 0xf>(v);  // row_shr:1
+      v += dpp_u32<0x112, 0xf>(v);  // row_shr:2
+      v += dpp_u32<0x114, 0xf>(v);  // row_shr:4
+      v += dpp_u32<0x118, 0xf>(v);  // row_shr:8
+      f[i] = v;
+    }
+    if (q == 15) {
+#pragma unroll
+      for (int k = 0; k < SMX_N_KINDS; ++k) c[j][k] = (f[k / 3] >> (10 * (k % 3))) & 1023u;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < CH_PER_BLOCK * SMX_N_KINDS; i += KH_NT) {
+      const int jj = i % CH_PER_BLOCK, k = i / CH_PER_BLOCK;
+      const i64 gg = blk * CH_PER_BLOCK + jj;
+      if (gg >= CA + CB) continue;
+      const int sd = gg >= CA;
+      const u32 v = c[jj][k];
+      cnt[((i64)sd * SMX_N_KINDS + k) * CM + (sd ? gg - CA : gg)] = v;
+      if (v) (sd ? m1 : m0) |= 1u << k;
+    }
+    __syncthreads();  // (c is rewritten by the next group)
+  }
+  if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) {
+    meta->bad_sym = 1;
+    if (long_host) __hip_atomic_store(long_host + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  m0 = wave_or_to_last(m0);
+  m1 = wave_or_to_last(m1);
+  if ((threadIdx.x & (WAVE - 1)) == WAVE - 1) {
+    if (m0) atomicOr(&km[0], m0);
+    if (m1) atomicOr(&km[1], m1);
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 && km[threadIdx.x]) {
+    const u32 cur = __hip_atomic_load(&meta->kmask[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cur | km[threadIdx.x]) != cur) atomicOr(&meta->kmask[threadIdx.x], km[threadIdx.x]);
+  }
+}
+
 __device__ __forceinline__ bool cs_present(const ComposeMeta* meta, int col) {
   return (meta->kmask[col >= SMX_N_KINDS] >> (col % SMX_N_KINDS)) & 1u;
 }
@@ -1647,9 +1761,24 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
   u32* ccnt = C.ws<u32>(B_CCNT);
   u64* sA = C.ws<u64>(B_SMP);
   u64* sB = sA + SMX_CEIL_DIV(C.na, (i64)CH) + 1;
-  hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK * KH_R)), dim3(KH_NT), 0, st, C.ops->kind,
-                     C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta,
-                     early ? early->flag_dev : nullptr);
+  if (KH_PERSIST) {
+    static int ncu_of[64] = {};  // CUs per device (a benign race: every writer stores the same)
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    int ncu = dev < 64 ? ncu_of[dev] : 0;
+    if (ncu == 0) {
+      HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      if (dev < 64) ncu_of[dev] = ncu;
+    }
+    const i64 ngrp = SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK);
+    const i64 grid = ngrp < (i64)ncu * KH_BLOCKS_PER_CU ? ngrp : (i64)ncu * KH_BLOCKS_PER_CU;
+    hipLaunchKernelGGL(k_khist2, dim3(grid > 0 ? grid : 1), dim3(KH_NT), 0, st, C.ops->kind, C.ops->ts, C.na, C.nb,
+                       C.ops->b_gap, CM, ccnt, sA, sB, meta, early ? early->flag_dev : nullptr);
+  } else {
+    hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK * KH_R)), dim3(KH_NT), 0, st,
+                       C.ops->kind, C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta,
+                       early ? early->flag_dev : nullptr);
+  }
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
                      C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na,
                      C.nb, W, tgt, cap / CH, bnd, meta, early ? early->flag_dev : nullptr);

@@ -229,6 +229,9 @@ __global__ void k_tb_unskip(TbArgs A0, const u32* __restrict__ lst, u32* __restr
 #define TBR_TK 16
 #endif
 // TBR_TK: tiles per wave step in k_tb_reduce
+#ifndef TBR_PREFETCH
+#define TBR_PREFETCH 1  // k_tb_reduce loads the next step's run bounds before this step's records are used
+#endif
 
 // One workgroup per bucket: LDS max over record indices, then each symbol's
 // values are fetched once: fin[sym] = (addr, file, ctx).
@@ -288,13 +291,21 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
   const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
   const u32 nb1 = A.nbk + 1;
   constexpr int NW = TBR_NT / WAVE;
-  for (int t0 = wv * TBR_TK; t0 < nt; t0 += NW * TBR_TK) {
-    u32 lo = 0, hi = 0;
+  // the run bounds of a step's tiles (lanes < TBR_TK), loaded one step ahead so that a
+  // step's record loads do not wait for its bounds
+  auto bounds = [&](int t0, u32* lo, u32* hi) {
+    *lo = *hi = 0;
     if (lane < TBR_TK && t0 + lane < nt) {
       const u32* lt = lst + (u64)(t0 + lane) * nb1;
-      lo = lt[b];
-      hi = lt[b + 1];
+      *lo = lt[b];
+      *hi = lt[b + 1];
     }
+  };
+  u32 lo_n = 0, hi_n = 0;
+  if (TBR_PREFETCH) bounds(wv * TBR_TK, &lo_n, &hi_n);
+  for (int t0 = wv * TBR_TK; t0 < nt; t0 += NW * TBR_TK) {
+    u32 lo = lo_n, hi = hi_n;
+    if (!TBR_PREFETCH) bounds(t0, &lo, &hi);
     u32 q[TBR_TK][2];
 #pragma unroll
     for (int k = 0; k < TBR_TK; ++k) {
@@ -306,6 +317,7 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
         q[k][u] = i < hk ? __builtin_nontemporal_load(&rec[rb + i]) : ~0u;
       }
     }
+    if (TBR_PREFETCH) bounds(t0 + NW * TBR_TK, &lo_n, &hi_n);
 #pragma unroll
     for (int k = 0; k < TBR_TK; ++k)
 #pragma unroll

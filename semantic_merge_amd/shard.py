@@ -220,9 +220,12 @@ class ShardedCompose:
         self._saved = []
         self.sbuf, self.src_map = None, None
         dv = self.dev
-        self.summary = torch.zeros(SUM, dtype=torch.int64, device=dv)
         H2 = 2 * max(self.H, 1)
-        self.xport = torch.zeros((3, H2), dtype=torch.int32, device=dv)     # sym, cls, src exports
+        # the summary and the halo exports (sym, cls, src) in one buffer: the order
+        # exchange gathers it as it is
+        self._sx = torch.zeros(SUM + 3 * H2 // 2, dtype=torch.int64, device=dv)
+        self.summary = self._sx[:SUM]
+        self.xport = self._sx[SUM:].view(torch.int32).view(3, H2)
         self.halo = torch.zeros((2, 3, max(self.H, 1)), dtype=torch.int32, device=dv)
         self.halo_dev = torch.zeros(4, dtype=torch.int64, device=dv)
         self.in_state = (0, 0)
@@ -713,7 +716,7 @@ class ShardedCompose:
             self.halo_dev.zero_()
             self._sh.order_gather = None
             return
-        self._gathered = self.comm.all_gather(torch.cat([self.summary, self.xport.reshape(-1).view(torch.int64)]))
+        self._gathered = self.comm.all_gather(self._sx)
         self._sh.order_gather = _ptr(self._gathered)
 
     def _walk(self, first_done: bool = False):
