@@ -345,6 +345,9 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
 #else
 #define RW_HT u32
 #endif
+#ifndef RW_W0G
+#define RW_W0G 1  // key word 0 read from the list's records in L2, not held in LDS: 2 KB less per list, more lists per CU
+#endif
 #ifndef RW_ABL
 #define RW_ABL 0  // timing ablations (wrong results): bit0 no replay, bit1 no grouping / replay,
                   // bit2 no key order, bit3 load only
@@ -412,7 +415,9 @@ struct RwLds {
   // waves per SIMD; a full table still terminates, every value finds its slot), two
   // per event otherwise
   static constexpr int HT = (RW_HT1 && CAP == RW_CAP) ? CAP : 2 * CAP;
+#if !RW_W0G
   u64 w0[CAP];          // key word 0 of each event (words 1-3 stay in global memory / L2)
+#endif
   u64 wv[CAP];          // value << 32 | op << 30 | index (record word RGA_WV)
   union {
     struct {
@@ -432,7 +437,12 @@ struct RwLds {
 template <class LDS>
 __device__ __forceinline__ bool ev_lt(const LDS& S, const u64* __restrict__ src, const smx_rga_ops& o, u32 a,
                                       u32 b) {
-  if (S.w0[a] != S.w0[b]) return S.w0[a] < S.w0[b];
+#if RW_W0G
+  const u64 wa = src[(u64)a * RGA_REC], wb = src[(u64)b * RGA_REC];  // (the list's records, L2-resident)
+#else
+  const u64 wa = S.w0[a], wb = S.w0[b];
+#endif
+  if (wa != wb) return wa < wb;
   return rga_key_lt(o, (u32)S.wv[a] & RGA_IDX_MASK, (u32)S.wv[b] & RGA_IDX_MASK);
 }
 
@@ -503,14 +513,16 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
       const u32 x = lane + (u32)i * WAVE;
       const u32 e = x / RGA_REC, wd = x - e * RGA_REC;
       if (x < cnt * RGA_REC) {
+#if !RW_W0G
         if (wd == 0) S.w0[e] = v[i];
+#endif
         if (wd == RGA_WV) S.wv[e] = v[i];
       }
     }
   }
   wave_lds_sync();
   if (RW_ABL & 8) {
-    if (lane == 0) rga_put_count(scnt, l, (u32)S.w0[lane] & 1u);
+    if (lane == 0) rga_put_count(scnt, l, (u32)S.wv[lane] & 1u);
     return;
   }
   const u64 lt = lanemask_lt();
@@ -634,7 +646,11 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
     const u32 a = (u32)k * 64u + lane;
     if (a < m) {
       pay[k] = S.gp[a];
+#if RW_W0G
+      key[k] = src[(u64)pay[k] * RGA_REC];
+#else
       key[k] = S.w0[pay[k]];
+#endif
     }
   }
   wave_lds_sync();  // gp / the hash table are rewritten below
