@@ -676,6 +676,58 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_down(u32* __restrict__ cnt, i64
   }
 }
 
+// Small merges (CM <= CS_SMALL_CM chunks per branch): each (side, kind) column scanned by
+// one block in one launch (k_cscan_up / mid / down are three launch latencies); the
+// totals and, in the last column's block, the T-order segment starts as in k_cscan_mid.
+#ifndef CS_SMALL_CM
+#define CS_SMALL_CM 16384
+#endif
+__global__ void __launch_bounds__(BLOCK) k_cscan_small(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
+                                                       ComposeMeta* meta, u64 nwin) {
+  __shared__ u32 s[NWAVES + 1];
+  const int col = blockIdx.x;
+  const int side = col / SMX_N_KINDS, k = col % SMX_N_KINDS;
+  const i64 C = SMX_CEIL_DIV(side ? nb : na, (i64)CH);
+  u32* colp = cnt + (i64)col * CM;
+  u32 carry = 0;
+  if (cs_present(meta, col)) {  // (an absent column's prefixes are its zero counts)
+    for (i64 t0 = 0; t0 < C; t0 += CS_TILE) {
+      const i64 b = t0 + (i64)threadIdx.x * 8;
+      u32 v[8];
+      u32 acc = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = b + j < C ? colp[b + j] : 0u;
+        acc += v[j];
+      }
+      u32 tot;
+      u32 run = carry + block_excl_scan<OpSum, u32>(acc, s, &tot);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (b + j < C) colp[b + j] = run;
+        run += v[j];
+      }
+      carry += tot;
+    }
+  }
+  if (threadIdx.x == 0) {
+    colp[C] = carry;  // prefix at the end of the branch (a window may start there)
+    atomicAdd((unsigned long long*)&meta->kcnt[k], (unsigned long long)carry);
+    if (k == KREN) meta->n_ren_side[side] = carry;
+    __threadfence();
+    if (atomicAdd((unsigned long long*)&meta->cs_done, 1ull) == (unsigned long long)gridDim.x - 1) {
+      __threadfence();
+      meta->n_win = nwin;
+      u64 acc = 0;
+      for (int kk = 0; kk < SMX_N_KINDS; ++kk) {
+        meta->base[kk] = acc;
+        acc += __hip_atomic_load(&meta->kcnt[kk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      meta->base[SMX_N_KINDS] = acc;
+    }
+  }
+}
+
 // Per-window counts: each kind and renames per branch (+ moves with a None value
 // in the generic layout).  Column-major [c][W].
 //  * presorted layout (perm == nullptr): branch position j is op j; only the kind
@@ -1783,7 +1835,9 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
                      C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na,
                      C.nb, W, tgt, cap / CH, bnd, meta, early ? early->flag_dev : nullptr);
   if (early) HIP_TRY(hipEventRecord(early->ev, st));
-  {
+  if (CM <= CS_SMALL_CM) {
+    hipLaunchKernelGGL(k_cscan_small, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, meta, (u64)W);
+  } else {
     const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);
     u32* tsum = C.ws<u32>(B_TSUM);
     hipLaunchKernelGGL(k_cscan_up, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT, tsum,
