@@ -477,7 +477,7 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
 // chunks with the next group's kind bytes loaded before the current group is counted,
 // counts branch-free, and publishes the kinds present once at its end.
 #ifndef KH_PERSIST
-#define KH_PERSIST 1
+#define KH_PERSIST 0  // off: config 3 plan 0.134 -> 0.151 ms with it (profiles/r04_h/ab_c3.txt)
 #endif
 #define KH_BLOCKS_PER_CU 4
 __device__ __forceinline__ void kh_load(const u8* __restrict__ kind, const u64* __restrict__ ts, i64 na, i64 nb,

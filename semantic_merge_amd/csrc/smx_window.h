@@ -218,7 +218,8 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #define WF_SMALL_TGT 256
 #endif
 #ifndef WF_SMALL_MAXN
-#define WF_SMALL_MAXN (1ll << 21)  // merges up to this many ops start with the small windows
+#define WF_SMALL_MAXN 0  // merges up to this many ops start with the small windows: off, config 2's
+                         // window stage 0.048 -> 0.218 ms with them (profiles/r04_h/ab_c2.txt)
 #endif
 #define WF_NCH (WF_CAP / WAVE)
 #define WF_WAVES (WF_NT / WAVE)

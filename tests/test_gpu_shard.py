@@ -426,7 +426,7 @@ def test_range_info_native_matches_reference_layout(na, nb, offb, order):
     from semantic_merge_amd._lib import lib
     from semantic_merge_amd.shard import RH
     rng = np.random.default_rng(na + nb + offb)
-    buf = np.zeros(offb + nb + 64, dtype=np.uint64)
+    buf = np.zeros(max(5 + na, offb + nb) + 64, dtype=np.uint64)
     a = np.sort(rng.integers(0, 2**64 - 1, na, dtype=np.uint64))
     b = np.sort(rng.integers(0, 2**64 - 1, nb, dtype=np.uint64))
     if not order and nb > 3:
