@@ -130,9 +130,28 @@ __device__ u32 walk_rank_next(const WalkArgs& W, int o, u64 x) {
     if (walk_side(W, m) == o && k-- == 0) return (u32)m;
 }
 
-// First rename of branch o at a local position >= from, else the halo.
+// First rename of branch o at a local position >= from, else the halo.  WALK_NEXT_VEC
+// sources are read per step, all in flight together (the scan usually ends within a
+// step: the branches' renames interleave), instead of one dependent load per position.
+#ifndef WALK_NEXT_VEC
+#define WALK_NEXT_VEC 8
+#endif
 __device__ __forceinline__ u32 walk_next(const WalkArgs& W, int o, u64 from) {
   u64 m = from;
+  if (WALK_NEXT_VEC > 1) {
+    static_assert(WALK_SCAN % (WALK_NEXT_VEC > 1 ? WALK_NEXT_VEC : 1) == 0, "whole steps");
+    for (int i = 0; i < WALK_SCAN; i += WALK_NEXT_VEC, m += WALK_NEXT_VEC) {
+      i32 js[WALK_NEXT_VEC > 1 ? WALK_NEXT_VEC : 1];
+#pragma unroll
+      for (int k = 0; k < WALK_NEXT_VEC; ++k) js[k] = m + k < W.nR ? W.tsrc[m + k] : 0;
+#pragma unroll
+      for (int k = 0; k < WALK_NEXT_VEC; ++k) {
+        if (m + k >= W.nR) return walk_halo(W, o, 0);
+        if (((u64)js[k] >= W.na_cap) == (o != 0)) return (u32)(m + k);
+      }
+    }
+    return walk_rank_next(W, o, m);
+  }
   for (int i = 0; i < WALK_SCAN; ++i, ++m) {
     if (m >= W.nR) return walk_halo(W, o, 0);
     if (walk_side(W, m) == o) return (u32)m;
