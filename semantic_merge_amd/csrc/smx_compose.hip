@@ -357,6 +357,9 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 #define KH_NT 512                  // 32 chunks per block: a column's counts fill a 128-byte line
 #endif
 #define CH_PER_BLOCK (KH_NT / 16)   // 16 lanes x 16 kind bytes per 256-op chunk
+#ifndef KH_BF
+#define KH_BF 1                    // branch-free byte counting (no per-byte early exit)
+#endif
 #ifndef KH_R
 #define KH_R 1                     // chunk rounds per block (4 measured slower: profiles/r02_k/khist_rounds_ab.txt)
 #endif
@@ -410,12 +413,13 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
     u32 pk[3] = {0u, 0u, 0u};  // kind k: bits 5 * (k % 6) of word k / 6
 #pragma unroll
     for (int y = 0; y < 16; ++y) {
-      if (y >= nv) break;
+      if (!KH_BF && y >= nv) break;
+      const bool ok = !KH_BF || y < nv;  // (branch-free: a lane past its chunk's end adds 0)
       u32 k = (w[rd][y >> 2] >> (8 * (y & 3))) & 0xffu;
-      bad |= k >= SMX_N_KINDS;
+      bad |= ok & (k >= SMX_N_KINDS);
       k = k < SMX_N_KINDS ? k : SMX_N_KINDS - 1;
       const u32 wd = (k * 43u) >> 8;  // k / 6 for k < 18
-      const u32 inc = 1u << (5u * (k - 6u * wd));
+      const u32 inc = ok ? 1u << (5u * (k - 6u * wd)) : 0u;
       pk[0] += wd == 0 ? inc : 0u;
       pk[1] += wd == 1 ? inc : 0u;
       pk[2] += wd == 2 ? inc : 0u;
