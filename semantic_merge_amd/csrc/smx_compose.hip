@@ -358,7 +358,7 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 #endif
 #define CH_PER_BLOCK (KH_NT / 16)   // 16 lanes x 16 kind bytes per 256-op chunk
 #ifndef KH_BF
-#define KH_BF 1                    // branch-free byte counting (no per-byte early exit)
+#define KH_BF 0                    // branch-free byte counting: plan 0.134 -> 0.137 ms (profiles/r04_k); off
 #endif
 #ifndef KH_R
 #define KH_R 1                     // chunk rounds per block (4 measured slower: profiles/r02_k/khist_rounds_ab.txt)

@@ -1253,7 +1253,23 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
   // The output phases' kernel arguments are read again here from the kernarg segment
   // (scalar loads through an opaque pointer): held from the kernel's start they were
   // spilled to VGPR lanes and reloaded one v_readlane each in these phases.
+#if WF_LATEARGS == 2
+  // only the eight output pointers re-read here (the rest of the arguments as loaded)
+  WinArgs Q = P;
+  {
+    const WinArgs* K = kernarg_late<WinArgs>();
+    Q.out_order = K->out_order;
+    Q.out_addr = K->out_addr;
+    Q.out_file = K->out_file;
+    Q.out_ctx = K->out_ctx;
+    Q.msym = K->msym;
+    Q.tsrc = K->tsrc;
+    Q.tsym = K->tsym;
+    Q.Rstr = K->Rstr;
+  }
+#else
   const WinArgs& Q = WF_LATEARGS ? *kernarg_late<WinArgs>() : P;
+#endif
   // 9. T-ordered records in final order (consecutive lanes -> consecutive T inside
   //    each kind: coalesced)
   const u64 nall = (u64)(Q.na + Q.nb);
