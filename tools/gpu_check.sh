@@ -7,7 +7,7 @@ STEPS=${*:-tests bench prof}
 R=$PWD; O=$R/gpurun_out/$TAG; mkdir -p "$O"
 for s in $STEPS; do
   case $s in
-    tests) timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
            tail -3 "$O/tests.log";;
     bench) timeout -k 10 300 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
            cat "$O/bench.json";;
