@@ -288,6 +288,132 @@ __global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* _
   }
 }
 
+// Two-byte list ids (257..65536 lists): the first pass partitions by the HIGH byte
+// (k_rrec_hist / k_rrec_scatter, stable), then one workgroup per high-byte bucket orders
+// its records by the low byte on its own (k_rrec_local): a count, a scan in LDS and a
+// stable scatter of tiles in stream order -- no global histogram, scan or bounds pass
+// (the bucket's list starts come from its scan), and no list ids written (the list
+// kernels read only the starts).  Bucket d is [dstart[d], dstart[d + 1]).
+#ifndef RGA_MSD
+#define RGA_MSD 1
+#endif
+#define RL_NT 1024
+#define RL_NW (RL_NT / WAVE)
+#define RL_ITEMS 4
+#define RL_TILE (RL_NT * RL_ITEMS)
+#define RL_SEG (RL_TILE / RL_NW)  // contiguous records per wave and tile
+#define RL_CU 8                   // count phase: keys in flight per lane
+#ifndef RL_PREFETCH
+#define RL_PREFETCH 0  // next tile loaded before the current one is written: slower (174 -> 285 us)
+#endif
+__global__ void __launch_bounds__(RL_NT) k_rrec_local(const u32* __restrict__ kin, const u64* __restrict__ rin,
+                                                      u64* __restrict__ rout,
+                                                      const u32* __restrict__ dstart, i64 nl,
+                                                      u32* __restrict__ lstart, u32* __restrict__ csum) {
+  __shared__ u32 cnt[RGA_NDIG];
+  __shared__ u32 run[RGA_NDIG];
+  __shared__ u16 wc[RL_NW][RGA_NDIG];
+  const u32 t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
+  const u32 d = blockIdx.x;
+  if (d == 0 && t < RGA_CS_MAX) csum[t] = 0u;  // (k_rga_bounds' other duty)
+  const u32 b0 = dstart[d], b1 = dstart[d + 1];
+  if (t < RGA_NDIG) cnt[t] = 0;
+  __syncthreads();
+  for (u32 i0 = b0 + t; i0 < b1; i0 += RL_NT * RL_CU) {  // RL_CU loads in flight per lane
+    u32 k[RL_CU];
+#pragma unroll
+    for (int j = 0; j < RL_CU; ++j) {
+      const u32 i = i0 + j * RL_NT;
+      k[j] = i < b1 ? kin[i] : ~0u;
+    }
+#pragma unroll
+    for (int j = 0; j < RL_CU; ++j)
+      if (i0 + j * RL_NT < b1) atomicAdd(&cnt[k[j] & 255u], 1u);
+  }
+  __syncthreads();
+  if (t < WAVE) {  // exclusive scan of the 256 low-byte counts, 4 per lane
+    u32 x[4], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[j] = cnt[4 * t + j];
+      sum += x[j];
+    }
+    u32 r = wave_incl_sum(sum) - sum;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      run[4 * t + j] = b0 + r;
+      r += x[j];
+    }
+  }
+  __syncthreads();
+  if (t < RGA_NDIG) {  // list starts (an empty list starts where the next one does)
+    const i64 l = (i64)d * RGA_NDIG + t;
+    if (l < nl) lstart[l] = run[t];
+  }
+  const u64 lt = lanemask_lt();
+  u32 key[RL_ITEMS], dr[RL_ITEMS];
+  u64 r0[RL_ITEMS], r1[RL_ITEMS];
+  auto load_tile = [&](u32 base) {
+#pragma unroll
+    for (int it = 0; it < RL_ITEMS; ++it) {
+      const u32 i = base + w * RL_SEG + it * WAVE + lane;
+      const bool valid = i < b1;
+      key[it] = valid ? kin[i] : 0u;
+      r0[it] = valid ? rin[(u64)i * RGA_REC] : 0ull;
+      r1[it] = valid ? rin[(u64)i * RGA_REC + 1] : 0ull;
+    }
+  };
+  if (b0 < b1) load_tile(b0);
+  for (u32 base = b0; base < b1; base += RL_TILE) {
+    for (u32 x = t; x < RL_NW * RGA_NDIG; x += RL_NT) (&wc[0][0])[x] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < RL_ITEMS; ++it) {
+      const u32 i = base + w * RL_SEG + it * WAVE + lane;
+      const bool valid = i < b1;
+      const u32 dd = key[it] & 255u;
+      const u64 peers = wave_peers<8>(dd, valid);
+      const u32 before = wc[w][dd];
+      dr[it] = dd | ((before + (u32)__popcll(peers & lt)) << 8);
+      if (valid && (peers >> lane) == 1ull) wc[w][dd] = (u16)(before + (u32)__popcll(peers));
+    }
+    __syncthreads();
+    if (t < RGA_NDIG) {  // per-wave offsets inside the digit's run of this tile
+      u32 acc = run[t];
+#pragma unroll
+      for (int q = 0; q < RL_NW; ++q) {
+        const u32 c = wc[q][t];
+        wc[q][t] = (u16)(acc - run[t]);
+        acc += c;
+      }
+      cnt[t] = acc;  // the run's next free position after this tile
+    }
+    __syncthreads();
+    u32 pk[RL_ITEMS];
+    u64 p0[RL_ITEMS], p1[RL_ITEMS];
+#pragma unroll
+    for (int it = 0; it < RL_ITEMS; ++it) {
+      const u32 dd = dr[it] & 255u;
+      pk[it] = run[dd] + wc[w][dd] + (dr[it] >> 8);
+      p0[it] = r0[it];
+      p1[it] = r1[it];
+    }
+    if (RL_PREFETCH && base + RL_TILE < b1) load_tile(base + RL_TILE);  // next tile in flight
+#pragma unroll
+    for (int it = 0; it < RL_ITEMS; ++it) {
+      const u32 i = base + w * RL_SEG + it * WAVE + lane;
+      if (i >= b1) continue;
+      const u32 pos = pk[it];
+      rout[(u64)pos * RGA_REC] = p0[it];
+      rout[(u64)pos * RGA_REC + 1] = p1[it];
+    }
+    __syncthreads();
+    if (t < RGA_NDIG) run[t] = cnt[t];
+    if (!RL_PREFETCH && base + RL_TILE < b1) load_tile(base + RL_TILE);
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ u32 rga_lend(const u32* lstart, u32 l, i64 nl, i64 n) {
   return l + 1 < nl ? lstart[l + 1] : (u32)n;
 }
@@ -409,8 +535,37 @@ __device__ __forceinline__ void wave_bitonic(u64 (&key)[8], u32 (&pay)[8], u32 l
   if constexpr (KK < 64u * K) wave_bitonic<K, KK * 2>(key, pay, lane);
 }
 
+// The same network over 64 * K packed 32-bit keys (rank fields above the event bits).
+template <int K, u32 KK, u32 J>
+__device__ __forceinline__ void wave_bitonic32_step(u32 (&key)[8], u32 lane) {
+  constexpr u32 mask = J == (KK >> 1) ? KK - 1 : J;
+  constexpr u32 lm = mask & 63u, sm = mask >> 6;
+  u32 nk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    u32 ok = key[k ^ (int)sm];
+    if (lm) ok = xshfl(ok, lm);
+    const bool lower = (((u32)k * 64u + lane) & J) == 0;
+    nk[k] = lower ? min(ok, key[k]) : max(ok, key[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) key[k] = nk[k];
+  if constexpr (J > 1) wave_bitonic32_step<K, KK, (J >> 1)>(key, lane);
+}
+
+template <int K, u32 KK = 2>
+__device__ __forceinline__ void wave_bitonic32(u32 (&key)[8], u32 lane) {
+  wave_bitonic32_step<K, KK, (KK >> 1)>(key, lane);
+  if constexpr (KK < 64u * K) wave_bitonic32<K, KK * 2>(key, lane);
+}
+
+#ifndef RW_PACK
+#define RW_PACK 1  // survivors' keys packed to 32 bits when the list's ranges allow (see rw_order)
+#endif
+
 template <int CAP>
 struct RwLds {
+  static constexpr int cap = CAP;
   // hash slots: one per event for k_rga_wave's lists (RW_HT1: 7.4 KB of LDS per list, five
   // waves per SIMD; a full table still terminates, every value finds its slot), two
   // per event otherwise
@@ -452,7 +607,49 @@ __device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, co
                                          u32 (&pay)[8], u32 m,
                                          u32 s0, u32 lane, u32* __restrict__ tmp_v, u32* __restrict__ tmp_s) {
   constexpr u32 N = 64u * K2;
-  wave_bitonic<K2>(key, pay, lane);
+  bool packed = false;
+#if RW_PACK
+  {  // word 0 = anchor << 32 | t's top half.  When the survivors' anchor and t ranges fit
+     // beside the event bits in 31 bits, sort (anchor - min, t - min, event) as one u32:
+     // one lane exchange and a min / max per step instead of three exchanges and selects.
+     // Equal packed fields <=> equal word 0, so the tie runs below are the same.
+    constexpr u32 PB = LDS::cap <= 256 ? 8 : 9;  // event bits
+    u32 amx = 0, anx = 0, tmx = 0, tnx = 0;
+#pragma unroll
+    for (int k = 0; k < K2; ++k)
+      if ((u32)k * 64u + lane < m) {
+        const u32 a = (u32)(key[k] >> 32), t = (u32)key[k];
+        amx = max(amx, a);
+        anx = max(anx, ~a);
+        tmx = max(tmx, t);
+        tnx = max(tnx, ~t);
+      }
+    amx = (u32)__builtin_amdgcn_readlane((int)wave_incl_max_u32(amx), WAVE - 1);
+    anx = (u32)__builtin_amdgcn_readlane((int)wave_incl_max_u32(anx), WAVE - 1);
+    tmx = (u32)__builtin_amdgcn_readlane((int)wave_incl_max_u32(tmx), WAVE - 1);
+    tnx = (u32)__builtin_amdgcn_readlane((int)wave_incl_max_u32(tnx), WAVE - 1);
+    const u32 amin = ~anx, tmin = ~tnx;
+    const u32 ba = 32u - (u32)__clz((int)(amx - amin)), bt = 32u - (u32)__clz((int)(tmx - tmin));
+    if (m > 0 && ba + bt + PB <= 31u) {
+      packed = true;
+      u32 pk[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pk[k] = ~0u;
+#pragma unroll
+      for (int k = 0; k < K2; ++k)
+        if ((u32)k * 64u + lane < m)
+          pk[k] = (((u32)(key[k] >> 32) - amin) << (bt + PB)) | (((u32)key[k] - tmin) << PB) | pay[k];
+      wave_bitonic32<K2>(pk, lane);
+#pragma unroll
+      for (int k = 0; k < K2; ++k) {
+        const bool v = (u32)k * 64u + lane < m;
+        key[k] = v ? (u64)(pk[k] >> PB) : ~0ull;
+        pay[k] = v ? pk[k] & ((1u << PB) - 1u) : RW_DEAD;
+      }
+    }
+  }
+#endif
+  if (!packed) wave_bitonic<K2>(key, pay, lane);
 #pragma unroll
   for (int k = 0; k < K2; ++k) {
     const u32 q = (u32)k * 64u + lane;
@@ -969,6 +1166,16 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
     u32* dstart = tsum + hscan_tsum_bytes(nblk, 256) / 4;
     u64* rbuf[2] = {npass % 2 ? rec : rec2, npass % 2 ? rec2 : rec};
     u32* kbuf[2] = {keys, keys2};
+    if (RGA_MSD && npass == 2) {  // high byte by the global pass, low byte per bucket
+      hipLaunchKernelGGL(k_rrec_hist<true>, dim3(nblk), dim3(BLOCK), 0, st, o, nullptr, 8, rhist, err);
+      hscan(rhist, nblk, 256u, tsum, dstart, st);
+      const int sgrid = nblk < g_rr_grid ? nblk : g_rr_grid;
+      hipLaunchKernelGGL(k_rrec_scatter<true>, dim3(sgrid), dim3(RR_NT), 0, st, o, nullptr, nullptr, keys2, rec2,
+                         8, rhist, err, (u32)nblk);
+      hipLaunchKernelGGL(k_rrec_local, dim3(RGA_NDIG), dim3(RL_NT), 0, st, keys2, rec2, rec, dstart, nl,
+                         lstart, scnt - RGA_CS_MAX);
+      npass = 0;  // (done: rec holds the list-ordered records, lstart their starts)
+    }
     for (int p = 0; p < npass; ++p) {
       if (p == 0)
         hipLaunchKernelGGL(k_rrec_hist<true>, dim3(nblk), dim3(BLOCK), 0, st, o, nullptr, 0, rhist, err);
@@ -984,8 +1191,9 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
         hipLaunchKernelGGL(k_rrec_scatter<false>, dim3(sgrid), dim3(RR_NT), 0, st, o, kbuf[(p - 1) & 1],
                            rbuf[(p - 1) & 1], kbuf[p & 1], rbuf[p & 1], 8 * p, rhist, err, (u32)nblk);
     }
-    hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, kbuf[(npass - 1) & 1], n, nl, lstart,
-                       scnt - RGA_CS_MAX);
+    if (npass)
+      hipLaunchKernelGGL(k_rga_bounds, dim3(grid), dim3(BLOCK), 0, st, kbuf[(npass - 1) & 1], n, nl, lstart,
+                         scnt - RGA_CS_MAX);
   }
   const int tomb = out->out_tomb != nullptr;
   hipLaunchKernelGGL(k_rga_wave, dim3(SMX_CEIL_DIV(nl, (i64)RW_WAVES)), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n,

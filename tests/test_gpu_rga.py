@@ -182,3 +182,36 @@ def test_rga_lists_at_capacity_all_values_distinct():
     b.list_id = lid.astype(np.uint32)
     b.value = np.arange(lid.size, dtype=np.uint32)  # distinct everywhere (first-seen order)
     _check(b)
+
+
+def test_rga_key_ranges_packed_and_wide_sorts():
+    """The list kernels sort survivors on 32-bit packed keys when a list's anchor and t
+    ranges fit beside the event bits (31 bits in all), on 64-bit keys otherwise: lists on
+    both sides of that line, full-range signed t, 32-bit anchors, and equal top halves
+    of t (ties on word 0 resolved by the full key)."""
+    b = synth.rga_batch(400_000, 2_000, 21)
+    rng = np.random.default_rng(21)
+    lid = b.list_id.astype(np.int64)
+    n = lid.size
+    reg = lid % 6
+    t = b.t.copy()
+    anchor = b.anchor.astype(np.int64)
+    full_t = rng.integers(-(1 << 63), (1 << 63) - 1, size=n, dtype=np.int64, endpoint=True)
+    t = np.where(reg == 0, full_t, t)
+    anchor = np.where(reg == 1, rng.integers(0, 1 << 32, size=n, dtype=np.int64), anchor)
+    low = rng.integers(0, 1 << 32, size=n, dtype=np.int64)
+    # 11 anchor bits + 12 t bits + 8 event bits = 31 (packed); 11 + 13 + 8 = 32 (64-bit keys)
+    for r, tb in ((2, 12), (3, 13)):
+        sel = reg == r
+        a = np.where(rng.random(n) < 0.5, 0, (1 << 11) - 1)
+        hi = rng.integers(0, 1 << tb, size=n, dtype=np.int64)
+        hi = np.where(rng.random(n) < 0.1, (1 << tb) - 1, hi)
+        anchor = np.where(sel, a + 5, anchor)
+        t = np.where(sel, (hi << 32) | low, t)
+    # equal top halves of t inside a list: word-0 ties broken by the low half, author, opid
+    sel = reg == 4
+    t = np.where(sel, (rng.integers(0, 3, size=n, dtype=np.int64) << 32) | low, t)
+    anchor = np.where(sel, anchor % 2, anchor)
+    b.t = t
+    b.anchor = anchor.astype(np.uint32)
+    _check(b)
