@@ -143,9 +143,9 @@ __device__ __forceinline__ void rrec_load(RTile<FIRST>& T, const smx_rga_ops& o,
 // records staged in LDS in digit order, then every digit's run written contiguously
 // (RREC_TILE / 256 records per run on average: whole cache lines).  The next tile's
 // loads are issued before the current tile's runs are written, so the two overlap.
-template <bool FIRST>
+template <bool FIRST, typename KO = u32>
 __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32* __restrict__ kin,
-                                                        const u64* __restrict__ rin, u32* __restrict__ kout,
+                                                        const u64* __restrict__ rin, KO* __restrict__ kout,
                                                         u64* __restrict__ rout, int shift,
                                                         const u32* __restrict__ offs, i32* __restrict__ err,
                                                         u32 ntiles) {
@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
 #pragma unroll 1
     for (u32 p = t; p < cnt; p += RR_NT) {
       const u32 d = (skey[p] >> shift) & 255u;
-      kout[gofs[d] + p - lstart[d]] = skey[p];
+      kout[gofs[d] + p - lstart[d]] = (KO)skey[p];  // (u8: the low byte, for k_rrec_local)
     }
 #pragma unroll 1
     for (u32 x = t; x < cnt * RGA_REC; x += RR_NT) {  // word-wise: consecutive lanes, consecutive words
@@ -276,6 +276,9 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
 #define RGA_CS_LISTS 256                   // lists per survivor-sum chunk
 #define RGA_CS_MAX 256                     // chunks (k_rga_out: one uint4 per lane)
 #define RGA_FUSED_MAX (RGA_CS_LISTS * RGA_CS_MAX)  // lists up to which k_rga_out finds its own offsets
+#ifndef RGA_OUT_PRE
+#define RGA_OUT_PRE 2
+#endif
 __global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* __restrict__ lstart,
                              u32* __restrict__ csum) {
   if (blockIdx.x == 0 && threadIdx.x < RGA_CS_MAX) csum[threadIdx.x] = 0u;
@@ -295,18 +298,20 @@ __global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* _
 // (the bucket's list starts come from its scan), and no list ids written (the list
 // kernels read only the starts).  Bucket d is [dstart[d], dstart[d + 1]).
 #ifndef RGA_MSD
-#define RGA_MSD 1
+#define RGA_MSD 1  // 0: LSD passes (k_rrec_hist / k_rrec_scatter twice, k_rga_bounds)
 #endif
 #define RL_NT 1024
 #define RL_NW (RL_NT / WAVE)
+#ifndef RL_ITEMS
 #define RL_ITEMS 4
+#endif
 #define RL_TILE (RL_NT * RL_ITEMS)
 #define RL_SEG (RL_TILE / RL_NW)  // contiguous records per wave and tile
 #define RL_CU 8                   // count phase: keys in flight per lane
-#ifndef RL_PREFETCH
-#define RL_PREFETCH 0  // next tile loaded before the current one is written: slower (174 -> 285 us)
-#endif
-__global__ void __launch_bounds__(RL_NT) k_rrec_local(const u32* __restrict__ kin, const u64* __restrict__ rin,
+struct __attribute__((aligned(16))) R16 {
+  u64 a, b;
+};
+__global__ void __launch_bounds__(RL_NT) k_rrec_local(const u8* __restrict__ kin, const u64* __restrict__ rin,
                                                       u64* __restrict__ rout,
                                                       const u32* __restrict__ dstart, i64 nl,
                                                       u32* __restrict__ lstart, u32* __restrict__ csum) {
@@ -319,16 +324,27 @@ __global__ void __launch_bounds__(RL_NT) k_rrec_local(const u32* __restrict__ ki
   const u32 b0 = dstart[d], b1 = dstart[d + 1];
   if (t < RGA_NDIG) cnt[t] = 0;
   __syncthreads();
-  for (u32 i0 = b0 + t; i0 < b1; i0 += RL_NT * RL_CU) {  // RL_CU loads in flight per lane
-    u32 k[RL_CU];
+  {  // 4 low bytes per load (aligned words over [b0, b1); the buffer has room past n)
+    const u32* kw = reinterpret_cast<const u32*>(kin);
+    const u32 w0 = b0 >> 2, w1 = (b1 + 3) >> 2;
+    for (u32 x0 = w0 + t; x0 < w1; x0 += RL_NT * RL_CU) {  // RL_CU loads in flight per lane
+      u32 k[RL_CU];
 #pragma unroll
-    for (int j = 0; j < RL_CU; ++j) {
-      const u32 i = i0 + j * RL_NT;
-      k[j] = i < b1 ? kin[i] : ~0u;
+      for (int j = 0; j < RL_CU; ++j) {
+        const u32 x = x0 + j * RL_NT;
+        k[j] = x < w1 ? kw[x] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < RL_CU; ++j) {
+        const u32 x = x0 + j * RL_NT;
+        if (x >= w1) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const u32 i = 4 * x + q;
+          if (i >= b0 && i < b1) atomicAdd(&cnt[(k[j] >> (8 * q)) & 255u], 1u);
+        }
+      }
     }
-#pragma unroll
-    for (int j = 0; j < RL_CU; ++j)
-      if (i0 + j * RL_NT < b1) atomicAdd(&cnt[k[j] & 255u], 1u);
   }
   __syncthreads();
   if (t < WAVE) {  // exclusive scan of the 256 low-byte counts, 4 per lane
@@ -351,66 +367,66 @@ __global__ void __launch_bounds__(RL_NT) k_rrec_local(const u32* __restrict__ ki
     if (l < nl) lstart[l] = run[t];
   }
   const u64 lt = lanemask_lt();
-  u32 key[RL_ITEMS], dr[RL_ITEMS];
-  u64 r0[RL_ITEMS], r1[RL_ITEMS];
-  auto load_tile = [&](u32 base) {
-#pragma unroll
-    for (int it = 0; it < RL_ITEMS; ++it) {
-      const u32 i = base + w * RL_SEG + it * WAVE + lane;
-      const bool valid = i < b1;
-      key[it] = valid ? kin[i] : 0u;
-      r0[it] = valid ? rin[(u64)i * RGA_REC] : 0ull;
-      r1[it] = valid ? rin[(u64)i * RGA_REC + 1] : 0ull;
-    }
-  };
-  if (b0 < b1) load_tile(b0);
+  // the tile's records staged in LDS in (low byte, stream) order, then written run by
+  // run: consecutive lanes store consecutive 16-byte records of one list
+  __shared__ R16 stg[RL_TILE];
+  __shared__ u8 sdig[RL_TILE];
+  __shared__ u32 tstart[RGA_NDIG], wsum[RGA_NDIG / WAVE];
   for (u32 base = b0; base < b1; base += RL_TILE) {
     for (u32 x = t; x < RL_NW * RGA_NDIG; x += RL_NT) (&wc[0][0])[x] = 0;
     __syncthreads();
+    u32 dr[RL_ITEMS];
+    R16 rv[RL_ITEMS];
 #pragma unroll
     for (int it = 0; it < RL_ITEMS; ++it) {
       const u32 i = base + w * RL_SEG + it * WAVE + lane;
       const bool valid = i < b1;
-      const u32 dd = key[it] & 255u;
+      const u32 dd = (valid ? kin[i] : 0u) & 255u;
+      rv[it].a = valid ? rin[(u64)i * RGA_REC] : 0ull;
+      rv[it].b = valid ? rin[(u64)i * RGA_REC + 1] : 0ull;
       const u64 peers = wave_peers<8>(dd, valid);
       const u32 before = wc[w][dd];
       dr[it] = dd | ((before + (u32)__popcll(peers & lt)) << 8);
       if (valid && (peers >> lane) == 1ull) wc[w][dd] = (u16)(before + (u32)__popcll(peers));
     }
     __syncthreads();
-    if (t < RGA_NDIG) {  // per-wave offsets inside the digit's run of this tile
-      u32 acc = run[t];
+    u32 tc = 0, inc = 0;
+    if (t < RGA_NDIG) {  // per-wave offsets inside the digit's share of the tile
 #pragma unroll
       for (int q = 0; q < RL_NW; ++q) {
         const u32 c = wc[q][t];
-        wc[q][t] = (u16)(acc - run[t]);
-        acc += c;
+        wc[q][t] = (u16)tc;
+        tc += c;
       }
-      cnt[t] = acc;  // the run's next free position after this tile
+      inc = wave_incl_sum(tc);
+      if (lane == WAVE - 1) wsum[w] = inc;
     }
     __syncthreads();
-    u32 pk[RL_ITEMS];
-    u64 p0[RL_ITEMS], p1[RL_ITEMS];
-#pragma unroll
-    for (int it = 0; it < RL_ITEMS; ++it) {
-      const u32 dd = dr[it] & 255u;
-      pk[it] = run[dd] + wc[w][dd] + (dr[it] >> 8);
-      p0[it] = r0[it];
-      p1[it] = r1[it];
+    if (t < RGA_NDIG) {
+      u32 ex = inc - tc;
+      for (u32 q = 0; q < w; ++q) ex += wsum[q];
+      tstart[t] = ex;
+      cnt[t] = tc;
     }
-    if (RL_PREFETCH && base + RL_TILE < b1) load_tile(base + RL_TILE);  // next tile in flight
+    __syncthreads();
 #pragma unroll
     for (int it = 0; it < RL_ITEMS; ++it) {
       const u32 i = base + w * RL_SEG + it * WAVE + lane;
       if (i >= b1) continue;
-      const u32 pos = pk[it];
-      rout[(u64)pos * RGA_REC] = p0[it];
-      rout[(u64)pos * RGA_REC + 1] = p1[it];
+      const u32 dd = dr[it] & 255u;
+      const u32 slot = tstart[dd] + wc[w][dd] + (dr[it] >> 8);
+      stg[slot] = rv[it];
+      sdig[slot] = (u8)dd;
     }
     __syncthreads();
-    if (t < RGA_NDIG) run[t] = cnt[t];
-    if (!RL_PREFETCH && base + RL_TILE < b1) load_tile(base + RL_TILE);
+    const u32 nv = min((u32)RL_TILE, b1 - base);
+    for (u32 j = t; j < nv; j += RL_NT) {
+      const u32 dd = sdig[j];
+      const u32 pos = run[dd] + (j - tstart[dd]);
+      *(R16*)(rout + (u64)pos * RGA_REC) = stg[j];
+    }
     __syncthreads();
+    if (t < RGA_NDIG) run[t] += cnt[t];
   }
 }
 
@@ -457,9 +473,14 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
 //     the rest of the key and the index (crdt.py:45-57).
 #define RW_CAP 256   // k_rga_wave; the deferred lists' kernel takes up to 2 * RW_CAP
 #define RW_WAVES 2   // lists per block
+#ifndef RW_PER_CU
+#define RW_PER_CU 16  // k_rga_wave workgroups per CU (persistent; 0: one wave per list)
+#endif
 #define RW_EMPTY 0xffffffffu
 #define RW_NIL 0xffffu
 #define RW_DEAD 0x400u
+#define RW_MOP 12       // member entries: event | op << RW_MOP
+#define RW_MEV 0xfffu
 #ifndef RW_HT1
 #define RW_HT1 1
 #endif
@@ -470,6 +491,20 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
 #define RW_HT u16
 #else
 #define RW_HT u32
+#endif
+#ifndef RW_OCC_W
+#define RW_OCC_W 8  // k_rga_wave: registers for this many waves per SIMD (0: compiler's choice)
+#endif
+#if RW_OCC_W
+#define RW_OCC __attribute__((amdgpu_waves_per_eu(RW_OCC_W, RW_OCC_W)))
+#else
+#define RW_OCC
+#endif
+#ifndef RW_LAUNDER
+#define RW_LAUNDER 1
+#endif
+#ifndef RW_MGP_UNION
+#define RW_MGP_UNION 1  // mem / gp share LDS: 9.5 KB per two-list workgroup, 16 per CU
 #endif
 #ifndef RW_W0G
 #define RW_W0G 1  // key word 0 read from the list's records in L2, not held in LDS: 2 KB less per list, more lists per CU
@@ -582,8 +617,14 @@ struct RwLds {
     } h;
     u64 gs[CAP];        // step 3: survivors' word 0, sorted
   };
-  u16 mem[CAP];         // group members, group by group, each in event order
-  u16 gp[CAP];          // step 3: survivors' events, sorted
+#if RW_MGP_UNION
+  union {               // (mem is dead once the groups are replayed)
+#else
+  struct {
+#endif
+    u16 mem[CAP];       // group members, group by group, each in event order (| op << RW_MOP)
+    u16 gp[CAP];        // step 3: survivors' events, sorted
+  };
   u8 st[CAP];           // bit0 present, bit1 tombstoned
 };
 
@@ -722,12 +763,12 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
     if (lane == 0) rga_put_count(scnt, l, (u32)S.wv[lane] & 1u);
     return;
   }
-  const u64 lt = lanemask_lt();
+  const u64 lt = lane ? ~0ull >> (WAVE - lane) : 0ull;  // (from `lane`: see k_rga_wave)
   constexpr int HB = RwLds<CAP>::HT == 256 ? 8 : RwLds<CAP>::HT == 512 ? 9 : 10;  // log2 of the hash slots
   static_assert(RwLds<CAP>::HT == 1 << HB, "hash slots");
-  u32 slot[8], rk[8];
+  u32 slot[8], rk[8], opk[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) slot[k] = rk[k] = 0;
+  for (int k = 0; k < 8; ++k) slot[k] = rk[k] = opk[k] = 0;
   if (RW_ABL & 2) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -743,7 +784,9 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
       const u32 e = (u32)k * 64u + lane;
       S.st[e] = 0;
       if (e < cnt) {
-        const u32 v = (u32)(S.wv[e] >> 32);
+        const u64 wv = S.wv[e];
+        const u32 v = (u32)(wv >> 32);
+        opk[k] = (u32)(wv >> 30) & 3u;
         u32 h = (v * 0x9E3779B1u) >> (32 - HB);
         for (;;) {
           const u32 old = atomicCAS(&S.h.hkey[h], RW_EMPTY, v);
@@ -784,7 +827,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const u32 e = (u32)k * 64u + lane;
-      if (e < cnt) S.mem[S.h.hbase[slot[k]] + rk[k]] = (u16)e;
+      if (e < cnt) S.mem[S.h.hbase[slot[k]] + rk[k]] = (u16)(e | opk[k] << RW_MOP);  // event, op
     }
     wave_lds_sync();
     // 2. the group's first event's lane replays the group in event order (crdt.py:29-43)
@@ -794,25 +837,48 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
       if (e >= cnt || rk[k] != 0) continue;
       const u32 b = S.h.hbase[slot[k]], c = S.h.hcnt[slot[k]];
       if (c == 1 || (RW_ABL & 1)) {
-        S.st[e] = ((u32)(S.wv[e] >> 30) & 3u) != 2;
+        S.st[e] = opk[k] != 2;
         continue;
       }
       for (u32 i = 0; i < c; ++i) {
-        const u32 x = S.mem[b + i];
-        const u32 op = (u32)(S.wv[x] >> 30) & 3u;
+        const u32 xm = S.mem[b + i];
+        const u32 x = xm & RW_MEV, op = xm >> RW_MOP;
         if (op == 2) {  // delete: every present element is tombstoned; creates nothing
           for (u32 j = 0; j < i; ++j) {
-            const u32 y = S.mem[b + j];
+            const u32 y = S.mem[b + j] & RW_MEV;
             if (S.st[y] & 1) S.st[y] |= 2;
           }
           continue;
         }
         if (op == 1) {  // move: pops the live element first in list order
           u32 best = RW_NIL;
+#if RW_W0G
+          u64 wb = 0;  // best's word 0: read when a second candidate shows up, then kept
+          bool wbl = false;
           for (u32 j = 0; j < i; ++j) {
-            const u32 y = S.mem[b + j];
+            const u32 y = S.mem[b + j] & RW_MEV;
+            if (S.st[y] != 1) continue;
+            if (best == RW_NIL) {
+              best = y;
+              continue;
+            }
+            if (!wbl) {
+              wb = src[(u64)best * RGA_REC];
+              wbl = true;
+            }
+            const u64 wy = src[(u64)y * RGA_REC];
+            if (wy < wb ||
+                (wy == wb && rga_key_lt(o, (u32)S.wv[y] & RGA_IDX_MASK, (u32)S.wv[best] & RGA_IDX_MASK))) {
+              best = y;
+              wb = wy;
+            }
+          }
+#else
+          for (u32 j = 0; j < i; ++j) {
+            const u32 y = S.mem[b + j] & RW_MEV;
             if (S.st[y] == 1 && (best == RW_NIL || ev_lt(S, src, o, y, best))) best = y;
           }
+#endif
           if (best != RW_NIL) S.st[best] = 0;
         }
         S.st[x] = 1;
@@ -869,50 +935,62 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
   if (lane == 0) rga_put_count(scnt, l, m);
 }
 
-__global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave(smx_rga_ops o, const u64* __restrict__ R,
+__global__ void __launch_bounds__(WAVE * RW_WAVES) RW_OCC k_rga_wave(smx_rga_ops o, const u64* __restrict__ R,
                                                              const u32* __restrict__ lstart,
-                                                             i64 n, i64 nl, u32* __restrict__ defer,
-                                                             u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
+                                                             i64 n, i64 nl, u32* __restrict__ tmp_v,
                                                              u32* __restrict__ tmp_s, u32* __restrict__ scnt,
                                                              int tomb) {
   __shared__ RwLds<RW_CAP> lds[RW_WAVES];
-  const u32 lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-  const u32 l = blockIdx.x * RW_WAVES + w;
-  if (l >= (u64)nl) return;
-  const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
-  if (cnt > RW_CAP) {
-    if (lane == 0) defer[atomicAdd(ndefer, 1u)] = l;
-    return;
+  const u32 lane = threadIdx.x & (WAVE - 1);
+  // the wave index as a scalar: the list index, its bounds and the slice base stay in
+  // SGPRs (scalar loads of lstart; LDS member offsets fold into the instructions)
+  const u32 w = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+  // persistent (RW_PER_CU workgroups per CU): each wave takes every (grid)-th list
+  for (u64 ll = (u64)blockIdx.x * RW_WAVES + w; ll < (u64)nl; ll += (u64)gridDim.x * RW_WAVES) {
+    const u32 l = (u32)ll;
+    const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
+    if (cnt > RW_CAP) continue;  // k_rga_wave2 / k_rga_big
+    // the lane id laundered per list: otherwise the compiler hoists every lane-derived
+    // constant of the list code out of the loop and keeps it live
+    u32 ln = lane;
+    if (RW_LAUNDER) asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    if (cnt <= 64)
+      rga_wave_list<1>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+    else if (cnt <= 128)
+      rga_wave_list<2>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+    else
+      rga_wave_list<4>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+    wave_lds_sync();  // the next list reuses the slice
   }
-  if (cnt <= 64)
-    rga_wave_list<1>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
-  else if (cnt <= 128)
-    rga_wave_list<2>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
-  else
-    rga_wave_list<4>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
 }
 
-// The deferred lists of RW_CAP + 1 .. 2 * RW_CAP events: the same wave per list with
-// twice the slots; longer ones go on to k_rga_big.
+// Lists of RW_CAP + 1 .. 2 * RW_CAP events: the same wave per list with twice the
+// slots; longer ones go on to k_rga_big.  Each wave sweeps 64 lists at a time for the
+// long ones itself (k_rga_wave skips them; no hand-off list).
 __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(smx_rga_ops o, const u64* __restrict__ R,
                                                               const u32* __restrict__ lstart,
-                                                              i64 n, i64 nl, const u32* __restrict__ todo,
-                                                              const u32* __restrict__ ntodo, u32* __restrict__ defer,
+                                                              i64 n, i64 nl, u32* __restrict__ defer,
                                                               u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
                                                               u32* __restrict__ tmp_s, u32* __restrict__ scnt,
                                                               int tomb) {
   __shared__ RwLds<2 * RW_CAP> lds[RW_WAVES];
   const u32 lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-  const u32 nt = *ntodo;
-  for (u32 i = blockIdx.x * RW_WAVES + w; i < nt; i += gridDim.x * RW_WAVES) {
-    const u32 l = todo[i];
-    const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
-    if (cnt > 2 * RW_CAP) {
-      if (lane == 0) defer[atomicAdd(ndefer, 1u)] = l;
-      continue;
+  const u64 nw = (u64)gridDim.x * RW_WAVES;
+  for (u64 l0 = ((u64)blockIdx.x * RW_WAVES + w) * WAVE; l0 < (u64)nl; l0 += nw * WAVE) {
+    const u64 me = l0 + lane;
+    const u32 c = me < (u64)nl ? rga_lend(lstart, (u32)me, nl, n) - lstart[me] : 0u;
+    u64 todo = __ballot(c > RW_CAP);
+    while (todo) {
+      const u32 l = (u32)(l0 + (u64)(__ffsll((unsigned long long)todo) - 1));
+      todo &= todo - 1;
+      const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
+      if (cnt > 2 * RW_CAP) {
+        if (lane == 0) defer[atomicAdd(ndefer, 1u)] = l;
+        continue;
+      }
+      rga_wave_list<8>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
+      wave_lds_sync();  // the next list reuses the slice
     }
-    rga_wave_list<8>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
-    wave_lds_sync();  // the next list reuses the slice
   }
 }
 
@@ -1023,18 +1101,34 @@ __global__ void __launch_bounds__(BLOCK) k_rga_out_fused(const u32* __restrict__
                                                         const u32* __restrict__ lstart, const u32* __restrict__ scnt,
                                                         i64 nl, smx_rga_out out) {
   const u32 lane = threadIdx.x & (WAVE - 1);
-  const i64 l = (i64)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE;
+  const i64 l = (i64)blockIdx.x * (BLOCK / WAVE) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));  // (scalar)
   if (l >= nl) return;
   const u32 c = (u32)l / RGA_CS_LISTS, c0 = c * RGA_CS_LISTS;
   const uint4 cs = reinterpret_cast<const uint4*>(scnt - RGA_CS_MAX)[lane];
   const uint4 ls = reinterpret_cast<const uint4*>(scnt + c0)[lane];
+  const u32 s0 = lstart[l], m = scnt[l];
+  // the first RGA_OUT_PRE * 64 survivors are read before the offset is known
+  u32 pv[RGA_OUT_PRE], ps[RGA_OUT_PRE];
+#pragma unroll
+  for (int j = 0; j < RGA_OUT_PRE; ++j) {
+    const u32 x = lane + (u32)j * WAVE;
+    pv[j] = x < m ? __builtin_nontemporal_load(&tmp_v[s0 + x]) : 0u;
+    ps[j] = x < m ? __builtin_nontemporal_load(&tmp_s[s0 + x]) : 0u;
+  }
   const u32 q = 4 * lane;
   u32 part = (q < c ? cs.x : 0u) + (q + 1 < c ? cs.y : 0u) + (q + 2 < c ? cs.z : 0u) + (q + 3 < c ? cs.w : 0u);
   const u32 r = (u32)l - c0;
   part += (q < r ? ls.x : 0u) + (q + 1 < r ? ls.y : 0u) + (q + 2 < r ? ls.z : 0u) + (q + 3 < r ? ls.w : 0u);
   const u32 d = (u32)__builtin_amdgcn_readlane((int)wave_incl_sum_u32(part), WAVE - 1);
-  const u32 s0 = lstart[l], m = scnt[l];
-  for (u32 x = lane; x < m; x += WAVE) {
+#pragma unroll
+  for (int j = 0; j < RGA_OUT_PRE; ++j) {
+    const u32 x = lane + (u32)j * WAVE;
+    if (x >= m) break;
+    out.out_value[d + x] = pv[j];
+    out.out_src[d + x] = (i32)(ps[j] & ~RGA_TOMB_BIT);
+    if (out.out_tomb) out.out_tomb[d + x] = ps[j] & RGA_TOMB_BIT ? 1 : 0;
+  }
+  for (u32 x = lane + RGA_OUT_PRE * WAVE; x < m; x += WAVE) {
     out.out_value[d + x] = __builtin_nontemporal_load(&tmp_v[s0 + x]);
     const u32 sx = __builtin_nontemporal_load(&tmp_s[s0 + x]);
     out.out_src[d + x] = (i32)(sx & ~RGA_TOMB_BIT);
@@ -1050,6 +1144,7 @@ __global__ void __launch_bounds__(BLOCK) k_rga_out_fused(const u32* __restrict__
 }
 
 // Per list (one wave each): its survivors, in list order, to their place in the output.
+// (k_rga_out_fused: RGA_OUT_PRE loads per lane issued with the offset's loads)
 __global__ void __launch_bounds__(BLOCK) k_rga_out(const u32* __restrict__ tmp_v, const u32* __restrict__ tmp_s,
                                                   const u32* __restrict__ lstart, const u32* __restrict__ scnt,
                                                   const u32* __restrict__ soff, i64 nl, smx_rga_out out) {
@@ -1072,6 +1167,7 @@ __global__ void k_rga_fin(const u32* __restrict__ soff_total, i64 n_lists, smx_r
 }
 
 static int g_rr_grid = 0;  // persistent scatter grid (RR_PER_CU per CU of the device)
+static int g_cus = 256;
 
 static bool o_ok(const smx_rga_ops* o) {
   return o->list && o->op && o->value && o->anchor && o->t && o->author && o->opid_hi && o->opid_lo;
@@ -1082,7 +1178,7 @@ struct RgaLayout {
   size_t total;
 };
 
-enum { R_REC, R_REC2, R_KEYS, R_KEYS2, R_RHIST, R_TV, R_TS, R_BST, R_GP, R_DEF1, R_DEF2, R_PART, R_LSTART, R_SCNT, R_SOFF, R_N };
+enum { R_REC, R_REC2, R_KEYS, R_KEYS2, R_RHIST, R_TV, R_TS, R_BST, R_GP, R_DEF2, R_PART, R_LSTART, R_SCNT, R_SOFF, R_N };
 
 static RgaLayout rga_layout(i64 n, i64 nl) {
   const i64 nn = n > 0 ? n : 1;
@@ -1095,7 +1191,7 @@ static RgaLayout rga_layout(i64 n, i64 nl) {
   }
   sz[R_BST] = (size_t)nn;
   sz[R_PART] = SCAN_NB * 8 + 64;  // + error word + totals
-  sz[R_LSTART] = sz[R_SOFF] = sz[R_DEF1] = sz[R_DEF2] = (size_t)(nl + 1) * 4;
+  sz[R_LSTART] = sz[R_SOFF] = sz[R_DEF2] = (size_t)(nl + 1) * 4;
   // scnt: RGA_CS_MAX chunk sums, then the counts padded to whole 256-list chunks
   sz[R_SCNT] = (size_t)(RGA_CS_MAX + SMX_CEIL_DIV(nl + 1, (i64)RGA_CS_LISTS) * RGA_CS_LISTS) * 4;
   RgaLayout L;
@@ -1145,9 +1241,8 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   u32* lstart = (u32*)(b + L.off[R_LSTART]);
   u32* scnt = (u32*)(b + L.off[R_SCNT]) + RGA_CS_MAX;  // (the chunk sums before it)
   u32* soff = (u32*)(b + L.off[R_SOFF]);
-  u32* def1 = (u32*)(b + L.off[R_DEF1]);
   u32* def2 = (u32*)(b + L.off[R_DEF2]);
-  u32* ndef = (u32*)(err + 4);  // two deferred-list counters
+  u32* ndef = (u32*)(err + 4);  // (ndef[1]: lists for k_rga_big)
   const smx_rga_ops o = *ops;
   const int grid = (int)(SMX_CEIL_DIV(n, (i64)BLOCK) < 8192 ? SMX_CEIL_DIV(n, (i64)BLOCK) : 8192);
 
@@ -1156,7 +1251,8 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
     int dev = 0, cus = 0;
     RGA_TRY(hipGetDevice(&dev));
     RGA_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    g_rr_grid = (cus > 0 ? cus : 256) * RR_PER_CU;
+    g_cus = cus > 0 ? cus : 256;
+    g_rr_grid = g_cus * RR_PER_CU;
   }
   {  // records grouped by list: LSD passes over the list id, ping-pong into rec
     int npass = 1;
@@ -1170,9 +1266,9 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
       hipLaunchKernelGGL(k_rrec_hist<true>, dim3(nblk), dim3(BLOCK), 0, st, o, nullptr, 8, rhist, err);
       hscan(rhist, nblk, 256u, tsum, dstart, st);
       const int sgrid = nblk < g_rr_grid ? nblk : g_rr_grid;
-      hipLaunchKernelGGL(k_rrec_scatter<true>, dim3(sgrid), dim3(RR_NT), 0, st, o, nullptr, nullptr, keys2, rec2,
-                         8, rhist, err, (u32)nblk);
-      hipLaunchKernelGGL(k_rrec_local, dim3(RGA_NDIG), dim3(RL_NT), 0, st, keys2, rec2, rec, dstart, nl,
+      hipLaunchKernelGGL((k_rrec_scatter<true, u8>), dim3(sgrid), dim3(RR_NT), 0, st, o, nullptr, nullptr, (u8*)keys2,
+                         rec2, 8, rhist, err, (u32)nblk);
+      hipLaunchKernelGGL(k_rrec_local, dim3(RGA_NDIG), dim3(RL_NT), 0, st, (const u8*)keys2, rec2, rec, dstart, nl,
                          lstart, scnt - RGA_CS_MAX);
       npass = 0;  // (done: rec holds the list-ordered records, lstart their starts)
     }
@@ -1196,10 +1292,16 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
                          scnt - RGA_CS_MAX);
   }
   const int tomb = out->out_tomb != nullptr;
-  hipLaunchKernelGGL(k_rga_wave, dim3(SMX_CEIL_DIV(nl, (i64)RW_WAVES)), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n,
-                     nl, def1, ndef, tmp_v, tmp_s, scnt, tomb);
-  hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, def1, ndef, def2,
-                     ndef + 1, tmp_v, tmp_s, scnt, tomb);
+  i64 wg = SMX_CEIL_DIV(nl, (i64)RW_WAVES);
+  if (RW_PER_CU > 0 && wg > (i64)g_cus * RW_PER_CU) wg = (i64)g_cus * RW_PER_CU;
+  const dim3 wgrid((u32)wg);
+  hipLaunchKernelGGL(k_rga_wave, wgrid, dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, tmp_v, tmp_s, scnt,
+                     tomb);
+  // lists of more than RW_CAP events (a few, if any).  (On a second stream beside
+  // k_rga_wave they measured no faster: their workgroups trail k_rga_wave's, and the
+  // join costs ~14 us, profiles/r04_s.)
+  hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, def2, ndef + 1,
+                     tmp_v, tmp_s, scnt, tomb);
   hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
                      tmp_s, scnt, tomb);
   if (nl <= RGA_FUSED_MAX) {  // each list's wave finds its own offset
