@@ -31,6 +31,9 @@
 // unless two events share anchor and the top half of t, and only then are t, author
 // and opid read from the input columns by event index (rga_key_lt).
 #define RGA_REC 2
+struct __attribute__((aligned(16))) R16 {  // one record (16-byte loads / stores)
+  u64 a, b;
+};
 #define RGA_WV 1  // the value / op / index word
 #define RGA_IDX_MASK 0x3fffffffu
 #define RGA_TOMB_BIT 0x80000000u  // tmp_s: the element is tombstoned (list mode, smx_rga_out.out_tomb)
@@ -53,16 +56,10 @@
 #define RREC_TILE (RR_NT * RREC_ITEMS)    // 3072 records (120 KB) per block and pass
 #define RREC_SEG (RREC_TILE / RR_NW)      // contiguous records per wave
 #define RGA_NDIG 256                      // digits per pass
+#ifndef RR_W16
+#define RR_W16 1  // runs written as 16-byte records (one store per record, not two)
+#endif
 static_assert(RREC_TILE % BLOCK == 0 && RREC_TILE <= 65535, "tile: k_rrec_hist blocks, u16 slots");
-
-__device__ __forceinline__ u32 rga_list_of(const smx_rga_ops& o, i64 i, i32* err) {
-  const u32 l = o.list[i];
-  if (l >= (u64)o.n_lists || o.op[i] > 2) {
-    *err = 1;
-    return 0;
-  }
-  return l;
-}
 
 template <bool FIRST>
 __global__ void __launch_bounds__(BLOCK) k_rrec_hist(smx_rga_ops o, const u32* __restrict__ keys, int shift,
@@ -71,11 +68,30 @@ __global__ void __launch_bounds__(BLOCK) k_rrec_hist(smx_rga_ops o, const u32* _
   h[threadIdx.x] = 0;
   __syncthreads();
   const i64 base = (i64)blockIdx.x * RREC_TILE;
+  constexpr int IT = RREC_TILE / BLOCK;
+  u32 key[IT], bad = 0;  // all loads first: a conditional error store between them would
+                         // order each iteration's loads after the previous check
 #pragma unroll
-  for (int it = 0; it < RREC_TILE / BLOCK; ++it) {
+  for (int it = 0; it < IT; ++it) {
     const i64 i = base + it * BLOCK + threadIdx.x;
-    if (i < o.n_ops) atomicAdd(&h[((FIRST ? rga_list_of(o, i, err) : keys[i]) >> shift) & 255u], 1u);
+    key[it] = 0;
+    if (i < o.n_ops) {
+      if constexpr (FIRST) {
+        const u32 l = o.list[i];
+        const bool b = l >= (u64)o.n_lists || o.op[i] > 2;  // (counted as list 0, as k_rrec_scatter places it)
+        key[it] = b ? 0u : l;
+        bad |= (u32)b;
+      } else {
+        key[it] = keys[i];
+      }
+    }
   }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const i64 i = base + it * BLOCK + threadIdx.x;
+    if (i < o.n_ops) atomicAdd(&h[(key[it] >> shift) & 255u], 1u);
+  }
+  if (bad) *err = 1;
   __syncthreads();
   hist[(i64)blockIdx.x * RGA_NDIG + threadIdx.x] = h[threadIdx.x];
 }
@@ -149,7 +165,7 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
                                                         u64* __restrict__ rout, int shift,
                                                         const u32* __restrict__ offs, i32* __restrict__ err,
                                                         u32 ntiles) {
-  __shared__ u64 srec[RREC_TILE * RGA_REC];  // 48 KB
+  __shared__ __attribute__((aligned(16))) u64 srec[RREC_TILE * RGA_REC];  // 48 KB
   __shared__ u32 skey[RREC_TILE];
   __shared__ u16 spos[RREC_TILE];            // tile record -> staged slot (pass 2+)
   __shared__ u16 wc[RR_NW][RGA_NDIG];        // per-wave digit counts, then offsets
@@ -254,6 +270,16 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
     __syncthreads();
     // the next tile's loads fly while this tile's runs are written
     if (tile + gridDim.x < ntiles) rrec_load<FIRST>(T, o, kin, rin, (i64)(tile + gridDim.x) * RREC_TILE, t, w, lane);
+#if RR_W16
+#pragma unroll 1
+    for (u32 p = t; p < cnt; p += RR_NT) {  // record-wise: consecutive lanes, consecutive 16-byte records
+      const u32 key = skey[p];
+      const u32 d = (key >> shift) & 255u;
+      const u32 dst = gofs[d] + p - lstart[d];
+      kout[dst] = (KO)key;  // (u8: the low byte, for k_rrec_local)
+      *reinterpret_cast<R16*>(rout + (u64)dst * RGA_REC) = reinterpret_cast<const R16*>(srec)[p];
+    }
+#else
 #pragma unroll 1
     for (u32 p = t; p < cnt; p += RR_NT) {
       const u32 d = (skey[p] >> shift) & 255u;
@@ -265,6 +291,7 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
       const u32 d = (skey[p] >> shift) & 255u;
       rout[(u64)(gofs[d] + p - lstart[d]) * RGA_REC + k] = srec[x];
     }
+#endif
     __syncthreads();  // LDS is rewritten by the next tile
   }
 }
@@ -308,9 +335,12 @@ __global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* _
 #define RL_TILE (RL_NT * RL_ITEMS)
 #define RL_SEG (RL_TILE / RL_NW)  // contiguous records per wave and tile
 #define RL_CU 8                   // count phase: keys in flight per lane
-struct __attribute__((aligned(16))) R16 {
-  u64 a, b;
-};
+#ifndef RL_S
+#define RL_S 2  // workgroups per bucket
+#endif
+#ifndef RL_PF
+#define RL_PF 0  // 1: the next tile's loads issued once this one is staged (measured slower: 0.58 -> 0.605 ms)
+#endif
 __global__ void __launch_bounds__(RL_NT) k_rrec_local(const u8* __restrict__ kin, const u64* __restrict__ rin,
                                                       u64* __restrict__ rout,
                                                       const u32* __restrict__ dstart, i64 nl,
@@ -318,11 +348,32 @@ __global__ void __launch_bounds__(RL_NT) k_rrec_local(const u8* __restrict__ kin
   __shared__ u32 cnt[RGA_NDIG];
   __shared__ u32 run[RGA_NDIG];
   __shared__ u16 wc[RL_NW][RGA_NDIG];
+  __shared__ u32 tstart[RGA_NDIG], wsum[RGA_NDIG / WAVE];
   const u32 t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
-  const u32 d = blockIdx.x;
-  if (d == 0 && t < RGA_CS_MAX) csum[t] = 0u;  // (k_rga_bounds' other duty)
+  // RL_S workgroups per bucket (two fit a CU): workgroup h scatters the h-th part of the
+  // bucket, after counting the whole bucket and the parts before its own
+  const u32 d = blockIdx.x / RL_S, h = blockIdx.x - d * RL_S;
+  if (blockIdx.x == 0 && t < RGA_CS_MAX) csum[t] = 0u;  // (k_rga_bounds' other duty)
   const u32 b0 = dstart[d], b1 = dstart[d + 1];
-  if (t < RGA_NDIG) cnt[t] = 0;
+  const u32 seg = (b1 - b0 + RL_S - 1) / RL_S;
+  const u32 sa = min(b0 + h * seg, b1), sb = min(sa + seg, b1);
+  u32 kd[RL_ITEMS], dr[RL_ITEMS];
+  R16 rv[RL_ITEMS];
+  auto load_tile = [&](u32 base) {
+#pragma unroll
+    for (int it = 0; it < RL_ITEMS; ++it) {
+      const u32 i = base + w * RL_SEG + it * WAVE + lane;
+      const bool valid = i < sb;
+      kd[it] = valid ? kin[i] : 0u;
+      rv[it].a = valid ? rin[(u64)i * RGA_REC] : 0ull;
+      rv[it].b = valid ? rin[(u64)i * RGA_REC + 1] : 0ull;
+    }
+  };
+  if (RL_PF && sa < sb) load_tile(sa);  // (in flight during the count)
+  if (t < RGA_NDIG) {
+    cnt[t] = 0;
+    tstart[t] = 0;  // (first: the counts of the parts before this workgroup's)
+  }
   __syncthreads();
   {  // 4 low bytes per load (aligned words over [b0, b1); the buffer has room past n)
     const u32* kw = reinterpret_cast<const u32*>(kin);
@@ -341,7 +392,11 @@ __global__ void __launch_bounds__(RL_NT) k_rrec_local(const u8* __restrict__ kin
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const u32 i = 4 * x + q;
-          if (i >= b0 && i < b1) atomicAdd(&cnt[(k[j] >> (8 * q)) & 255u], 1u);
+          if (i >= b0 && i < b1) {
+            const u32 dd = (k[j] >> (8 * q)) & 255u;
+            atomicAdd(&cnt[dd], 1u);
+            if (i < sa) atomicAdd(&tstart[dd], 1u);
+          }
         }
       }
     }
@@ -364,26 +419,24 @@ __global__ void __launch_bounds__(RL_NT) k_rrec_local(const u8* __restrict__ kin
   __syncthreads();
   if (t < RGA_NDIG) {  // list starts (an empty list starts where the next one does)
     const i64 l = (i64)d * RGA_NDIG + t;
-    if (l < nl) lstart[l] = run[t];
+    if (h == 0 && l < nl) lstart[l] = run[t];
+    run[t] += tstart[t];
   }
+  __syncthreads();
   const u64 lt = lanemask_lt();
   // the tile's records staged in LDS in (low byte, stream) order, then written run by
   // run: consecutive lanes store consecutive 16-byte records of one list
   __shared__ R16 stg[RL_TILE];
   __shared__ u8 sdig[RL_TILE];
-  __shared__ u32 tstart[RGA_NDIG], wsum[RGA_NDIG / WAVE];
-  for (u32 base = b0; base < b1; base += RL_TILE) {
+  for (u32 base = sa; base < sb; base += RL_TILE) {
+    if (!RL_PF) load_tile(base);
     for (u32 x = t; x < RL_NW * RGA_NDIG; x += RL_NT) (&wc[0][0])[x] = 0;
     __syncthreads();
-    u32 dr[RL_ITEMS];
-    R16 rv[RL_ITEMS];
 #pragma unroll
     for (int it = 0; it < RL_ITEMS; ++it) {
       const u32 i = base + w * RL_SEG + it * WAVE + lane;
-      const bool valid = i < b1;
-      const u32 dd = (valid ? kin[i] : 0u) & 255u;
-      rv[it].a = valid ? rin[(u64)i * RGA_REC] : 0ull;
-      rv[it].b = valid ? rin[(u64)i * RGA_REC + 1] : 0ull;
+      const bool valid = i < sb;
+      const u32 dd = kd[it] & 255u;
       const u64 peers = wave_peers<8>(dd, valid);
       const u32 before = wc[w][dd];
       dr[it] = dd | ((before + (u32)__popcll(peers & lt)) << 8);
@@ -412,14 +465,15 @@ __global__ void __launch_bounds__(RL_NT) k_rrec_local(const u8* __restrict__ kin
 #pragma unroll
     for (int it = 0; it < RL_ITEMS; ++it) {
       const u32 i = base + w * RL_SEG + it * WAVE + lane;
-      if (i >= b1) continue;
+      if (i >= sb) continue;
       const u32 dd = dr[it] & 255u;
       const u32 slot = tstart[dd] + wc[w][dd] + (dr[it] >> 8);
       stg[slot] = rv[it];
       sdig[slot] = (u8)dd;
     }
     __syncthreads();
-    const u32 nv = min((u32)RL_TILE, b1 - base);
+    if (RL_PF && base + RL_TILE < sb) load_tile(base + RL_TILE);  // in flight while this tile is written
+    const u32 nv = min((u32)RL_TILE, sb - base);
     for (u32 j = t; j < nv; j += RL_NT) {
       const u32 dd = sdig[j];
       const u32 pos = run[dd] + (j - tstart[dd]);
@@ -503,6 +557,12 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
 #ifndef RW_LAUNDER
 #define RW_LAUNDER 1
 #endif
+#ifndef RW_PINS
+#define RW_PINS 0  // 1: a lane's K hash inserts probed together (measured slower: 0.563 -> 0.576 ms)
+#endif
+#ifndef RW_W0R
+#define RW_W0R 1  // word 0 of a lane's own events kept in registers for the survivors' keys
+#endif
 #ifndef RW_MGP_UNION
 #define RW_MGP_UNION 1  // mem / gp share LDS: 9.5 KB per two-list workgroup, 16 per CU
 #endif
@@ -515,9 +575,40 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
 #endif
 
 
+#ifndef RW_XV
+#define RW_XV 0  // 1: exchanges on the VALU only (DPP, permlane swaps): measured 0.560 -> 0.57 ms, off
+#endif
 // v from lane ^ lm (lm a constant after unrolling): DPP for 1, 2, 3, 7, 15, a swizzle
 // within 32 lanes for 4, 8, 16, 31, a permute otherwise.
+__device__ __forceinline__ u32 xor32_swap(u32 v) {  // lane ^ 32 (v_permlane32_swap: VALU)
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return __lane_id() < 32 ? r[1] : r[0];
+}
+__device__ __forceinline__ u32 xor16_swap(u32 v) {  // lane ^ 16 (v_permlane16_swap: VALU)
+  const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return __lane_id() & 16 ? r[0] : r[1];
+}
+
 __device__ __forceinline__ u32 xshfl(u32 v, u32 lm) {
+#if RW_XV  // every exchange on the VALU (DPP, permlane swaps): no LDS-unit round trips
+  switch (lm) {
+    case 1: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    case 2: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    case 3: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x1B, 0xF, 0xF, false);
+    case 7: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    case 15: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+    case 4: {  // ^7 (row half mirror) then ^3 (quad perm 3,2,1,0)
+      const u32 x = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+      return (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x1B, 0xF, 0xF, false);
+    }
+    case 8: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    case 16: return xor16_swap(v);
+    case 31: return (u32)__builtin_amdgcn_update_dpp(0, (int)xor16_swap(v), 0x140, 0xF, 0xF, false);
+    case 32: return xor32_swap(v);
+    case 63: return (u32)__builtin_amdgcn_update_dpp(0, (int)xor16_swap(xor32_swap(v)), 0x140, 0xF, 0xF, false);
+    default: return (u32)__shfl_xor((int)v, (int)lm);
+  }
+#endif
   switch (lm) {
     case 1: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
     case 2: return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
@@ -735,6 +826,27 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
                                               u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
                                               u32* __restrict__ scnt) {
   const u64* src = R + (u64)s0 * RGA_REC;
+#if RW_W0R
+  u64 w0r[K];  // word 0 of this lane's events k * 64 + lane, kept for step 3
+  {  // every load in flight at once; word 1 of each event to LDS
+    u64 wvr[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const u32 e = (u32)k * 64u + lane;
+      w0r[k] = e < cnt ? src[(u64)e * RGA_REC] : ~0ull;
+      wvr[k] = e < cnt ? src[(u64)e * RGA_REC + RGA_WV] : 0ull;
+    }
+    for (u32 t = lane; t < RwLds<CAP>::HT; t += WAVE) {
+      S.h.hkey[t] = RW_EMPTY;
+      S.h.hcnt[t] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const u32 e = (u32)k * 64u + lane;
+      if (e < cnt) S.wv[e] = wvr[k];
+    }
+  }
+#else
   {  // every load in flight at once; words 0 and 4 of each event to LDS
     u64 v[RGA_REC * K];
 #pragma unroll
@@ -758,6 +870,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
       }
     }
   }
+#endif
   wave_lds_sync();
   if (RW_ABL & 8) {
     if (lane == 0) rga_put_count(scnt, l, (u32)S.wv[lane] & 1u);
@@ -779,6 +892,39 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
     // 1. value groups: each event's value into the hash table (CAS), its rank among
     //    the group's events (match within the wave, running counts across slots),
     //    then the groups laid out contiguously, each in event order
+#if RW_PINS
+    {  // all K of a lane's events probe together: one round of K CASes in flight per
+       // step instead of K dependent probe chains (the slot a group lands in does not
+       // matter; its members' order comes from the ranks below)
+      u32 v[K], pend = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const u32 e = (u32)k * 64u + lane;
+        S.st[e] = 0;
+        v[k] = 0;
+        if (e < cnt) {
+          const u64 wv = S.wv[e];
+          v[k] = (u32)(wv >> 32);
+          opk[k] = (u32)(wv >> 30) & 3u;
+          slot[k] = (v[k] * 0x9E3779B1u) >> (32 - HB);
+          pend |= 1u << k;
+        }
+      }
+      while (__ballot(pend != 0)) {
+        u32 old[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) old[k] = (pend >> k) & 1u ? atomicCAS(&S.h.hkey[slot[k]], RW_EMPTY, v[k]) : 0u;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if ((pend >> k) & 1u) {
+            if (old[k] == RW_EMPTY || old[k] == v[k])
+              pend &= ~(1u << k);
+            else
+              slot[k] = (slot[k] + 1) & (RwLds<CAP>::HT - 1);
+          }
+      }
+    }
+#else
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const u32 e = (u32)k * 64u + lane;
@@ -796,6 +942,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
         slot[k] = h;
       }
     }
+#endif
     wave_lds_sync();
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -900,7 +1047,13 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
     const u32 e = (u32)k * 64u + lane;
     const bool live = e < cnt && (tomb ? (S.st[e] & 1) != 0 : S.st[e] == 1);
     const u64 ball = __ballot(live);
-    if (live) S.gp[m + (u32)__popcll(ball & lt)] = (u16)e;
+    if (live) {
+      const u32 q = m + (u32)__popcll(ball & lt);
+      S.gp[q] = (u16)e;
+#if RW_W0R
+      S.gs[q] = w0r[k];  // (the hash table under gs is dead after step 2)
+#endif
+    }
     m += (u32)__popcll(ball);
   }
   wave_lds_sync();
@@ -909,7 +1062,9 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
     const u32 a = (u32)k * 64u + lane;
     if (a < m) {
       pay[k] = S.gp[a];
-#if RW_W0G
+#if RW_W0R
+      key[k] = S.gs[a];
+#elif RW_W0G
       key[k] = src[(u64)pay[k] * RGA_REC];
 #else
       key[k] = S.w0[pay[k]];
@@ -1264,11 +1419,13 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
     u32* kbuf[2] = {keys, keys2};
     if (RGA_MSD && npass == 2) {  // high byte by the global pass, low byte per bucket
       hipLaunchKernelGGL(k_rrec_hist<true>, dim3(nblk), dim3(BLOCK), 0, st, o, nullptr, 8, rhist, err);
+      // (one-launch column scan with the bucket starts from its last workgroup, on a
+      // [digit][tile] histogram: 18.7 + 34.3 us against hscan's 22 + 28.8, profiles/r04_ac)
       hscan(rhist, nblk, 256u, tsum, dstart, st);
       const int sgrid = nblk < g_rr_grid ? nblk : g_rr_grid;
       hipLaunchKernelGGL((k_rrec_scatter<true, u8>), dim3(sgrid), dim3(RR_NT), 0, st, o, nullptr, nullptr, (u8*)keys2,
                          rec2, 8, rhist, err, (u32)nblk);
-      hipLaunchKernelGGL(k_rrec_local, dim3(RGA_NDIG), dim3(RL_NT), 0, st, (const u8*)keys2, rec2, rec, dstart, nl,
+      hipLaunchKernelGGL(k_rrec_local, dim3(RGA_NDIG * RL_S), dim3(RL_NT), 0, st, (const u8*)keys2, rec2, rec, dstart, nl,
                          lstart, scnt - RGA_CS_MAX);
       npass = 0;  // (done: rec holds the list-ordered records, lstart their starts)
     }
