@@ -820,8 +820,9 @@ __device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, co
 }
 
 // tomb: list mode (crdt.py RGA.list) -- the tombstoned elements stay, flagged
+// Returns the list's survivor count (wave-uniform); scnt[l] is the caller's to write.
 template <int K, int CAP>
-__device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* __restrict__ R, u32 l, u32 s0, u32 cnt,
+__device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __restrict__ R, u32 l, u32 s0, u32 cnt,
                                               RwLds<CAP>& S, u32 lane, bool tomb,
                                               u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
                                               u32* __restrict__ scnt) {
@@ -872,10 +873,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
   }
 #endif
   wave_lds_sync();
-  if (RW_ABL & 8) {
-    if (lane == 0) rga_put_count(scnt, l, (u32)S.wv[lane] & 1u);
-    return;
-  }
+  if (RW_ABL & 8) return (u32)__builtin_amdgcn_readfirstlane((int)((u32)S.wv[lane] & 1u));
   const u64 lt = lane ? ~0ull >> (WAVE - lane) : 0ull;  // (from `lane`: see k_rga_wave)
   constexpr int HB = RwLds<CAP>::HT == 256 ? 8 : RwLds<CAP>::HT == 512 ? 9 : 10;  // log2 of the hash slots
   static_assert(RwLds<CAP>::HT == 1 << HB, "hash slots");
@@ -1087,7 +1085,7 @@ __device__ __forceinline__ void rga_wave_list(const smx_rga_ops& o, const u64* _
   } else {
     rw_order<8>(S, src, o, key, pay, m, s0, lane, tmp_v, tmp_s);
   }
-  if (lane == 0) rga_put_count(scnt, l, m);
+  return m;
 }
 
 __global__ void __launch_bounds__(WAVE * RW_WAVES) RW_OCC k_rga_wave(smx_rga_ops o, const u64* __restrict__ R,
@@ -1100,22 +1098,36 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) RW_OCC k_rga_wave(smx_rga_ops
   // the wave index as a scalar: the list index, its bounds and the slice base stay in
   // SGPRs (scalar loads of lstart; LDS member offsets fold into the instructions)
   const u32 w = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
-  // persistent (RW_PER_CU workgroups per CU): each wave takes every (grid)-th list
-  for (u64 ll = (u64)blockIdx.x * RW_WAVES + w; ll < (u64)nl; ll += (u64)gridDim.x * RW_WAVES) {
-    const u32 l = (u32)ll;
+  // persistent (RW_PER_CU workgroups per CU): each wave takes a contiguous range of
+  // lists and adds its survivors into the 256-list chunk sums once per chunk (one device
+  // atomic per list on a shared chunk word serialized the waves, and the next list's
+  // loads waited for it)
+  const u32 nw = gridDim.x * RW_WAVES, wid = blockIdx.x * RW_WAVES + w;
+  const u32 per = (u32)((nl + nw - 1) / nw);
+  const u32 L0 = min((u64)wid * per, (u64)nl), L1 = min((u64)L0 + per, (u64)nl);
+  u32 acc = 0;
+  for (u32 l = L0; l < L1; ++l) {
     const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
-    if (cnt > RW_CAP) continue;  // k_rga_wave2 / k_rga_big
-    // the lane id laundered per list: otherwise the compiler hoists every lane-derived
-    // constant of the list code out of the loop and keeps it live
-    u32 ln = lane;
-    if (RW_LAUNDER) asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-    if (cnt <= 64)
-      rga_wave_list<1>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
-    else if (cnt <= 128)
-      rga_wave_list<2>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
-    else
-      rga_wave_list<4>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
-    wave_lds_sync();  // the next list reuses the slice
+    if (cnt <= RW_CAP) {  // (longer lists: k_rga_wave2 / k_rga_big count themselves)
+      // the lane id laundered per list: otherwise the compiler hoists every lane-derived
+      // constant of the list code out of the loop and keeps it live
+      u32 ln = lane;
+      if (RW_LAUNDER) asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+      u32 m;
+      if (cnt <= 64)
+        m = rga_wave_list<1>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+      else if (cnt <= 128)
+        m = rga_wave_list<2>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+      else
+        m = rga_wave_list<4>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+      if (lane == 0) scnt[l] = m;
+      acc += m;
+      wave_lds_sync();  // the next list reuses the slice
+    }
+    if ((l + 1) % RGA_CS_LISTS == 0 || l + 1 == L1) {
+      if (lane == 0 && acc && l < RGA_FUSED_MAX) atomicAdd(scnt - RGA_CS_MAX + l / RGA_CS_LISTS, acc);
+      acc = 0;
+    }
   }
 }
 
@@ -1143,7 +1155,8 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(smx_rga_ops o, co
         if (lane == 0) defer[atomicAdd(ndefer, 1u)] = l;
         continue;
       }
-      rga_wave_list<8>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
+      const u32 m = rga_wave_list<8>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
+      if (lane == 0) rga_put_count(scnt, l, m);
       wave_lds_sync();  // the next list reuses the slice
     }
   }
