@@ -557,6 +557,9 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
 #ifndef RW_LAUNDER
 #define RW_LAUNDER 1
 #endif
+#ifndef RW_RREG
+#define RW_RREG 0  // 1: groups of 2-4 events replayed in registers (list kernel 199 -> 204 us: off)
+#endif
 #ifndef RW_PINS
 #define RW_PINS 0  // 1: a lane's K hash inserts probed together (measured slower: 0.563 -> 0.576 ms)
 #endif
@@ -985,6 +988,46 @@ __device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __
         S.st[e] = opk[k] != 2;
         continue;
       }
+#if RW_RREG
+      if (c <= 4) {  // small groups (most of them) replayed in registers: the members'
+                     // entries read at once, no chain of dependent LDS reads.  A move
+                     // with two live candidates (their list order needs the keys) takes
+                     // the general loop below instead.
+        u32 xm[4], sv[4] = {0u, 0u, 0u, 0u};
+        bool hard = false;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xm[i] = (u32)i < c ? S.mem[b + i] : 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if ((u32)i >= c) break;
+          const u32 op = xm[i] >> RW_MOP;
+          if (op == 2) {  // delete: every present element is tombstoned
+#pragma unroll
+            for (int j = 0; j < i; ++j) sv[j] |= (sv[j] & 1u) << 1;
+            continue;
+          }
+          if (op == 1) {  // move: pops the live element (the only one here)
+            u32 cand = 0;
+#pragma unroll
+            for (int j = 0; j < i; ++j) cand |= (u32)(sv[j] == 1u) << j;
+            if (cand & (cand - 1)) {
+              hard = true;
+              break;
+            }
+#pragma unroll
+            for (int j = 0; j < i; ++j)
+              if ((cand >> j) & 1u) sv[j] = 0u;
+          }
+          sv[i] = 1u;
+        }
+        if (!hard) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if ((u32)i < c) S.st[xm[i] & RW_MEV] = (u8)sv[i];
+          continue;
+        }
+      }
+#endif
       for (u32 i = 0; i < c; ++i) {
         const u32 xm = S.mem[b + i];
         const u32 x = xm & RW_MEV, op = xm >> RW_MOP;
