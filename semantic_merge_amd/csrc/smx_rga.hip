@@ -306,6 +306,9 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
 #ifndef RGA_OUT_PRE
 #define RGA_OUT_PRE 2
 #endif
+#ifndef RGA_OUT_LPW
+#define RGA_OUT_LPW 1  // lists per wave in k_rga_out_fused (4: 28.8 us either way, profiles/r04_aj)
+#endif
 __global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* __restrict__ lstart,
                              u32* __restrict__ csum) {
   if (blockIdx.x == 0 && threadIdx.x < RGA_CS_MAX) csum[threadIdx.x] = 0u;
@@ -560,8 +563,9 @@ __device__ __forceinline__ bool rec_lt(const u64* a, const u64* b, const smx_rga
 #ifndef RW_RREG
 #define RW_RREG 0  // 1: groups of 2-4 events replayed in registers (list kernel 199 -> 204 us: off)
 #endif
-#ifndef RW_PINS
-#define RW_PINS 0  // 1: a lane's K hash inserts probed together (measured slower: 0.563 -> 0.576 ms)
+#ifndef RW_PINS_K
+#define RW_PINS_K 16  // lists of K >= this: a lane's K hash inserts probed together (off: for
+                      // k_rga_wave's K = 4 0.563 -> 0.576 ms; k_rga_wave2's K = 8 26.9 us either way)
 #endif
 #ifndef RW_W0R
 #define RW_W0R 1  // word 0 of a lane's own events kept in registers for the survivors' keys
@@ -893,7 +897,7 @@ __device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __
     // 1. value groups: each event's value into the hash table (CAS), its rank among
     //    the group's events (match within the wave, running counts across slots),
     //    then the groups laid out contiguously, each in event order
-#if RW_PINS
+    if constexpr (K >= RW_PINS_K) {
     {  // all K of a lane's events probe together: one round of K CASes in flight per
        // step instead of K dependent probe chains (the slot a group lands in does not
        // matter; its members' order comes from the ranks below)
@@ -925,7 +929,7 @@ __device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __
           }
       }
     }
-#else
+    } else {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const u32 e = (u32)k * 64u + lane;
@@ -943,7 +947,7 @@ __device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __
         slot[k] = h;
       }
     }
-#endif
+    }
     wave_lds_sync();
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1308,49 +1312,66 @@ __global__ void __launch_bounds__(1024) k_rga_big(smx_rga_ops o, const u64* __re
 // + the counts of the chunk's earlier lists (one 16-byte read of each per lane, a wave
 // sum), then its survivors, in list order, to their place in the output.  The last
 // list's wave writes the total.  n_lists <= RGA_FUSED_MAX.
+// RGA_OUT_LPW consecutive lists per wave (one 256-list chunk): one offset sum serves
+// them all (the next list's offset is this one's plus its count), and all their first
+// survivors are read before it is known.
 __global__ void __launch_bounds__(BLOCK) k_rga_out_fused(const u32* __restrict__ tmp_v, const u32* __restrict__ tmp_s,
                                                         const u32* __restrict__ lstart, const u32* __restrict__ scnt,
                                                         i64 nl, smx_rga_out out) {
+  constexpr int LPW = RGA_OUT_LPW;
+  static_assert(RGA_CS_LISTS % LPW == 0, "a wave's lists share a chunk");
   const u32 lane = threadIdx.x & (WAVE - 1);
-  const i64 l = (i64)blockIdx.x * (BLOCK / WAVE) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));  // (scalar)
-  if (l >= nl) return;
-  const u32 c = (u32)l / RGA_CS_LISTS, c0 = c * RGA_CS_LISTS;
+  const i64 l0 = ((i64)blockIdx.x * (BLOCK / WAVE) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE))) * LPW;
+  if (l0 >= nl) return;
+  const u32 c = (u32)l0 / RGA_CS_LISTS, c0 = c * RGA_CS_LISTS;
   const uint4 cs = reinterpret_cast<const uint4*>(scnt - RGA_CS_MAX)[lane];
   const uint4 ls = reinterpret_cast<const uint4*>(scnt + c0)[lane];
-  const u32 s0 = lstart[l], m = scnt[l];
-  // the first RGA_OUT_PRE * 64 survivors are read before the offset is known
-  u32 pv[RGA_OUT_PRE], ps[RGA_OUT_PRE];
+  u32 s0[LPW], m[LPW];
 #pragma unroll
-  for (int j = 0; j < RGA_OUT_PRE; ++j) {
-    const u32 x = lane + (u32)j * WAVE;
-    pv[j] = x < m ? __builtin_nontemporal_load(&tmp_v[s0 + x]) : 0u;
-    ps[j] = x < m ? __builtin_nontemporal_load(&tmp_s[s0 + x]) : 0u;
+  for (int j = 0; j < LPW; ++j) {
+    const bool v = l0 + j < nl;
+    s0[j] = v ? lstart[l0 + j] : 0u;
+    m[j] = v ? scnt[l0 + j] : 0u;
   }
+  u32 pv[LPW][RGA_OUT_PRE], ps[LPW][RGA_OUT_PRE];
+#pragma unroll
+  for (int j = 0; j < LPW; ++j)
+#pragma unroll
+    for (int i = 0; i < RGA_OUT_PRE; ++i) {
+      const u32 x = lane + (u32)i * WAVE;
+      pv[j][i] = x < m[j] ? __builtin_nontemporal_load(&tmp_v[s0[j] + x]) : 0u;
+      ps[j][i] = x < m[j] ? __builtin_nontemporal_load(&tmp_s[s0[j] + x]) : 0u;
+    }
   const u32 q = 4 * lane;
   u32 part = (q < c ? cs.x : 0u) + (q + 1 < c ? cs.y : 0u) + (q + 2 < c ? cs.z : 0u) + (q + 3 < c ? cs.w : 0u);
-  const u32 r = (u32)l - c0;
+  const u32 r = (u32)l0 - c0;
   part += (q < r ? ls.x : 0u) + (q + 1 < r ? ls.y : 0u) + (q + 2 < r ? ls.z : 0u) + (q + 3 < r ? ls.w : 0u);
-  const u32 d = (u32)__builtin_amdgcn_readlane((int)wave_incl_sum_u32(part), WAVE - 1);
+  u32 d = (u32)__builtin_amdgcn_readlane((int)wave_incl_sum_u32(part), WAVE - 1);
 #pragma unroll
-  for (int j = 0; j < RGA_OUT_PRE; ++j) {
-    const u32 x = lane + (u32)j * WAVE;
-    if (x >= m) break;
-    out.out_value[d + x] = pv[j];
-    out.out_src[d + x] = (i32)(ps[j] & ~RGA_TOMB_BIT);
-    if (out.out_tomb) out.out_tomb[d + x] = ps[j] & RGA_TOMB_BIT ? 1 : 0;
-  }
-  for (u32 x = lane + RGA_OUT_PRE * WAVE; x < m; x += WAVE) {
-    out.out_value[d + x] = __builtin_nontemporal_load(&tmp_v[s0 + x]);
-    const u32 sx = __builtin_nontemporal_load(&tmp_s[s0 + x]);
-    out.out_src[d + x] = (i32)(sx & ~RGA_TOMB_BIT);
-    if (out.out_tomb) out.out_tomb[d + x] = sx & RGA_TOMB_BIT ? 1 : 0;
-  }
-  if (lane == 0) {
-    out.out_offsets[l] = d;
-    if (l == nl - 1) {
-      out.out_offsets[nl] = d + m;
-      out.counts[0] = d + m;
+  for (int j = 0; j < LPW; ++j) {
+    if (l0 + j >= nl) break;
+#pragma unroll
+    for (int i = 0; i < RGA_OUT_PRE; ++i) {
+      const u32 x = lane + (u32)i * WAVE;
+      if (x >= m[j]) break;
+      out.out_value[d + x] = pv[j][i];
+      out.out_src[d + x] = (i32)(ps[j][i] & ~RGA_TOMB_BIT);
+      if (out.out_tomb) out.out_tomb[d + x] = ps[j][i] & RGA_TOMB_BIT ? 1 : 0;
     }
+    for (u32 x = lane + RGA_OUT_PRE * WAVE; x < m[j]; x += WAVE) {
+      out.out_value[d + x] = __builtin_nontemporal_load(&tmp_v[s0[j] + x]);
+      const u32 sx = __builtin_nontemporal_load(&tmp_s[s0[j] + x]);
+      out.out_src[d + x] = (i32)(sx & ~RGA_TOMB_BIT);
+      if (out.out_tomb) out.out_tomb[d + x] = sx & RGA_TOMB_BIT ? 1 : 0;
+    }
+    if (lane == 0) {
+      out.out_offsets[l0 + j] = d;
+      if (l0 + j == nl - 1) {
+        out.out_offsets[nl] = d + m[j];
+        out.counts[0] = d + m[j];
+      }
+    }
+    d += m[j];
   }
 }
 
@@ -1518,7 +1539,7 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
                      tmp_s, scnt, tomb);
   if (nl <= RGA_FUSED_MAX) {  // each list's wave finds its own offset
-    hipLaunchKernelGGL(k_rga_out_fused, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE))), dim3(BLOCK), 0, st, tmp_v,
+    hipLaunchKernelGGL(k_rga_out_fused, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE * RGA_OUT_LPW))), dim3(BLOCK), 0, st, tmp_v,
                        tmp_s, lstart, scnt, nl, *out);
   } else {
     RGA_TRY((scan_excl<OpSum, u32, u32>(scnt, soff, nl, nullptr, part, totals, st)));
