@@ -9,10 +9,12 @@
 //    one with the smallest (key, index)) and always inserts a new element;
 //    delete tombstones every present element of that value (crdt.py:33-43).
 //  * materialize = live elements in (key, index) order (crdt.py:45-46).
-// Pipeline: stable LSD radix partition of 40-byte event records by list id (LDS-staged,
-// coalesced) -> list bounds -> one wave per list (k_rga_wave, in LDS): value groups by
-// hashing, one sequential replay per group, survivors ordered by (anchor, t, author,
-// opid, index) -> survivor-count scan -> compaction.
+// Pipeline: stable radix partition of 16-byte event records by list id (up to 65536
+// lists: the high byte by a global pass, the low byte per high-byte bucket, which also
+// gives the list starts; LDS-staged, coalesced) -> one wave per list (k_rga_wave,
+// persistent, in LDS): value groups by hashing, one sequential replay per group,
+// survivors ordered by (anchor, t, author, opid, index) -> compaction, each list's
+// output offset summed by its own wave from per-chunk survivor sums.
 #include <string>
 
 #include "smx_scan.h"
@@ -38,8 +40,9 @@ struct __attribute__((aligned(16))) R16 {  // one record (16-byte loads / stores
 #define RGA_IDX_MASK 0x3fffffffu
 #define RGA_TOMB_BIT 0x80000000u  // tmp_s: the element is tombstoned (list mode, smx_rga_out.out_tomb)
 
-// Grouping the events by list: a stable LSD radix partition of whole records on the
-// list id, 8 bits per pass (one pass up to 256 lists, two up to 65536, ...).  The first
+// Grouping the events by list: a stable radix partition of whole records on the list id,
+// 8 bits per pass (one pass up to 256 lists; up to 65536 the high byte here and the low
+// byte per bucket in k_rrec_local; beyond, LSD passes of this kernel).  The first
 // pass reads the input columns and packs the records; each pass stages a tile in LDS
 // in digit order and writes each digit's run of records contiguously, so every byte
 // moves in full cache lines.  Stable: each list's events stay in stream order.
