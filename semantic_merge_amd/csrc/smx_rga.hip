@@ -59,6 +59,9 @@ struct __attribute__((aligned(16))) R16 {  // one record (16-byte loads / stores
 #define RREC_TILE (RR_NT * RREC_ITEMS)    // 3072 records (120 KB) per block and pass
 #define RREC_SEG (RREC_TILE / RR_NW)      // contiguous records per wave
 #define RGA_NDIG 256                      // digits per pass
+#ifndef RR_HIST_OP
+#define RR_HIST_OP 0  // 1: the histogram pass also reads the op column (to count bad ops as list 0)
+#endif
 #ifndef RR_W16
 #define RR_W16 1  // runs written as 16-byte records (one store per record, not two)
 #endif
@@ -81,7 +84,9 @@ __global__ void __launch_bounds__(BLOCK) k_rrec_hist(smx_rga_ops o, const u32* _
     if (i < o.n_ops) {
       if constexpr (FIRST) {
         const u32 l = o.list[i];
-        const bool b = l >= (u64)o.n_lists || o.op[i] > 2;  // (counted as list 0, as k_rrec_scatter places it)
+        // a list id out of range counts as list 0, where k_rrec_scatter places it (an op
+        // > 2 fails the call there; its record still goes to its list)
+        const bool b = RR_HIST_OP ? l >= (u64)o.n_lists || o.op[i] > 2 : l >= (u64)o.n_lists;
         key[it] = b ? 0u : l;
         bad |= (u32)b;
       } else {
@@ -192,9 +197,10 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
       const bool valid = rrec_event(base, w, it, lane) < n;
       if constexpr (FIRST) {
         key[it] = T.list[it];
-        if (valid && (key[it] >= (u64)o.n_lists || T.op[it] > 2)) {
+        const bool badl = key[it] >= (u64)o.n_lists, bado = T.op[it] > 2;
+        if (valid && (badl || bado)) {
           *err = 1;
-          key[it] = 0;
+          if (badl || RR_HIST_OP) key[it] = 0;
         }
       } else {
         key[it] = T.key[it];
