@@ -169,6 +169,10 @@ def test_rga_hot_list_and_invalid_input():
     b.list_id[5] = 50
     with pytest.raises(Exception, match="n_lists"):
         rga_replay_device(b)
+    b.list_id[5] = 7
+    b.op[200_001] = 3  # an op beyond delete (checked by the partition's first pass)
+    with pytest.raises(Exception, match="op > 2"):
+        rga_replay_device(b)
 
 
 def test_rga_lists_at_capacity_all_values_distinct():
