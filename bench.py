@@ -52,13 +52,18 @@ sys.path.insert(0, REPO)
 METRIC = "op-log compose+conflict throughput (ops/s), 100M-op logs, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 PIPE_BYTES_PER_OP = 53         # 37 B in + 16 B out per op (+8 B per conflict)
-# The roofline kernel is the plan's dominant one, by the library's stage timers:
-#   stage      kernel                 algorithmic bytes per op of the merge
-#   window     k_window_f             41: the 37 B of input read once + the 4 B T-order index
-#   window_g   k_window_g             45: the 37 B + the 4 B sort permutation + the 4 B index
-#   segsort    k_segsort (2 launches) 52: ts, oid (24 B) read, sorted copies (24 B) + the
-#                                     permutation (4 B) written
-ROOF_STAGES = {"window": ("k_window_f", 41), "window_g": ("k_window_g", 45), "segsort": ("k_segsort", 52)}
+# The roofline kernel is the plan's dominant one, by the library's stage timers (the
+# stage with the largest time per merge; its launches are averaged, so a stage holds one
+# kernel instance -- the wide presorted windows have a stage of their own, apart from
+# the normal attempt that failed before them):
+#   stage        kernel (rocprof name prefix)  algorithmic bytes per op of the merge
+#   window       k_window_f<2048              41: the 37 B of input read once + the 4 B T-order index
+#   window_wide  k_window_f<8192              41: the same, 8192-op windows (config 5)
+#   window_g     k_window_g                   45: the 37 B + the 4 B sort permutation + the 4 B index
+#   segsort      k_segsort (2 launches)       52: ts, oid (24 B) read, sorted copies (24 B) + the
+#                                             permutation (4 B) written
+ROOF_STAGES = {"window": ("k_window_f<2048", 41), "window_wide": ("k_window_f<8192", 41),
+               "window_g": ("k_window_g", 45), "segsort": ("k_segsort", 52)}
 WINDOW_BYTES_PER_OP = ROOF_STAGES["window"][1]
 REF_PY_OPS_S = 47_600          # SURVEY §3.4 / BASELINE.md: reference compose_oplogs, 1 core, 1M ops
 FETCH_FACTOR, WRITE_FACTOR = 2.0, 1.0   # gfx950 FETCH_SIZE reads 1/2 of streamed bytes (guide)
@@ -116,7 +121,7 @@ def pmc_traffic(args) -> dict:
         tot += b
     out["pipeline_traffic"] = round(tot)
     out["per_kernel"] = dict(sorted(kern.items(), key=lambda x: -x[1])[:12])   # bytes per merge
-    out["per_kernel_all"] = {k.split("<")[0]: v for k, v in kern.items()}
+    out["per_kernel_all"] = {k.replace(" ", ""): v for k, v in kern.items()}
     out["factors"] = {"FETCH_SIZE": FETCH_FACTOR, "WRITE_SIZE": WRITE_FACTOR,
                       "note": "FETCH_SIZE x2 is calibrated on streaming reads (DESIGN.md §5); for "
                               "gather-dominated kernels (k_emit4) the x2 figure is an upper bound "
@@ -307,11 +312,12 @@ def main() -> None:
     stages = _lib.stage_times()
     # per-stage breakdown (every stage timed), outside the timed region
     lib.smx_set_profiling_stages(0xFFFFFFFF)
-    stages_all = stages
+    stages_all, n_breakdown = stages, args.steps
     if not args.no_breakdown:
         lib.smx_reset_stage_times()
         lib.smx_set_profiling(1)
-        for _ in range(min(args.steps, 5)):
+        n_breakdown = min(args.steps, 5)
+        for _ in range(n_breakdown):
             run()
         torch.cuda.synchronize(dev)
         lib.smx_set_profiling(0)
@@ -387,8 +393,8 @@ def main() -> None:
     roof_stage = max(ROOF_STAGES, key=lambda k: stages.get(k, (0.0, 0))[0])
     roof_kernel, roof_bpo = ROOF_STAGES[roof_stage]
     st_ms, st_calls = stages.get(roof_stage, (0.0, 0))
-    # per launch of the kernel: a failed presorted attempt shares the "window" stage with
-    # nothing else; the segmented sort's stage covers both branch launches of a merge
+    # per launch of the kernel (one segsort stage call covers both branch launches of a
+    # merge, and its 52 B/op both branches' bytes)
     win_avg = st_ms / max(st_calls, 1)
     achieved = roof_bpo * n / (win_avg * 1e-3) / 1e9 if win_avg > 0 else None
     pipe_gbs = (PIPE_BYTES_PER_OP * n_job + 8 * nconf) / (ms_step * 1e-3) / 1e9
@@ -462,14 +468,16 @@ def main() -> None:
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
             # HBM bytes per merge of that kernel (PMC passes; per launch for the one-launch
             # kernels, both branch launches for the segmented sort)
-            "traffic": round(pmc.pop("per_kernel_all").get(roof_kernel, 0))
+            "traffic": round(sum(v for k2, v in pmc.pop("per_kernel_all").items() if k2.startswith(roof_kernel)))
             if pmc and pmc.get("status") == "ok" else None,
             "bytes_per_op": roof_bpo,
             "avg_launch_ms": round(win_avg, 4),
         },
         "pmc": pmc,
-        "stages_ms_per_step": {k2: round(v[0] / max(v[1], 1), 4) for k2, v in stages_all.items()
-                               if v[1]},
+        # per merge: each stage's summed time over its launches in one merge, and how many
+        # times the merge entered it (breakdown leg: every stage timed, n_breakdown merges)
+        "stages_ms_per_step": {k2: round(v[0] / n_breakdown, 4) for k2, v in stages_all.items() if v[1]},
+        "stage_calls_per_step": {k2: round(v[1] / n_breakdown, 2) for k2, v in stages_all.items() if v[1]},
         "cpu_baseline": cpu,
         "end_to_end": e2e,
         "async_api": async_api,

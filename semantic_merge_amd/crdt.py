@@ -129,9 +129,12 @@ class RGA:
 
     Events are recorded and replayed on the GPU (``smx_rga_replay``) when the state is
     needed.  Reading ``list`` folds the pending events into the state and returns the
-    SAME list object on every read until new events arrive, so ``rga.list.append(e)`` or
-    ``rga.list[0].tombstone = True`` change the RGA as they do in the reference;
-    assigning ``rga.list = [...]`` replaces the state.  A later fold replays the state as
+    SAME list object on every read, before and after new events, so
+    ``rga.list.append(e)`` or ``rga.list[0].tombstone = True`` change the RGA as they do in
+    the reference; assigning ``rga.list = L`` makes ``L`` the state, and later events are
+    folded into ``L`` itself.  (The reference mutates the object at each call; here a
+    held reference sees the events at the next fold: the next read of ``list`` or
+    ``materialize()``.)  A later fold replays the state as
     a prefix of the stream (each live element as its insert; each tombstoned one as an
     insert of a private value that is then deleted, so no later event can touch it) and
     keeps the existing ``Elem`` objects: a later ``delete`` sets ``tombstone`` on them in
@@ -146,7 +149,11 @@ class RGA:
     @property
     def list(self) -> List[Elem]:
         if self._list is None or self._events:
-            self._list = self._fold()
+            out = self._fold()
+            if self._list is None:
+                self._list = out
+            else:  # the caller's list object is the state (crdt.py:27, 31, 36): fold into it
+                self._list[:] = out
             self._events = []
         return self._list
 

@@ -54,11 +54,14 @@ int smx_set_error(int code, const char* msg) { return set_err(code, msg ? msg : 
   } while (0)
 
 // gsort: the generic plan's sort and window planning; segsort: its segmented sort's
-// kernels alone (inside gsort); window_g: the generic window kernel (window: the
-// presorted one, including attempts that fail)
-enum Stage { ST_PLAN, ST_GSORT, ST_WINDOW, ST_WALK, ST_TABLES, ST_MVPREFIX, ST_EMIT, ST_SEGSORT, ST_WINDOW_G, ST_N };
+// kernels alone (inside gsort); window_g: the generic window kernel; window: the
+// presorted one at the normal or small capacity, including attempts that fail;
+// window_wide: its wide (8192-op) instance, a stage of its own so that a merge's
+// failed normal attempt is never averaged into the wide launch's time
+enum Stage { ST_PLAN, ST_GSORT, ST_WINDOW, ST_WALK, ST_TABLES, ST_MVPREFIX, ST_EMIT, ST_SEGSORT, ST_WINDOW_G,
+             ST_WINDOW_WIDE, ST_N };
 static const char* kStageNames[ST_N] = {"plan",   "gsort",    "window", "walk",    "tables",
-                                        "mvprefix", "emit", "segsort", "window_g"};
+                                        "mvprefix", "emit", "segsort", "window_g", "window_wide"};
 static std::mutex g_prof_mu;
 static int g_prof = 0;
 static u32 g_prof_mask = ~0u;  // the stages timed while profiling is on (smx_set_profiling_stages)
@@ -1767,7 +1770,8 @@ static int launch_presorted_windows(const Ctx& C, i64 W, i64 CM, int level) {
   P.perm = nullptr;
   P.W = W;
   P.ablate = knob("SMX_ABLATE", 0);
-  C.tm->begin(ST_WINDOW);
+  const int stage = wide ? ST_WINDOW_WIDE : ST_WINDOW;
+  C.tm->begin(stage);
 #if SMX_DIAG
   if (g_phase_dbg && !P.src_map && (size_t)W * WF_NSTAMP * 8 <= g_phase_dbg_bytes) {
     P.dbg = (u64*)g_phase_dbg;
@@ -1789,7 +1793,7 @@ static int launch_presorted_windows(const Ctx& C, i64 W, i64 CM, int level) {
     hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, false>), dim3(W), dim3(WF_NT), 0, st, P);
   }
   HIP_TRY(hipGetLastError());
-  C.tm->end(ST_WINDOW);
+  C.tm->end(stage);
   return SMX_OK;
 }
 
@@ -1863,6 +1867,9 @@ __global__ void k_plan_rearm(ComposeMeta* meta, u64 nwin) {
   if (meta->f_fail == F_LONG) meta->f_fail = 0;
   meta->n_win = nwin;
 }
+// (the chunk scans must write base[] and the prefixes even when k_fpart flagged F_LONG:
+// with SMX_CSCAN_FAILCHK they would leave early and the wide windows read stale prefixes)
+static_assert(!SMX_CSCAN_FAILCHK, "run_presorted_rewide reuses the failed plan's chunk prefixes and bases");
 static int run_presorted_rewide(const Ctx& C, i64 tgt, int level = WL_WIDE) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);

@@ -46,6 +46,14 @@ FIELDS = ("kind", "ts", "hi", "lo", "sym", "v0", "v1")
 S_KINDS, S_REN, S_MVNONE, S_FAIL = 0, 18, 20, 21
 S_OPEN, S_AHEAD, S_D, S_NCONF, S_NSKIP, S_OVER, S_WIDTH = 22, 23, 24, 25, 26, 27, 28
 S_TABOVER = 31   # a value too wide for the 32-bit partial tables (smx_shard.tab32)
+TAB32_MAX_BITS = 8  # the widest rank tag smx_shard_step accepts in 32-bit entries (smx_compose.hip TABLES)
+
+
+def tab32_bits(world: int) -> int:
+    """Tag bits of the 32-bit partial tables for `world` ranks (the tag is rank + 1), or 0
+    when the tag does not fit the library's limit: those worlds keep the 64-bit tables."""
+    b = int(world).bit_length()
+    return b if b <= TAB32_MAX_BITS else 0
 N_KINDS = 18
 SUM = _abi.SHARD_SUMMARY
 I64_MIN = -(2 ** 63)
@@ -236,10 +244,11 @@ class ShardedCompose:
         # the same tables with 32-bit entries: the rank tag in the top bits under a clear
         # sign bit (an int32 MAX keeps the last writer) -- half the all-reduce's bytes
         # whenever every value fits the rest (include/smx.h smx_shard.tab32)
-        self.tab_bits = int(self.world).bit_length()
+        self.tab_bits = tab32_bits(self.world)
         self.part32 = torch.zeros(3 * max(n_sym, 1) + 3, dtype=torch.int32, device=dv) \
-            if 31 - self.tab_bits >= 16 else None
+            if self.tab_bits else None
         self.tab32_used = 0  # tables steps that ran with 32-bit entries (tests, probes)
+        self.tab_redo = 0    # steps whose 32-bit tables overflowed and were redone with 64-bit entries
         self.n_xchg = 0      # ops this rank received from other ranks in the last exchange
         self.order_fixes = 0  # ORDER_FIX runs (dense timestamp ties) on this rank
         # every timestamp below 2^63 (ISO keys, dense ranks): the signed int64 order of
@@ -282,13 +291,17 @@ class ShardedCompose:
         """Buffer positions of the range info's keys: the first and last key of each
         branch slice, then RH keys from the head and RH from the tail of each (the tail
         right-aligned; short slices repeat their first position as padding)."""
-        ends, edges = [], []
+        ends, edges, live_e, live_g = [], [], [], []
         for o, n in ((self._oa, self.na_s), (self._ob, self.nb_s)):
             ends += [o, o + n - 1] if n else [0, 0]
+            live_e += [n > 0] * 2
             h = min(RH, n)
             pad = [o if n else 0]
             edges += [o + i for i in range(h)] + pad * (RH - h)
             edges += pad * (RH - h) + [o + n - h + i for i in range(h)]
+            live_g += [n > 0] * (2 * RH)
+        # an empty slice's entries read key 0, as k_range_info writes them
+        self._info_live = self.torch.tensor(live_e + live_g, dtype=self.torch.bool, device=self.dev)
         return self.torch.tensor(ends + edges, dtype=self.torch.int64, device=self.dev)
 
     def _range_info(self):
@@ -310,7 +323,7 @@ class ShardedCompose:
         if self._info_key != (self._oa, self._ob):
             self._info_idx = self._info_index()
             self._info_key = (self._oa, self._ob)
-        keys = _u64_key(self.buf["ts"].index_select(0, self._info_idx))
+        keys = _u64_key(self.buf["ts"].index_select(0, self._info_idx)) * self._info_live
         ok = self._one
         if check_order:
             for br, n in ((0, self.na_s), (1, self.nb_s)):
@@ -692,6 +705,7 @@ class ShardedCompose:
             if summ[:, S_FAIL].any():
                 self._fail(summ, err)
         if not final:  # the speculative tables do not hold: every rank redoes them
+            self.tab_redo += int(bool(summ[:, S_TABOVER].any()))
             self._tables(summ, rescatter=True)
         self.sum_walk = summ
         self._sum_host = np.ascontiguousarray(summ[self.rank], dtype=np.int64)

@@ -97,6 +97,34 @@ def test_rga_list_mutable_state_golden_gpu():
         assert _run_mutation_script(case["steps"]) == case["out"], f"rga mutation script {i}"
 
 
+def test_rga_list_object_held_across_events():
+    """The list object is the state (crdt.py:27): a reference held before insert / move /
+    delete, or a list the caller assigned, is the object the later events are folded into
+    (each Elem created by an event is new, base Elems are kept and tombstoned in place).
+    Expected states: the reference's own RGA on the same calls (checked in the build
+    container)."""
+    r = RGA()
+    r.insert(Key("root", 1, "u1", "o1"), "a")
+    lst = r.list
+    held = lst[0]
+    r.insert(Key("root", 0, "u1", "o2"), "b")
+    r.move("a", Key("root", 2, "u2", "o3"))
+    r.delete("b")
+    assert r.materialize() == ["a"]
+    assert r.list is lst
+    assert lst == [Elem(Key("root", 0, "u1", "o2"), "b", True), Elem(Key("root", 2, "u2", "o3"), "a", False)]
+    assert all(e is not held for e in lst)  # the moved element was popped (crdt.py:36)
+    L = [Elem(Key("a", 0, "u", "o1"), "x"), Elem(Key("c", 0, "u", "o2"), "y")]
+    r.list = L
+    x = L[0]
+    r.insert(Key("b", 0, "u", "o3"), "z")
+    r.delete("x")
+    assert r.list is L
+    assert L == [Elem(Key("a", 0, "u", "o1"), "x", True), Elem(Key("b", 0, "u", "o3"), "z"),
+                 Elem(Key("c", 0, "u", "o2"), "y")]
+    assert L[0] is x and x.tombstone  # tombstoned in place (crdt.py:40-43)
+
+
 def test_rga_list_out_of_key_order_fails_loudly():
     r = RGA()
     r.list = [Elem(Key("b", 0, "u", "o"), "x"), Elem(Key("a", 0, "u", "o"), "y")]

@@ -86,6 +86,11 @@ def _make(case):
             a = getattr(soa, f)
             a[i], a[j] = a[j].copy(), a[i].copy()
         return soa
+    if kind == "wide_value":  # one move's address id too wide for the 32-bit partial tables
+        soa = _make(("lift", n, n_sym, seed))
+        mv = np.flatnonzero(soa.kind == 0)
+        soa.v0[mv[len(mv) // 3]] = (1 << 30) + 7
+        return soa
     if kind == "lift":
         spec = synth.LiftSpec(n, n_sym, seed, ops_per_ms=64)
     elif kind == "adv":  # rename-heavy, 30% of symbols renamed on both sides: many conflicts
@@ -172,7 +177,7 @@ def _worker(rank, world, store_path, q, case, halo, mode="auto", backend="gloo")
         same = all(np.array_equal(x, y) for x, y in zip(first[0][:5], res2[:5]))
         _phase(q, rank, "destroy_process_group")
         q.put(("done", rank, (res, sc.in_state, (sc.exchange_mode, same, first[1], sc.order_fixes,
-                                                 sc.tab32_used))))
+                                                 sc.tab32_used, sc.tab_redo))))
     except Exception as e:  # report to the parent instead of hanging the collective
         q.put(("done", rank, (repr(e), None, None)))
         raise
@@ -198,7 +203,7 @@ def _check(case, world, halo=4096, mode="auto", want_mode=None, backend="gloo"):
         assert g.shape == r.shape, f"{case} x{world}: {name} shape {g.shape} vs {r.shape}"
         assert np.array_equal(g, r), f"{case} x{world}: {name} differs"
     for r in range(world):
-        emode, same, totals, _, _ = got[r][2]
+        emode, same, totals = got[r][2][:3]
         assert same, f"rank {r}: a second run differs"
         assert totals == (len(ref[0]), len(ref[4])), totals
         if want_mode:
@@ -285,6 +290,15 @@ def test_shard_eight_ranks_32bit_tables():
     assert all(got[r][2][4] == 2 for r in range(8)), [got[r][2][4] for r in range(8)]  # (two runs)
 
 
+def test_shard_32bit_table_overflow_redone_wide():
+    """A value too wide for the 32-bit partial tables (2 ranks: 2 tag bits, 29 value bits)
+    sets the shard's overflow flag (PartTab::put), the speculative tables are discarded and
+    every rank redoes them with 64-bit entries -- same output as the single merge."""
+    got, _ = _check(("wide_value", 200_000, 2_000, 4), 2, want_mode="range")
+    assert all(got[r][2][4] == 2 for r in range(2))   # the speculative 32-bit step ran (two runs)
+    assert all(got[r][2][5] == 2 for r in range(2)), [got[r][2][5] for r in range(2)]  # ... and was redone
+
+
 def test_shard_eight_ranks_sample_sort_shuffled():
     _check(("c2s", 400_000, 4_000, 7), 8, want_mode="sample")
 
@@ -357,40 +371,36 @@ def test_bench_two_ranks_sharded():
         assert out["value"] > 0 and "key-range shards" in out["config"]["parallelism"]
 
 
-def _full_worker(rank, world, store_path, q):
-    import hashlib
+_FIELDS = ("kind", "ts", "oid_hi", "oid_lo", "sym", "v0", "v1")
+
+
+def _full_worker(rank, world, store_path, q, datadir):
+    """One rank of the full-size config-3 merge: its index slices of the global logs,
+    memory-mapped from the files the parent wrote (the logs are generated once), one
+    sharded run, and this shard's results written back for the parent to assemble."""
     import torch
     import torch.distributed as dist
     _phase(q, rank, "init_process_group")
     _init(rank, world, store_path)
     try:
-        _phase(q, rank, "generate c3")
-        from semantic_merge_amd import shard, synth
-        soa = synth.lift_soa(synth.lift_logs(synth.CONFIGS["c3"]))
+        _phase(q, rank, "map c3")
+        from semantic_merge_amd import shard
+        from semantic_merge_amd.marshal import SoA
+        meta = np.load(os.path.join(datadir, "meta.npy"))
+        cols = {f: np.load(os.path.join(datadir, f + ".npy"), mmap_mode="r") for f in _FIELDS}
+        soa = SoA(int(meta[0]), int(meta[1]), n_sym=int(meta[2]), **cols)
         a, b, na, nb = shard.slices_from_soa(soa, rank, world, "cuda:0")
-        del soa
-        sc = shard.ShardedCompose(a, b, na, nb, 1_000_000, shard.Comm(), "cuda:0", mode="range")
+        del soa, cols
+        sc = shard.ShardedCompose(a, b, na, nb, int(meta[2]), shard.Comm(), "cuda:0", mode="range")
         del a, b
         _phase(q, rank, "run")
         sc.run()
         res = sc.results()
+        _phase(q, rank, "write results")
+        np.savez(os.path.join(datadir, f"res_{rank}.npz"), *res[:5], seg=np.asarray(res[5], np.int64))
         del sc
         torch.cuda.empty_cache()
-        _phase(q, rank, "gather outputs")
-        if rank == 0:  # gather the other shards' outputs, assemble, digest
-            parts = [res]
-            for r in range(1, world):
-                got = [None]
-                dist.recv_object_list(got, src=r)
-                parts.append(got[0])
-            glob = shard.assemble(parts)
-            h = hashlib.sha256()
-            for arr in glob:
-                h.update(np.ascontiguousarray(arr, dtype=np.int32).tobytes())
-            q.put(("done", rank, (len(glob[0]), len(glob[4]), h.hexdigest())))
-        else:
-            dist.send_object_list([res], dst=0)
-            q.put(("done", rank, None))
+        q.put(("done", rank, None))
     except Exception as e:  # report to the parent instead of hanging the collective
         q.put(("done", rank, repr(e)))
         raise
@@ -398,20 +408,51 @@ def _full_worker(rank, world, store_path, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(900)
-def test_shard_full_size_c3_two_ranks():
-    """Config 3 at full size (100M ops, 1M symbols) as one merge over two shards: the
-    assembled output's sha256 equals the C oracle's digest of the single merge
-    (tests/golden/full_digests.json)."""
+def _full_c3_sharded(world):
+    """Config 3 at full size (100M ops, 1M symbols) as ONE merge over `world` key-range
+    shards on this GPU (gloo): the assembled output's sha256 against the C oracle's
+    digest of the single merge (tests/golden/full_digests.json)."""
+    import hashlib
     import json
+    from semantic_merge_amd import shard, synth
     rec = {r["name"]: r for r in json.load(open(os.path.join(os.path.dirname(__file__), "golden",
                                                              "full_digests.json")))}["c3"]
-    got = _spawn(_full_worker, 2, (), timeout=400)
-    assert not isinstance(got[1], str), got[1]
-    assert not isinstance(got[0], str), got[0]
-    n_out, n_conf, digest = got[0]
-    assert (n_out, n_conf) == (rec["n_out"], rec["n_conflicts"])
-    assert digest == rec["sha256"]
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    datadir = tempfile.mkdtemp(prefix="smx_c3_", dir=base)
+    try:
+        soa = synth.lift_soa(synth.lift_logs(synth.CONFIGS["c3"]))
+        for f in _FIELDS:
+            np.save(os.path.join(datadir, f + ".npy"), getattr(soa, f))
+        np.save(os.path.join(datadir, "meta.npy"), np.array([soa.n_a, soa.n_b, soa.n_sym], np.int64))
+        del soa
+        got = _spawn(_full_worker, world, (datadir,), timeout=400)
+        for r in range(world):
+            assert got[r] is None, f"rank {r}: {got[r]}"
+        parts = []
+        for r in range(world):
+            z = np.load(os.path.join(datadir, f"res_{r}.npz"))
+            parts.append(tuple(z[f"arr_{i}"] for i in range(5)) + ([tuple(x) for x in z["seg"].tolist()],))
+        glob = shard.assemble(parts)
+        h = hashlib.sha256()
+        for arr in glob:
+            h.update(np.ascontiguousarray(arr, dtype=np.int32).tobytes())
+        assert (len(glob[0]), len(glob[4])) == (rec["n_out"], rec["n_conflicts"])
+        assert h.hexdigest() == rec["sha256"]
+    finally:
+        shutil.rmtree(datadir, ignore_errors=True)
+
+
+@pytest.mark.timeout(900)
+def test_shard_full_size_c3_two_ranks():
+    _full_c3_sharded(2)
+
+
+@pytest.mark.timeout(1100)
+def test_shard_full_size_c3_eight_ranks():
+    """BASELINE config 3's geometry (100M ops over 8 shards) rehearsed on one GPU with
+    8 gloo ranks: 7 key-range splitters, halos and region hand-offs at 7 boundaries, an
+    8-way MAX all-reduce of 1M-symbol tables -- against the single merge's digest."""
+    _full_c3_sharded(8)
 
 
 @pytest.mark.parametrize("na,nb,offb,order", [(1000, 777, 1200, True), (5, 40, 10, True), (0, 50, 3, True),

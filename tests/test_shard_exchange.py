@@ -296,3 +296,39 @@ def test_host_cuts_match_full_searches(seed):
         else:
             assert np.array_equal(got, want), (tau, got, want)
     assert declined < 20
+
+
+def test_tab32_bits_within_library_limit():
+    """The 32-bit partial tables are used only for worlds whose rank tag fits the limit
+    smx_shard_step accepts (tab32 <= 8 bits); larger worlds keep the 64-bit tables."""
+    from semantic_merge_amd.shard import TAB32_MAX_BITS, tab32_bits
+    assert TAB32_MAX_BITS == 8
+    assert tab32_bits(1) == 1 and tab32_bits(8) == 4 and tab32_bits(255) == 8
+    assert tab32_bits(256) == 0 and tab32_bits(1 << 14) == 0
+
+
+def test_range_info_empty_slice_keys_are_zero():
+    """The range info's host path (gloo, CPU tensors) reads key 0 for every entry of an
+    empty branch slice, as the device kernel k_range_info writes them (tests/test_gpu_shard.py
+    pins the device layout)."""
+    import torch.distributed as dist
+    from semantic_merge_amd import shard
+    from semantic_merge_amd.marshal import SoA
+    store = _store_path()
+    dist.init_process_group("gloo", store=dist.FileStore(store, 1), rank=0, world_size=1)
+    try:
+        full = _soa(2_000, 5, 64)
+        na = full.n_a
+        soa = SoA(na, 0, full.kind[:na], full.ts[:na], full.oid_hi[:na], full.oid_lo[:na], full.sym[:na],
+                  full.v0[:na], full.v1[:na], full.n_sym)
+        a, b, ga, gb = shard.slices_from_soa(soa, 0, 1, "cpu")
+        sc = shard.ShardedCompose(a, b, ga, gb, soa.n_sym, shard.Comm(), "cpu", halo_cap=64, mode="auto")
+        info = sc._range_info().numpy()
+        RH = shard.RH
+        assert info[0] == na and info[1] == 0
+        assert info[4] == 0 and info[5] == 0                       # B's first / last key
+        assert not info[9 + 2 * RH: 9 + 4 * RH].any()              # B's head and tail keys
+        assert info[9: 9 + 2 * RH].all()                           # A's are real keys (never 0 here)
+    finally:
+        dist.destroy_process_group()
+        shutil.rmtree(os.path.dirname(store), ignore_errors=True)
