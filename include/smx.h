@@ -316,6 +316,16 @@ int smx_rga_workspace_bytes(int64_t n_ops, int64_t n_lists, size_t* bytes);
 int smx_rga_replay(const smx_rga_ops* ops, const smx_rga_out* out, void* workspace,
                    size_t workspace_bytes, void* stream);
 
+/* smx_rga_replay with flags.  SMX_RGA_GROUPED: the caller's events come list by list
+ * (list ids never decrease -- what crdt.replay and the RGA drop-in build, one stream
+ * after another), so the library packs the records in place instead of partitioning
+ * them by list.  The claim is checked on the device: a list id that decreases makes the
+ * call redo itself through the partition (same results, the partition's cost).
+ * smx_rga_replay(...) == smx_rga_replay_ex(..., 0, stream). */
+#define SMX_RGA_GROUPED 1u
+int smx_rga_replay_ex(const smx_rga_ops* ops, const smx_rga_out* out, void* workspace,
+                      size_t workspace_bytes, uint32_t flags, void* stream);
+
 const char* smx_last_error(void);
 const char* smx_version(void);
 

@@ -102,6 +102,8 @@ class SmxRgaOut(C.Structure):
 
 
 # Every symbol include/smx.h declares (tests check the built library exports them).
+RGA_GROUPED = 1   # smx_rga_replay_ex flag (include/smx.h SMX_RGA_GROUPED)
+
 EXPORTS = (
     "smx_compose_workspace_bytes",
     "smx_compose",
@@ -118,6 +120,7 @@ EXPORTS = (
     "smx_reset_stage_times",
     "smx_rga_workspace_bytes",
     "smx_rga_replay",
+    "smx_rga_replay_ex",
     "smx_last_error",
     "smx_version",
 )
@@ -160,6 +163,9 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.smx_rga_replay.argtypes = [C.POINTER(SmxRgaOps), C.POINTER(SmxRgaOut), C.c_void_p,
                                    C.c_size_t, C.c_void_p]
     lib.smx_rga_replay.restype = C.c_int
+    lib.smx_rga_replay_ex.argtypes = [C.POINTER(SmxRgaOps), C.POINTER(SmxRgaOut), C.c_void_p,
+                                      C.c_size_t, C.c_uint32, C.c_void_p]
+    lib.smx_rga_replay_ex.restype = C.c_int
     lib.smx_last_error.argtypes = []
     lib.smx_last_error.restype = C.c_char_p
     lib.smx_version.argtypes = []

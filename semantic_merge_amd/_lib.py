@@ -236,10 +236,12 @@ def stage_times():
     return {L.smx_stage_name(i).decode(): (ms[i], calls[i]) for i in range(n)}
 
 
-def rga_replay_device(batch, device: str = "cuda", tombstones: bool = False):
+def rga_replay_device(batch, device: str = "cuda", tombstones: bool = False, grouped: bool = False):
     """(values, src, offsets) of a batched RGA replay computed on the GPU; with
     tombstones=True the whole list state (live and tombstoned elements, crdt.py RGA.list)
-    and a fourth array, the tombstone flags."""
+    and a fourth array, the tombstone flags.  grouped=True: the batch's events come list
+    by list (non-decreasing list ids, as crdt.marshal_streams builds them): the library
+    skips its partition by list (it checks the claim and partitions when it is false)."""
     torch = _torch()
     dev = torch.device(device)
     n = batch.n
@@ -263,8 +265,9 @@ def rga_replay_device(batch, device: str = "cuda", tombstones: bool = False):
     wst = torch.empty(max(ws.value, 1), dtype=torch.uint8, device=dev)
     ops = _abi.SmxRgaOps(n, batch.n_lists, *[_ptr(t) for t in ins])
     out = _abi.SmxRgaOut(_ptr(vals), _ptr(src), _ptr(offs), _ptr(counts), _ptr(tomb))
-    check(lib().smx_rga_replay(C.byref(ops), C.byref(out), _ptr(wst), ws.value,
-                               torch.cuda.current_stream(dev).cuda_stream))
+    check(lib().smx_rga_replay_ex(C.byref(ops), C.byref(out), _ptr(wst), ws.value,
+                                  _abi.RGA_GROUPED if grouped else 0,
+                                  torch.cuda.current_stream(dev).cuda_stream))
     torch.cuda.synchronize(dev)
     k = int(counts.item())
     res = (vals[:k].cpu().numpy().view(np.uint32), src[:k].cpu().numpy(), offs.cpu().numpy())

@@ -104,7 +104,7 @@ def replay(streams: Sequence[Sequence[Event]]) -> List[List[Any]]:
     """Materialize every stream (one RGA per stream) on the GPU."""
     from ._lib import rga_replay_device  # the HIP library; raises if missing
     batch = marshal_streams(streams)
-    _, src, offsets = rga_replay_device(batch)
+    _, src, offsets = rga_replay_device(batch, grouped=True)  # (marshal_streams: stream after stream)
     srcl = src.tolist()
     offl = offsets.tolist()
     return [[batch.values[s] for s in srcl[offl[i]:offl[i + 1]]] for i in range(len(streams))]
@@ -116,7 +116,7 @@ def replay_lists(streams: Sequence[Sequence[Event]]) -> List[List[Elem]]:
     tombstone)`` with the key and value of the event that created it."""
     from ._lib import rga_replay_device  # the HIP library; raises if missing
     batch = marshal_streams(streams)
-    _, src, offsets, tomb = rga_replay_device(batch, tombstones=True)
+    _, src, offsets, tomb = rga_replay_device(batch, tombstones=True, grouped=True)
     events = [ev for stream in streams for ev in stream]
     srcl, tl, offl = src.tolist(), tomb.tolist(), offsets.tolist()
     return [[Elem(events[s][1], events[s][2], bool(tb)) for s, tb in
@@ -219,6 +219,6 @@ def _replay_list_src(stream: Sequence[Event]) -> Tuple[List[int], List[int]]:
     of the final list, in list order."""
     from ._lib import rga_replay_device  # the HIP library; raises if missing
     batch = marshal_streams([stream])
-    _, src, offsets, tomb = rga_replay_device(batch, tombstones=True)
+    _, src, offsets, tomb = rga_replay_device(batch, tombstones=True, grouped=True)
     n = int(offsets[1])
     return src[:n].tolist(), tomb[:n].tolist()

@@ -1782,15 +1782,15 @@ static int launch_presorted_windows(const Ctx& C, i64 W, i64 CM, int level) {
   } else
 #endif
   if (wide) {
-    if (P.src_map) hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, true>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
-    else hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, false>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
+    if (P.src_map) hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, true, WF_RUNS_WIDE>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
+    else hipLaunchKernelGGL((k_window_f<WF_WIDE_CAP, WF_WIDE_NT, false, false, WF_RUNS_WIDE>), dim3(W), dim3(WF_WIDE_NT), 0, st, P);
   } else if (level == WL_SMALL) {
     if (P.src_map) hipLaunchKernelGGL((k_window_f<WF_SMALL_CAP, WF_SMALL_NT, false, true>), dim3(W), dim3(WF_SMALL_NT), 0, st, P);
     else hipLaunchKernelGGL((k_window_f<WF_SMALL_CAP, WF_SMALL_NT, false, false>), dim3(W), dim3(WF_SMALL_NT), 0, st, P);
   } else if (P.src_map) {
-    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, true>), dim3(W), dim3(WF_NT), 0, st, P);
+    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, true, WF_RUNS>), dim3(W), dim3(WF_NT), 0, st, P);
   } else {
-    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, false>), dim3(W), dim3(WF_NT), 0, st, P);
+    hipLaunchKernelGGL((k_window_f<WF_CAP, WF_NT, false, false, WF_RUNS>), dim3(W), dim3(WF_NT), 0, st, P);
   }
   HIP_TRY(hipGetLastError());
   C.tm->end(stage);

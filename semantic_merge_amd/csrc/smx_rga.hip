@@ -318,6 +318,44 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
 #ifndef RGA_OUT_LPW
 #define RGA_OUT_LPW 1  // lists per wave in k_rga_out_fused (4: 28.8 us either way, profiles/r04_aj)
 #endif
+// err word bits: RGA_E_INPUT a list id >= n_lists or an op > 2 (the call fails);
+// RGA_E_UNGROUPED a call that said its events come grouped by list (SMX_RGA_GROUPED) has a
+// list id that decreases: every list kernel leaves at once and the call is redone with
+// the partition
+#define RGA_E_INPUT 1
+#define RGA_E_UNGROUPED 2
+
+// Events already grouped by list (non-decreasing list ids: what crdt.replay and RGA
+// hand over, stream after stream): the records are packed in place of the partition --
+// one coalesced pass, four consecutive events per thread -- and the list starts come
+// from the steps of the list id.  Also zeroes the survivor chunk sums (k_rga_bounds' duty).
+__global__ void __launch_bounds__(BLOCK) k_rga_pack(smx_rga_ops o, u64* __restrict__ rout, u32* __restrict__ lstart,
+                                                    u32* __restrict__ csum, i32* __restrict__ err) {
+  const i64 n = o.n_ops, nl = o.n_lists;
+  if (blockIdx.x == 0 && threadIdx.x < RGA_CS_MAX) csum[threadIdx.x] = 0u;
+  u32 bad = 0;
+  // consecutive lanes, consecutive events: coalesced column loads, one 16-byte record store
+  for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (i64)gridDim.x * BLOCK) {
+    const u32 l = o.list[i], op = o.op[i], v = o.value[i], an = o.anchor[i];
+    const i64 t = o.t[i];
+    const u32 prev = i > 0 ? o.list[i - 1] : 0u;  // (the neighbour lane's load: an L1 hit)
+    bad |= (l >= (u64)nl || op > 2) ? (u32)(RGA_E_INPUT | RGA_E_UNGROUPED) : 0u;
+    bad |= i > 0 && l < prev ? (u32)RGA_E_UNGROUPED : 0u;
+    const u64 tt = (u64)t ^ 0x8000000000000000ull;
+    R16 r;
+    r.a = ((u64)an << 32) | (tt >> 32);
+    r.b = ((u64)v << 32) | ((op > 2 ? 0u : op) << 30) | (u32)i;
+    *reinterpret_cast<R16*>(rout + (u64)i * RGA_REC) = r;
+    // list starts: the lists in (prev, l] start here (from list 0 at the first event);
+    // after the last event the rest start at n (ids clamped: one out of range fails the call)
+    const u32 lo = i == 0 ? 0u : prev + 1u, hi = l < (u64)nl ? l : (u32)(nl - 1);
+    for (u32 L = lo; L <= hi; ++L) lstart[L] = (u32)i;
+    if (i == n - 1)
+      for (i64 L = (i64)hi + 1; L < nl; ++L) lstart[L] = (u32)n;
+  }
+  if (bad) atomicOr(err, (i32)bad);
+}
+
 __global__ void k_rga_bounds(const u32* __restrict__ keys, i64 n, i64 nl, u32* __restrict__ lstart,
                              u32* __restrict__ csum) {
   if (blockIdx.x == 0 && threadIdx.x < RGA_CS_MAX) csum[threadIdx.x] = 0u;
@@ -1148,8 +1186,9 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) RW_OCC k_rga_wave(smx_rga_ops
                                                              const u32* __restrict__ lstart,
                                                              i64 n, i64 nl, u32* __restrict__ tmp_v,
                                                              u32* __restrict__ tmp_s, u32* __restrict__ scnt,
-                                                             int tomb) {
+                                                             int tomb, const i32* __restrict__ gate) {
   __shared__ RwLds<RW_CAP> lds[RW_WAVES];
+  if (*gate & RGA_E_UNGROUPED) return;  // (a grouped call whose list ids decrease: redone partitioned)
   const u32 lane = threadIdx.x & (WAVE - 1);
   // the wave index as a scalar: the list index, its bounds and the slice base stay in
   // SGPRs (scalar loads of lstart; LDS member offsets fold into the instructions)
@@ -1195,8 +1234,9 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(smx_rga_ops o, co
                                                               i64 n, i64 nl, u32* __restrict__ defer,
                                                               u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
                                                               u32* __restrict__ tmp_s, u32* __restrict__ scnt,
-                                                              int tomb) {
+                                                              int tomb, const i32* __restrict__ gate) {
   __shared__ RwLds<2 * RW_CAP> lds[RW_WAVES];
+  if (*gate & RGA_E_UNGROUPED) return;
   const u32 lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   const u64 nw = (u64)gridDim.x * RW_WAVES;
   for (u64 l0 = ((u64)blockIdx.x * RW_WAVES + w) * WAVE; l0 < (u64)nl; l0 += nw * WAVE) {
@@ -1310,7 +1350,8 @@ __global__ void __launch_bounds__(1024) k_rga_big(smx_rga_ops o, const u64* __re
                                                   i64 nl, const u32* __restrict__ todo, const u32* __restrict__ ntodo,
                                                   u8* __restrict__ bst, u32* __restrict__ gp,
                                                   u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
-                                                  u32* __restrict__ scnt, int tomb) {
+                                                  u32* __restrict__ scnt, int tomb, const i32* __restrict__ gate) {
+  if (*gate & RGA_E_UNGROUPED) return;
   for (u32 item = blockIdx.x; item < *ntodo; item += gridDim.x) {
     __syncthreads();
     rga_big_list(o, R, todo[item], lstart, n, nl, bst, gp, tmp_v, tmp_s, scnt, tomb != 0);
@@ -1326,8 +1367,9 @@ __global__ void __launch_bounds__(1024) k_rga_big(smx_rga_ops o, const u64* __re
 // survivors are read before it is known.
 __global__ void __launch_bounds__(BLOCK) k_rga_out_fused(const u32* __restrict__ tmp_v, const u32* __restrict__ tmp_s,
                                                         const u32* __restrict__ lstart, const u32* __restrict__ scnt,
-                                                        i64 nl, smx_rga_out out) {
+                                                        i64 nl, smx_rga_out out, const i32* __restrict__ gate) {
   constexpr int LPW = RGA_OUT_LPW;
+  if (*gate & RGA_E_UNGROUPED) return;
   static_assert(RGA_CS_LISTS % LPW == 0, "a wave's lists share a chunk");
   const u32 lane = threadIdx.x & (WAVE - 1);
   const i64 l0 = ((i64)blockIdx.x * (BLOCK / WAVE) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE))) * LPW;
@@ -1388,7 +1430,9 @@ __global__ void __launch_bounds__(BLOCK) k_rga_out_fused(const u32* __restrict__
 // (k_rga_out_fused: RGA_OUT_PRE loads per lane issued with the offset's loads)
 __global__ void __launch_bounds__(BLOCK) k_rga_out(const u32* __restrict__ tmp_v, const u32* __restrict__ tmp_s,
                                                   const u32* __restrict__ lstart, const u32* __restrict__ scnt,
-                                                  const u32* __restrict__ soff, i64 nl, smx_rga_out out) {
+                                                  const u32* __restrict__ soff, i64 nl, smx_rga_out out,
+                                                  const i32* __restrict__ gate) {
+  if (*gate & RGA_E_UNGROUPED) return;
   const u32 lane = threadIdx.x & (WAVE - 1);
   const i64 l = (i64)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE;
   if (l >= nl) return;
@@ -1402,7 +1446,8 @@ __global__ void __launch_bounds__(BLOCK) k_rga_out(const u32* __restrict__ tmp_v
   if (lane == 0) out.out_offsets[l] = d;
 }
 
-__global__ void k_rga_fin(const u32* __restrict__ soff_total, i64 n_lists, smx_rga_out out) {
+__global__ void k_rga_fin(const u32* __restrict__ soff_total, i64 n_lists, smx_rga_out out, const i32* __restrict__ gate) {
+  if (*gate & RGA_E_UNGROUPED) return;
   out.out_offsets[n_lists] = *soff_total;
   out.counts[0] = *soff_total;
 }
@@ -1451,7 +1496,8 @@ extern "C" int smx_rga_workspace_bytes(int64_t n_ops, int64_t n_lists, size_t* b
   return SMX_OK;
 }
 
-static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, size_t wsb, hipStream_t st) {
+static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, size_t wsb, hipStream_t st,
+                    bool grouped) {
   const i64 n = ops->n_ops, nl = ops->n_lists;
   if (n < 0 || nl < 0 || n > (i64)RGA_IDX_MASK || nl >= (i64)0x7fffffff)
     return smx_set_error(SMX_E_ARG, "bad sizes");
@@ -1495,7 +1541,10 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
     g_cus = cus > 0 ? cus : 256;
     g_rr_grid = g_cus * RR_PER_CU;
   }
-  {  // records grouped by list: LSD passes over the list id, ping-pong into rec
+  if (grouped) {  // the caller's events come list by list: no partition
+    const int pgrid = (int)(SMX_CEIL_DIV(n, (i64)BLOCK) < 8192 ? SMX_CEIL_DIV(n, (i64)BLOCK) : 8192);
+    hipLaunchKernelGGL(k_rga_pack, dim3(pgrid), dim3(BLOCK), 0, st, *ops, rec, lstart, scnt - RGA_CS_MAX, err);
+  } else {  // records grouped by list: LSD passes over the list id, ping-pong into rec
     int npass = 1;
     while (npass < 4 && ((u64)(nl - 1) >> (8 * npass)) != 0) ++npass;
     const int nblk = (int)SMX_CEIL_DIV(n, (i64)RREC_TILE);
@@ -1539,35 +1588,42 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   if (RW_PER_CU > 0 && wg > (i64)g_cus * RW_PER_CU) wg = (i64)g_cus * RW_PER_CU;
   const dim3 wgrid((u32)wg);
   hipLaunchKernelGGL(k_rga_wave, wgrid, dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, tmp_v, tmp_s, scnt,
-                     tomb);
+                     tomb, (const i32*)err);
   // lists of more than RW_CAP events (a few, if any).  (On a second stream beside
   // k_rga_wave they measured no faster: their workgroups trail k_rga_wave's, and the
   // join costs ~14 us, profiles/r04_s.)
   hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, def2, ndef + 1,
-                     tmp_v, tmp_s, scnt, tomb);
+                     tmp_v, tmp_s, scnt, tomb, (const i32*)err);
   hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
-                     tmp_s, scnt, tomb);
+                     tmp_s, scnt, tomb, (const i32*)err);
   if (nl <= RGA_FUSED_MAX) {  // each list's wave finds its own offset
     hipLaunchKernelGGL(k_rga_out_fused, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE * RGA_OUT_LPW))), dim3(BLOCK), 0, st, tmp_v,
-                       tmp_s, lstart, scnt, nl, *out);
+                       tmp_s, lstart, scnt, nl, *out, (const i32*)err);
   } else {
     RGA_TRY((scan_excl<OpSum, u32, u32>(scnt, soff, nl, nullptr, part, totals, st)));
     hipLaunchKernelGGL(k_rga_out, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE))), dim3(BLOCK), 0, st, tmp_v, tmp_s,
-                       lstart, scnt, soff, nl, *out);
-    hipLaunchKernelGGL(k_rga_fin, dim3(1), dim3(1), 0, st, totals, nl, *out);
+                       lstart, scnt, soff, nl, *out, (const i32*)err);
+    hipLaunchKernelGGL(k_rga_fin, dim3(1), dim3(1), 0, st, totals, nl, *out, (const i32*)err);
   }
   RGA_TRY(hipGetLastError());
   i32 herr = 0;
   RGA_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
   RGA_TRY(hipStreamSynchronize(st));
-  if (herr) return smx_set_error(SMX_E_ARG, "invalid input: list >= n_lists or op > 2");
+  if (herr & RGA_E_INPUT) return smx_set_error(SMX_E_ARG, "invalid input: list >= n_lists or op > 2");
+  if (herr & RGA_E_UNGROUPED) return rga_impl(ops, out, ws, wsb, st, false);  // (not grouped after all)
   return SMX_OK;
 }
 
 
+extern "C" int smx_rga_replay_ex(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, size_t wsb,
+                                 uint32_t flags, void* stream) {
+  if (!ops) return SMX_E_ARG;
+  if (flags & ~(uint32_t)SMX_RGA_GROUPED) return smx_set_error(SMX_E_ARG, "unknown smx_rga_replay_ex flag");
+  (void)hipGetLastError();  // an earlier call's error (any library's) is not this call's
+  return rga_impl(ops, out, ws, wsb, (hipStream_t)stream, (flags & SMX_RGA_GROUPED) != 0);
+}
+
 extern "C" int smx_rga_replay(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, size_t wsb,
                               void* stream) {
-  if (!ops) return SMX_E_ARG;
-  (void)hipGetLastError();  // an earlier call's error (any library's) is not this call's
-  return rga_impl(ops, out, ws, wsb, (hipStream_t)stream);
+  return smx_rga_replay_ex(ops, out, ws, wsb, 0u, stream);
 }

@@ -291,6 +291,12 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_OUT2
 #define WF_OUT2 1    // steps 7-9 staged by final slot (inv), four slots per thread, 16-byte stores: window 1.271 -> 1.233 ms (profiles/r03_m/ab.txt)
 #endif
+#ifndef WF_RUNS
+#define WF_RUNS 1    // the normal presorted windows order by runs and (kind, run) groups (no merge / multisplit)
+#endif
+#ifndef WF_RUNS_WIDE
+#define WF_RUNS_WIDE 1  // ... and the wide ones (config 5: one run per window)
+#endif
 #ifndef WF_STB_KIND
 #define WF_STB_KIND 1  // v0 / v1 staged for moves and renames only (the other kinds output neither)
 #endif
@@ -299,7 +305,7 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #else
 #define WF_BOUNDS __launch_bounds__(WF_NT, WF_MINB)
 #endif
-template <int CAP, int NT, bool DBG, bool MAP>
+template <int CAP, int NT, bool DBG, bool MAP, bool RUNS = false>
 __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinArgs P) {
   // CAP ops per window on NT threads: (2048, 512) four windows per CU; (8192, 1024) one
   // window per CU for logs whose equal-timestamp groups need it (config 5)
@@ -443,7 +449,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     bad |= ok & ((kr >= SMX_N_KINDS) | (sym_r[i] >= (u64)P.n_sym));
     const u32 k = kr < SMX_N_KINDS ? kr : SMX_N_KINDS - 1;
     sts[e] = ts_r[i];
-    skind[e] = (u8)k;
+    if constexpr (!RUNS) skind[e] = (u8)k;  // (the run-grouped order keeps the kinds in registers)
     const bool mv = ok & (k == KMOVE), rn = ok & (k == KREN);
     const bool ha = v0_r[i] >= 0, hf = v1_r[i] >= 0;
     sym_r[i] = (sym_r[i] & SYM_MASK) | ((mv & ha) ? MS_HAS_A : 0u) | ((mv & hf) ? MS_HAS_F : 0u);
@@ -484,6 +490,8 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
   }
   if (bad) P.meta->bad_sym = 1;
   for (int i = t; i < NCH * SMX_N_KINDS; i += NT) (&ccnt[0][0])[i] = 0;
+  if constexpr (RUNS)  // the run-grouped order's bucket counters (fin is next written by step 6)
+    for (int i = t; i < CAP / 2; i += NT) reinterpret_cast<u32*>(fin)[i] = 0u;
   if (t <= SMX_N_KINDS) base[t] = base_v;
   if (t < SMX_N_KINDS) wck[t] = 0;
   if (t < SMX_N_KINDS + 2) woffk[t] = woff_x + woff_y;
@@ -528,6 +536,266 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
   }
 #endif
 
+  const int nch = (sz + WAVE - 1) / WAVE;
+  auto group_of = [&](int p, int* gs_o, int* ge_o) {
+    const int bit = p & 63;
+    int wi = p >> 6;
+    u64 word = gbits[wi] & (bit == 63 ? ~0ull : ((1ull << (bit + 1)) - 1));
+    while (word == 0) word = gbits[--wi];
+    *gs_o = wi * 64 + 63 - __clzll(word);
+    wi = p >> 6;
+    word = bit == 63 ? 0ull : (gbits[wi] & ~((1ull << (bit + 1)) - 1));
+    while (word == 0 && ++wi < nch) word = gbits[wi];
+    const int ge = word ? wi * 64 + __ffsll((unsigned long long)word) - 1 : sz;
+    *ge_o = ge < sz ? ge : sz;
+  };
+  bool btie = false;  // two equal 32-bit keys in one group (steps 2-5: the exact re-rank below)
+  // ---- Run-grouped order (RUNS): no merge, no multisplit.  Inside a branch part the
+  // timestamps never decrease, so the equal-timestamp ops of both parts form one run of
+  // the merged order S, which starts at S position spos(v) = #{A ops < v} + #{B ops < v}
+  // (A first on ties, compose.py:54).  Each run's heads (the first op of its value in a
+  // part) find spos by a 64-way search of the other part; the runs' dense index r comes
+  // from an occupancy mask over S positions.  An op's group is (kind, r) and the
+  // groups laid out kind-major ARE the window's T order of groups (T is ordered by kind,
+  // then timestamp): one histogram + scan of KD * R counters gives every group's start,
+  // then each group is ordered by (id, side, index) with interpolation buckets (one op
+  // per bucket on random ids) and a rank inside the bucket, equal 32-bit keys on the
+  // full ids.  A window with more than GMAX groups (very many distinct timestamps) fails
+  // the plan as a window too large (f_fail 2): the host retries with smaller windows.
+  constexpr bool runs_ok = RUNS;
+  if constexpr (RUNS) {
+    constexpr int OW = CAP / 32;     // occupancy words over S positions
+    constexpr int GMAX = 4 * CAP;    // group counters (u16, in sts once the timestamps are dead)
+    u32* occ = reinterpret_cast<u32*>(&ccnt[0][0]);  // (zeroed with ccnt before the load barrier)
+    static_assert(sizeof(ccnt) >= OW * sizeof(u32), "occupancy words inside ccnt");
+    __shared__ u16 occpre[OW];
+    __shared__ u16 lasth[NCH];       // last head at or before the end of each 64-op chunk
+    __shared__ u32 rinfo[2];         // groups fit, R
+    u16* sp = sl;                    // S position of each head's run (element space)
+    u32* gcnt = reinterpret_cast<u32*>(sts);             // group counters, two u16 per word
+    static_assert(GMAX / 2 * sizeof(u32) <= sizeof(sts), "group counters inside sts");
+    u32* bcnt = reinterpret_cast<u32*>(fin);             // bucket counters, two u16 per word (zeroed before the load barrier)
+    u32* mkey = reinterpret_cast<u32*>(sts);             // bucket order: 32-bit keys (after the group starts are dead)
+    u16* mel = reinterpret_cast<u16*>(reinterpret_cast<u32*>(sts) + CAP);  // ... and elements
+    // a. run heads, the order check, each head's run position
+    bool dec = false;
+    if (t == 0) {
+      dec = (a0 > 0 && na > 0 && prev_a > sts[0]) || (b0 > 0 && nb > 0 && prev_b > sts[na]);
+      win_publish_widths(P.meta, &vbw[0][0], WAVES, vcur);
+    }
+    u64 hbr[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int e = t + NT * i;
+      const bool valid = e < sz;
+      const bool first = e == 0 || e == na;
+      const u64 pv = sts[valid && !first ? e - 1 : 0];
+      const bool head = valid && (first || pv != ts_r[i]);
+      dec |= valid && !first && pv > ts_r[i];
+      hbr[i] = __ballot(head);
+      const int c = (NT * i) / WAVE + wv;  // this item's 64-op chunk (wave-uniform)
+      if (lane == 0 && c < NCH) gbits[c] = hbr[i];
+      // the heads of this chunk, one at a time with the whole wave: a 64-way search of
+      // the other part for #{ops < v} (two or three rounds of one LDS read per lane)
+      u64 hb = hbr[i];
+      while (hb) {
+        const int hl = __ffsll((unsigned long long)hb) - 1;
+        hb &= hb - 1;
+        const int eh = c * WAVE + hl;
+        const u64 v = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(ts_r[i] >> 32), hl) << 32) |
+                      (u64)(u32)__builtin_amdgcn_readlane((int)(u32)ts_r[i], hl);
+        const bool sa = eh < na;
+        const int o0 = sa ? na : 0, no = sa ? nb : na;
+        int lo = 0, len = no;  // answer in [lo, lo + len]; everything before lo is < v
+        while (len > 0) {
+          const int S = (len + WAVE - 1) / WAVE;
+          const int q = lane * S;
+          const bool pr = q < len && sts[o0 + lo + (q < len ? q : 0)] < v;
+          const int cnt = __popcll(__ballot(pr));
+          if (cnt == 0) break;
+          const int qp = lo + (cnt - 1) * S;  // the last sample below v
+          const int hi = min(qp + S, lo + len);
+          lo = qp + 1;
+          len = hi - lo;
+        }
+        const int spos = (sa ? eh : eh - na) + lo;
+        if (lane == 0) {
+          sp[eh] = (u16)spos;
+          atomicOr(&occ[spos >> 5], 1u << (spos & 31));
+        }
+      }
+    }
+    if (__syncthreads_or(dec)) {
+      if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
+      return;
+    }
+    // b. (wave 0) the last head of each chunk, the runs' dense index, the group count
+    const u32 kpres = __builtin_amdgcn_readfirstlane(kmask_r);
+    const int KD = __popc(kpres);
+    if (wv == 0) {
+      static_assert(NCH <= 2 * WAVE && OW <= 4 * WAVE, "one wave covers the chunks and occupancy words");
+      u32 carry = 0;  // (last head + 1; 0 = none yet)
+#pragma unroll
+      for (int c0 = 0; c0 < NCH; c0 += WAVE) {
+        const int c = c0 + lane;
+        const u64 hw = c < nch ? gbits[c] : 0ull;
+        u32 lh = hw ? (u32)(c * WAVE + 63 - __clzll(hw)) + 1u : 0u;
+        lh = max(wave_incl_max_u32(lh), carry);
+        if (c < NCH) lasth[c] = (u16)(lh ? lh - 1u : 0u);
+        carry = (u32)__builtin_amdgcn_readlane((int)lh, WAVE - 1);
+      }
+      u32 rsum = 0;
+#pragma unroll
+      for (int w0 = 0; w0 < OW; w0 += WAVE) {
+        const int x = w0 + lane;
+        const u32 o = x < OW ? occ[x] : 0u;
+        const u32 pc = (u32)__popc(o), inc = wave_incl_sum_u32(pc);
+        if (x < OW) occpre[x] = (u16)(rsum + inc - pc);
+        rsum += (u32)__builtin_amdgcn_readlane((int)inc, WAVE - 1);
+      }
+      if (lane == 0) {
+        rinfo[0] = (u32)KD * rsum <= (u32)GMAX && !(SMX_DIAG && P.ablate == 200);
+        rinfo[1] = rsum;
+      }
+    }
+    {  // the group counters (the timestamps are dead: every head has searched)
+      typedef u32 __attribute__((ext_vector_type(4))) z4;
+      for (int i = t; i < GMAX / 8; i += NT) reinterpret_cast<z4*>(gcnt)[i] = z4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();
+    if (!rinfo[0]) {  // more (kind, run) groups than counters: smaller windows (f_fail 2)
+      if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 2ull);
+      return;
+    }
+    {
+      const u32 R = rinfo[1];
+      // c. each op's run (its head: in its chunk, else the last head of the earlier
+      //    chunks), group g = dense kind * R + run, counted
+      const u64 lem = lanemask_lt() | (1ull << lane);
+      u32 g_r[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const int e = t + NT * i;
+        const int c = (NT * i) / WAVE + wv;
+        const u64 m = hbr[i] & lem;
+        const int h = m ? c * WAVE + 63 - __clzll(m) : (int)lasth[c > 0 ? c - 1 : 0];
+        const u32 k = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
+        g_r[i] = 0xffffffffu;
+        if (e < sz) {
+          const u32 s = sp[h];
+          const u32 r = occpre[s >> 5] + (u32)__popc(occ[s >> 5] & ((1u << (s & 31)) - 1u));
+          g_r[i] = (u32)__popc(kpres & ((1u << k) - 1u)) * R + r;
+          atomicAdd(&gcnt[g_r[i] >> 1], 1u << (16 * (g_r[i] & 1)));
+        }
+      }
+      __syncthreads();
+      // d. group starts: exclusive scan of the KD * R counters (kind-major = T order), in
+      //    passes of 4 * NT counters (one pass on config 3's windows: 6 kinds x 14 runs)
+      const int GS = KD * (int)R;
+      {
+        u32 carry = 0;
+        for (int g0 = 0; g0 < GS; g0 += 4 * NT) {  // (block-uniform)
+          const int x = g0 / 2 + 2 * t;  // words x, x + 1: counters 2x .. 2x + 3
+          const u32 w0 = 2 * x < GS ? gcnt[x] : 0u, w1 = 2 * x + 2 < GS ? gcnt[x + 1] : 0u;
+          const u32 c0 = w0 & 0xffffu, c1 = w0 >> 16, c2 = w1 & 0xffffu, c3 = w1 >> 16;
+          u32 tot;
+          const u32 run = carry + block_excl_scan<OpSum, u32, WAVES>(c0 + c1 + c2 + c3, &vbw[0][0], &tot);
+          if (2 * x < GS) gcnt[x] = run | ((run + c0) << 16);
+          if (2 * x + 2 < GS) gcnt[x + 1] = (run + c0 + c1) | ((run + c0 + c1 + c2) << 16);
+          carry += tot;
+        }
+      }
+      __syncthreads();
+      auto gstart = [&](int g) -> u32 {
+        return g < GS ? (gcnt[g >> 1] >> (16 * (g & 1))) & 0xffffu : (u32)sz;
+      };
+      // kinds: window-local start and count (kind k's groups are d(k) * R .. + R)
+      if (t <= SMX_N_KINDS) {
+        u32 s = (u32)sz, e = (u32)sz;
+        if (t < SMX_N_KINDS) {
+          const int d = __popc(kpres & ((1u << t) - 1u));
+          s = R ? gstart(d * (int)R) : 0u;
+          e = ((kpres >> t) & 1u) && R ? gstart((d + 1) * (int)R) : s;
+          wck[t] = e - s;
+        }
+        kbase[t] = s;
+      }
+      // e. interpolation bucket inside the group: b = gs + (ge - gs) * key / 2^32
+      u32 b_r[ITEMS], ar_r[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        b_r[i] = 0xffffffffu;
+        ar_r[i] = 0u;
+        if (g_r[i] == 0xffffffffu) continue;
+        const u32 gs = gstart((int)g_r[i]), ge = gstart((int)g_r[i] + 1);
+        const u32 b = gs + (u32)(((u64)(ge - gs) * hi_r[i]) >> 32);
+        b_r[i] = b;
+        ar_r[i] = (atomicAdd(&bcnt[b >> 1], 1u << (16 * (b & 1))) >> (16 * (b & 1))) & 0xffffu;
+      }
+      __syncthreads();
+      // f. bucket starts
+      {
+        constexpr int WPT = CAP / (2 * NT);
+        u32 cw[WPT], sum = 0;
+#pragma unroll
+        for (int i = 0; i < WPT; ++i) {
+          cw[i] = bcnt[WPT * t + i];
+          sum += (cw[i] & 0xffffu) + (cw[i] >> 16);
+        }
+        u32 tot;
+        u32 run = block_excl_scan<OpSum, u32, WAVES>(sum, &vbw[0][0], &tot);
+#pragma unroll
+        for (int i = 0; i < WPT; ++i) {
+          const u32 c0 = cw[i] & 0xffffu, c1 = cw[i] >> 16;
+          bcnt[WPT * t + i] = run | ((run + c0) << 16);
+          run += c0 + c1;
+        }
+      }
+      __syncthreads();
+      auto bstart = [&](u32 b) -> u32 {
+        return b < (u32)CAP ? (bcnt[b >> 1] >> (16 * (b & 1))) & 0xffffu : (u32)sz;
+      };
+      // g. members in bucket order: key and element
+      u32 slot_r[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        slot_r[i] = 0u;
+        if (b_r[i] == 0xffffffffu) continue;
+        const u32 s = bstart(b_r[i]) + ar_r[i];
+        slot_r[i] = s;
+        mkey[s] = hi_r[i];
+        mel[s] = (u16)(t + NT * i);
+      }
+      __syncthreads();
+      // h. rank inside the bucket on (key, full id, side, index); the final order
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const u32 b = b_r[i];
+        if (b == 0xffffffffu) continue;
+        const int e = t + NT * i;
+        const u32 lo = bstart(b), hi = bstart(b + 1), kp = hi_r[i];
+        u32 c = 0;
+        for (u32 q = lo; q < hi; ++q) {
+          if (q == slot_r[i]) continue;
+          const u32 x = mkey[q];
+          if (x != kp) {
+            c += x < kp;
+          } else {  // equal top 32 bits: the full ids, then element order = (side, index)
+            const int eo = mel[q];
+            const i64 jm = e < na ? a0 + e : bld + e, jo = eo < na ? a0 + eo : bld + eo;
+            const u64 hm = P.khi[jm], ho = P.khi[jo], lm = P.klo[jm], lo2 = P.klo[jo];
+            c += ho < hm || (ho == hm && (lo2 < lm || (lo2 == lm && eo < e)));
+          }
+        }
+        const u32 f = lo + c;
+        sord[f] = (u16)e;
+        inv[e] = (u16)f;
+        skS[f] = (u8)(k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1);
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (!RUNS) {  // steps 2-5: merge, multisplit, group order
   // 2. merge A part [0,na) with B part [na,sz) by timestamp, A first on ties
   //    (compose.py:54): merge path, ITEMS outputs per lane, with the kinds
   //    copied into S order.  Presorted-layout check: every adjacent pair of each
@@ -678,7 +946,6 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
 
   // 3. stable multisplit of S by rank (wave ballots); element, kind and rank stay in
   //    registers for the scatter (m = t + NT * j is chunk wv + WAVES * j)
-  const int nch = (sz + WAVE - 1) / WAVE;
   int me[ITEMS];
   u32 mkr[ITEMS];  // kind | rank << 8
 #pragma unroll
@@ -795,18 +1062,6 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
   //    window in 10^4 on random ids; every duplicate id) get the same rank and leave
   //    a rank without a slot: such a window is re-ranked exactly on (oid_hi, oid_lo,
   //    slot) -- slot order is (side, index) order inside a group.
-  auto group_of = [&](int p, int* gs_o, int* ge_o) {
-    const int bit = p & 63;
-    int wi = p >> 6;
-    u64 word = gbits[wi] & (bit == 63 ? ~0ull : ((1ull << (bit + 1)) - 1));
-    while (word == 0) word = gbits[--wi];
-    *gs_o = wi * 64 + 63 - __clzll(word);
-    wi = p >> 6;
-    word = bit == 63 ? 0ull : (gbits[wi] & ~((1ull << (bit + 1)) - 1));
-    while (word == 0 && ++wi < nch) word = gbits[wi];
-    const int ge = word ? wi * 64 + __ffsll((unsigned long long)word) - 1 : sz;
-    *ge_o = ge < sz ? ge : sz;
-  };
   // the group bounds of a wave's 64 consecutive slots from one read of every
   // group-start word (nch <= 32) and lane broadcasts: no dependent LDS chain
   // (NCH > 64: a second word per lane, gw1 / gnz1 for chunks 64..127)
@@ -826,7 +1081,6 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
   };
   const u64 le_mask = lanemask_lt() | (1ull << lane);
 #if WF_BUCKET
-  bool btie = false;  // two equal 32-bit keys in one group (the exact re-rank below)
 #endif
 #if WF_BUCKET
   // interpolation buckets over slot space: slot p of group [gs, ge) goes to bucket
@@ -1086,6 +1340,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
   }
   WSTAMP(10);
   WF_EXIT(8);
+  }  // (!RUNS)
   // 6. renames: rank among the window's renames of the same branch (final order).
   //    Computed in the collision-check phase into registers (rown aliases fin, which
   //    the exact re-rank still reads) and stored once no tie is known; redone after a

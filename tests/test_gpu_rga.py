@@ -149,8 +149,8 @@ def test_rga_list_mode_live_elements_match(n_ops, n_lists, seed):
     assert np.all(batch.op[ts[tomb]] != 2)  # tombstoned elements were created by inserts / moves
 
 
-def _check(batch):
-    gv, gs, go = rga_replay_device(batch)
+def _check(batch, grouped=False):
+    gv, gs, go = rga_replay_device(batch, grouped=grouped)
     ov, os_, oo = oracle.rga(batch.n_lists, batch.list_id, batch.op, batch.value, batch.anchor,
                              batch.t, batch.author, batch.opid_hi, batch.opid_lo)
     assert np.array_equal(go, oo)
@@ -170,6 +170,52 @@ def test_rga_batch_equals_oracle(n_ops, n_lists, seed):
 def test_rga_config4_full_size():
     """SURVEY §8(d) config 4 at its full size: 10M events over 50k lists, seed 13."""
     _check(synth.rga_batch(10_000_000, 50_000, 13))
+
+
+def _grouped(b):
+    """The same lists with each list's events together, in stream order (the shape
+    crdt.replay and RGA hand the library): a stable sort by list id, events re-indexed."""
+    from semantic_merge_amd.crdt import RgaBatch
+    p = np.argsort(b.list_id, kind="stable")
+    return RgaBatch(b.n_lists, b.list_id[p], b.op[p], b.value[p], b.anchor[p], b.t[p], b.author[p],
+                    b.opid_hi[p], b.opid_lo[p], [])
+
+
+@pytest.mark.timeout(300)
+def test_rga_config4_grouped_full_size():
+    """Config 4's 10M events over 50k lists, grouped list by list (the drop-in's shape):
+    the SMX_RGA_GROUPED path (records packed in place, no partition) against the C oracle."""
+    _check(_grouped(synth.rga_batch(10_000_000, 50_000, 13)), grouped=True)
+
+
+@pytest.mark.parametrize("n_ops,n_lists,seed", [(300_000, 1_000, 21), (200_000, 100_000, 22), (50_000, 30, 23)])
+def test_rga_grouped_equals_oracle(n_ops, n_lists, seed):
+    """Grouped batches with empty lists at the start, in the middle and at the end (list
+    ids from a sparse subset), and more lists than k_rga_out_fused takes."""
+    b = _grouped(synth.rga_batch(n_ops, n_lists, seed))
+    keep = (b.list_id % 3 != 0) & (b.list_id != b.n_lists - 1)
+    from semantic_merge_amd.crdt import RgaBatch
+    b = RgaBatch(b.n_lists, *(x[keep] for x in (b.list_id, b.op, b.value, b.anchor, b.t, b.author, b.opid_hi,
+                                                 b.opid_lo)), [])
+    assert b.list_id[0] > 0 and b.list_id[-1] < b.n_lists - 1
+    _check(b, grouped=True)
+
+
+def test_rga_grouped_claim_false_still_exact():
+    """SMX_RGA_GROUPED on interleaved events: the device check sees a list id decrease,
+    the list kernels stand down and the call redoes itself through the partition."""
+    _check(synth.rga_batch(400_000, 2_000, 24), grouped=True)
+
+
+def test_rga_grouped_invalid_input():
+    b = _grouped(synth.rga_batch(100_000, 50, 25))
+    b.list_id[-1] = 50  # out of range (last: the ids still never decrease)
+    with pytest.raises(Exception, match="n_lists"):
+        rga_replay_device(b, grouped=True)
+    b = _grouped(synth.rga_batch(100_000, 50, 25))
+    b.op[777] = 3
+    with pytest.raises(Exception, match="op > 2"):
+        rga_replay_device(b, grouped=True)
 
 
 def test_rga_dense_values_and_big_lists():

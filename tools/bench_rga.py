@@ -23,8 +23,6 @@ def main():
     def up(a, dt):
         return torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
 
-    ins = [up(b.list_id, np.int32), up(b.op, np.uint8), up(b.value, np.int32), up(b.anchor, np.int32),
-           up(b.t, np.int64), up(b.author, np.int32), up(b.opid_hi, np.int64), up(b.opid_lo, np.int64)]
     vals = torch.empty(n, dtype=torch.int32, device=dev)
     src = torch.empty(n, dtype=torch.int32, device=dev)
     offs = torch.empty(nl + 1, dtype=torch.int64, device=dev)
@@ -33,20 +31,39 @@ def main():
     ws = C.c_size_t(0)
     _lib.check(lib.smx_rga_workspace_bytes(n, nl, C.byref(ws)))
     wst = torch.empty(ws.value, dtype=torch.uint8, device=dev)
-    ops = _abi.SmxRgaOps(n, nl, *[t.data_ptr() for t in ins])
     out = _abi.SmxRgaOut(vals.data_ptr(), src.data_ptr(), offs.data_ptr(), counts.data_ptr())
     s = torch.cuda.current_stream().cuda_stream
-    for _ in range(2):
-        _lib.check(lib.smx_rga_replay(C.byref(ops), C.byref(out), wst.data_ptr(), ws.value, s))
-    torch.cuda.synchronize()
     steps = int(os.environ.get("RGA_STEPS", 5))
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        _lib.check(lib.smx_rga_replay(C.byref(ops), C.byref(out), wst.data_ptr(), ws.value, s))
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    if os.environ.get("RGA_NO_CPU"):  # A/B timing runs: the GPU leg only
-        print(json.dumps({"ms_per_step": round(dt * 1e3, 3), "value": round(n / dt, 1)}))
+
+    def timed(batch, flags):
+        """ms per call of smx_rga_replay_ex on the batch, device-resident."""
+        ins = [up(batch.list_id, np.int32), up(batch.op, np.uint8), up(batch.value, np.int32),
+               up(batch.anchor, np.int32), up(batch.t, np.int64), up(batch.author, np.int32),
+               up(batch.opid_hi, np.int64), up(batch.opid_lo, np.int64)]
+        ops = _abi.SmxRgaOps(n, nl, *[t.data_ptr() for t in ins])
+        for _ in range(2):
+            _lib.check(lib.smx_rga_replay_ex(C.byref(ops), C.byref(out), wst.data_ptr(), ws.value, flags, s))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            _lib.check(lib.smx_rga_replay_ex(C.byref(ops), C.byref(out), wst.data_ptr(), ws.value, flags, s))
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
+    # the drop-in's shape: each list's events together (crdt.replay / RGA hand over
+    # stream after stream), through SMX_RGA_GROUPED
+    from semantic_merge_amd.crdt import RgaBatch
+    p = np.argsort(b.list_id, kind="stable")
+    bg = RgaBatch(nl, b.list_id[p], b.op[p], b.value[p], b.anchor[p], b.t[p], b.author[p], b.opid_hi[p],
+                  b.opid_lo[p], [])
+    dtg = timed(bg, _abi.RGA_GROUPED)
+    del bg, p
+    dt = timed(b, 0)  # config 4 as generated: list ids interleaved
+    grouped = {"ms_per_step": round(dtg * 1e3, 3), "value": round(n / dtg, 1),
+               "roofline_frac": round(45 * n / dtg / 1e9 / 8000.0, 4),
+               "note": "the same events grouped list by list (the drop-in's shape), SMX_RGA_GROUPED: no partition"}
+    if os.environ.get("RGA_NO_CPU"):  # A/B timing runs: the GPU legs only
+        print(json.dumps({"ms_per_step": round(dt * 1e3, 3), "value": round(n / dt, 1), "grouped": grouped}))
         return
     from oracle import oracle
     m = min(n, 1_000_000)
@@ -61,6 +78,7 @@ def main():
                       "survivors": int(counts.item()),
                       "roofline": {"bound": "hbm", "bytes_per_event": 45, "achieved": round(gbs, 1),
                                    "peak": 8000.0, "unit": "GB/s", "frac": round(gbs / 8000.0, 4)},
+                      "grouped": grouped,
                       "cpu_baseline": {"value": round(int(sel.sum()) / ct, 1), "unit": "events/s",
                                        "cores": 1, "kind": "port",
                                        "sample": f"{int(sel.sum())} events of the first lists, oracle/crdt_ref.c"}}))

@@ -1,0 +1,45 @@
+#!/bin/bash
+# GPU-box steps for iterating (each under its own time limit; stops at the first failure):
+#   gpurun -- bash tools/gpu_steps.sh <tag> <step> [<step> ...]
+# steps: rga (RGA GPU tests), compose (compose GPU tests incl. full-size digests),
+#        gtests (the whole -m gpu suite), ab (tools/ab_libs.py, current vs tools/_build/var_old),
+#        ab5 (the same on config 5), rgabench (tools/bench_rga.py), bench (bench.py, no PMC / CPU
+#        legs), benchfull (bench.py default), c5 (bench.py --config c5), c2, prof, sq
+set -o pipefail
+TAG=${1:?tag}; shift
+R=$PWD; O=$R/gpurun_out/$TAG; mkdir -p "$O"
+run() {  # run <seconds> <log> <cmd...>
+  local lim=$1 log=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$O/$log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then echo "step $log failed rc=$rc"; tail -30 "$O/$log"; exit $rc; fi
+}
+for s in "$@"; do
+  case $s in
+    rga) run 600 rga_tests.log python -u -m pytest tests/test_gpu_rga.py -x -v --timeout 300 --timeout-method thread
+         tail -2 "$O/rga_tests.log";;
+    compose) run 900 compose_tests.log python -u -m pytest tests/test_gpu_compose.py tests/test_gpu_full.py -x -v --timeout 300 --timeout-method thread
+         tail -2 "$O/compose_tests.log";;
+    gtests) run 1100 tests.log python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread
+         tail -2 "$O/tests.log";;
+    ab) run 400 ab_c3.txt python -u tools/ab_libs.py --rounds 4 new=semantic_merge_amd/libsmx.so old=tools/_build/var_old/libsmx.so
+        tail -12 "$O/ab_c3.txt";;
+    ab5) run 400 ab_c5.txt python -u tools/ab_libs.py --config c5 --rounds 4 new=semantic_merge_amd/libsmx.so old=tools/_build/var_old/libsmx.so
+        tail -12 "$O/ab_c5.txt";;
+    rgabench) run 300 bench_rga.json python -u tools/bench_rga.py
+        tail -1 "$O/bench_rga.json";;
+    bench) run 300 bench.json python -u bench.py --no-cpu-baseline --no-pmc --no-e2e
+        tail -1 "$O/bench.json" | cut -c1-600;;
+    benchfull) run 600 bench_full.json python -u bench.py
+        tail -1 "$O/bench_full.json" | cut -c1-600;;
+    c5) run 300 bench_c5.json python -u bench.py --config c5 --steps 10 --no-cpu-baseline --no-e2e
+        tail -1 "$O/bench_c5.json" | cut -c1-600;;
+    c2) run 300 bench_c2.json python -u bench.py --config c2 --steps 50 --no-pmc --no-e2e
+        tail -1 "$O/bench_c2.json" | cut -c1-400;;
+    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o p -- python3 "$R/bench.py" --steps 8 --warmup 2 --no-cpu-baseline --no-pmc --no-e2e > "$O/prof.log" 2>&1) || { echo "prof failed"; tail -20 "$O/prof.log"; exit 1; }
+          python3 tools/prof_export.py "$O/prof" "$O/kernel_stats.csv" && head -8 "$O/kernel_stats.csv";;
+    sq) run 600 sq.log bash tools/pmc_sq.sh "$O/sq"
+        tail -3 "$O/sq.log";;
+    *) echo "unknown step $s"; exit 2;;
+  esac
+done
