@@ -322,6 +322,9 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
 // RGA_E_UNGROUPED a call that said its events come grouped by list (SMX_RGA_GROUPED) has a
 // list id that decreases: every list kernel leaves at once and the call is redone with
 // the partition
+#ifndef RGA_DIRECT
+#define RGA_DIRECT 1  // grouped calls: the list kernels read the input columns (no record pass)
+#endif
 #define RGA_E_INPUT 1
 #define RGA_E_UNGROUPED 2
 
@@ -348,6 +351,26 @@ __global__ void __launch_bounds__(BLOCK) k_rga_pack(smx_rga_ops o, u64* __restri
     *reinterpret_cast<R16*>(rout + (u64)i * RGA_REC) = r;
     // list starts: the lists in (prev, l] start here (from list 0 at the first event);
     // after the last event the rest start at n (ids clamped: one out of range fails the call)
+    const u32 lo = i == 0 ? 0u : prev + 1u, hi = l < (u64)nl ? l : (u32)(nl - 1);
+    for (u32 L = lo; L <= hi; ++L) lstart[L] = (u32)i;
+    if (i == n - 1)
+      for (i64 L = (i64)hi + 1; L < nl; ++L) lstart[L] = (u32)n;
+  }
+  if (bad) atomicOr(err, (i32)bad);
+}
+
+// Grouped events read in place by the list kernels (ColSrc): only the list starts, the
+// checks and the chunk sums' zeroing of k_rga_pack, reading the list ids and ops.
+__global__ void __launch_bounds__(BLOCK) k_rga_gbounds(smx_rga_ops o, u32* __restrict__ lstart,
+                                                       u32* __restrict__ csum, i32* __restrict__ err) {
+  const i64 n = o.n_ops, nl = o.n_lists;
+  if (blockIdx.x == 0 && threadIdx.x < RGA_CS_MAX) csum[threadIdx.x] = 0u;
+  u32 bad = 0;
+  for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (i64)gridDim.x * BLOCK) {
+    const u32 l = o.list[i], op = o.op[i];
+    const u32 prev = i > 0 ? o.list[i - 1] : 0u;
+    bad |= (l >= (u64)nl || op > 2) ? (u32)(RGA_E_INPUT | RGA_E_UNGROUPED) : 0u;
+    bad |= i > 0 && l < prev ? (u32)RGA_E_UNGROUPED : 0u;
     const u32 lo = i == 0 ? 0u : prev + 1u, hi = l < (u64)nl ? l : (u32)(nl - 1);
     for (u32 L = lo; L <= hi; ++L) lstart[L] = (u32)i;
     if (i == n - 1)
@@ -773,13 +796,39 @@ struct RwLds {
   u8 st[CAP];           // bit0 present, bit1 tombstoned
 };
 
+// Where a list kernel reads its events' record words (event e of the list at s0):
+//  RecSrc  the partitioned 16-byte records
+//  ColSrc  the input columns themselves (SMX_RGA_GROUPED: event s0 + e is the list's e-th
+//          event, so word 0 = anchor << 32 | t' >> 32 and word 1 = value << 32 | op << 30 |
+//          index are built at the load, no record pass)
+struct RecSrc {
+  const u64* p;  // the list's first record
+  __device__ __forceinline__ u64 w0(u32 e) const { return p[(u64)e * RGA_REC]; }
+  __device__ __forceinline__ u64 w1(u32 e) const { return p[(u64)e * RGA_REC + RGA_WV]; }
+};
+struct ColSrc {
+  const u32* anchor;
+  const i64* t;
+  const u32* value;
+  const u8* op;
+  u32 s0;
+  __device__ __forceinline__ u64 w0(u32 e) const {
+    const u32 j = s0 + e;
+    return ((u64)anchor[j] << 32) | (((u64)t[j] ^ 0x8000000000000000ull) >> 32);
+  }
+  __device__ __forceinline__ u64 w1(u32 e) const {
+    const u32 j = s0 + e, op3 = op[j];
+    return ((u64)value[j] << 32) | ((op3 > 2 ? 0u : op3) << 30) | j;
+  }
+};
+
 // Event a before event b of one list in (key, index) order (crdt.py:48-57): word 0
 // from LDS, the rest from the input columns by stream index (rare: equal word 0).
-template <class LDS>
-__device__ __forceinline__ bool ev_lt(const LDS& S, const u64* __restrict__ src, const smx_rga_ops& o, u32 a,
+template <class LDS, class SRC>
+__device__ __forceinline__ bool ev_lt(const LDS& S, const SRC& src, const smx_rga_ops& o, u32 a,
                                       u32 b) {
 #if RW_W0G
-  const u64 wa = src[(u64)a * RGA_REC], wb = src[(u64)b * RGA_REC];  // (the list's records, L2-resident)
+  const u64 wa = src.w0(a), wb = src.w0(b);  // (the list's records or columns, L2-resident)
 #else
   const u64 wa = S.w0[a], wb = S.w0[b];
 #endif
@@ -788,8 +837,8 @@ __device__ __forceinline__ bool ev_lt(const LDS& S, const u64* __restrict__ src,
 }
 
 // Step 3 over the survivors' (word 0, event) pairs held K2 per lane.
-template <int K2, class LDS>
-__device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, const smx_rga_ops& o, u64 (&key)[8],
+template <int K2, class LDS, class SRC>
+__device__ __forceinline__ void rw_order(LDS& S, const SRC& src, const smx_rga_ops& o, u64 (&key)[8],
                                          u32 (&pay)[8], u32 m,
                                          u32 s0, u32 lane, u32* __restrict__ tmp_v, u32* __restrict__ tmp_s) {
   constexpr u32 N = 64u * K2;
@@ -875,12 +924,12 @@ __device__ __forceinline__ void rw_order(LDS& S, const u64* __restrict__ src, co
 
 // tomb: list mode (crdt.py RGA.list) -- the tombstoned elements stay, flagged
 // Returns the list's survivor count (wave-uniform); scnt[l] is the caller's to write.
-template <int K, int CAP>
-__device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __restrict__ R, u32 l, u32 s0, u32 cnt,
+template <int K, int CAP, class SRC>
+__device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const SRC src, u32 l, u32 s0, u32 cnt,
                                               RwLds<CAP>& S, u32 lane, bool tomb,
                                               u32* __restrict__ tmp_v, u32* __restrict__ tmp_s,
                                               u32* __restrict__ scnt) {
-  const u64* src = R + (u64)s0 * RGA_REC;
+  static_assert(RW_W0R, "the record words come through src.w0 / src.w1");
 #if RW_W0R
   u64 w0r[K];  // word 0 of this lane's events k * 64 + lane, kept for step 3
   {  // every load in flight at once; word 1 of each event to LDS
@@ -888,8 +937,8 @@ __device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const u32 e = (u32)k * 64u + lane;
-      w0r[k] = e < cnt ? src[(u64)e * RGA_REC] : ~0ull;
-      wvr[k] = e < cnt ? src[(u64)e * RGA_REC + RGA_WV] : 0ull;
+      w0r[k] = e < cnt ? src.w0(e) : ~0ull;
+      wvr[k] = e < cnt ? src.w1(e) : 0ull;
     }
     for (u32 t = lane; t < RwLds<CAP>::HT; t += WAVE) {
       S.h.hkey[t] = RW_EMPTY;
@@ -907,7 +956,7 @@ __device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __
 #pragma unroll
     for (int i = 0; i < RGA_REC * K; ++i) {
       const u32 x = lane + (u32)i * WAVE;
-      v[i] = x < cnt * RGA_REC ? src[x] : 0ull;
+      v[i] = x < cnt * RGA_REC ? (x % RGA_REC ? src.w1(x / RGA_REC) : src.w0(x / RGA_REC)) : 0ull;
     }
     for (u32 t = lane; t < RwLds<CAP>::HT; t += WAVE) {
       S.h.hkey[t] = RW_EMPTY;
@@ -1102,10 +1151,10 @@ __device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __
               continue;
             }
             if (!wbl) {
-              wb = src[(u64)best * RGA_REC];
+              wb = src.w0(best);
               wbl = true;
             }
-            const u64 wy = src[(u64)y * RGA_REC];
+            const u64 wy = src.w0(y);
             if (wy < wb ||
                 (wy == wb && rga_key_lt(o, (u32)S.wv[y] & RGA_IDX_MASK, (u32)S.wv[best] & RGA_IDX_MASK))) {
               best = y;
@@ -1157,7 +1206,7 @@ __device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __
 #if RW_W0R
       key[k] = S.gs[a];
 #elif RW_W0G
-      key[k] = src[(u64)pay[k] * RGA_REC];
+      key[k] = src.w0(pay[k]);
 #else
       key[k] = S.w0[pay[k]];
 #endif
@@ -1182,6 +1231,7 @@ __device__ __forceinline__ u32 rga_wave_list(const smx_rga_ops& o, const u64* __
   return m;
 }
 
+template <bool DIRECT>
 __global__ void __launch_bounds__(WAVE * RW_WAVES) RW_OCC k_rga_wave(smx_rga_ops o, const u64* __restrict__ R,
                                                              const u32* __restrict__ lstart,
                                                              i64 n, i64 nl, u32* __restrict__ tmp_v,
@@ -1209,12 +1259,13 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) RW_OCC k_rga_wave(smx_rga_ops
       u32 ln = lane;
       if (RW_LAUNDER) asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
       u32 m;
-      if (cnt <= 64)
-        m = rga_wave_list<1>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
-      else if (cnt <= 128)
-        m = rga_wave_list<2>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
-      else
-        m = rga_wave_list<4>(o, R, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+      auto run = [&](auto src) {
+        if (cnt <= 64) return rga_wave_list<1>(o, src, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+        if (cnt <= 128) return rga_wave_list<2>(o, src, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+        return rga_wave_list<4>(o, src, l, s0, cnt, lds[w], ln, tomb != 0, tmp_v, tmp_s, scnt);
+      };
+      if constexpr (DIRECT) m = run(ColSrc{o.anchor, o.t, o.value, o.op, s0});
+      else m = run(RecSrc{R + (u64)s0 * RGA_REC});
       if (lane == 0) scnt[l] = m;
       acc += m;
       wave_lds_sync();  // the next list reuses the slice
@@ -1234,7 +1285,7 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(smx_rga_ops o, co
                                                               i64 n, i64 nl, u32* __restrict__ defer,
                                                               u32* __restrict__ ndefer, u32* __restrict__ tmp_v,
                                                               u32* __restrict__ tmp_s, u32* __restrict__ scnt,
-                                                              int tomb, const i32* __restrict__ gate) {
+                                                              int tomb, const i32* __restrict__ gate, int direct) {
   __shared__ RwLds<2 * RW_CAP> lds[RW_WAVES];
   if (*gate & RGA_E_UNGROUPED) return;
   const u32 lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
@@ -1247,11 +1298,22 @@ __global__ void __launch_bounds__(WAVE * RW_WAVES) k_rga_wave2(smx_rga_ops o, co
       const u32 l = (u32)(l0 + (u64)(__ffsll((unsigned long long)todo) - 1));
       todo &= todo - 1;
       const u32 s0 = lstart[l], cnt = rga_lend(lstart, l, nl, n) - s0;
+      if (direct) {  // grouped events, no partition: this long list's records from the columns
+        const ColSrc cs{o.anchor, o.t, o.value, o.op, s0};
+        u64* rw = const_cast<u64*>(R) + (u64)s0 * RGA_REC;
+        for (u32 e = lane; e < cnt; e += WAVE) {
+          R16 r;
+          r.a = cs.w0(e);
+          r.b = cs.w1(e);
+          *reinterpret_cast<R16*>(rw + (u64)e * RGA_REC) = r;
+        }
+        __threadfence_block();  // (this wave reads them back; k_rga_big after this kernel)
+      }
       if (cnt > 2 * RW_CAP) {
         if (lane == 0) defer[atomicAdd(ndefer, 1u)] = l;
         continue;
       }
-      const u32 m = rga_wave_list<8>(o, R, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
+      const u32 m = rga_wave_list<8>(o, RecSrc{R + (u64)s0 * RGA_REC}, l, s0, cnt, lds[w], lane, tomb != 0, tmp_v, tmp_s, scnt);
       if (lane == 0) rga_put_count(scnt, l, m);
       wave_lds_sync();  // the next list reuses the slice
     }
@@ -1541,9 +1603,13 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
     g_cus = cus > 0 ? cus : 256;
     g_rr_grid = g_cus * RR_PER_CU;
   }
+  const bool direct = grouped && RGA_DIRECT;  // the list kernels read the columns in place
   if (grouped) {  // the caller's events come list by list: no partition
     const int pgrid = (int)(SMX_CEIL_DIV(n, (i64)BLOCK) < 8192 ? SMX_CEIL_DIV(n, (i64)BLOCK) : 8192);
-    hipLaunchKernelGGL(k_rga_pack, dim3(pgrid), dim3(BLOCK), 0, st, *ops, rec, lstart, scnt - RGA_CS_MAX, err);
+    if (direct)
+      hipLaunchKernelGGL(k_rga_gbounds, dim3(pgrid), dim3(BLOCK), 0, st, *ops, lstart, scnt - RGA_CS_MAX, err);
+    else
+      hipLaunchKernelGGL(k_rga_pack, dim3(pgrid), dim3(BLOCK), 0, st, *ops, rec, lstart, scnt - RGA_CS_MAX, err);
   } else {  // records grouped by list: LSD passes over the list id, ping-pong into rec
     int npass = 1;
     while (npass < 4 && ((u64)(nl - 1) >> (8 * npass)) != 0) ++npass;
@@ -1587,13 +1653,17 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   i64 wg = SMX_CEIL_DIV(nl, (i64)RW_WAVES);
   if (RW_PER_CU > 0 && wg > (i64)g_cus * RW_PER_CU) wg = (i64)g_cus * RW_PER_CU;
   const dim3 wgrid((u32)wg);
-  hipLaunchKernelGGL(k_rga_wave, wgrid, dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, tmp_v, tmp_s, scnt,
-                     tomb, (const i32*)err);
+  if (direct)
+    hipLaunchKernelGGL(k_rga_wave<true>, wgrid, dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, tmp_v, tmp_s,
+                       scnt, tomb, (const i32*)err);
+  else
+    hipLaunchKernelGGL(k_rga_wave<false>, wgrid, dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, tmp_v, tmp_s,
+                       scnt, tomb, (const i32*)err);
   // lists of more than RW_CAP events (a few, if any).  (On a second stream beside
   // k_rga_wave they measured no faster: their workgroups trail k_rga_wave's, and the
   // join costs ~14 us, profiles/r04_s.)
   hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, def2, ndef + 1,
-                     tmp_v, tmp_s, scnt, tomb, (const i32*)err);
+                     tmp_v, tmp_s, scnt, tomb, (const i32*)err, (int)direct);
   hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
                      tmp_s, scnt, tomb, (const i32*)err);
   if (nl <= RGA_FUSED_MAX) {  // each list's wave finds its own offset

@@ -240,6 +240,15 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
       return;                                                              \
     }                                                                      \
   } while (0)
+// the run-grouped order's phase exits (diagnostic builds: SMX_ABLATE = 0x10000 + N, a value
+// clear of the bit-tested ablations 1, 2, 4 (N <= 3 only) and 16)
+#define RX_EXIT(N)                                                          \
+  do {                                                                      \
+    if (SMX_DIAG && P.ablate == 0x10000 + (N)) {                            \
+      if (t == 0 && sord[0] == 0xfffeu && fin[1] == 0xfffeu) P.meta->dup_key = 1; \
+      return;                                                               \
+    }                                                                       \
+  } while (0)
 #define WSTAMP(i)                                                                  \
   do {                                                                             \
     if (DBG && t == 0) P.dbg[w * WF_NSTAMP + (i)] = __builtin_amdgcn_s_memtime(); \
@@ -593,7 +602,9 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
       const bool head = valid && (first || pv != ts_r[i]);
       dec |= valid && !first && pv > ts_r[i];
       hbr[i] = __ballot(head);
-      const int c = (NT * i) / WAVE + wv;  // this item's 64-op chunk (wave-uniform)
+      // this item's 64-op chunk: wave-uniform, and said so (t / WAVE is a lane value to the
+      // compiler, which would then run the head searches below as lane-divergent loops)
+      const int c = __builtin_amdgcn_readfirstlane((NT * i) / WAVE + wv);
       if (lane == 0 && c < NCH) gbits[c] = hbr[i];
       // the heads of this chunk, one at a time with the whole wave: a 64-way search of
       // the other part for #{ops < v} (two or three rounds of one LDS read per lane)
@@ -629,6 +640,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
       if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
       return;
     }
+    RX_EXIT(1);
     // b. (wave 0) the last head of each chunk, the runs' dense index, the group count
     const u32 kpres = __builtin_amdgcn_readfirstlane(kmask_r);
     const int KD = __popc(kpres);
@@ -667,6 +679,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
       if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 2ull);
       return;
     }
+    RX_EXIT(2);
     {
       const u32 R = rinfo[1];
       // c. each op's run (its head: in its chunk, else the last head of the earlier
@@ -676,7 +689,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const int e = t + NT * i;
-        const int c = (NT * i) / WAVE + wv;
+        const int c = __builtin_amdgcn_readfirstlane((NT * i) / WAVE + wv);
         const u64 m = hbr[i] & lem;
         const int h = m ? c * WAVE + 63 - __clzll(m) : (int)lasth[c > 0 ? c - 1 : 0];
         const u32 k = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
@@ -689,6 +702,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
         }
       }
       __syncthreads();
+      RX_EXIT(3);
       // d. group starts: exclusive scan of the KD * R counters (kind-major = T order), in
       //    passes of 4 * NT counters (one pass on config 3's windows: 6 kinds x 14 runs)
       const int GS = KD * (int)R;
@@ -720,6 +734,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
         }
         kbase[t] = s;
       }
+      RX_EXIT(4);
       // e. interpolation bucket inside the group: b = gs + (ge - gs) * key / 2^32
       u32 b_r[ITEMS], ar_r[ITEMS];
 #pragma unroll
@@ -733,6 +748,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
         ar_r[i] = (atomicAdd(&bcnt[b >> 1], 1u << (16 * (b & 1))) >> (16 * (b & 1))) & 0xffffu;
       }
       __syncthreads();
+      RX_EXIT(5);
       // f. bucket starts
       {
         constexpr int WPT = CAP / (2 * NT);
@@ -755,6 +771,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
       auto bstart = [&](u32 b) -> u32 {
         return b < (u32)CAP ? (bcnt[b >> 1] >> (16 * (b & 1))) & 0xffffu : (u32)sz;
       };
+      RX_EXIT(6);
       // g. members in bucket order: key and element
       u32 slot_r[ITEMS];
 #pragma unroll
@@ -767,23 +784,41 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
         mel[s] = (u16)(t + NT * i);
       }
       __syncthreads();
+      RX_EXIT(7);
       // h. rank inside the bucket on (key, full id, side, index); the final order
+      //    (per-lane loops: one op per bucket on average; a wave-uniform loop over the
+      //    ITEMS buckets together spilled registers)
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const u32 b = b_r[i];
         if (b == 0xffffffffu) continue;
         const int e = t + NT * i;
-        const u32 lo = bstart(b), hi = bstart(b + 1), kp = hi_r[i];
+        const u32 b1 = b + 1 < (u32)CAP ? b + 1 : (u32)CAP - 1;  // (branch-free bucket bounds)
+        const u32 lo = (bcnt[b >> 1] >> (16 * (b & 1))) & 0xffffu;
+        const u32 hw = (bcnt[b1 >> 1] >> (16 * (b1 & 1))) & 0xffffu;
+        const u32 hi = b + 1 < (u32)CAP ? hw : (u32)sz, kp = hi_r[i];
         u32 c = 0;
-        for (u32 q = lo; q < hi; ++q) {
-          if (q == slot_r[i]) continue;
+        bool tie = false;
+#pragma unroll 1
+        for (u32 q = lo; q < hi; ++q) {  // (own slot: x == kp, not a tie)
           const u32 x = mkey[q];
-          if (x != kp) {
-            c += x < kp;
-          } else {  // equal top 32 bits: the full ids, then element order = (side, index)
+          c += x < kp;
+          tie |= (x == kp) & (q != slot_r[i]);
+        }
+        if (tie) {  // equal top 32 bits (rare): the full ids, then element order = (side, index)
+          c = 0;
+          const i64 jm = e < na ? a0 + e : bld + e;
+          const u64 hm = P.khi[jm], lm = P.klo[jm];
+#pragma unroll 1
+          for (u32 q = lo; q < hi; ++q) {
+            const u32 x = mkey[q];
+            if (x != kp || q == slot_r[i]) {
+              c += x < kp;
+              continue;
+            }
             const int eo = mel[q];
-            const i64 jm = e < na ? a0 + e : bld + e, jo = eo < na ? a0 + eo : bld + eo;
-            const u64 hm = P.khi[jm], ho = P.khi[jo], lm = P.klo[jm], lo2 = P.klo[jo];
+            const i64 jo = eo < na ? a0 + eo : bld + eo;
+            const u64 ho = P.khi[jo], lo2 = P.klo[jo];
             c += ho < hm || (ho == hm && (lo2 < lm || (lo2 == lm && eo < e)));
           }
         }
@@ -793,6 +828,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
         skS[f] = (u8)(k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1);
       }
       __syncthreads();
+      RX_EXIT(8);
     }
   }
   if constexpr (!RUNS) {  // steps 2-5: merge, multisplit, group order
