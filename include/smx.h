@@ -133,7 +133,13 @@ int smx_release_graphs(void* stream);
 #define SMX_PLAN_RADIX 2     /* unordered logs: radix sort on (ts, oid_hi) */
 #define SMX_PLAN_RADIX_LO 3  /* ... and oid_lo (duplicate (ts, oid_hi) pairs) */
 #define SMX_PLAN_PRESORTED_WIDE 4 /* ordered logs, groups up to 8192 ops: wide presorted windows */
+#define SMX_PLAN_SMALL 5     /* merges of at most 2048 ops (any order): one workgroup, one launch */
 int smx_last_plan(void);
+
+/* Merges of at most n ops (clamped to 0..2048; default 2048) run as SMX_PLAN_SMALL, one
+ * workgroup and one launch; 0 sends every merge through the window plans.  Process-wide;
+ * returns the previous limit. */
+int64_t smx_set_small_limit(int64_t n);
 
 /*
  * Sharded single merge: one process per GPU, shard r of G.

@@ -72,7 +72,7 @@ class SmxShard(C.Structure):
 SHARD_ORDER, SHARD_WALK, SHARD_TABLES, SHARD_EMIT = 0, 1, 2, 3
 SHARD_ORDER_FIX = 4
 SHARD_SCATTER = 5
-PLAN_NAMES = ("presorted", "segmented", "radix", "radix+oid_lo", "presorted-wide")  # smx_last_plan()
+PLAN_NAMES = ("presorted", "segmented", "radix", "radix+oid_lo", "presorted-wide", "small")  # smx_last_plan()
 SHARD_SUMMARY = 32
 
 
@@ -111,6 +111,7 @@ EXPORTS = (
     "smx_compose_finish",
     "smx_release_graphs",
     "smx_last_plan",
+    "smx_set_small_limit",
     "smx_shard_step",
     "smx_shard_range_info",
     "smx_set_profiling",
@@ -141,6 +142,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.smx_release_graphs.restype = C.c_int
     lib.smx_last_plan.argtypes = []
     lib.smx_last_plan.restype = C.c_int
+    lib.smx_set_small_limit.argtypes = [C.c_int64]
+    lib.smx_set_small_limit.restype = C.c_int64
     lib.smx_shard_step.argtypes = [C.POINTER(SmxOps), C.POINTER(SmxShard), C.POINTER(SmxComposeOut),
                                    C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]
     lib.smx_shard_step.restype = C.c_int

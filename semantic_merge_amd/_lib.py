@@ -227,6 +227,11 @@ def compose_soa(soa: SoA, device: str = "cuda"):
     return session(device).compose(soa)
 
 
+def set_small_limit(n: int) -> int:
+    """Merges of at most n ops (0..2048) take the one-workgroup plan; returns the old limit."""
+    return int(lib().smx_set_small_limit(int(n)))
+
+
 def stage_times():
     """{stage: (total_ms, calls)} accumulated while smx_set_profiling(1)."""
     L = lib()

@@ -28,6 +28,7 @@
 //   k_emit      compacted output of every op after the move block: order, addr,
 //               file, ctx
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -35,6 +36,7 @@
 
 #include "smx_sort.h"
 #include "smx_window.h"
+#include "smx_small.h"
 #include "smx_tables.h"
 
 
@@ -59,9 +61,9 @@ int smx_set_error(int code, const char* msg) { return set_err(code, msg ? msg : 
 // window_wide: its wide (8192-op) instance, a stage of its own so that a merge's
 // failed normal attempt is never averaged into the wide launch's time
 enum Stage { ST_PLAN, ST_GSORT, ST_WINDOW, ST_WALK, ST_TABLES, ST_MVPREFIX, ST_EMIT, ST_SEGSORT, ST_WINDOW_G,
-             ST_WINDOW_WIDE, ST_N };
+             ST_WINDOW_WIDE, ST_SMALL, ST_N };
 static const char* kStageNames[ST_N] = {"plan",   "gsort",    "window", "walk",    "tables",
-                                        "mvprefix", "emit", "segsort", "window_g", "window_wide"};
+                                        "mvprefix", "emit", "segsort", "window_g", "window_wide", "small"};
 static std::mutex g_prof_mu;
 static int g_prof = 0;
 static u32 g_prof_mask = ~0u;  // the stages timed while profiling is on (smx_set_profiling_stages)
@@ -2492,6 +2494,14 @@ static int early_fail_of(int dev, EarlyFail* e) {
   return SMX_E_HIP;  // (more than four devices per host thread: no early flag)
 }
 
+#ifndef SMX_SMALL
+#define SMX_SMALL 1  // merges of at most SMALL_N ops: one workgroup, one launch (k_compose_small)
+#endif
+
+// Largest merge (ops) the one-workgroup path takes (smx_set_small_limit; 0: never).
+static std::atomic<int64_t> g_small_max{SMX_SMALL ? SMALL_N : 0};
+static inline bool small_merge(i64 n) { return n <= g_small_max.load(std::memory_order_relaxed); }
+
 #ifndef SMX_EARLY_MIN
 #define SMX_EARLY_MIN (1ll << 22)  // ops from which a synchronous merge waits for k_khist's verdict
 #endif
@@ -2508,6 +2518,14 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
   StageTimer tm(st, timed);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
   int rc;
+  if (small_merge(n)) {  // the whole merge in one workgroup (smx_small.h)
+    tm.begin(ST_SMALL);
+    hipLaunchKernelGGL(k_compose_small, dim3(1), dim3(SMALL_NT), 0, st, *ops, *out, C.ws<ComposeMeta>(B_META));
+    HIP_TRY(hipGetLastError());
+    tm.end(ST_SMALL);
+    tm.flush();
+    return SMX_OK;
+  }
   // A large synchronous merge (not captured): the host waits for k_khist's verdict while
   // the windows run, and launches no tail (~20 launches that would only see the failure)
   // behind a plan that fails for sure -- smx_compose_finish then runs the fallback plan.
@@ -2675,13 +2693,14 @@ static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, vo
   int rc = check_args(ops, out, ws, ws_bytes, &L);
   if (rc) return rc;
   const i64 n = ops->n_a + ops->n_b;
-  g_plan = SMX_PLAN_PRESORTED;
+  const bool small = small_merge(n);
+  g_plan = small ? SMX_PLAN_SMALL : SMX_PLAN_PRESORTED;
   if (n == 0) {
     HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));
     return SMX_OK;
   }
   const bool timed = profiling_on() != 0;
-  if (SMX_GRAPH && st != nullptr && !timed && !knob("SMX_NO_GRAPH", 0)) {
+  if (SMX_GRAPH && !small && st != nullptr && !timed && !knob("SMX_NO_GRAPH", 0)) {
     bool done = false;
     if ((rc = compose_async_graph(ops, out, ws, ws_bytes, L, st, &done))) return rc;
     if (done) return SMX_OK;
@@ -3087,6 +3106,11 @@ extern "C" int smx_compose(const smx_ops* ops, const smx_compose_out* out, void*
 }
 
 extern "C" int smx_last_plan(void) { return g_plan; }
+
+extern "C" int64_t smx_set_small_limit(int64_t n) {
+  const int64_t v = n < 0 ? 0 : n > SMALL_N ? SMALL_N : n;
+  return g_small_max.exchange(SMX_SMALL ? v : 0);
+}
 
 extern "C" int smx_set_profiling(int enabled) {
   std::lock_guard<std::mutex> g(g_prof_mu);

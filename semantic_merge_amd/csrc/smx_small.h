@@ -1,0 +1,396 @@
+// smx_small.h — a whole merge in one workgroup, for merges of at most SMALL_N ops (the
+// CLI's merges: one op log per branch from a single diff, thousands of ops).
+//
+// The pipeline of the large merges (plan, windows, walk, tables, emit: ~25 launches)
+// is latency, not work, at these sizes.  Here one 1024-thread workgroup holds the merge
+// in LDS and runs the reference's composition (semmerge/compose.py:11-114) start to end:
+//   1. T = the stable order of A||B by (precedence, timestamp, id, side, index)
+//      (compose.py:16-21 sorted() per branch + the A-first merge :51-56).  Branch logs
+//      ordered by (timestamp, id) -- lift.ts emits them so -- are merged by rank (each
+//      op binary-searches the other branch), then split stably by precedence (wave
+//      ballots per kind, one scan); logs in any other order take a bitonic sort of the
+//      op indices on the full key;
+//   2. the DivergentRename walk (compose.py:60-70, 88-98) over the rename block of T:
+//      the reference's two heads, restricted to renames (T is ordered by precedence
+//      first, so both heads are renames exactly while both branches are in their rename
+//      blocks); a conflict skips both heads and records (A-op, B-op).  Between two
+//      conflicts the heads step through the rename block in T order, so one wave tests
+//      the next 64 head pairs at once (each lane's pair from a prefix count of A's
+//      renames) and jumps to the first conflict: one step per conflict or per 64 renames;
+//   3. the chains (compose.py:27-28, 71-82, 99-110): per-symbol last writers in T order
+//      in an LDS hash table on the symbol -- the final move address / file and the final
+//      non-skipped rename; a move with a None value looks back for its symbol's last
+//      non-None one (the inclusive prefix the reference's move_chain holds);
+//   4. materialize (compose.py:30-49): each op of T that is not skipped, at T minus the
+//      skips before it, with the ids it sees.
+// Same outputs, same meta fields as smx_compose's large-merge path.
+#pragma once
+
+#include "smx_common.h"
+
+#define SMALL_N 2048  // ops per merge
+#define SMALL_NT 1024
+#define SMALL_HT 4096  // hash slots (symbols), a power of two >= 2 * SMALL_N
+#define SMALL_EMPTY 0xffffffffu
+
+__global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_compose_out out, ComposeMeta* meta) {
+  constexpr int IT = SMALL_N / SMALL_NT;
+  constexpr int NW = SMALL_NT / WAVE;
+  // keys of the sort (dead after it: the hash table takes their place)
+  __shared__ __attribute__((aligned(16))) u64 keys[3][SMALL_N];
+  u64* kts = keys[0];
+  u64* khi = keys[1];
+  u64* klo = keys[2];
+  __shared__ u8 skd[SMALL_N];     // kind by element
+  __shared__ u16 ord[SMALL_N];    // T -> element
+  __shared__ u16 mrg[SMALL_N];    // ordered logs: (key, side, index) order -> element
+  __shared__ u32 ssym[SMALL_N];   // by element
+  __shared__ i32 sv0[SMALL_N], sv1[SMALL_N];
+  __shared__ u8 skip[SMALL_N];    // by T: a rename the walk skipped
+  __shared__ u16 rat[SMALL_N + 1];  // rename block: A's renames before T
+  __shared__ u16 posA[SMALL_N], posB[SMALL_N];  // the i-th rename of a side: its T
+  __shared__ u32 symA[SMALL_N], symB[SMALL_N];
+  __shared__ i32 nnA[SMALL_N], nnB[SMALL_N];    // ... its newName id
+  __shared__ u32 wcnt[SMX_N_KINDS * NW];          // per (kind, wave): ops, then their start
+  __shared__ u32 sscan[NW + 1];
+  __shared__ u32 sinfo[8];  // [2] nmv, [3] rend
+  u32* hkey = reinterpret_cast<u32*>(keys[0]);              // [SMALL_HT] symbol of the slot
+  u16* hw = reinterpret_cast<u16*>(keys[1]);                 // [3][SMALL_HT]: T + 1 of the last
+                                                             // addr / file writer and of the
+                                                             // last kept rename (0: none)
+  static_assert(SMALL_HT * 4 <= SMALL_N * 8 && 3 * SMALL_HT * 2 <= 2 * SMALL_N * 8, "hash table in the keys");
+  static_assert(SMX_N_KINDS * NW <= 5 * WAVE, "kind scan: 5 counters per lane");
+  const int t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
+  const i64 na = ops.n_a, nb = ops.n_b;
+  const int n = (int)(na + nb);
+  if (t < 8) sinfo[t] = 0;
+  if (t < (int)(sizeof(ComposeMeta) / 4)) reinterpret_cast<u32*>(meta)[t] = 0u;
+  // 1. load (B op j is stored at j + b_gap)
+  u32 bad = 0;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = t + SMALL_NT * i;
+    if (e < n) {
+      const i64 j = e < na ? (i64)e : (i64)e + ops.b_gap;
+      const u32 k = ops.kind[j], s = ops.sym[j];
+      bad |= (k >= SMX_N_KINDS) | (s >= (u64)ops.n_sym);
+      skd[e] = (u8)(k < SMX_N_KINDS ? k : SMX_N_KINDS - 1);
+      kts[e] = ops.ts[j];
+      khi[e] = ops.oid_hi[j];
+      klo[e] = ops.oid_lo[j];
+      ssym[e] = s;
+      sv0[e] = ops.v0[j];
+      sv1[e] = ops.v1[j];
+    }
+    skip[e] = 0;
+  }
+  if (__syncthreads_or(bad)) {  // invalid input: the call fails (as the large path: counts -1)
+    if (t == 0) {
+      meta->bad_sym = 1;
+      out.counts[0] = -1;
+      out.counts[1] = -1;
+    }
+    return;
+  }
+  auto key_lt = [&](u32 x, u32 y) -> bool {  // (ts, id) of x < that of y
+    if (kts[x] != kts[y]) return kts[x] < kts[y];
+    if (khi[x] != khi[y]) return khi[x] < khi[y];
+    return klo[x] < klo[y];
+  };
+  // are both branch logs ordered by (ts, id)?
+  bool unord = false;
+  {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = t + SMALL_NT * i;
+      if (e < n && e != 0 && e != (int)na) unord |= key_lt((u32)e, (u32)e - 1u);
+    }
+    unord = __syncthreads_or(unord);
+  }
+  if (!unord) {
+    // 1a. merge by rank: an A op goes after B's ops with a smaller key, a B op after
+    //     A's ops with a key not larger (ties: A first)
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = t + SMALL_NT * i;
+      if (e >= n) continue;
+      const bool sa = e < (int)na;
+      int lo = sa ? (int)na : 0, hi = sa ? n : (int)na;  // search the other branch
+      const int base = lo;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const bool before = sa ? key_lt((u32)mid, (u32)e) : !key_lt((u32)e, (u32)mid);
+        if (before) lo = mid + 1;
+        else hi = mid;
+      }
+      mrg[(sa ? e : e - (int)na) + (lo - base)] = (u16)e;
+    }
+    __syncthreads();
+    // 1b. stable split by kind: the rank inside the wave from one ballot pair per kind,
+    //     the wave's start from a scan over (kind, wave)
+    u32 k0, k1, r0 = 0, r1 = 0;
+    {
+      const int m = 2 * t;
+      k0 = m < n ? skd[mrg[m]] : 0xffu;
+      k1 = m + 1 < n ? skd[mrg[m + 1]] : 0xffu;
+      const u64 lt = lanemask_lt();
+#pragma unroll 1
+      for (u32 k = 0; k < SMX_N_KINDS; ++k) {
+        const u64 b0 = __ballot(k0 == k), b1 = __ballot(k1 == k);
+        const u32 c = (u32)__popcll(b0 & lt) + (u32)__popcll(b1 & lt);
+        if (k0 == k) r0 = c;
+        if (k1 == k) r1 = c + (k0 == k);
+        if (lane == 0) wcnt[k * NW + w] = (u32)__popcll(b0) + (u32)__popcll(b1);
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+      u32 v[5], s = 0;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const int x = 5 * lane + q;
+        v[q] = x < SMX_N_KINDS * NW ? wcnt[x] : 0u;
+        s += v[q];
+      }
+      u32 run = wave_incl_sum_u32(s) - s;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const int x = 5 * lane + q;
+        if (x < SMX_N_KINDS * NW) wcnt[x] = run;
+        run += v[q];
+      }
+    }
+    __syncthreads();
+    if (2 * t < n) ord[wcnt[k0 * NW + w] + r0] = mrg[2 * t];
+    if (2 * t + 1 < n) ord[wcnt[k1 * NW + w] + r1] = mrg[2 * t + 1];
+  } else {
+    // logs in any order: a bitonic sort of the op indices on the full key; elements
+    // past n sort last (their slots are never read)
+    auto less = [&](u32 x, u32 y) -> bool {  // x before y in T (x != y)
+      if ((int)x >= n || (int)y >= n) return (int)y >= n && (int)x < n;
+      if (skd[x] != skd[y]) return skd[x] < skd[y];
+      if (kts[x] != kts[y]) return kts[x] < kts[y];
+      if (khi[x] != khi[y]) return khi[x] < khi[y];
+      if (klo[x] != klo[y]) return klo[x] < klo[y];
+      return x < y;  // (side, index): A before B, then the branch index
+    };
+#pragma unroll
+    for (int i = 0; i < IT; ++i) ord[t + SMALL_NT * i] = (u16)(t + SMALL_NT * i);
+    __syncthreads();
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int k = 2; k <= P; k <<= 1) {
+      for (int jj = k >> 1; jj > 0; jj >>= 1) {
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+          const int a = t + SMALL_NT * i;
+          const int b = a ^ jj;
+          if (a < P && b > a) {
+            const u32 x = ord[a], y = ord[b];
+            const bool up = (a & k) == 0;
+            if (up ? less(y, x) : less(x, y)) {
+              ord[a] = (u16)y;
+              ord[b] = (u16)x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  __syncthreads();
+  // the move block [0, nmv), the rename block [nmv, rend): at the kind boundaries
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int T = t * IT + i;
+    if (T >= n) continue;
+    const u32 k = skd[ord[T]], kn = T + 1 < n ? skd[ord[T + 1]] : 0xffu;
+    if (k <= SMX_KIND_MOVE && kn > SMX_KIND_MOVE) sinfo[2] = (u32)T + 1u;
+    if (k <= SMX_KIND_RENAME && kn > SMX_KIND_RENAME) sinfo[3] = (u32)T + 1u;
+  }
+  __syncthreads();
+  const int nmv = (int)sinfo[2], rend = (int)sinfo[3];
+  // 2. the rename lists of the two sides, in T order
+  u32 isa[IT], acc = 0;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int T = t * IT + i;
+    isa[i] = T >= nmv && T < rend && ord[T] < (u32)na;
+    acc += isa[i];
+  }
+  u32 n_ren_a;
+  u32 ra = block_excl_scan<OpSum, u32, NW>(acc, sscan, &n_ren_a);  // (syncs)
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int T = t * IT + i;
+    if (T >= nmv && T <= rend) rat[T] = (u16)ra;
+    if (T >= nmv && T < rend) {
+      const u32 e = ord[T];
+      if (isa[i]) {
+        posA[ra] = (u16)T;
+        symA[ra] = ssym[e];
+        nnA[ra] = sv0[e];
+      } else {
+        const int j = T - nmv - (int)ra;
+        posB[j] = (u16)T;
+        symB[j] = ssym[e];
+        nnB[j] = sv0[e];
+      }
+    }
+    ra += isa[i];
+  }
+  if (t == 0 && rend == n) rat[n] = (u16)n_ren_a;  // (T == n is no thread's)
+  __syncthreads();
+  if (w == 0) {
+    // the walk: state (ia, ib) = the heads' indices in the side lists (wave-uniform)
+    const int nA = (int)n_ren_a, nB = rend - nmv - nA;
+    int ia = 0, ib = 0;
+    u32 nc = 0;
+    while (ia < nA && ib < nB) {
+      const int pa = posA[ia], pb = posB[ib];
+      // lane k: the heads after k steps without a conflict -- first the leading side's
+      // renames before the other head, then every rename of the block in T order
+      int xa, xb;
+      const int g = pa < pb ? (int)rat[pb] - ia : (pa - nmv - (int)rat[pa]) - ib;
+      if (lane < g) {
+        xa = pa < pb ? ia + lane : ia;
+        xb = pa < pb ? ib : ib + lane;
+      } else {
+        const int q = (pa < pb ? pb : pa) + (lane - g);
+        xa = q < rend ? (int)rat[q] : nA;
+        xb = q < rend ? q - nmv - xa : nB;
+      }
+      const bool valid = xa < nA && xb < nB;
+      const bool conf = valid && symA[xa] == symB[xb] && nnA[xa] != nnB[xb];
+      const u64 cm = __ballot(conf), im = __ballot(!valid);
+      const int jc = cm ? __builtin_ctzll(cm) : WAVE, ji = im ? __builtin_ctzll(im) : WAVE;
+      if (jc < ji) {
+        const int ca = __builtin_amdgcn_readlane(xa, jc), cb = __builtin_amdgcn_readlane(xb, jc);
+        if (lane == 0) {
+          const int ta = posA[ca], tb = posB[cb];
+          if ((i64)nc < out.conflict_cap) {
+            out.conflicts[2 * nc] = (i32)ord[ta];
+            out.conflicts[2 * nc + 1] = (i32)ord[tb];
+          }
+          skip[ta] = 1;
+          skip[tb] = 1;
+        }
+        ++nc;
+        ia = ca + 1;
+        ib = cb + 1;
+      } else if (ji < WAVE) {
+        break;
+      } else {
+        ia = __builtin_amdgcn_readlane(xa, WAVE - 1);
+        ib = __builtin_amdgcn_readlane(xb, WAVE - 1);
+      }
+    }
+    if (lane == 0) {
+      out.counts[0] = (i64)(n - 2 * (int)nc);
+      out.counts[1] = (i64)nc;
+      meta->n_conf = nc;
+      meta->n_skip = 2 * nc;
+    }
+  }
+  // the keys are dead: the hash table takes their LDS
+  for (int i = t; i < SMALL_HT; i += SMALL_NT) {
+    hkey[i] = SMALL_EMPTY;
+    hw[i] = hw[SMALL_HT + i] = hw[2 * SMALL_HT + i] = 0;
+  }
+  __syncthreads();
+  // 3. the chains: every op's symbol slot (moves and renames insert, the rest look up)
+  auto slot_of = [&](u32 s, bool ins) -> int {
+    u32 h = (s * 2654435761u) >> (32 - 12);
+    for (int probe = 0; probe < SMALL_HT; ++probe, h = (h + 1) & (SMALL_HT - 1)) {
+      const u32 cur = hkey[h];
+      if (cur == s) return (int)h;
+      if (cur == SMALL_EMPTY) {
+        if (!ins) return -1;
+        const u32 old = atomicCAS(&hkey[h], SMALL_EMPTY, s);
+        if (old == SMALL_EMPTY || old == s) return (int)h;
+      }
+    }
+    return -1;  // (unreachable: at most SMALL_N symbols in SMALL_HT slots)
+  };
+  int slot_r[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int T = t + SMALL_NT * i;
+    slot_r[i] = -1;
+    if (T >= rend) continue;
+    slot_r[i] = slot_of(ssym[ord[T]], true);
+  }
+  __syncthreads();
+  // last writers: T + 1 packed in u16 (T < SMALL_N); an atomic max on a u16 is emulated
+  // with a CAS loop on its 32-bit word
+  auto max16 = [&](u16* base, int h, u32 v) {
+    u32* wd = reinterpret_cast<u32*>(base) + (h >> 1);
+    const u32 sh = 16u * (u32)(h & 1);
+    u32 old = *wd;
+    while (((old >> sh) & 0xffffu) < v) {
+      const u32 nw = (old & ~(0xffffu << sh)) | (v << sh);
+      const u32 got = atomicCAS(wd, old, nw);
+      if (got == old) break;
+      old = got;
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int T = t + SMALL_NT * i;
+    if (slot_r[i] < 0) continue;
+    const u32 e = ord[T];
+    if (T < nmv) {
+      if (sv0[e] >= 0) max16(hw, slot_r[i], (u32)T + 1u);
+      if (sv1[e] >= 0) max16(hw + SMALL_HT, slot_r[i], (u32)T + 1u);
+    } else if (!skip[T]) {  // a kept rename (compose.py:71-72)
+      max16(hw + 2 * SMALL_HT, slot_r[i], (u32)T + 1u);
+    }
+  }
+  // skips before each T (renames only): exclusive scan of the skip flags, IT per thread
+  u32 sk[IT];
+  acc = 0;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    sk[i] = (t * IT + i) < n ? skip[t * IT + i] : 0u;
+    acc += sk[i];
+  }
+  u32 tot;
+  const u32 sbase = block_excl_scan<OpSum, u32, NW>(acc, sscan, &tot);  // (syncs)
+  // 4. materialize: T -> T - skips before it
+  u32 run = sbase;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int T = t * IT + i;
+    const u32 before = run;
+    run += sk[i];
+    if (T >= n || sk[i]) continue;
+    const u32 e = ord[T];
+    const u32 k = skd[e], s = ssym[e];
+    i32 a = SMX_NONE, f = SMX_NONE, c = SMX_NONE;
+    if (T < nmv) {
+      // the inclusive prefix of the symbol's moves: its own value, else the last earlier
+      // non-None one (compose.py:73-82 then 37-41)
+      a = sv0[e];
+      f = sv1[e];
+      for (int q = T - 1; q >= 0 && (a < 0 || f < 0); --q) {
+        const u32 eq = ord[q];
+        if (ssym[eq] != s) continue;
+        if (a < 0 && sv0[eq] >= 0) a = sv0[eq];
+        if (f < 0 && sv1[eq] >= 0) f = sv1[eq];
+      }
+    } else {
+      const int h = slot_of(s, false);
+      if (h >= 0) {
+        const u32 wa = hw[h], wf = hw[SMALL_HT + h], wr = hw[2 * SMALL_HT + h];
+        if (wa) a = sv0[ord[wa - 1]];
+        if (wf) f = sv1[ord[wf - 1]];
+        if (k != SMX_KIND_RENAME && wr) c = sv1[ord[wr - 1]];  // renameContext: non-renames only
+      }
+    }
+    const u32 o = (u32)T - before;
+    out.order[o] = (i32)e;
+    out.addr[o] = a;
+    out.file[o] = f;
+    out.ctx[o] = c;
+  }
+}

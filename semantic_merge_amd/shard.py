@@ -248,6 +248,7 @@ class ShardedCompose:
         self.part32 = torch.zeros(3 * max(n_sym, 1) + 3, dtype=torch.int32, device=dv) \
             if self.tab_bits else None
         self.tab32_used = 0  # tables steps that ran with 32-bit entries (tests, probes)
+        self.emit_redo = 0   # steps whose speculative tables and EMIT were redone
         self.tab_redo = 0    # steps whose 32-bit tables overflowed and were redone with 64-bit entries
         self.n_xchg = 0      # ops this rank received from other ranks in the last exchange
         self.order_fixes = 0  # ORDER_FIX runs (dense timestamp ties) on this rank
@@ -676,16 +677,20 @@ class ShardedCompose:
         self.comm.all_reduce_max(self.part)        # last writers and value widths together
 
     def run(self) -> None:
-        """One sharded composition (collective: every rank calls it).  Host syncs: the
-        exchange's split sizes, then one read of the gathered walk summaries; the tables
-        and their all_reduce are enqueued before that read (speculatively: redone when
-        the walk re-ran, an ORDER failed or a move has a None value)."""
+        """One sharded composition (collective: every rank calls it).  One host sync in
+        the pipeline: the exchange's split sizes.  Everything after it -- ORDER, WALK, the
+        tables and their all_reduce, EMIT -- is enqueued speculatively, and the gathered
+        walk summaries are read once at the end, when the step's work is done; in the
+        rare case they call for it (the walk re-ran for a region handed across shards, an
+        ORDER failed, a table value was too wide for 32 bits, a move has a None value)
+        the tables and EMIT are redone."""
         self.exchange()
         self._step(_abi.SHARD_ORDER)
         self._order_exchange()
         self.in_dev.zero_()
         self._step(_abi.SHARD_WALK)
         self._tables(None, rescatter=False, wide=False)
+        self._emit(None)
         summ, reran = self._walk(first_done=True)
         final = (not reran and not summ[:, S_FAIL].any() and summ[:, S_MVNONE].sum() == 0
                  and not summ[:, S_TABOVER].any())
@@ -704,15 +709,24 @@ class ShardedCompose:
             summ, _ = self._walk()
             if summ[:, S_FAIL].any():
                 self._fail(summ, err)
-        if not final:  # the speculative tables do not hold: every rank redoes them
+        if not final:  # the speculative tables and EMIT do not hold: every rank redoes them
             self.tab_redo += int(bool(summ[:, S_TABOVER].any()))
+            self.emit_redo += 1
             self._tables(summ, rescatter=True)
+            self._emit(summ)
         self.sum_walk = summ
-        self._sum_host = np.ascontiguousarray(summ[self.rank], dtype=np.int64)
-        self._sh.summary_host = self._sum_host.ctypes.data
-        self._step(_abi.SHARD_EMIT)
         if self.restore:
             self._restore()
+
+    def _emit(self, summ: Optional[np.ndarray]) -> None:
+        """EMIT from the gathered summaries, or speculatively (summ None: before they are
+        read, as if no move had a None value -- run() redoes it when one has)."""
+        if summ is None:
+            self._sum_host = np.zeros(self.summary.numel(), np.int64)
+        else:
+            self._sum_host = np.ascontiguousarray(summ[self.rank], dtype=np.int64)
+        self._sh.summary_host = self._sum_host.ctypes.data
+        self._step(_abi.SHARD_EMIT)
 
     def _fail(self, summ: np.ndarray, err=None):
         f = int(np.bitwise_or.reduce(summ[:, S_FAIL]))

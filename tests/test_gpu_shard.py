@@ -89,7 +89,9 @@ def _make(case):
     if kind == "wide_value":  # one move's address id too wide for the 32-bit partial tables
         soa = _make(("lift", n, n_sym, seed))
         mv = np.flatnonzero(soa.kind == 0)
-        soa.v0[mv[len(mv) // 3]] = (1 << 30) + 7
+        # every move of one symbol: its shard's last writer of the address is then wide
+        s = soa.sym[mv[len(mv) // 3]]
+        soa.v0[mv[soa.sym[mv] == s]] = (1 << 30) + 7
         return soa
     if kind == "lift":
         spec = synth.LiftSpec(n, n_sym, seed, ops_per_ms=64)

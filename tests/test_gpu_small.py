@@ -1,0 +1,70 @@
+"""GPU parity of the small-merge plan (SMX_PLAN_SMALL, smx_small.h: merges of at most 2048
+ops in one workgroup) against the golden vectors and the CPU oracle, and the same cases
+forced through the window plans (smx_set_small_limit(0)) so both paths stay covered."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from semantic_merge_amd import synth
+from semantic_merge_amd._lib import DeviceCompose, compose_soa, set_small_limit
+
+from _util import assert_case, load
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["small", "windows"])
+def plan(request):
+    old = set_small_limit(2048 if request.param == "small" else 0)
+    yield request.param
+    set_small_limit(old)
+
+
+def _eq(gpu, ref, label):
+    for name, g, r in zip(("order", "addr", "file", "ctx", "conflicts"), gpu, ref):
+        assert g.shape == r.shape, f"{label}: {name} shape {g.shape} vs {r.shape}"
+        if not np.array_equal(g, r):
+            bad = np.flatnonzero(g.reshape(-1) != r.reshape(-1))[:5]
+            raise AssertionError(f"{label}: {name} differs at {bad.tolist()}")
+
+
+def test_golden_both_plans(plan):
+    for name, case in load("compose_scenarios.json").items():
+        assert_case(compose_soa, case, f"{plan} {name}")
+    for i, case in enumerate(load("compose_cases.json")):
+        assert_case(compose_soa, case, f"{plan} case {i}")
+
+
+SPECS = [
+    synth.LiftSpec(1, 1, 3),
+    synth.LiftSpec(2, 1, 4),
+    synth.LiftSpec(17, 3, 5, ops_per_ms=1),
+    synth.LiftSpec(1000, 100, 6),
+    synth.LiftSpec(1000, 20, 7, shuffle=True),
+    synth.LiftSpec(2000, 30, 8, ops_per_ms=4096, mix=synth.ADVERSARIAL_MIX, rename_overlap=1.0),
+    synth.LiftSpec(2047, 5, 9, ops_per_ms=1, mix=synth.ADVERSARIAL_MIX, divergent=0.5),
+    synth.LiftSpec(2048, 2048, 10, shuffle=True, mix=synth.ADVERSARIAL_MIX),
+    synth.LiftSpec(2048, 1, 12, ops_per_ms=1),
+]
+
+
+@pytest.mark.parametrize("spec", SPECS, ids=lambda s: f"{s.n_total}x{s.n_sym}s{s.seed}")
+def test_synthetic_small(plan, spec):
+    soa = synth.lift_soa(synth.lift_logs(spec))
+    _eq(compose_soa(soa), oracle.compose(soa), f"{plan} {spec}")
+    assert (DeviceCompose.last_plan() == "small") == (plan == "small")
+
+
+def test_size_boundary():
+    """2048 ops take the small plan, 2049 the window plans; both match the oracle."""
+    for n, small in ((2048, True), (2049, False)):
+        soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(n, 40, 13, mix=synth.ADVERSARIAL_MIX)))
+        _eq(compose_soa(soa), oracle.compose(soa), f"n={n}")
+        assert (DeviceCompose.last_plan() == "small") == small
+
+
+def test_invalid_symbol_fails(plan):
+    soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(300, 10, 14)))
+    soa.sym[5] = soa.n_sym  # out of range
+    with pytest.raises(Exception):
+        compose_soa(soa)

@@ -10,7 +10,7 @@ HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 
 
 
 def test_header_and_exports_agree():
-    declared = set(re.findall(r"^(?:int|const char\*)\s+(smx_\w+)\(", open(HDR).read(), re.M))
+    declared = set(re.findall(r"^(?:int|int64_t|const char\*)\s+(smx_\w+)\(", open(HDR).read(), re.M))
     assert declared == set(_abi.EXPORTS)
 
 

@@ -2,7 +2,7 @@
 # GPU-box steps for iterating (each under its own time limit; stops at the first failure):
 #   gpurun -- bash tools/gpu_steps.sh <tag> <step> [<step> ...]
 # steps: rga (RGA GPU tests), compose (compose GPU tests incl. full-size digests),
-#        gtests (the whole -m gpu suite), ab (tools/ab_libs.py, current vs tools/_build/var_old),
+#        small (small-plan tests + tools/small_merge_probe.py), gtests (the whole -m gpu suite), ab (tools/ab_libs.py, current vs tools/_build/var_old),
 #        ab5 (the same on config 5), rgabench (tools/bench_rga.py), bench (bench.py, no PMC / CPU
 #        legs), benchfull (bench.py default), c5 (bench.py --config c5), c2, prof, sq
 set -o pipefail
@@ -20,6 +20,18 @@ for s in "$@"; do
          tail -2 "$O/rga_tests.log";;
     compose) run 900 compose_tests.log python -u -m pytest tests/test_gpu_compose.py tests/test_gpu_full.py -x -v --timeout 300 --timeout-method thread
          tail -2 "$O/compose_tests.log";;
+    small) run 300 small_tests.log python -u -m pytest tests/test_gpu_small.py -x -v --timeout 120 --timeout-method thread
+         tail -2 "$O/small_tests.log"
+         run 300 small_probe.json python -u tools/small_merge_probe.py --sizes 1000,2000,10000,1000000 --verify
+         tail -1 "$O/small_probe.json";;
+    smallprof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/sprof" -o p -- python3 "$R/tools/small_merge_probe.py" --sizes 1000,2000 --reps 30 > "$O/sprof.log" 2>&1) || { echo "smallprof failed"; tail -20 "$O/sprof.log"; exit 1; }
+          python3 tools/prof_export.py "$O/sprof" "$O/small_kernel_stats.csv" && head -5 "$O/small_kernel_stats.csv";;
+    c2prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/c2prof" -o p -- python3 "$R/tools/small_merge_probe.py" --sizes 1000000 --reps 20 > "$O/c2prof.log" 2>&1) || { echo "c2prof failed"; tail -20 "$O/c2prof.log"; exit 1; }
+          python3 tools/prof_timeline.py "$O/c2prof" 40 > "$O/c2_timeline.txt" && tail -42 "$O/c2_timeline.txt";;
+    shard) run 900 shard_tests.log python -u -m pytest tests/test_gpu_shard.py -x -v --timeout 400 --timeout-method thread
+         tail -2 "$O/shard_tests.log"
+         run 300 shard_probe.txt python -u tools/shard_probe.py 8
+         tail -6 "$O/shard_probe.txt";;
     gtests) run 1100 tests.log python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread
          tail -2 "$O/tests.log";;
     ab) run 400 ab_c3.txt python -u tools/ab_libs.py --rounds 4 new=semantic_merge_amd/libsmx.so old=tools/_build/var_old/libsmx.so
