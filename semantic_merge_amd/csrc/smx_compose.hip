@@ -3107,6 +3107,15 @@ extern "C" int smx_compose(const smx_ops* ops, const smx_compose_out* out, void*
 
 extern "C" int smx_last_plan(void) { return g_plan; }
 
+#ifdef SMALL_STAMPS
+// diagnostic builds only: the small kernel's phase stamps of its last call (wall clock, 100 MHz)
+extern "C" int smx_diag_small_stamps(uint64_t* host16) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_small_stamp), 16 * sizeof(u64)));
+  return SMX_OK;
+}
+#endif
+
 extern "C" int64_t smx_set_small_limit(int64_t n) {
   const int64_t v = n < 0 ? 0 : n > SMALL_N ? SMALL_N : n;
   return g_small_max.exchange(SMX_SMALL ? v : 0);

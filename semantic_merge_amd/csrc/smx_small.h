@@ -6,10 +6,11 @@
 // in LDS and runs the reference's composition (semmerge/compose.py:11-114) start to end:
 //   1. T = the stable order of A||B by (precedence, timestamp, id, side, index)
 //      (compose.py:16-21 sorted() per branch + the A-first merge :51-56).  Branch logs
-//      ordered by (timestamp, id) -- lift.ts emits them so -- are merged by rank (each
-//      op binary-searches the other branch), then split stably by precedence (wave
-//      ballots per kind, one scan); logs in any other order take a bitonic sort of the
-//      op indices on the full key;
+//      whose timestamps do not decrease (lift.ts emits them so) are ordered in merged
+//      runs of equal timestamps (a binary search in the other branch places each run;
+//      interpolation buckets on the id order it), then split stably by precedence (wave
+//      ballots per kind, one scan); logs in any other order, or ids whose top bits
+//      cluster, take a bitonic sort of the op indices on the full key;
 //   2. the DivergentRename walk (compose.py:60-70, 88-98) over the rename block of T:
 //      the reference's two heads, restricted to renames (T is ordered by precedence
 //      first, so both heads are renames exactly while both branches are in their rename
@@ -32,6 +33,19 @@
 #define SMALL_NT 1024
 #define SMALL_HT 4096  // hash slots (symbols), a power of two >= 2 * SMALL_N
 #define SMALL_EMPTY 0xffffffffu
+#define SMALL_BKT 32  // largest interpolation bucket ranked by counting (larger: bitonic sort)
+
+#ifdef SMALL_STAMPS  // phase timestamps of the last call (diagnostic builds, tools/small_phases.py)
+__device__ u64 g_small_stamp[16];
+#define SMALL_STAMP(i) \
+  do {                 \
+    if (threadIdx.x == 0) g_small_stamp[i] = wall_clock64(); \
+  } while (0)
+#else
+#define SMALL_STAMP(i) \
+  do {                 \
+  } while (0)
+#endif
 
 __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_compose_out out, ComposeMeta* meta) {
   constexpr int IT = SMALL_N / SMALL_NT;
@@ -43,14 +57,15 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
   u64* klo = keys[2];
   __shared__ u8 skd[SMALL_N];     // kind by element
   __shared__ u16 ord[SMALL_N];    // T -> element
-  __shared__ u16 mrg[SMALL_N];    // ordered logs: (key, side, index) order -> element
+  __shared__ u16 mrg[SMALL_N];    // ordered logs: (ts, id, index) order -> element
   __shared__ u32 ssym[SMALL_N];   // by element
   __shared__ i32 sv0[SMALL_N], sv1[SMALL_N];
   __shared__ u8 skip[SMALL_N];    // by T: a rename the walk skipped
-  __shared__ u16 rat[SMALL_N + 1];  // rename block: A's renames before T
+  __shared__ u16 rat[SMALL_N + 1];  // rename block: A's renames before T (1a, 1b: run ends)
   __shared__ u16 posA[SMALL_N], posB[SMALL_N];  // the i-th rename of a side: its T
-  __shared__ u32 symA[SMALL_N], symB[SMALL_N];
-  __shared__ i32 nnA[SMALL_N], nnB[SMALL_N];    // ... its newName id
+  __shared__ u64 sn[SMALL_N];                   // rename block, by T: symbol << 32 | newName
+                                                // (1b: bucket counts and fill)
+  __shared__ u32 nxtA[SMALL_N + 1], nxtB[SMALL_N + 1];  // next rename of a side at or after T
   __shared__ u32 wcnt[SMX_N_KINDS * NW];          // per (kind, wave): ops, then their start
   __shared__ u32 sscan[NW + 1];
   __shared__ u32 sinfo[8];  // [2] nmv, [3] rend
@@ -65,6 +80,7 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
   const int n = (int)(na + nb);
   if (t < 8) sinfo[t] = 0;
   if (t < (int)(sizeof(ComposeMeta) / 4)) reinterpret_cast<u32*>(meta)[t] = 0u;
+  SMALL_STAMP(0);
   // 1. load (B op j is stored at j + b_gap)
   u32 bad = 0;
 #pragma unroll
@@ -83,6 +99,8 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
       sv1[e] = ops.v1[j];
     }
     skip[e] = 0;
+    reinterpret_cast<u32*>(sn)[e] = 0u;  // (1b's bucket counts and fill)
+    reinterpret_cast<u32*>(sn)[SMALL_N + e] = 0u;
   }
   if (__syncthreads_or(bad)) {  // invalid input: the call fails (as the large path: counts -1)
     if (t == 0) {
@@ -92,41 +110,115 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
     }
     return;
   }
+  SMALL_STAMP(1);
   auto key_lt = [&](u32 x, u32 y) -> bool {  // (ts, id) of x < that of y
     if (kts[x] != kts[y]) return kts[x] < kts[y];
     if (khi[x] != khi[y]) return khi[x] < khi[y];
     return klo[x] < klo[y];
   };
-  // are both branch logs ordered by (ts, id)?
-  bool unord = false;
+  // 1a. the runs of equal timestamps of each branch (blocked: thread t holds ops IT t ..):
+  //     a run's start from a max-scan of the start flags, its end stored at its start (in
+  //     rat, free until step 2).  A decreasing timestamp sends the merge to the bitonic sort.
+  bool slow = false;
+  u32 rs[IT];
   {
+    u32 mx = 0;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int e = t + SMALL_NT * i;
-      if (e < n && e != 0 && e != (int)na) unord |= key_lt((u32)e, (u32)e - 1u);
+      const int e = t * IT + i;
+      const bool first = e == 0 || e == (int)na;
+      rs[i] = e < n && (first || kts[e] != kts[e - 1]) ? (u32)e : 0u;
+      slow |= e < n && !first && kts[e] < kts[e - 1];
+      mx = rs[i] > mx ? rs[i] : mx;
     }
-    unord = __syncthreads_or(unord);
-  }
-  if (!unord) {
-    // 1a. merge by rank: an A op goes after B's ops with a smaller key, a B op after
-    //     A's ops with a key not larger (ties: A first)
+    u32 tot;
+    u32 run = block_excl_scan<OpMax, u32, NW>(mx, sscan, &tot);  // (syncs)
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int e = t + SMALL_NT * i;
+      const int e = t * IT + i;
+      run = rs[i] > run ? rs[i] : run;
+      rs[i] = run;
+      if (e < n && (e + 1 == n || e + 1 == (int)na || kts[e + 1] != kts[e])) rat[run] = (u16)(e + 1);
+    }
+    slow = __syncthreads_or(slow);
+  }
+  SMALL_STAMP(2);
+  if (!slow) {
+    // 1b. each op's merged run: the ops of both branches with its timestamp, which start at
+    //     (own ops before its run) + (the other branch's ops with a smaller timestamp, by a
+    //     binary search); inside it, interpolation buckets on the top 32 id bits (one op per
+    //     bucket on random ids; counts in LDS, one scan), then each op ranks itself on
+    //     (id, index) among its bucket's ops.  Ties: A before B = the lower index.
+    u32* bcnt = reinterpret_cast<u32*>(sn);  // [SMALL_N] bucket counts, then starts
+    u32* bfill = bcnt + SMALL_N;             // [SMALL_N] bucket fill
+    u32 bk[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = t * IT + i;
+      bk[i] = 0;
       if (e >= n) continue;
       const bool sa = e < (int)na;
-      int lo = sa ? (int)na : 0, hi = sa ? n : (int)na;  // search the other branch
+      const u64 ts = kts[e];
+      int lo = sa ? (int)na : 0, hi = sa ? n : (int)na;  // the other branch: first ts >= ours
       const int base = lo;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        const bool before = sa ? key_lt((u32)mid, (u32)e) : !key_lt((u32)e, (u32)mid);
-        if (before) lo = mid + 1;
+        if (kts[mid] < ts) lo = mid + 1;
         else hi = mid;
       }
-      mrg[(sa ? e : e - (int)na) + (lo - base)] = (u16)e;
+      const u32 eq = lo < (sa ? n : (int)na) && kts[lo] == ts ? (u32)rat[lo] - (u32)lo : 0u;
+      const u32 s0 = rs[i], len = (u32)rat[s0] - s0 + eq;
+      const u32 m0 = (s0 - (sa ? 0u : (u32)na)) + (u32)(lo - base);
+      bk[i] = m0 + (u32)(((u64)len * (u32)(khi[e] >> 32)) >> 32);
+      atomicAdd(&bcnt[bk[i]], 1u);
     }
     __syncthreads();
-    // 1b. stable split by kind: the rank inside the wave from one ballot pair per kind,
+    {
+      u32 c[IT], a = 0;
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        c[i] = bcnt[t * IT + i];
+        a += c[i];
+      }
+      u32 tot;
+      u32 run = block_excl_scan<OpSum, u32, NW>(a, sscan, &tot);  // (syncs)
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        bcnt[t * IT + i] = run;
+        run += c[i];
+      }
+    }
+    __syncthreads();
+    bool big = false;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = t * IT + i;
+      if (e >= n) continue;
+      const u32 b = bk[i], b0 = bcnt[b], b1 = b + 1 < (u32)SMALL_N ? bcnt[b + 1] : (u32)n;
+      ord[b0 + atomicAdd(&bfill[b], 1u)] = (u16)e;
+      big |= b1 - b0 > SMALL_BKT;
+    }
+    slow = __syncthreads_or(big);
+    if (!slow) {
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        const int e = t * IT + i;
+        if (e >= n) continue;
+        const u32 b = bk[i], b0 = bcnt[b], b1 = b + 1 < (u32)SMALL_N ? bcnt[b + 1] : (u32)n;
+        const u64 h = khi[e], l = klo[e];
+        u32 r = 0;
+        for (u32 q = b0; q < b1; ++q) {
+          const u32 x = ord[q];
+          const u64 hx = khi[x], lx = klo[x];
+          r += hx < h || (hx == h && (lx < l || (lx == l && x < (u32)e)));
+        }
+        mrg[b0 + r] = (u16)e;
+      }
+    }
+  }
+  if (!slow) {
+    __syncthreads();
+    // 1d. stable split by kind: the rank inside the wave from one ballot pair per kind,
     //     the wave's start from a scan over (kind, wave)
     u32 k0, k1, r0 = 0, r1 = 0;
     {
@@ -199,6 +291,10 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
     }
   }
   __syncthreads();
+  SMALL_STAMP(3);
+#ifdef SMALL_STAMPS
+  if (t == 0) g_small_stamp[15] = slow;
+#endif
   // the move block [0, nmv), the rename block [nmv, rend): at the kind boundaries
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
@@ -210,7 +306,8 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
   }
   __syncthreads();
   const int nmv = (int)sinfo[2], rend = (int)sinfo[3];
-  // 2. the rename lists of the two sides, in T order
+  SMALL_STAMP(4);
+  // 2. the rename lists of the two sides, in T order, and each rename's (symbol, newName)
   u32 isa[IT], acc = 0;
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
@@ -226,64 +323,98 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
     if (T >= nmv && T <= rend) rat[T] = (u16)ra;
     if (T >= nmv && T < rend) {
       const u32 e = ord[T];
-      if (isa[i]) {
-        posA[ra] = (u16)T;
-        symA[ra] = ssym[e];
-        nnA[ra] = sv0[e];
-      } else {
-        const int j = T - nmv - (int)ra;
-        posB[j] = (u16)T;
-        symB[j] = ssym[e];
-        nnB[j] = sv0[e];
-      }
+      sn[T] = (u64)ssym[e] << 32 | (u32)sv0[e];
+      if (isa[i]) posA[ra] = (u16)T;
+      else posB[T - nmv - (int)ra] = (u16)T;
     }
     ra += isa[i];
   }
   if (t == 0 && rend == n) rat[n] = (u16)n_ren_a;  // (T == n is no thread's)
   __syncthreads();
+  // the next rename of each side at or after T: its position << 16 | its index
+  const int nA = (int)__builtin_amdgcn_readfirstlane((int)n_ren_a), nB = rend - nmv - nA;
+#pragma unroll
+  for (int i = 0; i <= IT; ++i) {
+    const int T = i < IT ? t * IT + i : n;
+    if (T < nmv || T > rend || (i == IT && (t != 0 || rend != n))) continue;
+    const int ia = rat[T], ib = T - nmv - ia;
+    nxtA[T] = (u32)(ia < nA ? posA[ia] : rend) << 16 | (u32)ia;
+    nxtB[T] = (u32)(ib < nB ? posB[ib] : rend) << 16 | (u32)ib;
+  }
+  __syncthreads();
+  SMALL_STAMP(5);
   if (w == 0) {
-    // the walk: state (ia, ib) = the heads' indices in the side lists (wave-uniform)
-    const int nA = (int)n_ren_a, nB = rend - nmv - nA;
-    int ia = 0, ib = 0;
+    // the walk.  The heads (position << 16 | index in the side's list) are wave-uniform.
+    // Lane k takes the heads after k steps without a conflict: the leading side's renames
+    // before the other head first (its list, read ahead), then every rename of the block
+    // in T order (the next renames of both sides at that position).
+    u32 hA = (u32)__builtin_amdgcn_readfirstlane((int)nxtA[nmv]);
+    u32 hB = (u32)__builtin_amdgcn_readfirstlane((int)nxtB[nmv]);
     u32 nc = 0;
-    while (ia < nA && ib < nB) {
-      const int pa = posA[ia], pb = posB[ib];
-      // lane k: the heads after k steps without a conflict -- first the leading side's
-      // renames before the other head, then every rename of the block in T order
-      int xa, xb;
-      const int g = pa < pb ? (int)rat[pb] - ia : (pa - nmv - (int)rat[pa]) - ib;
-      if (lane < g) {
-        xa = pa < pb ? ia + lane : ia;
-        xb = pa < pb ? ib : ib + lane;
-      } else {
-        const int q = (pa < pb ? pb : pa) + (lane - g);
-        xa = q < rend ? (int)rat[q] : nA;
-        xb = q < rend ? q - nmv - xa : nB;
-      }
-      const bool valid = xa < nA && xb < nB;
-      const bool conf = valid && symA[xa] == symB[xb] && nnA[xa] != nnB[xb];
-      const u64 cm = __ballot(conf), im = __ballot(!valid);
-      const int jc = cm ? __builtin_ctzll(cm) : WAVE, ji = im ? __builtin_ctzll(im) : WAVE;
-      if (jc < ji) {
-        const int ca = __builtin_amdgcn_readlane(xa, jc), cb = __builtin_amdgcn_readlane(xb, jc);
-        if (lane == 0) {
-          const int ta = posA[ca], tb = posB[cb];
-          if ((i64)nc < out.conflict_cap) {
-            out.conflicts[2 * nc] = (i32)ord[ta];
-            out.conflicts[2 * nc + 1] = (i32)ord[tb];
+    while ((int)(hA & 0xffffu) < nA && (int)(hB & 0xffffu) < nB) {
+      const int pa = (int)(hA >> 16), pb = (int)(hB >> 16);
+      const bool ldA = pa < pb;
+      const int il = (int)((ldA ? hA : hB) & 0xffffu) + lane;
+      const int cl = il < (ldA ? nA : nB) ? (int)(ldA ? posA[il] : posB[il]) : rend;
+      const int other = ldA ? pb : pa;
+      const int g = (int)__popcll(__ballot(cl < other));
+      const int q = other + lane - g;
+      const int qc = q < rend ? q : rend;
+      const u32 xA2 = nxtA[qc], xB2 = nxtB[qc];
+      const u32 xl = (u32)cl << 16 | (u32)il;
+      const u32 xA = lane < g ? (ldA ? xl : hA) : xA2;
+      const u32 xB = lane < g ? (ldA ? hB : xl) : xB2;
+      const int pA = (int)(xA >> 16), pB = (int)(xB >> 16);
+      const bool valid = (int)(xA & 0xffffu) < nA && (int)(xB & 0xffffu) < nB;
+      const u64 sa = sn[valid ? pA : nmv], sb = sn[valid ? pB : nmv];
+      // the heads after a conflict here, and its ops: loaded beside the pair (the compiler
+      // would sink them into the conflict branch, one more LDS round trip there)
+      u32 nA1 = nxtA[valid ? pA + 1 : rend], nB1 = nxtB[valid ? pB + 1 : rend];
+      u32 oA = ord[valid ? pA : 0], oB = ord[valid ? pB : 0];
+      asm volatile("" : "+v"(nA1), "+v"(nB1), "+v"(oA), "+v"(oB));
+      const bool conf = valid && (sa >> 32) == (sb >> 32) && (u32)sa != (u32)sb;
+      // after a conflict here, are both heads past this pair?  Then the walk goes on at
+      // the merged state of position max + 1, which a later lane already holds: the wave
+      // follows a run of conflicts with scalar steps over the ballots, not one pass each
+      const int pmax = pA > pB ? pA : pB;
+      const bool jmp = (nA1 >> 16) > (u32)pmax && (nB1 >> 16) > (u32)pmax;
+      const u64 cm = __ballot(conf), im = __ballot(!valid), jm = __ballot(jmp);
+      const int knl = g + (pmax + 1 - other);  // the lane of position max + 1
+      u64 rec = 0;  // the lanes whose pair conflicts on this pass, in walk order
+      int k = 0;
+      bool done = false;
+      while (true) {
+        const u64 ge = ~0ull << k;  // (k < WAVE)
+        const int jc = (cm & ge) ? __builtin_ctzll(cm & ge) : WAVE;
+        const int ji = (im & ge) ? __builtin_ctzll(im & ge) : WAVE;
+        if (jc < ji) {
+          rec |= 1ull << jc;
+          const int kn = __builtin_amdgcn_readlane(knl, jc);
+          if (((jm >> jc) & 1) && kn < WAVE) {
+            k = kn;
+            continue;
           }
-          skip[ta] = 1;
-          skip[tb] = 1;
+          hA = (u32)__builtin_amdgcn_readlane((int)nA1, jc);
+          hB = (u32)__builtin_amdgcn_readlane((int)nB1, jc);
+        } else if (ji < WAVE) {
+          done = true;
+        } else {
+          hA = (u32)__builtin_amdgcn_readlane((int)xA, WAVE - 1);
+          hB = (u32)__builtin_amdgcn_readlane((int)xB, WAVE - 1);
         }
-        ++nc;
-        ia = ca + 1;
-        ib = cb + 1;
-      } else if (ji < WAVE) {
         break;
-      } else {
-        ia = __builtin_amdgcn_readlane(xa, WAVE - 1);
-        ib = __builtin_amdgcn_readlane(xb, WAVE - 1);
       }
+      if ((rec >> lane) & 1) {  // the pass's conflicts, each by its own lane
+        const u32 ci = nc + (u32)__popcll(rec & lanemask_lt());
+        if ((i64)ci < out.conflict_cap) {
+          out.conflicts[2 * ci] = (i32)oA;
+          out.conflicts[2 * ci + 1] = (i32)oB;
+        }
+        skip[pA] = 1;
+        skip[pB] = 1;
+      }
+      nc += (u32)__popcll(rec);
+      if (done) break;
     }
     if (lane == 0) {
       out.counts[0] = (i64)(n - 2 * (int)nc);
@@ -291,6 +422,7 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
       meta->n_conf = nc;
       meta->n_skip = 2 * nc;
     }
+    SMALL_STAMP(6);
   }
   // the keys are dead: the hash table takes their LDS
   for (int i = t; i < SMALL_HT; i += SMALL_NT) {
@@ -298,6 +430,7 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
     hw[i] = hw[SMALL_HT + i] = hw[2 * SMALL_HT + i] = 0;
   }
   __syncthreads();
+  SMALL_STAMP(7);
   // 3. the chains: every op's symbol slot (moves and renames insert, the rest look up)
   auto slot_of = [&](u32 s, bool ins) -> int {
     u32 h = (s * 2654435761u) >> (32 - 12);
@@ -321,6 +454,7 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
     slot_r[i] = slot_of(ssym[ord[T]], true);
   }
   __syncthreads();
+  SMALL_STAMP(8);
   // last writers: T + 1 packed in u16 (T < SMALL_N); an atomic max on a u16 is emulated
   // with a CAS loop on its 32-bit word
   auto max16 = [&](u16* base, int h, u32 v) {
@@ -356,6 +490,7 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
   }
   u32 tot;
   const u32 sbase = block_excl_scan<OpSum, u32, NW>(acc, sscan, &tot);  // (syncs)
+  SMALL_STAMP(9);
   // 4. materialize: T -> T - skips before it
   u32 run = sbase;
 #pragma unroll
@@ -393,4 +528,8 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
     out.file[o] = f;
     out.ctx[o] = c;
   }
+#ifdef SMALL_STAMPS
+  __syncthreads();
+  SMALL_STAMP(10);
+#endif
 }

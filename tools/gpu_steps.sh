@@ -28,6 +28,8 @@ for s in "$@"; do
           python3 tools/prof_export.py "$O/sprof" "$O/small_kernel_stats.csv" && head -5 "$O/small_kernel_stats.csv";;
     c2prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/c2prof" -o p -- python3 "$R/tools/small_merge_probe.py" --sizes 1000000 --reps 20 > "$O/c2prof.log" 2>&1) || { echo "c2prof failed"; tail -20 "$O/c2prof.log"; exit 1; }
           python3 tools/prof_timeline.py "$O/c2prof" 40 > "$O/c2_timeline.txt" && tail -42 "$O/c2_timeline.txt";;
+    smallph) SMX_LIB=$R/tools/_build/var_stamps/libsmx.so run 300 small_phases.json python -u tools/small_phases.py
+          tail -1 "$O/small_phases.json";;
     shard) run 900 shard_tests.log python -u -m pytest tests/test_gpu_shard.py -x -v --timeout 400 --timeout-method thread
          tail -2 "$O/shard_tests.log"
          run 300 shard_probe.txt python -u tools/shard_probe.py 8
