@@ -366,15 +366,39 @@ __global__ void __launch_bounds__(BLOCK) k_rga_gbounds(smx_rga_ops o, u32* __res
   const i64 n = o.n_ops, nl = o.n_lists;
   if (blockIdx.x == 0 && threadIdx.x < RGA_CS_MAX) csum[threadIdx.x] = 0u;
   u32 bad = 0;
-  for (i64 i = (i64)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (i64)gridDim.x * BLOCK) {
-    const u32 l = o.list[i], op = o.op[i];
-    const u32 prev = i > 0 ? o.list[i - 1] : 0u;
-    bad |= (l >= (u64)nl || op > 2) ? (u32)(RGA_E_INPUT | RGA_E_UNGROUPED) : 0u;
-    bad |= i > 0 && l < prev ? (u32)RGA_E_UNGROUPED : 0u;
-    const u32 lo = i == 0 ? 0u : prev + 1u, hi = l < (u64)nl ? l : (u32)(nl - 1);
-    for (u32 L = lo; L <= hi; ++L) lstart[L] = (u32)i;
-    if (i == n - 1)
-      for (i64 L = (i64)hi + 1; L < nl; ++L) lstart[L] = (u32)n;
+  // four consecutive events per thread: one 16-byte list-id load and one 4-byte op load
+  // when aligned (the columns are the caller's: checked, else event by event)
+  const bool vec = ((reinterpret_cast<uintptr_t>(o.list) | reinterpret_cast<uintptr_t>(o.op)) & 3) == 0 &&
+                   (reinterpret_cast<uintptr_t>(o.list) & 15) == 0;
+  for (i64 i0 = ((i64)blockIdx.x * BLOCK + threadIdx.x) * 4; i0 < n; i0 += (i64)gridDim.x * BLOCK * 4) {
+    u32 l4[4], op4[4];
+    if (vec && i0 + 4 <= n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(o.list + i0);
+      const u32 ob = *reinterpret_cast<const u32*>(o.op + i0);
+      l4[0] = v.x, l4[1] = v.y, l4[2] = v.z, l4[3] = v.w;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) op4[u] = (ob >> (8 * u)) & 0xffu;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        l4[u] = i0 + u < n ? (u32)o.list[i0 + u] : 0u;
+        op4[u] = i0 + u < n ? (u32)o.op[i0 + u] : 0u;
+      }
+    }
+    u32 prev = i0 > 0 ? (u32)o.list[i0 - 1] : 0u;  // (the neighbour lane's line: an L1 hit)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const i64 i = i0 + u;
+      if (i >= n) break;
+      const u32 l = l4[u], op = op4[u];
+      bad |= (l >= (u64)nl || op > 2) ? (u32)(RGA_E_INPUT | RGA_E_UNGROUPED) : 0u;
+      bad |= i > 0 && l < prev ? (u32)RGA_E_UNGROUPED : 0u;
+      const u32 lo = i == 0 ? 0u : prev + 1u, hi = l < (u64)nl ? l : (u32)(nl - 1);
+      for (u32 L = lo; L <= hi; ++L) lstart[L] = (u32)i;
+      if (i == n - 1)
+        for (i64 L = (i64)hi + 1; L < nl; ++L) lstart[L] = (u32)n;
+      prev = l;
+    }
   }
   if (bad) atomicOr(err, (i32)bad);
 }
@@ -1407,6 +1431,10 @@ __device__ void rga_big_list(const smx_rga_ops& o, const u64* __restrict__ R, u3
   if (t == 0) rga_put_count(scnt, l, m);
 }
 
+#ifndef RGA_BIG_GRID
+#define RGA_BIG_GRID 32  // workgroups of k_rga_big (lists of > 2 RW_CAP events, one per workgroup at a time;
+                         // 256 cost ~5 us of launch on every call, most of which have none)
+#endif
 __global__ void __launch_bounds__(1024) k_rga_big(smx_rga_ops o, const u64* __restrict__ R,
                                                   const u32* __restrict__ lstart, i64 n,
                                                   i64 nl, const u32* __restrict__ todo, const u32* __restrict__ ntodo,
@@ -1607,7 +1635,8 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   if (grouped) {  // the caller's events come list by list: no partition
     const int pgrid = (int)(SMX_CEIL_DIV(n, (i64)BLOCK) < 8192 ? SMX_CEIL_DIV(n, (i64)BLOCK) : 8192);
     if (direct)
-      hipLaunchKernelGGL(k_rga_gbounds, dim3(pgrid), dim3(BLOCK), 0, st, *ops, lstart, scnt - RGA_CS_MAX, err);
+      hipLaunchKernelGGL(k_rga_gbounds, dim3((int)SMX_CEIL_DIV((i64)pgrid, (i64)4)), dim3(BLOCK), 0, st, *ops, lstart,
+                         scnt - RGA_CS_MAX, err);
     else
       hipLaunchKernelGGL(k_rga_pack, dim3(pgrid), dim3(BLOCK), 0, st, *ops, rec, lstart, scnt - RGA_CS_MAX, err);
   } else {  // records grouped by list: LSD passes over the list id, ping-pong into rec
@@ -1664,7 +1693,7 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   // join costs ~14 us, profiles/r04_s.)
   hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, def2, ndef + 1,
                      tmp_v, tmp_s, scnt, tomb, (const i32*)err, (int)direct);
-  hipLaunchKernelGGL(k_rga_big, dim3(256), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
+  hipLaunchKernelGGL(k_rga_big, dim3(RGA_BIG_GRID), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,
                      tmp_s, scnt, tomb, (const i32*)err);
   if (nl <= RGA_FUSED_MAX) {  // each list's wave finds its own offset
     hipLaunchKernelGGL(k_rga_out_fused, dim3(SMX_CEIL_DIV(nl, (i64)(BLOCK / WAVE * RGA_OUT_LPW))), dim3(BLOCK), 0, st, tmp_v,

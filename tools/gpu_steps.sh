@@ -30,6 +30,9 @@ for s in "$@"; do
           python3 tools/prof_timeline.py "$O/c2prof" 40 > "$O/c2_timeline.txt" && tail -42 "$O/c2_timeline.txt";;
     smallph) SMX_LIB=$R/tools/_build/var_stamps/libsmx.so run 300 small_phases.json python -u tools/small_phases.py
           tail -1 "$O/small_phases.json";;
+    rgaprof) (cd /tmp && export TMPDIR=/tmp && RGA_NO_CPU=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/rgaprof" -o p -- python3 "$R/tools/bench_rga.py" > "$O/rgaprof.log" 2>&1) || { echo "rgaprof failed"; tail -20 "$O/rgaprof.log"; exit 1; }
+          python3 tools/prof_export.py "$O/rgaprof" "$O/rga_kernel_stats.csv" && head -14 "$O/rga_kernel_stats.csv"
+          python3 tools/prof_timeline.py "$O/rgaprof" 200 > "$O/rga_timeline.txt";;
     shard) run 900 shard_tests.log python -u -m pytest tests/test_gpu_shard.py -x -v --timeout 400 --timeout-method thread
          tail -2 "$O/shard_tests.log"
          run 300 shard_probe.txt python -u tools/shard_probe.py 8
