@@ -2543,12 +2543,15 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
   if (use_early) {
     HIP_TRY(hipEventSynchronize(early.ev));
     if (((volatile u32*)early.flag_host)[0]) {
+      const bool bad = ((volatile u32*)early.flag_host)[1] != 0;
       if (verdict) {
         verdict->failed = true;
-        verdict->bad = ((volatile u32*)early.flag_host)[1] != 0;
+        verdict->bad = bad;
       }
-      hipLaunchKernelGGL(k_counts_failed, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), out->counts);
-      HIP_TRY(hipGetLastError());
+      if (!verdict || bad) {  // (smx_compose's finish runs the fallback plan next: it writes the counts)
+        hipLaunchKernelGGL(k_counts_failed, dim3(1), dim3(1), 0, st, C.ws<ComposeMeta>(B_META), out->counts);
+        HIP_TRY(hipGetLastError());
+      }
       tm.flush();
       return SMX_OK;
     }
