@@ -261,12 +261,21 @@ __global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB,
     bool lg = false;
     for (i64 c = k; c + D < ca; c += nt) lg |= sA[c] == sA[c + D];
     for (i64 c = k; c + D < cb; c += nt) lg |= sB[c] == sB[c + D];
-    if (__ballot(lg) && (threadIdx.x & (WAVE - 1)) == 0 &&
+    const u64 lgw = __ballot(lg);
+    if (lgw && (threadIdx.x & (WAVE - 1)) == 0 &&
         __hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != F_LONG) {
       atomicOr((unsigned long long*)&meta->f_fail, F_LONG);
       // ... and, on the synchronous path, to the host (pinned, coherent), which then
       // launches no tail behind this failed plan
       if (long_host) __hip_atomic_store(long_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // a wave that saw the plan fail leaves its boundaries unsearched, as 0 (k_window_f
+    // leaves before its loads on F_LONG, and a zero boundary only ever gives an empty or
+    // an oversized window; the wide plan redoes them) -- on config 5 the snap's gallops
+    // over 4096-op timestamp runs were most of this kernel
+    if (lgw) {
+      if (k <= W) bnd[2 * k] = bnd[2 * k + 1] = 0;
+      return;
     }
   }
   if (k > W) return;
