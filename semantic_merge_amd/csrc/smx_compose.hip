@@ -1763,8 +1763,14 @@ struct EarlyFail {
 // shorter windows per CU), normal, wide (timestamp groups no normal window holds).
 enum WinLevel { WL_SMALL, WL_NORMAL, WL_WIDE };
 static i64 level_cap(int lv) { return lv == WL_SMALL ? WF_SMALL_CAP : lv == WL_WIDE ? WF_WIDE_CAP : WF_CAP; }
-static int first_level(const Ctx& C) { return C.n <= WF_SMALL_MAXN ? WL_SMALL : WL_NORMAL; }
+// (SMX_FIRST_WIDE, diagnostic builds: start at the wide windows, so that SMX_ABLATE's
+// phase exits reach the wide instance)
+static int first_level(const Ctx& C) {
+  if (knob("SMX_FIRST_WIDE", 0)) return WL_WIDE;
+  return C.n <= WF_SMALL_MAXN ? WL_SMALL : WL_NORMAL;
+}
 static i64 first_tgt(const Ctx& C) {
+  if (first_level(C) == WL_WIDE) return knob("SMX_WIN_TGT", WF_WIDE_CAP);
   return first_level(C) == WL_SMALL ? knob("SMX_WIN_TGT", WF_SMALL_TGT) : knob("SMX_WIN_TGT", WIN_TGT);
 }
 

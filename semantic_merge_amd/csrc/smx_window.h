@@ -644,6 +644,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     // b. (wave 0) the last head of each chunk, the runs' dense index, the group count
     const u32 kpres = __builtin_amdgcn_readfirstlane(kmask_r);
     const int KD = __popc(kpres);
+    const int kbits_r = 32 - __clz((int)(max(KD, 1) - 1));  // bits of a dense kind
     if (wv == 0) {
       static_assert(NCH <= 2 * WAVE && OW <= 4 * WAVE, "one wave covers the chunks and occupancy words");
       u32 carry = 0;  // (last head + 1; 0 = none yet)
@@ -694,10 +695,29 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
         const int h = m ? c * WAVE + 63 - __clzll(m) : (int)lasth[c > 0 ? c - 1 : 0];
         const u32 k = k_r[i] < SMX_N_KINDS ? k_r[i] : SMX_N_KINDS - 1;
         g_r[i] = 0xffffffffu;
+        u32 r = 0, dk = 0;
         if (e < sz) {
           const u32 s = sp[h];
-          const u32 r = occpre[s >> 5] + (u32)__popc(occ[s >> 5] & ((1u << (s & 31)) - 1u));
-          g_r[i] = (u32)__popc(kpres & ((1u << k) - 1u)) * R + r;
+          r = occpre[s >> 5] + (u32)__popc(occ[s >> 5] & ((1u << (s & 31)) - 1u));
+          dk = (u32)__popc(kpres & ((1u << k) - 1u));
+          g_r[i] = dk * R + r;
+        }
+        // the wide windows: a wave inside one run (config 5: one run per window) has at
+        // most KD distinct groups, counted per group by its lowest lane (a per-lane LDS
+        // atomic on a handful of words serialises: wide window 0.422 -> 0.406 ms on config 5);
+        // otherwise, and in the normal windows (many runs, where the test costs more than it
+        // saves), one atomic per op
+        bool agg = false;
+        if constexpr (CAP > WF_CAP) {
+          const u64 vm = __ballot(e < sz);
+          const u32 r0 = (u32)__builtin_amdgcn_readfirstlane((int)r);
+          agg = vm && __ballot(e < sz && r != r0) == 0;
+        }
+        if (agg) {
+          const u64 peers = wave_peers_n(dk, e < sz, kbits_r);
+          if (e < sz && (peers & lanemask_lt()) == 0)
+            atomicAdd(&gcnt[g_r[i] >> 1], (u32)__popcll(peers) << (16 * (g_r[i] & 1)));
+        } else if (e < sz) {
           atomicAdd(&gcnt[g_r[i] >> 1], 1u << (16 * (g_r[i] & 1)));
         }
       }
@@ -1522,6 +1542,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
   __syncthreads();
   WSTAMP(13);
   WF_EXIT(10);
+  RX_EXIT(9);
   // 8. natural-head DivergentRename flags -> candidate slots; window exports
   win_rename_flags<NT, NCH>(
       P, w, woffk[KREN], RN, cntA, cntB, posl, gbits,
@@ -1540,6 +1561,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
       });
   WSTAMP(14);
   WF_EXIT(11);
+  RX_EXIT(10);
 
   // The output phases' kernel arguments are read again here from the kernarg segment
   // (scalar loads through an opaque pointer): held from the kernel's start they were
