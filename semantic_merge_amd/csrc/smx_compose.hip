@@ -1445,10 +1445,7 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
   u64* skipbits = C.ws<u64>(B_SKIPBITS);
   u32* skiplist = C.ws<u32>(B_SKIPLIST);
   u32* part = C.ws<u32>(B_PART);
-  {
-    const int rc = zero_async(skipbits, (size_t)(SMX_CEIL_DIV(n, (i64)64) + 1) * 8, st);
-    if (rc) return rc;
-  }
+  const u64 nskipw = (u64)SMX_CEIL_DIV(n, (i64)64) + 1;  // (cleared by k_boundary)
   const WalkArgs Wk = walk_args(C, sh);
   u32* cslot = C.ws<u32>(B_CSLOT);
   u32* wcand = C.ws<u32>(B_WCAND);
@@ -1467,19 +1464,25 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
   const u64* ncand_dev = &meta->n_cand;
   const i64 Wmax = max_windows(n);
   const int gsmall = 256;  // grid for loops over the (few) candidates
-  hipLaunchKernelGGL(k_boundary, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, meta, cslot, wcand, wtot);
+  hipLaunchKernelGGL(k_boundary, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, meta, cslot, wcand, wtot, skipbits,
+                     nskipw);
   if (sh && (sh->in_d > 0 || sh->in_state_dev))
     hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d,
                        (const i64*)sh->in_state_dev, meta, C.out->conflicts, (u64)C.out->conflict_cap, skiplist,
                        skipbits);
   // (one k_scan1 block over the window counts measured slower on config 3: walk 0.165 ->
   // 0.185 ms, profiles/r03_w; small merges are launch-bound: one block)
-  if (Wmax <= WALK_SCAN1_MAXW)
-    hipLaunchKernelGGL(k_scan1<OpSum>, dim3(1), dim3(S1_NT), 0, st, wtot, wcoff, (const u64*)&meta->n_win,
-                       (u64)Wmax, ncand32);
-  else
-    HIP_TRY((scan_excl<OpSum, u32, u32>(wtot, wcoff, Wmax, &meta->n_win, part, ncand32, st)));
-  hipLaunchKernelGGL(k_cand_compact, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, cslot, wcoff, ncand_dev, cand);
+  if (Wmax <= WALK_CC_FUSED_MAXW) {
+    hipLaunchKernelGGL(k_cand_scan_compact, dim3(1), dim3(S1_NT), 0, st, Wk, wtot, wcoff, (u64)Wmax, ncand32, cslot,
+                       cand);
+  } else {
+    if (Wmax <= WALK_SCAN1_MAXW)
+      hipLaunchKernelGGL(k_scan1<OpSum>, dim3(1), dim3(S1_NT), 0, st, wtot, wcoff, (const u64*)&meta->n_win,
+                         (u64)Wmax, ncand32);
+    else
+      HIP_TRY((scan_excl<OpSum, u32, u32>(wtot, wcoff, Wmax, &meta->n_win, part, ncand32, st)));
+    hipLaunchKernelGGL(k_cand_compact, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, cslot, wcoff, ncand_dev, cand);
+  }
   hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
   if (n <= WALK_FUSED_MAXN) {  // small merges: max scan, clusters and sum scan in one block
     hipLaunchKernelGGL(k_cluster_fused, dim3(1), dim3(S1_NT), 0, st, Wk, cand, q, pm, nconf, meta, nreal, coff,

@@ -269,7 +269,11 @@ __device__ u32 replay_region(const WalkArgs& W, u32 p, ReplayState& st, u32* nco
 // candidates.  Re-running it (sharded walk rounds) rewrites the same slots.  Block
 // 0 also resets the walk's counters in meta.
 __global__ void __launch_bounds__(BLOCK) k_boundary(WalkArgs W0, ComposeMeta* meta, u32* __restrict__ cslot,
-                                                    const u32* __restrict__ wcand, u32* __restrict__ wtot) {
+                                                    const u32* __restrict__ wcand, u32* __restrict__ wtot,
+                                                    u64* __restrict__ skipbits, u64 nskipw) {
+  // the skip bits of the walk (k_replay_in / k_replay_write set them) start cleared:
+  // done here rather than by a zero-fill launch of its own
+  for (u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x; i < nskipw; i += (u64)gridDim.x * BLOCK) skipbits[i] = 0ull;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     meta->n_cand = 0;
     meta->n_conf = 0;
@@ -361,6 +365,29 @@ __global__ void __launch_bounds__(S1_NT) k_scan1(const u32* __restrict__ in, u32
                                                  const u64* n_dev, u64 cap, u32* total_lo) {
   __shared__ u32 s[S1_NT / WAVE + 1];
   scan1_block<Op>(in, out, min(*n_dev, cap), total_lo, s);  // cap: the arrays' capacity
+}
+
+// Small merges (launch-bound): the window-count scan and the candidate compaction in one
+// block (k_scan1<OpSum> then k_cand_compact), a barrier between them.
+#ifndef WALK_CC_FUSED_MAXW
+#define WALK_CC_FUSED_MAXW 4096
+#endif
+__global__ void __launch_bounds__(S1_NT) k_cand_scan_compact(WalkArgs W0, const u32* __restrict__ wtot,
+                                                             u32* __restrict__ woff, u64 cap, u32* total_lo,
+                                                             const u32* __restrict__ cslot, u32* __restrict__ out) {
+  __shared__ u32 s[S1_NT / WAVE + 1];
+  const WalkArgs W = walk_load(W0);
+  const u64 nw = min(W.Wn, cap);
+  scan1_block<OpSum>(wtot, woff, nw, total_lo, s);
+  __syncthreads();  // (global writes of this block: visible to it after the barrier)
+  if (W.fail) return;
+  const u32 total = *total_lo;
+  for (u64 w = threadIdx.x; w < nw; w += S1_NT) {
+    const u32 o = woff[w];
+    const u32 e = w + 1 < nw ? woff[w + 1] : total;
+    const u64 Mb = W.wren[2 * w];
+    for (u32 i = 0; o + i < e; ++i) out[o + i] = cslot[Mb + i];
+  }
 }
 
 // Incoming open region (sharded merge): the previous shards' walk ended with

@@ -303,6 +303,9 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_RUNS
 #define WF_RUNS 1    // the normal presorted windows order by runs and (kind, run) groups (no merge / multisplit)
 #endif
+#ifndef WF_GAGG
+#define WF_GAGG 1  // step c's group counts aggregated per wave: 1 the wide windows, 2 every window
+#endif
 #ifndef WF_RUNS_WIDE
 #define WF_RUNS_WIDE 1  // ... and the wide ones (config 5: one run per window)
 #endif
@@ -708,13 +711,16 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
         // otherwise, and in the normal windows (many runs, where the test costs more than it
         // saves), one atomic per op
         bool agg = false;
-        if constexpr (CAP > WF_CAP) {
+        u32 r0 = 0;
+        if constexpr (WF_GAGG >= 2 || (WF_GAGG == 1 && CAP > WF_CAP)) {
           const u64 vm = __ballot(e < sz);
-          const u32 r0 = (u32)__builtin_amdgcn_readfirstlane((int)r);
-          agg = vm && __ballot(e < sz && r != r0) == 0;
+          r0 = (u32)__builtin_amdgcn_readfirstlane((int)r);
+          // (WF_GAGG 2: also a wave over two runs, one more ballot)
+          agg = vm && __ballot(e < sz && r - r0 > (WF_GAGG >= 2 ? 1u : 0u)) == 0;
         }
         if (agg) {
-          const u64 peers = wave_peers_n(dk, e < sz, kbits_r);
+          const u64 peers = WF_GAGG >= 2 ? wave_peers_n(dk << 1 | (r - r0), e < sz, kbits_r + 1)
+                                         : wave_peers_n(dk, e < sz, kbits_r);
           if (e < sz && (peers & lanemask_lt()) == 0)
             atomicAdd(&gcnt[g_r[i] >> 1], (u32)__popcll(peers) << (16 * (g_r[i] & 1)));
         } else if (e < sz) {
