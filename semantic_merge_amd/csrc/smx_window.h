@@ -303,6 +303,12 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_RUNS
 #define WF_RUNS 1    // the normal presorted windows order by runs and (kind, run) groups (no merge / multisplit)
 #endif
+#ifndef WF_HEADLIST
+#define WF_HEADLIST 0  // run-grouped step a, 1: every head binary-searches a list of the other part's
+                       // heads at once (three more barriers): window 1.196 -> 1.241 ms on config 3,
+                       // wide 0.409 -> 0.416 on config 5 (profiles/r05_x), off; 0: one head at a time
+                       // with the whole wave, a 64-way search of the other part's timestamps
+#endif
 #ifndef WF_GAGG
 #define WF_GAGG 1  // step c's group counts aggregated per wave: 1 the wide windows, 2 every window
 #endif
@@ -583,6 +589,10 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
     __shared__ u16 occpre[OW];
     __shared__ u16 lasth[NCH];       // last head at or before the end of each 64-op chunk
     __shared__ u32 rinfo[2];         // groups fit, R
+#if WF_HEADLIST
+    __shared__ u16 hpre[NCH + 1];    // heads before each chunk (and in all)
+    __shared__ u32 hna;              // the A part's heads (index of B's first head)
+#endif
     u16* sp = sl;                    // S position of each head's run (element space)
     u32* gcnt = reinterpret_cast<u32*>(sts);             // group counters, two u16 per word
     static_assert(GMAX / 2 * sizeof(u32) <= sizeof(sts), "group counters inside sts");
@@ -609,6 +619,7 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
       // compiler, which would then run the head searches below as lane-divergent loops)
       const int c = __builtin_amdgcn_readfirstlane((NT * i) / WAVE + wv);
       if (lane == 0 && c < NCH) gbits[c] = hbr[i];
+#if !WF_HEADLIST
       // the heads of this chunk, one at a time with the whole wave: a 64-way search of
       // the other part for #{ops < v} (two or three rounds of one LDS read per lane)
       u64 hb = hbr[i];
@@ -638,11 +649,69 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
           atomicOr(&occ[spos >> 5], 1u << (spos & 31));
         }
       }
+#endif
     }
+#if WF_HEADLIST
+    if (t == 0) hna = 0xffffu;  // (no B part: every head is A's)
+#endif
     if (__syncthreads_or(dec)) {
       if (t == 0) atomicOr((unsigned long long*)&P.meta->f_fail, 1ull);
       return;
     }
+#if WF_HEADLIST
+    // the heads of both parts in one list, element order (A's first): hel[j], with the
+    // heads before each chunk from one wave's scan of the chunk ballots
+    u16* hel = sord;  // (free until step h)
+    if (wv == 0) {
+      const u32 h0 = lane < NCH ? (u32)__popcll(gbits[lane]) : 0u;
+      const u32 h1 = lane + WAVE < NCH ? (u32)__popcll(gbits[lane + WAVE]) : 0u;
+      const u32 i0 = wave_incl_sum_u32(h0), i1 = wave_incl_sum_u32(h1);
+      const u32 t0 = (u32)__builtin_amdgcn_readlane((int)i0, WAVE - 1);
+      if (lane < NCH) hpre[lane] = (u16)(i0 - h0);
+      if (lane + WAVE < NCH) hpre[lane + WAVE] = (u16)(t0 + i1 - h1);
+      if (lane == WAVE - 1) hpre[NCH] = (u16)(t0 + i1);
+    }
+    __syncthreads();
+    {
+      const u64 lt = lanemask_lt();
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const int e = t + NT * i;
+        const int c = __builtin_amdgcn_readfirstlane((NT * i) / WAVE + wv);
+        if ((hbr[i] >> lane) & 1ull) {
+          const u32 j = (u32)hpre[c] + (u32)__popcll(hbr[i] & lt);
+          hel[j] = (u16)e;
+          if (e == na) hna = j;
+        }
+      }
+    }
+    __syncthreads();
+    {
+      // each head: #{other part's ops < v} = the index of the other part's first head
+      // whose timestamp is >= v (that op starts a run), by a binary search of the head list
+      const u32 nH = hpre[NCH], nHA = hna == 0xffffu ? nH : hna;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const int e = t + NT * i;
+        if (!((hbr[i] >> lane) & 1ull)) continue;
+        const u64 v = ts_r[i];
+        const bool sa = e < na;
+        const u32 end = sa ? nH : nHA;
+        u32 lo = sa ? nHA : 0u, hi = end;
+        while (lo < hi) {
+          const u32 mid = (lo + hi) >> 1;
+          if (sts[hel[mid]] < v) lo = mid + 1;
+          else hi = mid;
+        }
+        const int o0 = sa ? na : 0, no = sa ? nb : na;
+        const int cnt = lo < end ? (int)hel[lo] - o0 : no;
+        const int spos = (sa ? e : e - na) + cnt;
+        sp[e] = (u16)spos;
+        atomicOr(&occ[spos >> 5], 1u << (spos & 31));
+      }
+    }
+    __syncthreads();
+#endif
     RX_EXIT(1);
     // b. (wave 0) the last head of each chunk, the runs' dense index, the group count
     const u32 kpres = __builtin_amdgcn_readfirstlane(kmask_r);
