@@ -30,6 +30,8 @@ Rank 0 at N = 1 also reports, after the timed steps (never inside them):
         reference's own compose_oplogs as measured in the build container
   end_to_end     the drop-in compose_oplogs on a config-2-shaped log of Op objects:
         native marshal, device compose, native materialise
+  small_merge    a 1k-op merge (the CLI's size): device latency on resident buffers (the
+        one-workgroup plan) and the drop-in on Op objects
 """
 from __future__ import annotations
 
@@ -204,6 +206,47 @@ def end_to_end(n_ops: int) -> dict:
             "marshal_s": round(t[1] - t[0], 4), "device_s": round(t[2] - t[1], 4),
             "materialize_s": round(t[3] - t[2], 4), "total_s": round(tot, 4),
             "note": "compose_oplogs drop-in on Op objects; device_s includes host<->device copies"}
+
+
+def small_merge(n_ops: int = 1000, reps: int = 50) -> dict:
+    """A CLI-sized merge (one diff per branch): the device leg on resident buffers
+    (DeviceCompose.run + its sync; the one-workgroup plan) and the whole drop-in on Op
+    objects (marshal, device with its copies, materialise); medians."""
+    import torch
+    from semantic_merge_amd import synth
+    from semantic_merge_amd._lib import DeviceCompose, compose_soa
+    from semantic_merge_amd.marshal import marshal_native
+    from semantic_merge_amd.materialize import materialize_conflicts, materialize_ops_native
+    from semantic_merge_amd.oplog import ops_from_dicts
+
+    logs = synth.lift_logs(synth.LiftSpec(n_ops, max(n_ops // 100, 10), 7))
+    soa = synth.lift_soa(logs)
+    dc = DeviceCompose(soa)
+    for _ in range(5):
+        dc.run()
+    torch.cuda.synchronize()
+    td = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        dc.run()
+        torch.cuda.synchronize()
+        td.append(time.perf_counter() - t0)
+    plan = DeviceCompose.last_plan()
+    A, B = synth.lift_op_dicts(logs)
+    oa, ob = ops_from_dicts(A), ops_from_dicts(B)
+    ops = oa + ob
+    te = []
+    for _ in range(max(reps // 2, 1)):
+        t0 = time.perf_counter()
+        sa = marshal_native(oa, ob)
+        order, addr, file, ctx, pairs = compose_soa(sa)
+        materialize_ops_native(ops, sa.kind, sa.strings, order, addr, file, ctx)
+        materialize_conflicts(ops, pairs)
+        te.append(time.perf_counter() - t0)
+    return {"n_ops": n_ops, "plan": plan, "device_ms": round(float(np.median(td)) * 1e3, 4),
+            "dropin_ms": round(float(np.median(te)) * 1e3, 4),
+            "note": "device_ms: smx_compose on resident buffers + one sync; dropin_ms: compose_oplogs "
+                    "on Op objects (marshal, copies, device, materialise)"}
 
 
 def main() -> None:
@@ -403,11 +446,16 @@ def main() -> None:
     pmc = pmc_traffic(args) if solo and not args.no_pmc else None
     cpu = cpu_baseline(soa, args) if solo and not args.no_cpu_baseline else None
     e2e = None
+    small = None
     if solo and not args.no_e2e:
         try:
             e2e = end_to_end(args.e2e_ops)
         except Exception as exc:  # reported, never fatal for the headline
             e2e = {"status": f"failed: {exc}"}
+        try:
+            small = small_merge()
+        except Exception as exc:
+            small = {"status": f"failed: {exc}"}
 
     if strong:
         par = f"key-range shards x{world}, strong scaling (packed RCCL all-to-all + all-gathers + MAX all-reduce)"
@@ -480,6 +528,7 @@ def main() -> None:
         "stage_calls_per_step": {k2: round(v[1] / n_breakdown, 2) for k2, v in stages_all.items() if v[1]},
         "cpu_baseline": cpu,
         "end_to_end": e2e,
+        "small_merge": small,
         "async_api": async_api,
         "graph_api": graph_api,
     }

@@ -2518,7 +2518,10 @@ static int early_fail_of(int dev, EarlyFail* e) {
 
 // Largest merge (ops) the one-workgroup path takes (smx_set_small_limit; 0: never).
 static std::atomic<int64_t> g_small_max{SMX_SMALL ? SMALL_N : 0};
-static inline bool small_merge(i64 n) { return n <= g_small_max.load(std::memory_order_relaxed); }
+// (symbol ids index the small kernel's hash table with 0xffffffff as its empty mark)
+static inline bool small_merge(const smx_ops* ops) {
+  return ops->n_a + ops->n_b <= g_small_max.load(std::memory_order_relaxed) && ops->n_sym <= 0xffffffffll;
+}
 
 #ifndef SMX_EARLY_MIN
 #define SMX_EARLY_MIN (1ll << 22)  // ops from which a synchronous merge waits for k_khist's verdict
@@ -2536,7 +2539,7 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
   StageTimer tm(st, timed);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
   int rc;
-  if (small_merge(n)) {  // the whole merge in one workgroup (smx_small.h)
+  if (small_merge(ops)) {  // the whole merge in one workgroup (smx_small.h)
     tm.begin(ST_SMALL);
     hipLaunchKernelGGL(k_compose_small, dim3(1), dim3(SMALL_NT), 0, st, *ops, *out, C.ws<ComposeMeta>(B_META));
     HIP_TRY(hipGetLastError());
@@ -2714,7 +2717,7 @@ static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, vo
   int rc = check_args(ops, out, ws, ws_bytes, &L);
   if (rc) return rc;
   const i64 n = ops->n_a + ops->n_b;
-  const bool small = small_merge(n);
+  const bool small = small_merge(ops);
   g_plan = small ? SMX_PLAN_SMALL : SMX_PLAN_PRESORTED;
   if (n == 0) {
     HIP_TRY(hipMemsetAsync(out->counts, 0, 2 * sizeof(int64_t), st));

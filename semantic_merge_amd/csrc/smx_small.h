@@ -75,6 +75,7 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
                                                              // last kept rename (0: none)
   static_assert(SMALL_HT * 4 <= SMALL_N * 8 && 3 * SMALL_HT * 2 <= 2 * SMALL_N * 8, "hash table in the keys");
   static_assert(SMX_N_KINDS * NW <= 5 * WAVE, "kind scan: 5 counters per lane");
+  static_assert(sizeof(ComposeMeta) % 4 == 0 && sizeof(ComposeMeta) / 4 <= SMALL_NT, "meta zeroed one word per thread");
   const int t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
   const i64 na = ops.n_a, nb = ops.n_b;
   const int n = (int)(na + nb);
