@@ -1675,7 +1675,7 @@ static int side_stream(hipStream_t caller, SideStream** out) {
 #define SMX_TB_OVERLAP 1
 #endif
 #ifndef SMX_TB_OVERLAP_MIN
-#define SMX_TB_OVERLAP_MIN (1 << 22)  // ops
+#define SMX_TB_OVERLAP_MIN (1 << 18)  // ops (config 2: 0.1746 -> 0.1724 ms with the overlap, profiles/r05_x/c2_overlap_ab.txt; graph replay makes the fork/join cheap)
 #endif
 // launch_tail forks the table scatter onto the side stream for this merge
 static bool n_side_needed(const smx_ops* ops) {
@@ -1696,7 +1696,7 @@ static int launch_tail(const Ctx& C) {
   if (width < 1) width = 1;
   if (width > TB_WIDTH) width = TB_WIDTH;
   const u64 nbk = SMX_CEIL_DIV((u64)n_sym, width);
-  // small merges are launch-bound: the fork/join costs more than the overlap saves
+  // the smallest merges are launch-bound: below SMX_TB_OVERLAP_MIN the fork/join costs more than the overlap saves
   SideStream* S = nullptr;
   if (SMX_TB_OVERLAP && nbk <= TB_MAXBK && C.n >= SMX_TB_OVERLAP_MIN && !knob("SMX_TB_SERIAL", 0)) {
     int rc = side_stream(C.st, &S);
