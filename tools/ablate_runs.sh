@@ -1,5 +1,8 @@
 #!/bin/bash
-# window phase exits on config 5's shape (wide windows first) and config 3's, 20M ops
+# Run-grouped window phase exits (SMX_ABLATE 16, 0x10000 + step, 109, 0; diagnostic build
+# tools/_build/var_diag) on config 5's shape (wide windows first, SMX_FIRST_WIDE) and on
+# config 3's, 20M ops each, SQ counters per exit (tools/sq_ablate.sh):
+#   gpurun -- bash tools/ablate_runs.sh gpurun_out/<tag>      (profiles/r05_ablate)
 set -o pipefail
 O=$1; mkdir -p "$O"
 V="16 65537 65538 65539 65540 65541 65542 65543 65544 109 65545 65546 0"
