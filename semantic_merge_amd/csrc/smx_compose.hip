@@ -395,6 +395,12 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
   // KH_R rounds of CH_PER_BLOCK chunks per block; every round's loads are issued first
   u32 w[KH_R][4];
   int nvr[KH_R];
+  // timestamp samples for k_fpart: first op of each A chunk, last op of each full B chunk
+  // (stored after the counting: their loads then wait beside the kind bytes', not ahead of
+  // them; separate registers for A and B, or the second load waits on the first)
+  u64 smpA[KH_R], smpB[KH_R];
+  u64* atA[KH_R];
+  u64* atB[KH_R];
 #pragma unroll
   for (int rd = 0; rd < KH_R; ++rd) {
     const i64 g = ((i64)blockIdx.x * KH_R + rd) * CH_PER_BLOCK + j;
@@ -405,11 +411,6 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
     const int nv = g < CA + CB ? (int)(len - r0 < 0 ? 0 : (len - r0 < 16 ? len - r0 : 16)) : 0;
     nvr[rd] = nv;
     const u8* src = kind + (side ? na + bgap : 0) + r0;
-    // timestamp samples for k_fpart: first op of each A chunk, last op of each full B chunk
-    if (g < CA + CB) {
-      if (!side && q == 0) sA[cc] = ts[cc * CH];
-      if (side && q == 15 && nv == 16) sB[cc] = ts[na + bgap + cc * CH + CH - 1];
-    }
     w[rd][0] = w[rd][1] = w[rd][2] = w[rd][3] = 0u;
     if (nv == 16 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
       const uint4 v = *reinterpret_cast<const uint4*>(src);
@@ -418,6 +419,18 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
 #pragma unroll
       for (int y = 0; y < 16; ++y)
         if (y < nv) w[rd][y >> 2] |= (u32)src[y] << (8 * (y & 3));
+    }
+    atA[rd] = atB[rd] = nullptr;
+    smpA[rd] = smpB[rd] = 0;
+    if (g < CA + CB) {
+      if (!side && q == 0) {
+        atA[rd] = sA + cc;
+        smpA[rd] = ts[cc * CH];
+      }
+      if (side && q == 15 && nv == 16) {
+        atB[rd] = sB + cc;
+        smpB[rd] = ts[na + bgap + cc * CH + CH - 1];
+      }
     }
   }
   bool bad = false;
@@ -458,6 +471,11 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
 #pragma unroll
       for (int k = 0; k < SMX_N_KINDS; ++k) c[rd * CH_PER_BLOCK + j][k] = (f[k / 3] >> (10 * (k % 3))) & 1023u;
     }
+  }
+#pragma unroll
+  for (int rd = 0; rd < KH_R; ++rd) {
+    if (atA[rd]) *atA[rd] = smpA[rd];
+    if (atB[rd]) *atB[rd] = smpB[rd];
   }
   if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) {
     meta->bad_sym = 1;
