@@ -399,8 +399,8 @@ def main() -> None:
         else:
             async_api = {"status": "plan needed the synchronous fallback"}
 
-    # The same merges with the timers off: from the second one on, the library replays
-    # the merge's ~25 launches as one HIP graph (smx_compose.hip compose_async_graph).
+    # The same merges with the timers off (what a caller gets: direct launches; the
+    # library's own graph replay, SMX_GRAPH, is off by default since round 5).
     graph_api = None
     if not sharded and world == 1 and not args.no_async:
         for _ in range(2):
@@ -413,7 +413,7 @@ def main() -> None:
         el_graph = time.perf_counter() - t1
         graph_api = {"ms_per_step": round(el_graph / args.steps * 1e3, 4),
                      "value": round(n_job * args.steps / el_graph, 1),
-                     "note": "smx_compose per merge, timers off: the merge replayed as one HIP graph"}
+                     "note": "smx_compose per merge, stage timers off"}
 
     if args.verify and not sharded:
         from oracle import oracle

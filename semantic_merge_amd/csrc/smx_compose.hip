@@ -2609,7 +2609,10 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
 // timestamps recorded by a replayed graph read back as 0 ms on this ROCm
 // (profiles/r03_i/bench.json: every stage 0.0), so timed merges enqueue directly.
 #ifndef SMX_GRAPH
-#define SMX_GRAPH 1
+#define SMX_GRAPH 0  // off: on this ROCm the replay is slower than enqueueing the launches
+                     // (timers off: config 2 0.183 -> 0.160 ms, config 3 2.381 -> 2.352 ms
+                     // without it, profiles/r05_x/graph_ab.txt): the first kernel waits for the
+                     // whole graph's submission, while direct launches start the GPU at once
 #endif
 #define GRAPH_CACHE 8
 struct GraphEntry {
