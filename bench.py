@@ -67,6 +67,7 @@ PIPE_BYTES_PER_OP = 53         # 37 B in + 16 B out per op (+8 B 
 ROOF_STAGES = {"window": ("k_window_f<2048", 41), "window_wide": ("k_window_f<8192", 41),
                "window_g": ("k_window_g", 45), "segsort": ("k_segsort", 52)}
 WINDOW_BYTES_PER_OP = ROOF_STAGES["window"][1]
+ROOF_STEPS = 3  # timed steps whose roofline-kernel launches carry HIP events
 REF_PY_OPS_S = 47_600          # SURVEY §3.4 / BASELINE.md: reference compose_oplogs, 1 core, 1M ops
 FETCH_FACTOR, WRITE_FACTOR = 2.0, 1.0   # gfx950 FETCH_SIZE reads 1/2 of streamed bytes (guide)
 
@@ -330,9 +331,9 @@ def main() -> None:
     torch.cuda.set_stream(stream)
     lib = _lib.lib()
     # the timed steps carry HIP events around the roofline kernels' stages only (an event
-    # pair around every stage of every merge cost ~2% of config 3's step); timed merges
-    # enqueue their launches directly (the graph replay is the graph_api leg).  The full
-    # per-stage breakdown comes from an untimed leg after them.
+    # pair around every stage of every merge cost ~2% of config 3's step), and only in the
+    # last ROOF_STEPS of them.  The full per-stage breakdown comes from an untimed leg
+    # after them.
     names = [lib.smx_stage_name(i).decode() for i in range(32)]
     lib.smx_set_profiling_stages(sum(1 << i for i, nm in enumerate(names) if nm in ROOF_STAGES))
     lib.smx_set_profiling(1)
@@ -343,8 +344,15 @@ def main() -> None:
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    # the roofline kernel's launches are timed (HIP events) in the last ROOF_STEPS steps of
+    # the timed region (steady state); the others run without events (each event pair
+    # drains the queue around the kernel: ~18 us per config-3 merge)
+    roof_from = args.steps - min(args.steps, ROOF_STEPS)
+    lib.smx_set_profiling(0)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if i == roof_from:
+            lib.smx_set_profiling(1)
         run()
     torch.cuda.synchronize(dev)
     if dist:
@@ -520,6 +528,7 @@ def main() -> None:
             if pmc and pmc.get("status") == "ok" else None,
             "bytes_per_op": roof_bpo,
             "avg_launch_ms": round(win_avg, 4),
+            "timed_launches": int(st_calls),
         },
         "pmc": pmc,
         # per merge: each stage's summed time over its launches in one merge, and how many
