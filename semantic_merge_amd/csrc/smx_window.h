@@ -303,6 +303,9 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_RUNS
 #define WF_RUNS 1    // the normal presorted windows order by runs and (kind, run) groups (no merge / multisplit)
 #endif
+#ifndef WF_LOREG
+#define WF_LOREG 1  // run-grouped step h: a bucket's start from the op's slot and arrival rank (no LDS read)
+#endif
 #ifndef WF_HEADLIST
 #define WF_HEADLIST 0  // run-grouped step a, 1: every head binary-searches a list of the other part's
                        // heads at once (three more barriers): window 1.196 -> 1.241 ms on config 3,
@@ -889,7 +892,11 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
         if (b == 0xffffffffu) continue;
         const int e = t + NT * i;
         const u32 b1 = b + 1 < (u32)CAP ? b + 1 : (u32)CAP - 1;  // (branch-free bucket bounds)
+#if WF_LOREG
+        const u32 lo = slot_r[i] - ar_r[i];  // (the bucket's start: this op's slot less its arrival rank)
+#else
         const u32 lo = (bcnt[b >> 1] >> (16 * (b & 1))) & 0xffffu;
+#endif
         const u32 hw = (bcnt[b1 >> 1] >> (16 * (b1 & 1))) & 0xffffu;
         const u32 hi = b + 1 < (u32)CAP ? hw : (u32)sz, kp = hi_r[i];
         u32 c = 0;
