@@ -303,6 +303,10 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #ifndef WF_RUNS
 #define WF_RUNS 1    // the normal presorted windows order by runs and (kind, run) groups (no merge / multisplit)
 #endif
+#ifndef WF_HBATCH
+#define WF_HBATCH 0  // run-grouped step h, 1: the ITEMS buckets' ends and first members read together:
+                     // window 1.181 -> 1.439 ms on config 3 (more live registers), off
+#endif
 #ifndef WF_LOREG
 #define WF_LOREG 1  // run-grouped step h: a bucket's start from the op's slot and arrival rank (no LDS read)
 #endif
@@ -886,6 +890,19 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
       // h. rank inside the bucket on (key, full id, side, index); the final order
       //    (per-lane loops: one op per bucket on average; a wave-uniform loop over the
       //    ITEMS buckets together spilled registers)
+#if WF_HBATCH
+      // every item's bucket end and first member read together (independent LDS reads:
+      // one round trip for the ITEMS buckets; a bucket holds one op on average), the
+      // rest of a bucket by the loop below
+      u32 hw_r[ITEMS], x0_r[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const u32 b = b_r[i] == 0xffffffffu ? 0u : b_r[i];
+        const u32 b1 = b + 1 < (u32)CAP ? b + 1 : (u32)CAP - 1;
+        hw_r[i] = bcnt[b1 >> 1];
+        x0_r[i] = mkey[slot_r[i] - ar_r[i]];
+      }
+#endif
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const u32 b = b_r[i];
@@ -897,12 +914,26 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinAr
 #else
         const u32 lo = (bcnt[b >> 1] >> (16 * (b & 1))) & 0xffffu;
 #endif
+#if WF_HBATCH
+        const u32 hw = (hw_r[i] >> (16 * (b1 & 1))) & 0xffffu;
+#else
         const u32 hw = (bcnt[b1 >> 1] >> (16 * (b1 & 1))) & 0xffffu;
+#endif
         const u32 hi = b + 1 < (u32)CAP ? hw : (u32)sz, kp = hi_r[i];
         u32 c = 0;
         bool tie = false;
+#if WF_HBATCH
+        {  // the first member (lo < hi: this op is in the bucket)
+          const u32 x = x0_r[i];
+          c += x < kp;
+          tie |= (x == kp) & (lo != slot_r[i]);
+        }
+#pragma unroll 1
+        for (u32 q = lo + 1; q < hi; ++q) {
+#else
 #pragma unroll 1
         for (u32 q = lo; q < hi; ++q) {  // (own slot: x == kp, not a tie)
+#endif
           const u32 x = mkey[q];
           c += x < kp;
           tie |= (x == kp) & (q != slot_r[i]);
