@@ -29,6 +29,7 @@
 //               file, ctx
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -2242,6 +2243,25 @@ __global__ void __launch_bounds__(SEG_NT) k_segsort(const u64* __restrict__ ts, 
 }
 
 
+// Host wait for a stream: with SMX_SPIN_US > 0 a short spin on hipStreamQuery first, then
+// the blocking sync.  Off for the merges: spinning measured slower there (config 2
+// 0.161 -> 0.166 ms, profiles/r05_x/spin_ab.txt), while the RGA call gains from it
+// (smx_rga.hip RGA_SPIN_US).
+#ifndef SMX_SPIN_US
+#define SMX_SPIN_US 0
+#endif
+static hipError_t stream_wait(hipStream_t st) {
+  if (SMX_SPIN_US > 0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipStreamQuery(st);
+      if (e != hipErrorNotReady) return e;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(SMX_SPIN_US)) break;
+    }
+  }
+  return hipStreamSynchronize(st);
+}
+
 static int read_meta(const Ctx& C, ComposeMeta* hm);
 
 // GEN_SEG: when the segmented sort cannot order this log it flags seg_over and f_fail
@@ -2345,7 +2365,7 @@ static int read_meta(const Ctx& C, ComposeMeta* hm) {
   ComposeMeta*& pinned = holder.p;
   if (!pinned) HIP_TRY(hipHostMalloc((void**)&pinned, sizeof(ComposeMeta), hipHostMallocDefault));
   HIP_TRY(hipMemcpyAsync(pinned, C.ws<ComposeMeta>(B_META), sizeof(ComposeMeta), hipMemcpyDeviceToHost, C.st));
-  HIP_TRY(hipStreamSynchronize(C.st));
+  HIP_TRY(stream_wait(C.st));
   std::memcpy(hm, pinned, sizeof(ComposeMeta));
   return SMX_OK;
 }

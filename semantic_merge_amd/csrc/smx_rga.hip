@@ -15,6 +15,7 @@
 // persistent, in LDS): value groups by hashing, one sequential replay per group,
 // survivors ordered by (anchor, t, author, opid, index) -> compaction, each list's
 // output offset summed by its own wave from per-chunk survivor sums.
+#include <chrono>
 #include <string>
 
 #include "smx_scan.h"
@@ -1586,6 +1587,25 @@ extern "C" int smx_rga_workspace_bytes(int64_t n_ops, int64_t n_lists, size_t* b
   return SMX_OK;
 }
 
+// Host wait for a stream: a short spin on hipStreamQuery, then the blocking sync.  A call
+// ends within a millisecond, and a blocking sync wakes the calling thread ~10-20 us after
+// the stream's last packet: 10M events 0.520 -> 0.502 ms, grouped 0.297 -> 0.287 ms
+// (profiles/r05_x/spin_ab.txt; RGA_SPIN_US 0: block at once).
+#ifndef RGA_SPIN_US
+#define RGA_SPIN_US 20000
+#endif
+static hipError_t stream_wait(hipStream_t st) {
+  if (RGA_SPIN_US > 0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipStreamQuery(st);
+      if (e != hipErrorNotReady) return e;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(RGA_SPIN_US)) break;
+    }
+  }
+  return hipStreamSynchronize(st);
+}
+
 static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, size_t wsb, hipStream_t st,
                     bool grouped) {
   const i64 n = ops->n_ops, nl = ops->n_lists;
@@ -1707,7 +1727,7 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
   RGA_TRY(hipGetLastError());
   i32 herr = 0;
   RGA_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
-  RGA_TRY(hipStreamSynchronize(st));
+  RGA_TRY(stream_wait(st));
   if (herr & RGA_E_INPUT) return smx_set_error(SMX_E_ARG, "invalid input: list >= n_lists or op > 2");
   if (herr & RGA_E_UNGROUPED) return rga_impl(ops, out, ws, wsb, st, false);  // (not grouped after all)
   return SMX_OK;
