@@ -2,9 +2,13 @@
 # GPU-box steps for iterating (each under its own time limit; stops at the first failure):
 #   gpurun -- bash tools/gpu_steps.sh <tag> <step> [<step> ...]
 # steps: rga (RGA GPU tests), compose (compose GPU tests incl. full-size digests),
-#        small (small-plan tests + tools/small_merge_probe.py), gtests (the whole -m gpu suite), ab (tools/ab_libs.py, current vs tools/_build/var_old),
-#        ab5 (the same on config 5), rgabench (tools/bench_rga.py), bench (bench.py, no PMC / CPU
-#        legs), benchfull (bench.py default), c5 (bench.py --config c5), c2, prof, sq
+#        small (small-plan tests + tools/small_merge_probe.py), smallprof (its kernel trace),
+#        smallph (phase stamps, tools/_build/var_stamps), gtests (the whole -m gpu suite),
+#        ab / ab5 (tools/ab_libs.py, current vs tools/_build/var_old, configs 3 / 5),
+#        rgabench (tools/bench_rga.py), rgaprof (its kernel trace and timeline), bench (bench.py,
+#        no PMC / CPU legs), benchfull (bench.py default), c5, c2 (bench.py configs), c2prof
+#        (config-2 kernel timeline), shard (sharded GPU tests + tools/shard_probe.py), prof
+#        (config-3 kernel stats), sq (tools/pmc_sq.sh)
 set -o pipefail
 TAG=${1:?tag}; shift
 R=$PWD; O=$R/gpurun_out/$TAG; mkdir -p "$O"
