@@ -2572,7 +2572,40 @@ static inline bool small_merge(const smx_ops* ops) {
 struct EarlyVerdict {
   bool failed = false;  // the presorted plan fails for sure (f_fail F_LONG)
   bool bad = false;     // ... and k_khist saw an invalid kind
+  // a small merge's verdict word in mapped pinned host memory (synchronous calls):
+  // k_compose_small stores seq << 1 | bad there, and finish reads it after the stream
+  // wait instead of copying the meta block back (one copy packet less per call)
+  u64* hrec = nullptr;       // (device address)
+  const u64* hrec_host = nullptr;
+  u64 hseq = 0;
+  bool rec_used = false;
 };
+
+struct SmallRec {  // one per host thread, freed when the thread exits
+  u64* h = nullptr;
+  u64* d = nullptr;
+  u64 seq = 0;
+  ~SmallRec() {
+    if (h) (void)hipHostFree(h);
+  }
+};
+static SmallRec* small_rec() {
+  static thread_local SmallRec r;
+  if (!r.h) {
+    if (hipHostMalloc((void**)&r.h, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) !=
+        hipSuccess) {
+      r.h = nullptr;
+      return nullptr;
+    }
+    *(volatile u64*)r.h = 0;
+    if (hipHostGetDevicePointer((void**)&r.d, r.h, 0) != hipSuccess) {
+      (void)hipHostFree(r.h);
+      r.h = nullptr;
+      return nullptr;
+    }
+  }
+  return &r;
+}
 
 static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* ws, const Layout& L,
                          hipStream_t st, bool timed, bool early_ok = false, EarlyVerdict* verdict = nullptr) {
@@ -2582,7 +2615,10 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
   int rc;
   if (small_merge(ops)) {  // the whole merge in one workgroup (smx_small.h)
     tm.begin(ST_SMALL);
-    hipLaunchKernelGGL(k_compose_small, dim3(1), dim3(SMALL_NT), 0, st, *ops, *out, C.ws<ComposeMeta>(B_META));
+    u64* hrec = verdict ? verdict->hrec : nullptr;
+    if (hrec) verdict->rec_used = true;
+    hipLaunchKernelGGL(k_compose_small, dim3(1), dim3(SMALL_NT), 0, st, *ops, *out, C.ws<ComposeMeta>(B_META), hrec,
+                       hrec ? verdict->hseq : (u64)0);
     HIP_TRY(hipGetLastError());
     tm.end(ST_SMALL);
     tm.flush();
@@ -2774,6 +2810,7 @@ static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, vo
     if (done) return SMX_OK;
   }
   EarlyVerdict ev;
+  if (verdict) ev = *verdict;  // (the caller's verdict word, if any)
   if ((rc = enqueue_async(ops, out, ws, L, st, timed, early_ok, &ev))) return rc;
   if (verdict) *verdict = ev;
   if (ev.failed && SMX_GRAPH && st != nullptr) {  // a graph of a plan that fails is not worth capturing
@@ -2800,11 +2837,22 @@ static int compose_finish_impl(const smx_ops* ops, const smx_compose_out* out, v
   StageTimer tm(st, profiling_on() != 0);
   Ctx C{ops, out, st, L, (char*)ws, na, nb, n, n_sym, 0, na, &tm};
   ComposeMeta hm;
+  bool have = false;
   if (known && known->failed) {
     std::memset(&hm, 0, sizeof(hm));
     hm.f_fail = F_LONG;
     hm.bad_sym = known->bad ? 1 : 0;
-  } else if ((rc = read_meta(C, &hm))) {
+    have = true;
+  } else if (known && known->rec_used) {  // the small plan: its verdict word, no meta copy
+    HIP_TRY(stream_wait(st));
+    const u64 v = *(volatile const u64*)known->hrec_host;
+    if ((v >> 1) == known->hseq) {
+      std::memset(&hm, 0, sizeof(hm));
+      hm.bad_sym = (u32)(v & 1);
+      have = true;
+    }
+  }
+  if (!have && (rc = read_meta(C, &hm))) {
     return rc;
   }
   if (hm.bad_sym) return set_err(SMX_E_ARG, "invalid input: sym[i] >= n_sym or kind[i] >= 18");
@@ -3165,6 +3213,11 @@ extern "C" int smx_compose(const smx_ops* ops, const smx_compose_out* out, void*
   int rc;
   try {
     EarlyVerdict ev;
+    if (SmallRec* r = small_merge(ops) ? small_rec() : nullptr) {
+      ev.hrec = r->d;
+      ev.hrec_host = r->h;
+      ev.hseq = ++r->seq;
+    }
     rc = compose_async_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream, true, &ev);
     if (!rc) rc = compose_finish_impl(ops, out, workspace, workspace_bytes, (hipStream_t)stream, &ev);
   } catch (const std::exception& e) {

@@ -47,7 +47,8 @@ __device__ u64 g_small_stamp[16];
   } while (0)
 #endif
 
-__global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_compose_out out, ComposeMeta* meta) {
+__global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_compose_out out, ComposeMeta* meta,
+                                                                u64* hrec, u64 hseq) {
   constexpr int IT = SMALL_N / SMALL_NT;
   constexpr int NW = SMALL_NT / WAVE;
   // keys of the sort (dead after it: the hash table takes their place)
@@ -108,6 +109,7 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
       meta->bad_sym = 1;
       out.counts[0] = -1;
       out.counts[1] = -1;
+      if (hrec) *hrec = hseq << 1 | 1u;  // the verdict word (smx_compose's synchronous call)
     }
     return;
   }
@@ -422,6 +424,7 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
       out.counts[1] = (i64)nc;
       meta->n_conf = nc;
       meta->n_skip = 2 * nc;
+      if (hrec) *hrec = hseq << 1;  // read after the stream wait: the kernel's end publishes it
     }
     SMALL_STAMP(6);
   }
