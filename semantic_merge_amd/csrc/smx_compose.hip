@@ -982,6 +982,8 @@ struct EmitArgs {
   i32* out_ctx;
   i64* counts;
   int status_none;  // report pending None-value moves (single merge) in counts[0]
+  u64* hrec;        // or null: the synchronous call's verdict word (EarlyVerdict)
+  u64 hseq;
 };
 
 #ifndef SMX_EMIT_NT
@@ -1037,6 +1039,8 @@ __global__ void EMIT_BOUNDS k_emit(EmitArgs E) {
     const bool bad = M->bad_sym != 0;
     E.counts[0] = bad ? -1 : M->f_fail ? -2 : (M->n_move_none && E.status_none) ? -3 : (i64)(E.n - M->n_skip);
     E.counts[1] = bad ? -1 : (i64)M->n_conf;
+    // seq << 1 | 1: smx_compose_finish has work left (or an error) and reads the meta
+    if (E.hrec) *E.hrec = E.hseq << 1 | ((bad || M->f_fail || (M->n_move_none && M->kcnt[KMOVE])) ? 1u : 0u);
   }
   if (M->f_fail | M->bad_sym) return;
   const u64 nskip = M->n_skip;
@@ -1144,6 +1148,8 @@ __global__ void EMIT_BOUNDS k_emit4(EmitArgs E) {
     const bool bad = M->bad_sym != 0;
     E.counts[0] = bad ? -1 : M->f_fail ? -2 : (M->n_move_none && E.status_none) ? -3 : (i64)(E.n - M->n_skip);
     E.counts[1] = bad ? -1 : (i64)M->n_conf;
+    // seq << 1 | 1: smx_compose_finish has work left (or an error) and reads the meta
+    if (E.hrec) *E.hrec = E.hseq << 1 | ((bad || M->f_fail || (M->n_move_none && M->kcnt[KMOVE])) ? 1u : 0u);
   }
   if (M->f_fail | M->bad_sym) return;
   const u64 nskip = M->n_skip;
@@ -1378,6 +1384,8 @@ struct Ctx {
   i64 src_a, src_b;  // global source index of local op j (see WinArgs)
   StageTimer* tm;
   const i32* src_map = nullptr;
+  u64* hrec = nullptr;  // the synchronous call's verdict word (k_emit stores it), or null
+  u64 hseq = 0;
   template <typename T>
   T* ws(int b) const { return (T*)(base + L.off[b]); }
 };
@@ -1613,7 +1621,8 @@ static int launch_emit(const Ctx& C, bool packable, const smx_shard* sh) {
   const i64 n = C.n;
   EmitArgs E{C.ws<i32>(B_TSRC), C.ws<u32>(B_TSYM), C.ws<u64>(B_SKIPBITS), C.ws<u32>(B_SKIPLIST),
              C.ws<int4>(B_FIN), meta, (u64)n, (u32)(C.n_sym - 1), packable ? 1 : 0, (u64)C.na, C.src_a,
-             C.src_b, C.src_map, C.out->order, C.out->addr, C.out->file, C.out->ctx, C.out->counts, sh ? 0 : 1};
+             C.src_b, C.src_map, C.out->order, C.out->addr, C.out->file, C.out->ctx, C.out->counts, sh ? 0 : 1,
+             sh ? nullptr : C.hrec, C.hseq};
   const i64 ewaves = SMX_CEIL_DIV(n, (i64)EMIT_WT);
   const bool al16 = ((uintptr_t)C.out->order | (uintptr_t)C.out->addr | (uintptr_t)C.out->file |
                      (uintptr_t)C.out->ctx) % 16 == 0;
@@ -2572,13 +2581,16 @@ static inline bool small_merge(const smx_ops* ops) {
 struct EarlyVerdict {
   bool failed = false;  // the presorted plan fails for sure (f_fail F_LONG)
   bool bad = false;     // ... and k_khist saw an invalid kind
-  // a small merge's verdict word in mapped pinned host memory (synchronous calls):
-  // k_compose_small stores seq << 1 | bad there, and finish reads it after the stream
-  // wait instead of copying the meta block back (one copy packet less per call)
+  // the merge's verdict word in mapped pinned host memory (synchronous calls): the
+  // last kernel (k_compose_small, k_emit) stores seq << 1 | bit there, and finish reads
+  // it after the stream wait instead of copying the meta block back (one copy packet
+  // less per call).  bit: the small plan's invalid input; the large plan's "finish
+  // has work left" (an error, a failed plan, None-value moves), which reads the meta.
   u64* hrec = nullptr;       // (device address)
   const u64* hrec_host = nullptr;
   u64 hseq = 0;
   bool rec_used = false;
+  bool rec_small = false;
 };
 
 struct SmallRec {  // one per host thread, freed when the thread exits
@@ -2616,7 +2628,7 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
   if (small_merge(ops)) {  // the whole merge in one workgroup (smx_small.h)
     tm.begin(ST_SMALL);
     u64* hrec = verdict ? verdict->hrec : nullptr;
-    if (hrec) verdict->rec_used = true;
+    if (hrec) verdict->rec_used = verdict->rec_small = true;
     hipLaunchKernelGGL(k_compose_small, dim3(1), dim3(SMALL_NT), 0, st, *ops, *out, C.ws<ComposeMeta>(B_META), hrec,
                        hrec ? verdict->hseq : (u64)0);
     HIP_TRY(hipGetLastError());
@@ -2653,6 +2665,11 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
       tm.flush();
       return SMX_OK;
     }
+  }
+  if (verdict && verdict->hrec) {  // k_emit publishes the verdict: finish skips the meta copy
+    C.hrec = verdict->hrec;
+    C.hseq = verdict->hseq;
+    verdict->rec_used = true;
   }
   if (!knob("SMX_ABLATE", 0) && (rc = launch_tail(C))) return rc;  // SMX_ABLATE (diagnostic builds): window only
   tm.flush();
@@ -2843,13 +2860,13 @@ static int compose_finish_impl(const smx_ops* ops, const smx_compose_out* out, v
     hm.f_fail = F_LONG;
     hm.bad_sym = known->bad ? 1 : 0;
     have = true;
-  } else if (known && known->rec_used) {  // the small plan: its verdict word, no meta copy
+  } else if (known && known->rec_used) {  // the verdict word: no meta copy when there is no work left
     HIP_TRY(stream_wait(st));
     const u64 v = *(volatile const u64*)known->hrec_host;
     if ((v >> 1) == known->hseq) {
       std::memset(&hm, 0, sizeof(hm));
-      hm.bad_sym = (u32)(v & 1);
-      have = true;
+      hm.bad_sym = v & 1;
+      have = known->rec_small || !(v & 1);
     }
   }
   if (!have && (rc = read_meta(C, &hm))) {
@@ -3213,7 +3230,7 @@ extern "C" int smx_compose(const smx_ops* ops, const smx_compose_out* out, void*
   int rc;
   try {
     EarlyVerdict ev;
-    if (SmallRec* r = small_merge(ops) ? small_rec() : nullptr) {
+    if (SmallRec* r = small_rec()) {
       ev.hrec = r->d;
       ev.hrec_host = r->h;
       ev.hseq = ++r->seq;
