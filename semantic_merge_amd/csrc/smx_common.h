@@ -57,6 +57,8 @@ struct ComposeMeta {
   u64 n_win;                 // windows of the plan that ran
   u32 kmask[2];              // presorted plan: kinds present per branch (k_khist)
   u64 cs_done;               // k_cscan_mid blocks done (the last one writes base[])
+  u32 wk_done[2];            // k_boundary / k_replay_q blocks done (fused walk steps:
+                             // the last block runs the next single-block step, resets it)
 };
 
 // Per-symbol final states (addr, file, ctx).  When the bit widths of (value + 1)

@@ -251,17 +251,18 @@ __global__ void k_meta_init(ComposeMeta* meta) {
 // B[CH*j + CH-1]; 1/256 of the keys, cache-resident): the first level of the
 // search runs on them, the second inside one chunk.  The snap gallops back over
 // the (short) run of equal timestamps.
-__global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB, const u64* __restrict__ sA,
-                        const u64* __restrict__ sB, i64 na, i64 nb, i64 W, i64 tgt, i64 D, i64* __restrict__ bnd,
-                        ComposeMeta* meta, u32* long_host) {
-  const i64 k = (i64)blockIdx.x * BLOCK + threadIdx.x;
+__device__ __forceinline__ void fpart_body(const u64* __restrict__ ts, const u64* __restrict__ tsB,
+                                           const u64* __restrict__ sA, const u64* __restrict__ sB, i64 na, i64 nb,
+                                           i64 W, i64 tgt, i64 D, i64* __restrict__ bnd, ComposeMeta* meta,
+                                           u32* long_host, i64 blk, i64 nblk) {
+  const i64 k = blk * BLOCK + threadIdx.x;
   if (SMX_KHIST_LONG) {
     // A chunk sample equal to the sample D chunks (one window capacity) later (A: first
     // ops of chunks c and c + D; B: last ops of full chunks): that timestamp group alone
     // overflows a window, so the presorted plan cannot hold.  Flagged before the windows
     // run: k_window_f then leaves before its loads (6: a window too large, and smaller
     // windows cannot help).  Grid-stride over the samples, off the search's path.
-    const i64 nt = (i64)gridDim.x * BLOCK, ca = SMX_CEIL_DIV(na, (i64)CH), cb = nb / CH;
+    const i64 nt = nblk * BLOCK, ca = SMX_CEIL_DIV(na, (i64)CH), cb = nb / CH;
     bool lg = false;
     for (i64 c = k; c + D < ca; c += nt) lg |= sA[c] == sA[c + D];
     for (i64 c = k; c + D < cb; c += nt) lg |= sB[c] == sB[c + D];
@@ -343,6 +344,11 @@ __global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB,
   }
   bnd[2 * k] = r[0];
   bnd[2 * k + 1] = r[1];
+}
+__global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB, const u64* __restrict__ sA,
+                        const u64* __restrict__ sB, i64 na, i64 nb, i64 W, i64 tgt, i64 D, i64* __restrict__ bnd,
+                        ComposeMeta* meta, u32* long_host) {
+  fpart_body(ts, tsB, sA, sB, na, nb, W, tgt, D, bnd, meta, long_host, blockIdx.x, gridDim.x);
 }
 
 // Generic windows over branch logs sorted by (ts, oid): fixed diagonals of WIN_CAP.
@@ -722,10 +728,8 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_down(u32* __restrict__ cnt, i64
 #ifndef CS_SMALL_CM
 #define CS_SMALL_CM 16384
 #endif
-__global__ void __launch_bounds__(BLOCK) k_cscan_small(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
-                                                       ComposeMeta* meta, u64 nwin) {
-  __shared__ u32 s[NWAVES + 1];
-  const int col = blockIdx.x;
+__device__ __forceinline__ void cscan_small_body(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM, ComposeMeta* meta,
+                                                 u64 nwin, int col, u32* s) {
   const int side = col / SMX_N_KINDS, k = col % SMX_N_KINDS;
   const i64 C = SMX_CEIL_DIV(side ? nb : na, (i64)CH);
   u32* colp = cnt + (i64)col * CM;
@@ -755,7 +759,7 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_small(u32* __restrict__ cnt, i6
     atomicAdd((unsigned long long*)&meta->kcnt[k], (unsigned long long)carry);
     if (k == KREN) meta->n_ren_side[side] = carry;
     __threadfence();
-    if (atomicAdd((unsigned long long*)&meta->cs_done, 1ull) == (unsigned long long)gridDim.x - 1) {
+    if (atomicAdd((unsigned long long*)&meta->cs_done, 1ull) == (unsigned long long)(2 * SMX_N_KINDS - 1)) {
       __threadfence();
       meta->n_win = nwin;
       u64 acc = 0;
@@ -766,6 +770,26 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_small(u32* __restrict__ cnt, i6
       meta->base[SMX_N_KINDS] = acc;
     }
   }
+}
+#ifndef SMX_FPART_CS
+#define SMX_FPART_CS 1  // small merges: k_fpart and k_cscan_small in one launch
+#endif
+__global__ void __launch_bounds__(BLOCK) k_cscan_small(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
+                                                       ComposeMeta* meta, u64 nwin) {
+  __shared__ u32 s[NWAVES + 1];
+  cscan_small_body(cnt, na, nb, CM, meta, nwin, blockIdx.x, s);
+}
+// Small merges (launch-bound): k_fpart and k_cscan_small are independent (both read
+// only k_khist's outputs), so one launch runs both: the first nfp blocks are k_fpart's,
+// the last 2 * SMX_N_KINDS k_cscan_small's columns.
+__global__ void __launch_bounds__(BLOCK) k_fpart_cscan(const u64* __restrict__ ts, const u64* __restrict__ tsB,
+                                                       const u64* __restrict__ sA, const u64* __restrict__ sB, i64 na,
+                                                       i64 nb, i64 W, i64 tgt, i64 D, i64* __restrict__ bnd,
+                                                       ComposeMeta* meta, u32* long_host, u32* __restrict__ cnt,
+                                                       i64 CM, i64 nfp) {
+  __shared__ u32 s[NWAVES + 1];
+  if ((i64)blockIdx.x < nfp) fpart_body(ts, tsB, sA, sB, na, nb, W, tgt, D, bnd, meta, long_host, blockIdx.x, nfp);
+  else cscan_small_body(cnt, na, nb, CM, meta, (u64)W, (int)(blockIdx.x - nfp), s);
 }
 
 // Per-window counts: each kind and renames per branch (+ moves with a None value
@@ -1468,6 +1492,11 @@ static WalkArgs walk_args(const Ctx& C, const smx_shard* sh) {
 
 // DivergentRename walk (smx_walk.h): conflicts, skip bits, sorted skip list.
 // Every size is read on the device from meta: no host sync.
+#ifndef SMX_WALK_LB
+#define SMX_WALK_LB 0  // 1: the one-block walk steps run in the last block of the grid before
+                       // them; slower: config 2 walk 0.040 -> 0.056 ms (profiles/r05_wlb/ab_c2.txt),
+                       // the device-scope fences of every block cost more than the launches
+#endif
 static int launch_walk(const Ctx& C, const smx_shard* sh) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
@@ -1494,15 +1523,25 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
   const u64* ncand_dev = &meta->n_cand;
   const i64 Wmax = max_windows(n);
   const int gsmall = 256;  // grid for loops over the (few) candidates
-  hipLaunchKernelGGL(k_boundary, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, meta, cslot, wcand, wtot, skipbits,
-                     nskipw);
+  // small single merges: the one-block steps run in the last block of the grid before
+  // them (k_boundary_cc, k_replay_q_cl), two launches fewer
+  const bool lb_cc = SMX_WALK_LB && !sh && Wmax <= WALK_CC_FUSED_MAXW;
+  const bool lb_cl = SMX_WALK_LB && !sh && n <= WALK_FUSED_MAXN;
+  if (lb_cc)
+    hipLaunchKernelGGL(k_boundary_cc, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, meta, cslot, wcand, wtot,
+                       skipbits, nskipw, wcoff, (u64)Wmax, ncand32, cand);
+  else
+    hipLaunchKernelGGL(k_boundary, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, meta, cslot, wcand, wtot, skipbits,
+                       nskipw);
   if (sh && (sh->in_d > 0 || sh->in_state_dev))
     hipLaunchKernelGGL(k_replay_in, dim3(1), dim3(1), 0, st, Wk, (int)sh->in_ahead, (u32)sh->in_d,
                        (const i64*)sh->in_state_dev, meta, C.out->conflicts, (u64)C.out->conflict_cap, skiplist,
                        skipbits);
   // (one k_scan1 block over the window counts measured slower on config 3: walk 0.165 ->
   // 0.185 ms, profiles/r03_w; small merges are launch-bound: one block)
-  if (Wmax <= WALK_CC_FUSED_MAXW) {
+  if (lb_cc) {
+    // (k_boundary_cc's last block did the scan and the compaction)
+  } else if (Wmax <= WALK_CC_FUSED_MAXW) {
     hipLaunchKernelGGL(k_cand_scan_compact, dim3(1), dim3(S1_NT), 0, st, Wk, wtot, wcoff, (u64)Wmax, ncand32, cslot,
                        cand);
   } else {
@@ -1513,11 +1552,15 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
       HIP_TRY((scan_excl<OpSum, u32, u32>(wtot, wcoff, Wmax, &meta->n_win, part, ncand32, st)));
     hipLaunchKernelGGL(k_cand_compact, dim3(grid_for(Wmax)), dim3(BLOCK), 0, st, Wk, cslot, wcoff, ncand_dev, cand);
   }
-  hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
-  if (n <= WALK_FUSED_MAXN) {  // small merges: max scan, clusters and sum scan in one block
+  if (lb_cl) {
+    hipLaunchKernelGGL(k_replay_q_cl, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf, pm, nreal, coff,
+                       (u64)n, nconf32);
+  } else if (n <= WALK_FUSED_MAXN) {  // small merges: max scan, clusters and sum scan in one block
+    hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
     hipLaunchKernelGGL(k_cluster_fused, dim3(1), dim3(S1_NT), 0, st, Wk, cand, q, pm, nconf, meta, nreal, coff,
                        (u64)n, nconf32);
   } else {
+    hipLaunchKernelGGL(k_replay_q, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, meta, q, nconf);
     hipLaunchKernelGGL(k_scan1<OpMax>, dim3(1), dim3(S1_NT), 0, st, q, pm, ncand_dev, (u64)n, (u32*)nullptr);
     hipLaunchKernelGGL(k_cluster, dim3(gsmall), dim3(BLOCK), 0, st, Wk, cand, q, pm, nconf, meta, nreal);
     hipLaunchKernelGGL(k_scan1<OpSum>, dim3(1), dim3(S1_NT), 0, st, nreal, coff, ncand_dev, (u64)n, nconf32);
@@ -1890,11 +1933,19 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
                        C.ops->kind, C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta,
                        early ? early->flag_dev : nullptr);
   }
-  hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
-                     C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na,
-                     C.nb, W, tgt, cap / CH, bnd, meta, early ? early->flag_dev : nullptr);
+  const i64 nfp = SMX_CEIL_DIV(W + 1, (i64)BLOCK);
+  const bool fused = SMX_FPART_CS && CM <= CS_SMALL_CM && !early;
+  if (fused)
+    hipLaunchKernelGGL(k_fpart_cscan, dim3(nfp + 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, C.ops->ts,
+                       C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na, C.nb, W, tgt, cap / CH, bnd, meta,
+                       (u32*)nullptr, ccnt, CM, nfp);
+  else
+    hipLaunchKernelGGL(k_fpart, dim3(nfp), dim3(BLOCK), 0, st, C.ops->ts, C.ops->ts + C.na + C.ops->b_gap, sA, sB,
+                       C.na, C.nb, W, tgt, cap / CH, bnd, meta, early ? early->flag_dev : nullptr);
   if (early) HIP_TRY(hipEventRecord(early->ev, st));
-  if (CM <= CS_SMALL_CM) {
+  if (fused) {
+    // (k_fpart_cscan scanned the columns)
+  } else if (CM <= CS_SMALL_CM) {
     hipLaunchKernelGGL(k_cscan_small, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, meta, (u64)W);
   } else {
     const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);

@@ -268,9 +268,11 @@ __device__ u32 replay_region(const WalkArgs& W, u32 p, ReplayState& st, u32* nco
 // window's in-window candidates in its slots; wtot[w] = all of the window's
 // candidates.  Re-running it (sharded walk rounds) rewrites the same slots.  Block
 // 0 also resets the walk's counters in meta.
-__global__ void __launch_bounds__(BLOCK) k_boundary(WalkArgs W0, ComposeMeta* meta, u32* __restrict__ cslot,
-                                                    const u32* __restrict__ wcand, u32* __restrict__ wtot,
-                                                    u64* __restrict__ skipbits, u64 nskipw) {
+// (cslot and wtot carry no __restrict__: k_boundary_cc's last block reads what the
+// other blocks wrote there)
+__device__ __forceinline__ void boundary_body(WalkArgs W0, ComposeMeta* meta, u32* cslot,
+                                              const u32* __restrict__ wcand, u32* wtot,
+                                              u64* __restrict__ skipbits, u64 nskipw) {
   // the skip bits of the walk (k_replay_in / k_replay_write set them) start cleared:
   // done here rather than by a zero-fill launch of its own
   for (u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x; i < nskipw; i += (u64)gridDim.x * BLOCK) skipbits[i] = 0ull;
@@ -310,6 +312,27 @@ __global__ void __launch_bounds__(BLOCK) k_boundary(WalkArgs W0, ComposeMeta* me
     wtot[w] = c0 + cnt;
   }
 }
+__global__ void __launch_bounds__(BLOCK) k_boundary(WalkArgs W0, ComposeMeta* meta, u32* cslot,
+                                                    const u32* __restrict__ wcand, u32* wtot,
+                                                    u64* __restrict__ skipbits, u64 nskipw) {
+  boundary_body(W0, meta, cslot, wcand, wtot, skipbits, nskipw);
+}
+
+// Fused steps of small merges (launch-bound): every block counts itself done and the
+// last one runs the next single-block step, after a device-scope fence each side (the
+// other blocks' writes are then visible to it); it also resets the counter, which the
+// plan's meta zero-fill started at 0.
+__device__ __forceinline__ bool walk_last_block(u32* ctr) {
+  __shared__ u32 last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(ctr, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!last) return false;
+  __threadfence();
+  if (threadIdx.x == 0) *ctr = 0u;
+  return true;
+}
 
 // One thread per window: its candidate slots -> cand[] at the window's offset
 // (woff = exclusive scan of wtot; the total is meta->n_cand).
@@ -336,11 +359,11 @@ __global__ void __launch_bounds__(BLOCK) k_cand_compact(WalkArgs W0, const u32* 
 #ifndef WALK_FUSED_MAXN
 #define WALK_FUSED_MAXN (1ll << 22)  // k_cluster_fused up to this many ops
 #endif
-template <typename Op>
+template <typename Op, int NT = S1_NT>
 __device__ __forceinline__ void scan1_block(const u32* __restrict__ in, u32* __restrict__ out, u64 n,
                                             u32* total_lo, u32* s) {
   u32 carry = Op::template identity<u32>();
-  for (u64 r0 = 0; r0 < n; r0 += S1_NT * 8) {
+  for (u64 r0 = 0; r0 < n; r0 += NT * 8) {
     const u64 b = r0 + threadIdx.x * 8;
     u32 v[8];
     u32 acc = Op::template identity<u32>();
@@ -350,7 +373,7 @@ __device__ __forceinline__ void scan1_block(const u32* __restrict__ in, u32* __r
       acc = Op::apply(acc, v[j]);
     }
     u32 tot;
-    u32 run = Op::apply(carry, block_excl_scan<Op, u32, S1_NT / WAVE>(acc, s, &tot));
+    u32 run = Op::apply(carry, block_excl_scan<Op, u32, NT / WAVE>(acc, s, &tot));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (b + j < n) out[b + j] = run;
@@ -372,22 +395,36 @@ __global__ void __launch_bounds__(S1_NT) k_scan1(const u32* __restrict__ in, u32
 #ifndef WALK_CC_FUSED_MAXW
 #define WALK_CC_FUSED_MAXW 4096
 #endif
-__global__ void __launch_bounds__(S1_NT) k_cand_scan_compact(WalkArgs W0, const u32* __restrict__ wtot,
-                                                             u32* __restrict__ woff, u64 cap, u32* total_lo,
-                                                             const u32* __restrict__ cslot, u32* __restrict__ out) {
-  __shared__ u32 s[S1_NT / WAVE + 1];
-  const WalkArgs W = walk_load(W0);
+template <int NT>
+__device__ __forceinline__ void cand_scan_compact_body(const WalkArgs& W, const u32* wtot, u32* woff, u64 cap,
+                                                       u32* total_lo, const u32* cslot, u32* out, u32* s) {
   const u64 nw = min(W.Wn, cap);
-  scan1_block<OpSum>(wtot, woff, nw, total_lo, s);
+  scan1_block<OpSum, NT>(wtot, woff, nw, total_lo, s);
   __syncthreads();  // (global writes of this block: visible to it after the barrier)
   if (W.fail) return;
   const u32 total = *total_lo;
-  for (u64 w = threadIdx.x; w < nw; w += S1_NT) {
+  for (u64 w = threadIdx.x; w < nw; w += NT) {
     const u32 o = woff[w];
     const u32 e = w + 1 < nw ? woff[w + 1] : total;
     const u64 Mb = W.wren[2 * w];
     for (u32 i = 0; o + i < e; ++i) out[o + i] = cslot[Mb + i];
   }
+}
+__global__ void __launch_bounds__(S1_NT) k_cand_scan_compact(WalkArgs W0, const u32* __restrict__ wtot,
+                                                             u32* __restrict__ woff, u64 cap, u32* total_lo,
+                                                             const u32* __restrict__ cslot, u32* __restrict__ out) {
+  __shared__ u32 s[S1_NT / WAVE + 1];
+  cand_scan_compact_body<S1_NT>(walk_load(W0), wtot, woff, cap, total_lo, cslot, out, s);
+}
+// k_boundary, then (its last block) k_cand_scan_compact: one launch
+__global__ void __launch_bounds__(BLOCK) k_boundary_cc(WalkArgs W0, ComposeMeta* meta, u32* cslot,
+                                                       const u32* __restrict__ wcand, u32* wtot,
+                                                       u64* __restrict__ skipbits, u64 nskipw, u32* woff, u64 cap,
+                                                       u32* total_lo, u32* cand) {
+  boundary_body(W0, meta, cslot, wcand, wtot, skipbits, nskipw);
+  if (!walk_last_block(&meta->wk_done[0])) return;
+  __shared__ u32 s[NWAVES + 1];
+  cand_scan_compact_body<BLOCK>(walk_load(W0), wtot, woff, cap, total_lo, cslot, cand, s);
 }
 
 // Incoming open region (sharded merge): the previous shards' walk ended with
@@ -423,8 +460,8 @@ __global__ void k_replay_in(WalkArgs W0, int in_ahead, u32 in_d, const i64* in_d
   }
 }
 
-__global__ void k_replay_q(WalkArgs W0, const u32* __restrict__ cand, const ComposeMeta* meta,
-                           u32* __restrict__ q, u32* __restrict__ nconf) {
+__device__ __forceinline__ void replay_q_body(WalkArgs W0, const u32* __restrict__ cand, const ComposeMeta* meta,
+                                              u32* q, u32* nconf) {
   const WalkArgs W = walk_load(W0);
   if (W.fail) return;
   const u64 nc = meta->n_cand;
@@ -442,6 +479,10 @@ __global__ void k_replay_q(WalkArgs W0, const u32* __restrict__ cand, const Comp
     }
     nconf[c] = k;
   }
+}
+__global__ void k_replay_q(WalkArgs W0, const u32* __restrict__ cand, const ComposeMeta* meta,
+                           u32* __restrict__ q, u32* __restrict__ nconf) {
+  replay_q_body(W0, cand, meta, q, nconf);
 }
 
 // Real region starts: the first candidate of each cluster (no earlier candidate's
@@ -481,19 +522,34 @@ __global__ void k_cluster(WalkArgs W0, const u32* __restrict__ cand, u32* __rest
 }
 // Small merges (launch-bound): k_scan1<OpMax> (pm), k_cluster and k_scan1<OpSum> (coff,
 // the conflict total) in one block, barriers between the phases.
+template <int NT>
+__device__ __forceinline__ void cluster_fused_body(WalkArgs W0, const u32* __restrict__ cand, u32* q, u32* pm,
+                                                   u32* nconf, const ComposeMeta* meta, u32* nreal, u32* coff,
+                                                   u64 cap, u32* total_lo, u32* s) {
+  const WalkArgs W = walk_load(W0);
+  const u64 nc = min(meta->n_cand, cap);
+  scan1_block<OpMax, NT>(q, pm, nc, nullptr, s);
+  __syncthreads();  // (global writes of this block: visible to it after the barrier)
+  if (!W.fail) cluster_walk(W, cand, q, pm, nconf, meta, nreal, threadIdx.x, NT);
+  __syncthreads();
+  scan1_block<OpSum, NT>(nreal, coff, W.fail ? 0 : nc, total_lo, s);
+}
 __global__ void __launch_bounds__(S1_NT) k_cluster_fused(WalkArgs W0, const u32* __restrict__ cand,
                                                          u32* __restrict__ q, u32* __restrict__ pm,
                                                          u32* __restrict__ nconf, const ComposeMeta* meta,
                                                          u32* __restrict__ nreal, u32* __restrict__ coff, u64 cap,
                                                          u32* total_lo) {
   __shared__ u32 s[S1_NT / WAVE + 1];
-  const WalkArgs W = walk_load(W0);
-  const u64 nc = min(meta->n_cand, cap);
-  scan1_block<OpMax>(q, pm, nc, nullptr, s);
-  __syncthreads();  // (global writes of this block: visible to it after the barrier)
-  if (!W.fail) cluster_walk(W, cand, q, pm, nconf, meta, nreal, threadIdx.x, S1_NT);
-  __syncthreads();
-  scan1_block<OpSum>(nreal, coff, W.fail ? 0 : nc, total_lo, s);
+  cluster_fused_body<S1_NT>(W0, cand, q, pm, nconf, meta, nreal, coff, cap, total_lo, s);
+}
+// k_replay_q, then (its last block) k_cluster_fused: one launch
+__global__ void __launch_bounds__(BLOCK) k_replay_q_cl(WalkArgs W0, const u32* __restrict__ cand, ComposeMeta* meta,
+                                                       u32* q, u32* nconf, u32* pm, u32* nreal, u32* coff, u64 cap,
+                                                       u32* total_lo) {
+  replay_q_body(W0, cand, meta, q, nconf);
+  if (!walk_last_block(&meta->wk_done[1])) return;
+  __shared__ u32 s[NWAVES + 1];
+  cluster_fused_body<BLOCK>(W0, cand, q, pm, nconf, meta, nreal, coff, cap, total_lo, s);
 }
 
 // Writes the conflict pairs, skip-list entries and skip bits of every real
