@@ -1748,6 +1748,9 @@ static int side_stream(hipStream_t caller, SideStream** out) {
 #ifndef SMX_TB_OVERLAP
 #define SMX_TB_OVERLAP 1
 #endif
+#ifndef SMX_TB_UNSKIP_MAXN
+#define SMX_TB_UNSKIP_MAXN (1 << 22)  // up to: k_tb_reduce reads the skip bits; above: k_tb_unskip
+#endif
 #ifndef SMX_TB_OVERLAP_MIN
 #define SMX_TB_OVERLAP_MIN (1 << 18)  // ops (config 2: 0.1746 -> 0.1724 ms with the overlap, profiles/r05_x/c2_overlap_ab.txt; graph replay makes the fork/join cheap)
 #endif
@@ -1796,7 +1799,8 @@ static int launch_tail(const Ctx& C) {
   TbArgs A = tb_args(C);
   A.width = (u32)width;
   A.nbk = (u32)nbk;
-  A.keep_skip = 1u;
+  // small merges: no k_tb_unskip launch, k_tb_reduce tests the skip bits of the renames
+  A.keep_skip = C.n <= SMX_TB_UNSKIP_MAXN ? 2u : 1u;
   u32* lst = C.ws<u32>(B_TBHIST);
   u32* rec = C.ws<u32>(B_REC);
   const int nblk = (int)SMX_CEIL_DIV((u64)C.n, (u64)TB_TILE);
@@ -1813,7 +1817,8 @@ static int launch_tail(const Ctx& C) {
   C.tm->end(ST_WALK);
   HIP_TRY(hipStreamWaitEvent(st, S->join, 0));
   C.tm->begin(ST_TABLES);
-  hipLaunchKernelGGL(k_tb_unskip, dim3(1024), dim3(BLOCK), 0, st, A, lst, rec, C.ws<u32>(B_SKIPLIST));
+  if (A.keep_skip == 1u)
+    hipLaunchKernelGGL(k_tb_unskip, dim3(1024), dim3(BLOCK), 0, st, A, lst, rec, C.ws<u32>(B_SKIPLIST));
   hipLaunchKernelGGL(k_tb_reduce, dim3(nbk), dim3(TBR_NT), 0, st, A, lst, rec, n_sym, C.ws<int4>(B_FIN),
                      PartTab{nullptr, 0u, 0, nullptr});
   HIP_TRY(hipGetLastError());

@@ -51,7 +51,8 @@ struct TbArgs {
   u32 nbk;          // buckets
   u32 smax;         // n_sym - 1 (clamp)
   u32 keep_skip;    // k_tb_scatter keeps every rename (it runs beside the walk; the
-                    // skipped renames' records are killed afterwards by k_tb_unskip)
+                    // skipped renames' records are killed afterwards by k_tb_unskip --
+                    // or, when 2, passed over by k_tb_reduce through the skip bits)
   u64 nMv, nR;      // filled on the device by tb_load
 };
 
@@ -280,7 +281,7 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
     if ((u64)(r1 - 1) < A.nMv) {
       if (q & REC_HAS_A) atomicMax(&tA[ls], r1);
       if (q & REC_HAS_F) atomicMax(&tF[ls], r1);
-    } else {
+    } else if (A.keep_skip != 2u || !tb_skipped(A, (u64)(r1 - 1) - A.nMv)) {
       atomicMax(&tC[ls], r1);
     }
   };
