@@ -68,3 +68,25 @@ def test_invalid_symbol_fails(plan):
     soa.sym[5] = soa.n_sym  # out of range
     with pytest.raises(Exception):
         compose_soa(soa)
+
+
+def test_verdict_word_sequence():
+    """Synchronous calls read the merge's verdict word (the last kernel's seq << 1 | bit in
+    pinned host memory) instead of the meta block: failures and successes of both plans,
+    interleaved on one thread, each see their own verdict."""
+    def soa_of(n, seed, bad=False):
+        soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(n, max(n // 20, 1), seed, mix=synth.ADVERSARIAL_MIX)))
+        if bad:
+            soa.sym[n // 2] = soa.n_sym
+        return soa
+
+    seq = [(300, False), (300, True), (1000, False), (5000, False), (5000, True), (700, False),
+           (5000, False), (2048, True), (2048, False)]
+    for i, (n, bad) in enumerate(seq):
+        soa = soa_of(n, 40 + i, bad)
+        if bad:
+            with pytest.raises(Exception):
+                compose_soa(soa)
+        else:
+            _eq(compose_soa(soa), oracle.compose(soa), f"step {i}: n={n}")
+            assert (DeviceCompose.last_plan() == "small") == (n <= 2048)
