@@ -88,6 +88,39 @@ PyObject* map_get(PyObject* m, PyObject* key, PyObject* dflt) {
   return PyObject_CallMethodObjArgs(m, N.get, key, dflt, nullptr);
 }
 
+// Whether instances of cls keep the fields `names` as plain instance-dict entries: the
+// generic attribute protocol (no __getattribute__ / __getattr__ / __setattr__
+// override) and no data descriptor of those names anywhere in the MRO.  Then
+// getattr(obj, name) is obj.__dict__[name] when present (else the class attribute),
+// and setattr is an instance-dict store.  Decided once per class.
+struct PlainFields {
+  std::vector<std::pair<PyTypeObject*, bool>> seen;
+  bool check(PyTypeObject* cls, PyObject* names) {
+    for (auto& e : seen)
+      if (e.first == cls) return e.second;
+    bool ok = cls->tp_getattro == PyObject_GenericGetAttr && cls->tp_setattro == PyObject_GenericSetAttr &&
+              cls->tp_dictoffset != 0;
+    for (Py_ssize_t i = 0; ok && i < PyTuple_GET_SIZE(names); ++i) {
+      PyObject* d = _PyType_Lookup(cls, PyTuple_GET_ITEM(names, i));  // (borrowed, no error)
+      if (d && Py_TYPE(d)->tp_descr_set) ok = false;
+    }
+    seen.emplace_back(cls, ok);
+    return ok;
+  }
+};
+
+// getattr(obj, name) for a PlainFields class: the instance dict's entry (borrowed) or,
+// when it has none, the generic lookup (new reference in *hold).
+PyObject* plain_get(PyObject* obj, PyObject* name, Ref& hold) {
+  PyObject** dp = _PyObject_GetDictPtr(obj);
+  if (dp && *dp && PyDict_CheckExact(*dp)) {
+    PyObject* v = PyDict_GetItemWithError(*dp, name);
+    if (v || PyErr_Occurred()) return v;
+  }
+  hold.reset(PyObject_GetAttr(obj, name));
+  return hold.p;
+}
+
 // ---------------------------------------------------------------- key encodings (marshal.py)
 
 // ISO-8601 "YYYY-MM-DDTHH:MM:SS[.fff]Z" -> int(YYYYMMDDhhmmss) * 2000 + (2*fff | 1999).
@@ -180,6 +213,24 @@ int packed_key(PyObject* s, uint64_t* hi, uint64_t* lo) {
   return 1;
 }
 
+// The int object of id i (borrowed): one per id for the module's lifetime, shared by
+// every call (the interners' dict values; no allocation per new value).
+PyObject* id_object(long long i) {
+  static std::vector<PyObject*> ids;
+  if (i < (long long)ids.size()) return ids[(size_t)i];
+  if (i >= (1ll << 26)) {  // (beyond 64M ids: no cache, the dict keeps its own reference)
+    static Ref last;
+    last.reset(PyLong_FromLongLong(i));
+    return last.p;
+  }
+  while ((long long)ids.size() <= i) {
+    PyObject* o = PyLong_FromLongLong((long long)ids.size());
+    if (!o) return nullptr;
+    ids.push_back(o);
+  }
+  return ids[(size_t)i];
+}
+
 struct Interner {  // value -> dense id, first-seen order
   PyObject* map = nullptr;
   PyObject* list = nullptr;  // optional: keeps the values in id order
@@ -195,8 +246,8 @@ struct Interner {  // value -> dense id, first-seen order
     if (got) return PyLong_AsLongLong(got);
     if (PyErr_Occurred()) return -1;
     const long long id = next++;
-    Ref v(PyLong_FromLongLong(id));
-    if (!v || PyDict_SetItem(map, key, v.p) < 0) return -1;
+    PyObject* v = id_object(id);
+    if (!v || PyDict_SetItem(map, key, v) < 0) return -1;
     if (list && PyList_Append(list, key) < 0) return -1;
     return id;
   }
@@ -231,6 +282,13 @@ struct Marshaler {
     *dst = (int32_t)id;
     return true;
   }
+  PlainFields plain;  // op / target classes whose fields are read from the instance dict
+  // getattr(o, name): the instance dict's entry on a PlainFields class (the same value)
+  PyObject* get(PyObject* o, PyObject* name, PyObject* names, Ref& hold) {
+    if (plain.check(Py_TYPE(o), names)) return plain_get(o, name, hold);
+    hold.reset(PyObject_GetAttr(o, name));
+    return hold.p;
+  }
   bool add(PyObject* op) {
     const size_t k = kind.size();
     kind.push_back(0);
@@ -241,35 +299,38 @@ struct Marshaler {
     v0.push_back(-1);
     v1.push_back(-1);
     // precedence.get(op.type, 99) (compose.py:18)
-    Ref type(PyObject_GetAttr(op, N.type));
+    Ref ht, hp, hi_, hg, hs, hpa;
+    PyObject* type = get(op, N.type, N.kw_op, ht);
     if (!type) return false;
-    PyObject* r = PyDict_GetItemWithError(kind_rank, type.p);
+    PyObject* r = PyDict_GetItemWithError(kind_rank, type);
     if (!r && PyErr_Occurred()) return false;
     const int kr = r ? (int)PyLong_AsLong(r) : unknown;
     kind[k] = (uint8_t)kr;
     // str(op.provenance.get("timestamp", "1970-01-01T00:00:00Z")) (compose.py:17)
-    Ref prov(PyObject_GetAttr(op, N.provenance));
+    PyObject* prov = get(op, N.provenance, N.kw_op, hp);
     if (!prov) return false;
-    Ref tso(map_get(prov.p, N.timestamp, default_ts));
+    Ref tso(map_get(prov, N.timestamp, default_ts));
     if (!tso) return false;
     Ref tss(PyObject_Str(tso.p));
     if (!tss || PyList_Append(ts_list.p, tss.p) < 0) return false;
     if (ts_ok && !iso_key(tss.p, &ts[k])) ts_ok = false;
     // op.id (compose.py:18)
-    Ref id(PyObject_GetAttr(op, N.id));
-    if (!id || PyList_Append(id_list.p, id.p) < 0) return false;
-    if (all_uuid && !uuid_key(id.p, &hi[k], &lo[k])) all_uuid = false;
+    PyObject* id = get(op, N.id, N.kw_op, hi_);
+    if (!id || PyList_Append(id_list.p, id) < 0) return false;
+    if (all_uuid && !uuid_key(id, &hi[k], &lo[k])) all_uuid = false;
     // target.symbolId: dict key / == (compose.py:33,64)
-    Ref tgt(PyObject_GetAttr(op, N.target));
+    PyObject* tgt = get(op, N.target, N.kw_op, hg);
     if (!tgt) return false;
-    Ref s(PyObject_GetAttr(tgt.p, N.symbolId));
+    PyObject* s = get(tgt, N.symbolId, N.kw_target, hs);
     if (!s) return false;
-    const long long si = syms(s.p);
+    const long long si = syms(s);
     if (si < 0) return false;
     sym[k] = (uint32_t)si;
     if (kr != kmove && kr != krename) return true;
-    Ref params(PyObject_GetAttr(op, N.params));
-    if (!params) return false;
+    PyObject* pp = get(op, N.params, N.kw_op, hpa);
+    if (!pp) return false;
+    Py_INCREF(pp);
+    Ref params(pp);
     if (kr == krename) {  // newName: '!=' class (compose.py:66) and str(newName) (compose.py:72)
       Ref name(map_get(params.p, N.newName, Py_None));
       if (!name) return false;
@@ -427,13 +488,25 @@ PyObject* copy_tree(PyObject* x, std::vector<PyObject*>& seen, bool* tree, int d
   return y.release();
 }
 
-PyObject* deep_copy(PyObject* x, PyObject* deepcopy) {
-  if (PyDict_CheckExact(x) && PyDict_GET_SIZE(x) == 0) return PyDict_New();
+// *fresh (when given): the copy is a native one -- a tree whose containers nothing else,
+// not even the copy itself, refers to -- rather than copy.deepcopy's.
+PyObject* deep_copy(PyObject* x, PyObject* deepcopy, bool* fresh = nullptr) {
+  if (fresh) *fresh = true;
+  if (PyDict_CheckExact(x)) {
+    if (PyDict_GET_SIZE(x) == 0) return PyDict_New();
+    // a flat dict of atoms (params / provenance as lift.ts writes them): one table copy
+    // (copy_tree's first test, without its bookkeeping)
+    Py_ssize_t pos = 0;
+    PyObject *key, *val;
+    bool flat = true;
+    while (flat && PyDict_Next(x, &pos, &key, &val)) flat = is_atom(key) && is_atom(val);
+    if (flat) return PyDict_Copy(x);
+  }
   std::vector<PyObject*> seen;
   bool tree = true;
   PyObject* y = copy_tree(x, seen, &tree, 0);
   if (y || tree) return y;  // copied, or a real error
-
+  if (fresh) *fresh = false;
   return PyObject_CallOneArg(deepcopy, x);
 }
 
@@ -462,6 +535,30 @@ struct Ctor {
     if (m < 0 && PyErr_Occurred()) return -1;
     seen.emplace_back(cls, m);
     return m;
+  }
+  // mode 1 on a PlainFields class: object.__new__, then the instance dict built at once
+  // (what one setattr per field in order leaves: the same keys in the same order)
+  PyObject* make_plain(PyTypeObject* cls, PyObject* const* args, PyObject* names) {
+    Ref obj(PyBaseObject_Type.tp_new(cls, N.empty, nullptr));
+    if (!obj) return nullptr;
+    PyObject** dp = _PyObject_GetDictPtr(obj.p);
+    if (!dp || *dp) return make_attrs(obj.release(), 1, args, names);
+    const Py_ssize_t nf = PyTuple_GET_SIZE(names);
+    Ref d(_PyDict_NewPresized(nf));
+    if (!d) return nullptr;
+    for (Py_ssize_t i = 0; i < nf; ++i)
+      if (PyDict_SetItem(d.p, PyTuple_GET_ITEM(names, i), args[i]) < 0) return nullptr;
+    *dp = d.release();
+    return obj.release();
+  }
+  PyObject* make_attrs(PyObject* o, int m, PyObject* const* args, PyObject* names) {
+    Ref obj(o);
+    for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(names); ++i) {
+      PyObject* nm = PyTuple_GET_ITEM(names, i);
+      const int rc = m == 1 ? PyObject_SetAttr(obj.p, nm, args[i]) : PyObject_GenericSetAttr(obj.p, nm, args[i]);
+      if (rc < 0) return nullptr;
+    }
+    return obj.release();
   }
   PyObject* make(PyTypeObject* cls, PyObject* const* args, PyObject* names) {
     const int m = mode(cls, names);
@@ -492,6 +589,67 @@ PyObject* make_target(Ctor& ctor, PyTypeObject* tcls, PyObject* sym, PyObject* a
   PyObject* a[2] = {sym, addr};
   return ctor.make(tcls, a, N.kw_target);
 }
+
+// Software prefetch of the object graph a clone reads, a few ops ahead in output order
+// (ops are visited in T order, i.e. in no relation to where they sit in memory: most
+// reads were cache misses).  Only reads what earlier stages already pulled in, and
+// only objects whose type is checked first; a prefetch never changes behaviour.
+inline void pf(const void* p) { __builtin_prefetch(p, 0, 3); }
+inline PyObject* inst_dict(PyObject* o) {
+  PyObject** dp = _PyObject_GetDictPtr(o);
+  return dp ? *dp : nullptr;
+}
+inline void pf_dict_tables(PyObject* d) {  // the dict's key and value tables
+  if (d && PyDict_CheckExact(d)) {
+    pf(((PyDictObject*)d)->ma_keys);
+    if (((PyDictObject*)d)->ma_values) pf(((PyDictObject*)d)->ma_values);
+  }
+}
+inline void pf_dict_values(PyObject* d) {  // ... and each value object
+  if (!d || !PyDict_CheckExact(d)) return;
+  Py_ssize_t pos = 0;
+  PyObject *k, *v;
+  while (PyDict_Next(d, &pos, &k, &v)) pf(v);
+}
+struct OpPrefetch {
+  PyObject* ops;
+  const int32_t* order;
+  Py_ssize_t m, n_ops;
+  PyObject* at(Py_ssize_t j) const {
+    if (j >= m) return nullptr;
+    const int32_t s = order[j];
+    return s >= 0 && s < n_ops ? PyList_GET_ITEM(ops, s) : nullptr;
+  }
+  void step(Py_ssize_t t) const {
+    if (PyObject* o = at(t + 24)) pf(o);
+    if (PyObject* o = at(t + 18)) pf(inst_dict(o));
+    if (PyObject* o = at(t + 12)) pf_dict_tables(inst_dict(o));
+    if (PyObject* o = at(t + 8)) pf_dict_values(inst_dict(o));  // the field objects
+    if (PyObject* o = at(t + 4)) {  // the fields' own tables; the target's dict
+      PyObject* d = inst_dict(o);
+      if (d && PyDict_CheckExact(d)) {
+        Py_ssize_t pos = 0;
+        PyObject *k, *v;
+        while (PyDict_Next(d, &pos, &k, &v)) {
+          if (PyDict_CheckExact(v)) pf_dict_tables(v);
+          else if (!PyUnicode_CheckExact(v) && !PyLong_CheckExact(v)) pf(inst_dict(v));
+        }
+      }
+    }
+    if (PyObject* o = at(t + 2)) {  // the fields' values; the target's tables
+      PyObject* d = inst_dict(o);
+      if (d && PyDict_CheckExact(d)) {
+        Py_ssize_t pos = 0;
+        PyObject *k, *v;
+        while (PyDict_Next(d, &pos, &k, &v)) {
+          if (PyDict_CheckExact(v)) pf_dict_values(v);
+          else if (!PyUnicode_CheckExact(v) && !PyLong_CheckExact(v)) pf_dict_tables(inst_dict(v));
+        }
+      }
+    }
+  }
+};
+
 
 // materialize_ops(ops, kind, strings, order, addr, file, ctx, kmove, krename, deepcopy, ctor_mode)
 // -> List[Op] (materialize.py; compose.py:30-49 on a compose.py:117-127 clone)
@@ -526,13 +684,79 @@ PyObject* materialize_ops(PyObject*, PyObject* args) {
 
   Ref out(PyList_New(m));
   if (!out) return nullptr;
+  PlainFields plain;
+  const OpPrefetch pfo{ops, order, m, n_ops};
   for (Py_ssize_t t = 0; t < m; ++t) {
+    pfo.step(t);
     const int32_t src = order[t];
     if (src < 0 || src >= n_ops) {
       PyErr_SetString(PyExc_IndexError, "source index out of range");
       return nullptr;
     }
     PyObject* op = PyList_GET_ITEM(ops, src);
+    // Fast path: a plain (non-frozen) dataclass Op over a plain dataclass Target, both
+    // with instance-dict fields (PlainFields).  The clone is then built already
+    // materialised -- the final target, the edited params -- which is what constructing
+    // it and then assigning its attributes (compose.py:30-49 on :117-127) leaves behind:
+    // the generated __init__ only stores its arguments.
+    {
+      PyTypeObject* ocls = Py_TYPE(op);
+      const int om = ctor.mode(ocls, N.kw_op);
+      if (om < 0) return nullptr;
+      if (om == 1 && plain.check(ocls, N.kw_op)) {
+        Ref h0, h1, h2, h3, h4, h5, h6, h7, h8, h9;
+        PyObject* tg = plain_get(op, N.target, h0);
+        if (!tg) return nullptr;
+        PyTypeObject* tcls = Py_TYPE(tg);
+        const int tm = ctor.mode(tcls, N.kw_target);
+        if (tm < 0) return nullptr;
+        if (tm >= 1 && plain.check(tcls, N.kw_target)) {
+          PyObject *id, *sv, *ty, *tsym, *taddr;
+          if (!(id = plain_get(op, N.id, h1)) || !(sv = plain_get(op, N.schemaVersion, h2)) ||
+              !(ty = plain_get(op, N.type, h3)) || !(tsym = plain_get(tg, N.symbolId, h4)) ||
+              !(taddr = plain_get(tg, N.addressId, h5)))
+            return nullptr;
+          const int k = kind[src];
+          const int32_t a = addr[t], f = file[t], c = ctx[t];
+          PyObject *sa = nullptr, *sf = nullptr, *sc = nullptr;
+          if ((a >= 0 && !(sa = str_at(a))) || (f >= 0 && !(sf = str_at(f))) || (c >= 0 && !(sc = str_at(c))))
+            return nullptr;
+          PyObject* ta[2] = {tsym, sa ? sa : taddr};
+          bool p_fresh = false;
+          Ref p, g, e, pr, ntgt(tm == 1 ? ctor.make_plain(tcls, ta, N.kw_target) : ctor.make(tcls, ta, N.kw_target));
+          if (!ntgt) return nullptr;
+          {
+            PyObject* x;
+            if (!(x = plain_get(op, N.params, h6)) || !(p.reset(deep_copy(x, deepcopy, &p_fresh)), p)) return nullptr;
+            if (!(x = plain_get(op, N.guards, h7)) || !(g.reset(deep_copy(x, deepcopy)), g)) return nullptr;
+            if (!(x = plain_get(op, N.effects, h8)) || !(e.reset(deep_copy(x, deepcopy)), e)) return nullptr;
+            if (!(x = plain_get(op, N.provenance, h9)) || !(pr.reset(deep_copy(x, deepcopy)), pr)) return nullptr;
+          }
+          if (k == kmove) {
+            if (sa && PyObject_SetItem(p.p, N.newAddress, sa) < 0) return nullptr;
+            if (sf && PyObject_SetItem(p.p, N.newFile, sf) < 0) return nullptr;
+          }
+          if (k == krename && sf &&
+              (PyObject_SetItem(p.p, N.newFile, sf) < 0 || PyObject_SetItem(p.p, N.file, sf) < 0))
+            return nullptr;
+          if (sc && k != krename) {  // {**params, "renameContext": ...}: a fresh dict
+            if (p_fresh && PyDict_CheckExact(p.p)) {  // (a native copy: referred to from nowhere else)
+              if (PyDict_SetItem(p.p, N.renameContext, sc) < 0) return nullptr;
+            } else {
+              Ref nd(PyDict_New());
+              if (!nd || PyDict_Update(nd.p, p.p) < 0 || PyDict_SetItem(nd.p, N.renameContext, sc) < 0)
+                return nullptr;
+              p.reset(nd.release());
+            }
+          }
+          PyObject* a8[8] = {id, sv, ty, ntgt.p, p.p, g.p, e.p, pr.p};
+          PyObject* clone = ctor.make_plain(ocls, a8, N.kw_op);
+          if (!clone) return nullptr;
+          PyList_SET_ITEM(out.p, t, clone);
+          continue;
+        }
+      }
+    }
     Ref tgt(PyObject_GetAttr(op, N.target));
     if (!tgt) return nullptr;
     PyTypeObject* tcls = Py_TYPE(tgt.p);
