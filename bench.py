@@ -325,8 +325,7 @@ def main() -> None:
         run = dc.run
         log(f"[rank {rank}] resident on {dev}; workspace {dc.ws_bytes / 2**30:.2f} GiB")
 
-    # a stream of its own (not the null stream): smx_compose replays its asynchronous
-    # part as a HIP graph from the second merge on (smx_compose.hip compose_async_graph)
+    # a stream of its own (not the null stream)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     lib = _lib.lib()
@@ -407,8 +406,7 @@ def main() -> None:
         else:
             async_api = {"status": "plan needed the synchronous fallback"}
 
-    # The same merges with the timers off (what a caller gets: direct launches; the
-    # library's own graph replay, SMX_GRAPH, is off by default since round 5).
+    # The same merges with the timers off (what a caller gets: direct launches).
     graph_api = None
     if not sharded and world == 1 and not args.no_async:
         for _ in range(2):

@@ -20,13 +20,8 @@
  * workspace (the library's side stream and fork/join events are kept per caller
  * stream; tests/test_gpu_async.py runs two threads on one GPU).
  *
- * Graph cache: the second smx_compose / smx_compose_async with the same (stream,
- * inputs, outputs, workspace) captures the merge's launches into a HIP graph that
- * later calls replay.  The library keeps the stream handle only as part of that key:
- * it never synchronizes the caller's stream after a call returns (eviction waits on
- * an event of its own), so the stream may be destroyed at any time.
- * smx_release_graphs(stream) (NULL: every stream) drops the cached graphs, e.g.
- * before freeing the buffers they were captured with.
+ * The library keeps no handle to the caller's stream after a call returns, so the
+ * stream may be destroyed at any time.
  *
  * Return value: 0 on success, a negative SMX_E* code otherwise; the message is
  * available from smx_last_error() (thread-local).  Nothing aborts the process.
@@ -124,7 +119,8 @@ int smx_compose_async(const smx_ops* ops, const smx_compose_out* out, void* work
 int smx_compose_finish(const smx_ops* ops, const smx_compose_out* out, void* workspace,
                        size_t workspace_bytes, void* stream);
 
-/* Drop the library's cached merge graphs of `stream` (NULL: of every stream). */
+/* Kept for callers of rounds 3-5 (which cached merge graphs per stream): the library
+ * caches none now; returns SMX_OK. */
 int smx_release_graphs(void* stream);
 
 /* The order plan the last composition on this thread ran (bench reporting). */

@@ -774,6 +774,9 @@ __device__ __forceinline__ void cscan_small_body(u32* __restrict__ cnt, i64 na, 
 #ifndef SMX_FPART_CS
 #define SMX_FPART_CS 1  // small merges: k_fpart and k_cscan_small in one launch
 #endif
+#ifndef SMX_CSCAN_LB
+#define SMX_CSCAN_LB 0  // large merges: k_fpart and a single-pass look-back column scan in one launch
+#endif
 __global__ void __launch_bounds__(BLOCK) k_cscan_small(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
                                                        ComposeMeta* meta, u64 nwin) {
   __shared__ u32 s[NWAVES + 1];
@@ -790,6 +793,115 @@ __global__ void __launch_bounds__(BLOCK) k_fpart_cscan(const u64* __restrict__ t
   __shared__ u32 s[NWAVES + 1];
   if ((i64)blockIdx.x < nfp) fpart_body(ts, tsB, sA, sB, na, nb, W, tgt, D, bnd, meta, long_host, blockIdx.x, nfp);
   else cscan_small_body(cnt, na, nb, CM, meta, (u64)W, (int)(blockIdx.x - nfp), s);
+}
+
+// Large merges: the chunk-column scans of k_cscan_up / mid / down (three launches) as one
+// single-pass scan with decoupled look-back (tiles of CS_TILE chunks), in the same launch
+// as k_fpart (both read only k_khist's outputs).  Scan blocks take tickets in column-major
+// (column, tile) order, so a tile only ever waits on tiles that took earlier tickets and
+// are resident or done; each tile publishes its sum (AGG), adds the sums of the tiles
+// before it until one that published its inclusive prefix (INC), then publishes its own.
+// lb[0] is the ticket counter, lb[1 + col * NTL + tile] the status words (zeroed with the
+// meta at the plan's start).
+#define CSL_AGG (1ull << 62)
+#define CSL_INC (2ull << 62)
+#define CSL_VAL 0xffffffffull
+__device__ __forceinline__ void cscan_finish_col(u32* colp, i64 C, int side, int k, u64 total, ComposeMeta* meta,
+                                                 u64 nwin) {
+  colp[C] = (u32)total;  // prefix at the end of the branch (a window may start there)
+  atomicAdd((unsigned long long*)&meta->kcnt[k], (unsigned long long)total);
+  if (k == KREN) meta->n_ren_side[side] = total;
+  __threadfence();
+  if (atomicAdd((unsigned long long*)&meta->cs_done, 1ull) == (unsigned long long)(2 * SMX_N_KINDS - 1)) {
+    __threadfence();
+    meta->n_win = nwin;
+    u64 acc = 0;
+    for (int kk = 0; kk < SMX_N_KINDS; ++kk) {
+      meta->base[kk] = acc;
+      acc += __hip_atomic_load(&meta->kcnt[kk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    meta->base[SMX_N_KINDS] = acc;
+  }
+}
+__device__ __forceinline__ void cscan_lb_body(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM, i64 NTL,
+                                              u64* __restrict__ lb, ComposeMeta* meta, u64 nwin, u32* s,
+                                              u32* sh) {
+  if (threadIdx.x == 0) sh[0] = (u32)atomicAdd((unsigned long long*)&lb[0], 1ull);
+  __syncthreads();
+  const i64 tk = sh[0];
+  const int col = (int)(tk / NTL);
+  const i64 t = tk % NTL;
+  if (col >= 2 * SMX_N_KINDS) return;
+  const int side = col / SMX_N_KINDS, k = col % SMX_N_KINDS;
+  const i64 C = SMX_CEIL_DIV(side ? nb : na, (i64)CH);
+  const i64 ntc = C > 0 ? SMX_CEIL_DIV(C, (i64)CS_TILE) : 1;  // tiles of this column
+  if (t >= ntc) return;
+  u32* colp = cnt + (i64)col * CM;
+  if (!cs_present(meta, col)) {  // an all-zero column: its prefixes are its counts
+    if (t == 0 && threadIdx.x == 0) cscan_finish_col(colp, C, side, k, 0, meta, nwin);
+    return;
+  }
+  const i64 b = t * CS_TILE + (i64)threadIdx.x * 8;
+  u32 v[8];
+  u32 acc = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    v[j] = b + j < C ? colp[b + j] : 0u;
+    acc += v[j];
+  }
+  u32 tot;
+  u32 run = block_excl_scan<OpSum, u32>(acc, s, &tot);
+  if (threadIdx.x < WAVE) {  // wave 0: the look-back, 64 predecessors a step
+    const int lane = threadIdx.x;
+    u64* st = lb + 1 + (i64)col * NTL;
+    // (relaxed read-modify-writes at device scope: the status word carries all it tells,
+    // and release / acquire ordering would write back and invalidate the XCD's L2 each time)
+    if (t > 0 && lane == 0) (void)atomicExch((unsigned long long*)&st[t], (unsigned long long)(CSL_AGG | tot));
+    u32 prefix = 0;
+    for (i64 q = t - 1; q >= 0;) {  // tiles q, q - 1, ... in lanes 0, 1, ... (before the column: INC 0)
+      const i64 i = q - lane;
+      const u64 x = i >= 0 ? (u64)atomicOr((unsigned long long*)&st[i], 0ull) : CSL_INC;
+      const u64 inc = __ballot((x & CSL_INC) != 0), none = __ballot((x & (CSL_INC | CSL_AGG)) == 0);
+      const int f = inc ? __ffsll((unsigned long long)inc) - 1 : WAVE - 1;  // the nearest INC (or the window's end)
+      const u64 upto = f == WAVE - 1 ? ~0ull : (2ull << f) - 1;
+      if (none & upto) continue;  // a tile up to there has not published yet: read again
+      const u32 sum = (u32)__builtin_amdgcn_readlane((int)wave_incl_sum_u32(lane <= f ? (u32)(x & CSL_VAL) : 0u),
+                                                      WAVE - 1);
+      prefix += sum;
+      if (inc) break;
+      q -= WAVE;
+    }
+    if (lane == 0) {
+      (void)atomicExch((unsigned long long*)&st[t], (unsigned long long)(CSL_INC | (u64)(prefix + tot)));
+      sh[1] = prefix;
+      if (t == ntc - 1) cscan_finish_col(colp, C, side, k, (u64)prefix + tot, meta, nwin);
+    }
+  }
+  __syncthreads();
+  run += sh[1];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (b + j < C) colp[b + j] = run;
+    run += v[j];
+  }
+}
+__global__ void __launch_bounds__(BLOCK) k_fpart_cslb(const u64* __restrict__ ts, const u64* __restrict__ tsB,
+                                                      const u64* __restrict__ sA, const u64* __restrict__ sB, i64 na,
+                                                      i64 nb, i64 W, i64 tgt, i64 D, i64* __restrict__ bnd,
+                                                      ComposeMeta* meta, u32* long_host, u32* __restrict__ cnt,
+                                                      i64 CM, i64 NTL, u64* __restrict__ lb, i64 nfp) {
+  __shared__ u32 s[NWAVES + 1];
+  __shared__ u32 sh[2];
+  if ((i64)blockIdx.x < nfp) fpart_body(ts, tsB, sA, sB, na, nb, W, tgt, D, bnd, meta, long_host, blockIdx.x, nfp);
+  else cscan_lb_body(cnt, na, nb, CM, NTL, lb, meta, (u64)W, s, sh);
+}
+
+// k_zero over two ranges in one launch (the meta and the look-back scan's status words)
+__global__ void k_zero2(u32* __restrict__ p, u64 nw, u32* __restrict__ q, u64 nq) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nw + nq; i += (u64)gridDim.x * blockDim.x) {
+    if (i < nw) p[i] = 0u;
+    else q[i - nw] = 0u;
+  }
 }
 
 // Per-window counts: each kind and renames per branch (+ moves with a None value
@@ -1372,7 +1484,7 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_TBHIST] = (size_t)(TB_MAXBK + 1) * SMX_CEIL_DIV(nn, (i64)TB_TILE) * 4;  // k_tb_scatter's lst
   sz[B_CCNT] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)256) + 2) * 4;
   sz[B_SMP] = (size_t)(SMX_CEIL_DIV(nn, (i64)CH) + 4) * 8;
-  sz[B_TSUM] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)CH * CS_TILE) + 2) * 4;
+  sz[B_TSUM] = (size_t)(2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)CH * CS_TILE) + 2) + 1) * 8;  // (u32 tile sums, or the look-back scan's u64 status words)
   Layout L{};
   size_t acc = 0;
   for (int i = 0; i < B_N; ++i) {
@@ -1738,8 +1850,16 @@ static int side_stream(hipStream_t caller, SideStream** out) {
   } else {
     HIP_TRY(hipStreamCreateWithFlags(&S->s, hipStreamNonBlocking));
   }
-  HIP_TRY(hipEventCreateWithFlags(&S->fork, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&S->join, hipEventDisableTiming));
+  // (device-scope events: both streams are on this device.  A default event's record
+  // also fences at system scope -- an L2 write-back the next kernel on the recording
+  // stream waits behind: ~11 us before k_boundary and ~6 us before the reduce on config 3,
+  // profiles/r06_c/c3_timeline.txt)
+#ifndef SMX_SIDE_SYSFENCE
+#define SMX_SIDE_SYSFENCE 0
+#endif
+  const unsigned evf = hipEventDisableTiming | (SMX_SIDE_SYSFENCE ? 0u : hipEventDisableSystemFence);
+  HIP_TRY(hipEventCreateWithFlags(&S->fork, evf));
+  HIP_TRY(hipEventCreateWithFlags(&S->join, evf));
   g_side[g_nside++] = S;
   *out = S;
   return SMX_OK;
@@ -1906,16 +2026,26 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
   i64* bnd = C.ws<i64>(B_BND);
   C.tm->begin(ST_PLAN);
   static_assert(sizeof(ComposeMeta) % 4 == 0, "meta is zeroed by words");
-  {
-    const int rc = zero_async(meta, sizeof(ComposeMeta), st);
-    if (rc) return rc;
-  }
   if (tgt < WIN_TGT_MIN) tgt = WIN_TGT_MIN;
   const i64 cap = level_cap(level);
   if (tgt > cap) tgt = cap;
   tgt -= tgt % CH;  // chunk-aligned diagonals (k_fpart's sampled first level)
   const i64 W = SMX_CEIL_DIV(C.n, tgt);
   const i64 CM = SMX_CEIL_DIV(C.na > C.nb ? C.na : C.nb, (i64)CH) + 1;
+  // the column scan: one block per column (small merges, with k_fpart), a single-pass
+  // look-back scan with k_fpart (SMX_CSCAN_LB), or k_cscan_up / mid / down
+  const bool cs_small = CM <= CS_SMALL_CM;
+  const bool cs_lb = SMX_CSCAN_LB && !cs_small;
+  const i64 NTL = SMX_CEIL_DIV(CM, (i64)CS_TILE);
+  u64* lb = C.ws<u64>(B_TSUM);  // (the look-back scan's ticket and status words)
+  if (cs_lb) {
+    hipLaunchKernelGGL(k_zero2, dim3(8), dim3(BLOCK), 0, st, (u32*)meta, (u64)(sizeof(ComposeMeta) / 4), (u32*)lb,
+                       (u64)(1 + 2 * SMX_N_KINDS * NTL) * 2);
+    HIP_TRY(hipGetLastError());
+  } else {
+    const int rc = zero_async(meta, sizeof(ComposeMeta), st);
+    if (rc) return rc;
+  }
   const i64 nchunk = SMX_CEIL_DIV(C.na, (i64)CH) + SMX_CEIL_DIV(C.nb, (i64)CH);
   u32* ccnt = C.ws<u32>(B_CCNT);
   u64* sA = C.ws<u64>(B_SMP);
@@ -1939,8 +2069,12 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
                        early ? early->flag_dev : nullptr);
   }
   const i64 nfp = SMX_CEIL_DIV(W + 1, (i64)BLOCK);
-  const bool fused = SMX_FPART_CS && CM <= CS_SMALL_CM && !early;
-  if (fused)
+  const bool fused = SMX_FPART_CS && cs_small && !early;
+  if (cs_lb)
+    hipLaunchKernelGGL(k_fpart_cslb, dim3(nfp + 2 * SMX_N_KINDS * NTL), dim3(BLOCK), 0, st, C.ops->ts,
+                       C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na, C.nb, W, tgt, cap / CH, bnd, meta,
+                       early ? early->flag_dev : nullptr, ccnt, CM, NTL, lb, nfp);
+  else if (fused)
     hipLaunchKernelGGL(k_fpart_cscan, dim3(nfp + 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, C.ops->ts,
                        C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na, C.nb, W, tgt, cap / CH, bnd, meta,
                        (u32*)nullptr, ccnt, CM, nfp);
@@ -1948,9 +2082,9 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
     hipLaunchKernelGGL(k_fpart, dim3(nfp), dim3(BLOCK), 0, st, C.ops->ts, C.ops->ts + C.na + C.ops->b_gap, sA, sB,
                        C.na, C.nb, W, tgt, cap / CH, bnd, meta, early ? early->flag_dev : nullptr);
   if (early) HIP_TRY(hipEventRecord(early->ev, st));
-  if (fused) {
-    // (k_fpart_cscan scanned the columns)
-  } else if (CM <= CS_SMALL_CM) {
+  if (fused || cs_lb) {
+    // (k_fpart_cscan / k_fpart_cslb scanned the columns)
+  } else if (cs_small) {
     hipLaunchKernelGGL(k_cscan_small, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, meta, (u64)W);
   } else {
     const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);
@@ -2610,7 +2744,9 @@ static int early_fail_of(int dev, EarlyFail* e) {
     if (Slot& s = slots[i]; s.dev < 0) {
       HIP_TRY(hipHostMalloc((void**)&s.e.flag_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
       HIP_TRY(hipHostGetDevicePointer((void**)&s.e.flag_dev, s.e.flag_host, 0));
-      HIP_TRY(hipEventCreateWithFlags(&s.e.ev, hipEventDisableTiming));
+      // (no system-scope fence: k_khist / k_fpart store the flag itself at system scope,
+      // and a missed flag only costs the tail launched behind a plan that then fails)
+      HIP_TRY(hipEventCreateWithFlags(&s.e.ev, hipEventDisableTiming | (SMX_SIDE_SYSFENCE ? 0u : hipEventDisableSystemFence)));
       s.dev = dev;
       *e = s.e;
       return SMX_OK;
@@ -2651,14 +2787,20 @@ struct EarlyVerdict {
 
 struct SmallRec {  // one per host thread, freed when the thread exits
   u64* h = nullptr;
-  u64* d = nullptr;
+  u64* d = nullptr;  // its device address as the device `dev` sees it
+  int dev = -1;
   u64 seq = 0;
   ~SmallRec() {
     if (h) (void)hipHostFree(h);
   }
 };
+// The thread's verdict word: pinned, mapped, portable host memory.  Its device address is
+// taken on the device current at the call and taken again when a later call runs on
+// another device (no reliance on one address serving every device).
 static SmallRec* small_rec() {
   static thread_local SmallRec r;
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return nullptr;
   if (!r.h) {
     if (hipHostMalloc((void**)&r.h, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) !=
         hipSuccess) {
@@ -2666,11 +2808,15 @@ static SmallRec* small_rec() {
       return nullptr;
     }
     *(volatile u64*)r.h = 0;
+  }
+  if (r.dev != cur) {
     if (hipHostGetDevicePointer((void**)&r.d, r.h, 0) != hipSuccess) {
-      (void)hipHostFree(r.h);
-      r.h = nullptr;
-      return nullptr;
+      (void)hipGetLastError();
+      r.d = nullptr;
+      r.dev = -1;
+      return nullptr;  // (the caller then reads the meta block instead)
     }
+    r.dev = cur;
   }
   return &r;
 }
@@ -2732,134 +2878,15 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
   return SMX_OK;
 }
 
-// The asynchronous part of a merge is ~25 launches whose arguments depend only on the
-// sizes and the buffers, never on the data: on a (non-null) stream, the second merge
-// with the same (stream, ops, outputs, workspace) captures it into a HIP graph that
-// this and later merges replay -- one launch instead of ~25 (the host launch cost the
-// per-merge sync would otherwise expose; a one-off merge never pays for a capture).
-// Not inside a caller's own capture, and not while the stage timers are on: event
-// timestamps recorded by a replayed graph read back as 0 ms on this ROCm
-// (profiles/r03_i/bench.json: every stage 0.0), so timed merges enqueue directly.
-#ifndef SMX_GRAPH
-#define SMX_GRAPH 0  // off: on this ROCm the replay is slower than enqueueing the launches
-                     // (timers off: config 2 0.183 -> 0.160 ms, config 3 2.381 -> 2.352 ms
-                     // without it, profiles/r05_x/graph_ab.txt): the first kernel waits for the
-                     // whole graph's submission, while direct launches start the GPU at once
-#endif
-#define GRAPH_CACHE 8
-struct GraphEntry {
-  hipStream_t st = nullptr;
-  int dev = -1;
-  smx_ops ops{};
-  smx_compose_out out{};
-  void* ws = nullptr;
-  size_t ws_bytes = 0;
-  hipGraphExec_t exec = nullptr;
-  hipGraph_t graph = nullptr;  // kept while exec lives: on this ROCm an exec replays
-                               // node parameters its graph owns (destroying the graph
-                               // after instantiation corrupted the later replays)
-  hipEvent_t done = nullptr;   // recorded behind every replay: eviction waits on it, never
-                               // on the caller's stream (which may be gone by then, or in
-                               // the middle of the caller's own capture)
-  u64 used = 0;
-  bool nograph = false;        // capturing this key failed: enqueue directly
-};
-static std::mutex g_graph_mu;
-static GraphEntry g_graph[GRAPH_CACHE];
-static u64 g_graph_tick = 0;
-
-static void graph_release_locked(GraphEntry& e) {
-  if (e.exec) {
-    if (e.done) (void)hipEventSynchronize(e.done);  // its last replay finishes first
-    (void)hipGraphExecDestroy(e.exec);
-    if (e.graph) (void)hipGraphDestroy(e.graph);
-  }
-  if (e.done) (void)hipEventDestroy(e.done);
-  e = GraphEntry{};
-}
-
-static bool graph_key_eq(const GraphEntry& g, hipStream_t st, int dev, const smx_ops* ops,
-                         const smx_compose_out* out, void* ws, size_t ws_bytes) {
-  return g.used && g.st == st && g.dev == dev && g.ws == ws && g.ws_bytes == ws_bytes &&
-         std::memcmp(&g.ops, ops, sizeof(smx_ops)) == 0 && std::memcmp(&g.out, out, sizeof(smx_compose_out)) == 0;
-}
-
-static int compose_async_graph(const smx_ops* ops, const smx_compose_out* out, void* ws, size_t ws_bytes,
-                               const Layout& L, hipStream_t st, bool* done) {
-  *done = false;
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  HIP_TRY(hipStreamIsCapturing(st, &cs));
-  if (cs != hipStreamCaptureStatusNone) return SMX_OK;  // the caller is capturing: plain enqueue
-  std::lock_guard<std::mutex> g(g_graph_mu);  // (per-entry state: held through the launch)
-  GraphEntry* ent = nullptr;
-  for (auto& e : g_graph)
-    if (graph_key_eq(e, st, dev, ops, out, ws, ws_bytes)) ent = &e;
-  if (!ent) {  // first sight of this key: remember it, enqueue directly
-    ent = &g_graph[0];
-    for (auto& e : g_graph)
-      if (!e.used || (ent->used && e.used < ent->used)) ent = &e;
-    graph_release_locked(*ent);  // the least recently used one, if the cache is full
-    ent->st = st;
-    ent->dev = dev;
-    ent->ops = *ops;
-    ent->out = *out;
-    ent->ws = ws;
-    ent->ws_bytes = ws_bytes;
-    ent->used = ++g_graph_tick;
-    return SMX_OK;
-  }
-  if (ent->nograph) return SMX_OK;
-  if (!ent->exec) {  // seen before: capture
-    if (n_side_needed(ops)) {  // the table scatter's side stream exists before the capture
-      SideStream* S = nullptr;
-      int rc = side_stream(st, &S);
-      if (rc) return rc;
-    }
-    hipGraph_t graph = nullptr;
-    if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-      (void)hipGetLastError();
-      ent->nograph = true;  // a graph is an optimisation only: the plain path runs
-      return SMX_OK;
-    }
-    const int rc = enqueue_async(ops, out, ws, L, st, false);
-    const hipError_t ce = hipStreamEndCapture(st, &graph);
-    hipGraphExec_t exec = nullptr;
-    hipError_t ie = hipErrorUnknown;
-    if (!rc && ce == hipSuccess && graph) ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    if (rc || ce != hipSuccess || ie != hipSuccess) {
-      if (exec) (void)hipGraphExecDestroy(exec);
-      if (graph) (void)hipGraphDestroy(graph);
-      if (rc) return rc;
-      (void)hipGetLastError();
-      ent->nograph = true;  // a graph is an optimisation only: the plain path runs
-      return SMX_OK;
-    }
-    if (hipEventCreateWithFlags(&ent->done, hipEventDisableTiming) != hipSuccess) {
-      (void)hipGraphExecDestroy(exec);
-      (void)hipGraphDestroy(graph);
-      (void)hipGetLastError();
-      ent->done = nullptr;
-      ent->nograph = true;
-      return SMX_OK;
-    }
-    ent->exec = exec;
-    ent->graph = graph;
-  }
-  ent->used = ++g_graph_tick;
-  HIP_TRY(hipGraphLaunch(ent->exec, st));
-  HIP_TRY(hipEventRecord(ent->done, st));
-  *done = true;
-  return SMX_OK;
-}
-
-// Drop the cached graphs of one stream (all of them for a null stream): each waits
-// for its last replay through the library's own event.
+// The library once replayed a merge's ~25 launches as one cached HIP graph from the second
+// merge of a (stream, buffers) key on.  On this ROCm the replay measured slower than
+// enqueueing the launches (config 2 0.183 -> 0.160 ms, config 3 2.381 -> 2.352 ms without
+// it, profiles/r05_x/graph_ab.txt: the graph's first kernel waits for the whole
+// submission), so the cache was removed in round 6; a caller's own capture of
+// smx_compose_async stays supported (tests/test_gpu_async.py).  smx_release_graphs is
+// kept in the ABI and releases nothing.
 extern "C" int smx_release_graphs(void* stream) {
-  std::lock_guard<std::mutex> g(g_graph_mu);
-  for (auto& e : g_graph)
-    if (e.used && (stream == nullptr || e.st == (hipStream_t)stream)) graph_release_locked(e);
+  (void)stream;
   return SMX_OK;
 }
 
@@ -2877,22 +2904,10 @@ static int compose_async_impl(const smx_ops* ops, const smx_compose_out* out, vo
     return SMX_OK;
   }
   const bool timed = profiling_on() != 0;
-  if (SMX_GRAPH && !small && st != nullptr && !timed && !knob("SMX_NO_GRAPH", 0)) {
-    bool done = false;
-    if ((rc = compose_async_graph(ops, out, ws, ws_bytes, L, st, &done))) return rc;
-    if (done) return SMX_OK;
-  }
   EarlyVerdict ev;
   if (verdict) ev = *verdict;  // (the caller's verdict word, if any)
   if ((rc = enqueue_async(ops, out, ws, L, st, timed, early_ok, &ev))) return rc;
   if (verdict) *verdict = ev;
-  if (ev.failed && SMX_GRAPH && st != nullptr) {  // a graph of a plan that fails is not worth capturing
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> g(g_graph_mu);
-    for (auto& e : g_graph)
-      if (graph_key_eq(e, st, dev, ops, out, ws, ws_bytes) && !e.exec) e.nograph = true;
-  }
   return SMX_OK;
 }
 

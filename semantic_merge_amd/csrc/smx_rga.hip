@@ -15,6 +15,7 @@
 // persistent, in LDS): value groups by hashing, one sequential replay per group,
 // survivors ordered by (anchor, t, author, opid, index) -> compaction, each list's
 // output offset summed by its own wave from per-chunk survivor sums.
+#include <algorithm>
 #include <chrono>
 #include <string>
 
@@ -1590,18 +1591,33 @@ extern "C" int smx_rga_workspace_bytes(int64_t n_ops, int64_t n_lists, size_t* b
 // Host wait for a stream: a short spin on hipStreamQuery, then the blocking sync.  A call
 // ends within a millisecond, and a blocking sync wakes the calling thread ~10-20 us after
 // the stream's last packet: 10M events 0.520 -> 0.502 ms, grouped 0.297 -> 0.287 ms
-// (profiles/r05_x/spin_ab.txt; RGA_SPIN_US 0: block at once).
+// (profiles/r05_x/spin_ab.txt).  The spin is adaptive per calling thread: twice the
+// previous call's wait, between RGA_SPIN_MIN_US and RGA_SPIN_US (a long batch, or many
+// caller threads, no longer burn a core for a fixed 20 ms; RGA_SPIN_US 0: block at once).
 #ifndef RGA_SPIN_US
-#define RGA_SPIN_US 20000
+#define RGA_SPIN_US 2000
+#endif
+#ifndef RGA_SPIN_MIN_US
+#define RGA_SPIN_MIN_US 200
 #endif
 static hipError_t stream_wait(hipStream_t st) {
+  static thread_local long long last_us = RGA_SPIN_US / 2;  // this thread's previous wait
   if (RGA_SPIN_US > 0) {
+    const long long budget = std::min<long long>(RGA_SPIN_US, std::max<long long>(RGA_SPIN_MIN_US, 2 * last_us));
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
       const hipError_t e = hipStreamQuery(st);
-      if (e != hipErrorNotReady) return e;
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(RGA_SPIN_US)) break;
+      const long long us =
+          std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+      if (e != hipErrorNotReady) {
+        last_us = us;
+        return e;
+      }
+      if (us > budget) break;
     }
+    const hipError_t e = hipStreamSynchronize(st);
+    last_us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    return e;
   }
   return hipStreamSynchronize(st);
 }

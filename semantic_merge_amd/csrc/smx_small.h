@@ -484,6 +484,49 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
       max16(hw + 2 * SMALL_HT, slot_r[i], (u32)T + 1u);
     }
   }
+  // The moves' inclusive prefixes (compose.py:73-82), only when a move has a None value:
+  // one wave walks the move block in T order, 64 moves a step.  A move's last earlier
+  // non-None writer of its symbol is the highest earlier lane of the step with its slot
+  // and a value (peers ballots), else the slot's running writer; the step's last writer
+  // per slot then becomes the running one.  O(moves / 64) steps, whatever the values.
+  u16* pwa = posA;  // by T: T' + 1 of the move's prefix addr / file writer (0: none);
+  u16* pwf = posB;  // (posA / posB are dead after the walk)
+  u16* la = reinterpret_cast<u16*>(sn);  // by slot: the running writers (sn is dead after
+  u16* lf = la + SMALL_HT;               // the walk; klo is not: hw's third table lies in it)
+  static_assert(2 * SMALL_HT * 2 <= SMALL_N * 8, "running writers in sn");
+  bool none_here = false;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int T = t + SMALL_NT * i;
+    if (T < nmv) none_here |= (sv0[ord[T]] < 0) | (sv1[ord[T]] < 0);
+  }
+  const bool any_none = __syncthreads_or(none_here);  // (also orders the last-writer maxes)
+  if (any_none) {
+    for (int i = t; i < SMALL_HT; i += SMALL_NT) la[i] = lf[i] = 0;
+    __syncthreads();
+    if (w == 0) {
+      const u64 lt = lanemask_lt();
+      for (int c0 = 0; c0 < nmv; c0 += WAVE) {
+        const int T = c0 + lane;
+        const bool v = T < nmv;
+        const u32 e = v ? ord[T] : 0u;
+        const int h = v ? slot_of(ssym[e], false) : 0;  // (every move inserted its slot)
+        const bool ha = v && sv0[e] >= 0, hf = v && sv1[e] >= 0;
+        const u64 peers = wave_peers_n((u32)h, v, 12);
+        const u64 pa = __ballot(ha) & peers, pf = __ballot(hf) & peers;
+        const u32 ra = v ? la[h] : 0u, rf = v ? lf[h] : 0u;  // (read before the step's updates)
+        if (v) {
+          pwa[T] = (u16)((pa & lt) ? (u32)(c0 + 63 - __clzll(pa & lt)) + 1u : ra);
+          pwf[T] = (u16)((pf & lt) ? (u32)(c0 + 63 - __clzll(pf & lt)) + 1u : rf);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (ha && (pa >> lane) == 1ull) la[h] = (u16)(T + 1);
+        if (hf && (pf >> lane) == 1ull) lf[h] = (u16)(T + 1);
+        wave_lds_sync();
+      }
+    }
+    __syncthreads();
+  }
   // skips before each T (renames only): exclusive scan of the skip flags, IT per thread
   u32 sk[IT];
   acc = 0;
@@ -511,12 +554,8 @@ __global__ void __launch_bounds__(SMALL_NT) k_compose_small(smx_ops ops, smx_com
       // non-None one (compose.py:73-82 then 37-41)
       a = sv0[e];
       f = sv1[e];
-      for (int q = T - 1; q >= 0 && (a < 0 || f < 0); --q) {
-        const u32 eq = ord[q];
-        if (ssym[eq] != s) continue;
-        if (a < 0 && sv0[eq] >= 0) a = sv0[eq];
-        if (f < 0 && sv1[eq] >= 0) f = sv1[eq];
-      }
+      if (a < 0 && pwa[T]) a = sv0[ord[pwa[T] - 1]];  // (any_none: a None value was seen)
+      if (f < 0 && pwf[T]) f = sv1[ord[pwf[T] - 1]];
     } else {
       const int h = slot_of(s, false);
       if (h >= 0) {

@@ -79,11 +79,11 @@ def test_long_groups_fail_before_the_tail():
     """>= 4M ops whose timestamp groups (8192 ops) no 2048-op presorted window holds:
     k_khist flags the plan; the synchronous merge launches no tail behind it and takes
     the wide presorted windows, the asynchronous one reports -2 and finish runs them.  Both equal the oracle,
-    and so do repeated merges of the same buffers (no graph is captured for them)."""
+    and so do repeated merges of the same buffers."""
     soa = _lift(4_300_000, 3_000, 19, ops_per_ms=4096, mix=synth.ADVERSARIAL_MIX)
     dc = _lib.DeviceCompose(soa)
-    s = dc.torch.cuda.Stream()  # a non-null stream: the library's graph cache sees the key
-    for rep in range(3):  # first sight of the key, then the calls a graph would serve
+    s = dc.torch.cuda.Stream()  # a non-null stream
+    for rep in range(3):  # repeated merges of the same buffers
         dc.order.fill_(-7)
         dc.torch.cuda.synchronize()
         dc.run(stream=s)
@@ -163,10 +163,11 @@ def test_two_threads_compose_concurrently():
                 assert np.array_equal(g, r), f"thread {t} merge {k}: {name}"
 
 
-def test_graph_replay_reads_current_inputs():
-    """smx_compose on a non-null stream replays a HIP graph from the second merge with the
-    same buffers on: every replay recomputes from the inputs as they are at launch --
-    new data in the same buffers (same sizes) gives that data's composition."""
+def test_repeated_merges_read_current_inputs():
+    """Repeated smx_compose calls on the same buffers (a non-null stream) recompute from
+    the inputs as they are at launch -- new data in the same buffers (same sizes) gives
+    that data's composition (nothing is cached between calls; the library's graph replay
+    of round 3-5 was removed in round 6)."""
     import torch
     spec = synth.LiftSpec(600_000, 4_000, 31)
     soas = [synth.lift_soa(synth.lift_logs(synth.LiftSpec(**{**spec.__dict__, "seed": sd}))) for sd in (31, 32, 33)]
@@ -185,15 +186,14 @@ def test_graph_replay_reads_current_inputs():
 
 
 def test_stage_timers_time_every_merge():
-    """With the stage timers on, merges enqueue directly (no graph replay: a replayed
-    graph's event timestamps read back as 0 ms) and every merge's stages get a time;
-    with the timers off again the merge goes back to the graph replay."""
+    """With the stage timers on every merge's stages get a time, and merges with the
+    timers off again still equal the oracle."""
     import torch
     soa = _lift(300_000, 3_000, 34)
     dc = _lib.DeviceCompose(soa)
     s = torch.cuda.Stream()
     L = _lib.lib()
-    for _ in range(3):  # the key is seen, captured and replayed before the timed merges
+    for _ in range(3):  # untimed merges before the timed ones
         dc.run(s)
     s.synchronize()
     L.smx_set_profiling(1)
@@ -210,4 +210,4 @@ def test_stage_timers_time_every_merge():
     _check(dc, soa, "timed merges")
     dc.run(s)
     s.synchronize()
-    _check(dc, soa, "graph replay after the timed merges")
+    _check(dc, soa, "untimed merge after the timed merges")

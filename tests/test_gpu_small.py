@@ -90,3 +90,23 @@ def test_verdict_word_sequence():
         else:
             _eq(compose_soa(soa), oracle.compose(soa), f"step {i}: n={n}")
             assert (DeviceCompose.last_plan() == "small") == (n <= 2048)
+
+
+@pytest.mark.parametrize("shape", ["file_none", "addr_none", "mixed", "one_symbol"])
+def test_none_valued_moves(plan, shape):
+    """Moves whose newAddress or newFile is None see their symbol's inclusive prefix of
+    non-None values (compose.py:73-82): whole histories without a file, without an address,
+    None values mixed in, and one symbol whose ~500 moves chain through every step of the
+    small plan's prefix pass (was a backwards scan per move)."""
+    spec = synth.LiftSpec(2048, 1 if shape == "one_symbol" else 64, 21, ops_per_ms=3)
+    soa = synth.lift_soa(synth.lift_logs(spec))
+    rng = np.random.default_rng(5)
+    mv = np.flatnonzero(soa.kind == synth.KIND_RANK["moveDecl"])
+    if shape == "file_none":
+        soa.v1[mv[soa.sym[mv] % 2 == 0]] = -1  # half the symbols never have a file
+    elif shape == "addr_none":
+        soa.v0[mv[soa.sym[mv] % 3 == 0]] = -1
+    else:
+        soa.v0[mv[rng.random(len(mv)) < 0.6]] = -1
+        soa.v1[mv[rng.random(len(mv)) < 0.6]] = -1
+    _eq(compose_soa(soa), oracle.compose(soa), f"{plan} {shape}")

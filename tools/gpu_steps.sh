@@ -59,6 +59,8 @@ for s in "$@"; do
         tail -1 "$O/bench_c2.json" | cut -c1-400;;
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o p -- python3 "$R/bench.py" --steps 8 --warmup 2 --no-cpu-baseline --no-pmc --no-e2e > "$O/prof.log" 2>&1) || { echo "prof failed"; tail -20 "$O/prof.log"; exit 1; }
           python3 tools/prof_export.py "$O/prof" "$O/kernel_stats.csv" && head -8 "$O/kernel_stats.csv";;
+    c3tl) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/c3tl" -o p -- python3 "$R/bench.py" --steps 4 --warmup 2 --no-cpu-baseline --no-pmc --no-e2e --no-breakdown --no-async > "$O/c3tl.log" 2>&1) || { echo "c3tl failed"; tail -20 "$O/c3tl.log"; exit 1; }
+          python3 tools/prof_timeline.py "$O/c3tl" 60 > "$O/c3_timeline.txt" && tail -62 "$O/c3_timeline.txt";;
     sq) run 600 sq.log bash tools/pmc_sq.sh "$O/sq"
         tail -3 "$O/sq.log";;
     *) echo "unknown step $s"; exit 2;;
