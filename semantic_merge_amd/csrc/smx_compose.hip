@@ -774,9 +774,6 @@ __device__ __forceinline__ void cscan_small_body(u32* __restrict__ cnt, i64 na, 
 #ifndef SMX_FPART_CS
 #define SMX_FPART_CS 1  // small merges: k_fpart and k_cscan_small in one launch
 #endif
-#ifndef SMX_CSCAN_LB
-#define SMX_CSCAN_LB 0  // large merges: k_fpart and a single-pass look-back column scan in one launch
-#endif
 __global__ void __launch_bounds__(BLOCK) k_cscan_small(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
                                                        ComposeMeta* meta, u64 nwin) {
   __shared__ u32 s[NWAVES + 1];
@@ -793,115 +790,6 @@ __global__ void __launch_bounds__(BLOCK) k_fpart_cscan(const u64* __restrict__ t
   __shared__ u32 s[NWAVES + 1];
   if ((i64)blockIdx.x < nfp) fpart_body(ts, tsB, sA, sB, na, nb, W, tgt, D, bnd, meta, long_host, blockIdx.x, nfp);
   else cscan_small_body(cnt, na, nb, CM, meta, (u64)W, (int)(blockIdx.x - nfp), s);
-}
-
-// Large merges: the chunk-column scans of k_cscan_up / mid / down (three launches) as one
-// single-pass scan with decoupled look-back (tiles of CS_TILE chunks), in the same launch
-// as k_fpart (both read only k_khist's outputs).  Scan blocks take tickets in column-major
-// (column, tile) order, so a tile only ever waits on tiles that took earlier tickets and
-// are resident or done; each tile publishes its sum (AGG), adds the sums of the tiles
-// before it until one that published its inclusive prefix (INC), then publishes its own.
-// lb[0] is the ticket counter, lb[1 + col * NTL + tile] the status words (zeroed with the
-// meta at the plan's start).
-#define CSL_AGG (1ull << 62)
-#define CSL_INC (2ull << 62)
-#define CSL_VAL 0xffffffffull
-__device__ __forceinline__ void cscan_finish_col(u32* colp, i64 C, int side, int k, u64 total, ComposeMeta* meta,
-                                                 u64 nwin) {
-  colp[C] = (u32)total;  // prefix at the end of the branch (a window may start there)
-  atomicAdd((unsigned long long*)&meta->kcnt[k], (unsigned long long)total);
-  if (k == KREN) meta->n_ren_side[side] = total;
-  __threadfence();
-  if (atomicAdd((unsigned long long*)&meta->cs_done, 1ull) == (unsigned long long)(2 * SMX_N_KINDS - 1)) {
-    __threadfence();
-    meta->n_win = nwin;
-    u64 acc = 0;
-    for (int kk = 0; kk < SMX_N_KINDS; ++kk) {
-      meta->base[kk] = acc;
-      acc += __hip_atomic_load(&meta->kcnt[kk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    meta->base[SMX_N_KINDS] = acc;
-  }
-}
-__device__ __forceinline__ void cscan_lb_body(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM, i64 NTL,
-                                              u64* __restrict__ lb, ComposeMeta* meta, u64 nwin, u32* s,
-                                              u32* sh) {
-  if (threadIdx.x == 0) sh[0] = (u32)atomicAdd((unsigned long long*)&lb[0], 1ull);
-  __syncthreads();
-  const i64 tk = sh[0];
-  const int col = (int)(tk / NTL);
-  const i64 t = tk % NTL;
-  if (col >= 2 * SMX_N_KINDS) return;
-  const int side = col / SMX_N_KINDS, k = col % SMX_N_KINDS;
-  const i64 C = SMX_CEIL_DIV(side ? nb : na, (i64)CH);
-  const i64 ntc = C > 0 ? SMX_CEIL_DIV(C, (i64)CS_TILE) : 1;  // tiles of this column
-  if (t >= ntc) return;
-  u32* colp = cnt + (i64)col * CM;
-  if (!cs_present(meta, col)) {  // an all-zero column: its prefixes are its counts
-    if (t == 0 && threadIdx.x == 0) cscan_finish_col(colp, C, side, k, 0, meta, nwin);
-    return;
-  }
-  const i64 b = t * CS_TILE + (i64)threadIdx.x * 8;
-  u32 v[8];
-  u32 acc = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    v[j] = b + j < C ? colp[b + j] : 0u;
-    acc += v[j];
-  }
-  u32 tot;
-  u32 run = block_excl_scan<OpSum, u32>(acc, s, &tot);
-  if (threadIdx.x < WAVE) {  // wave 0: the look-back, 64 predecessors a step
-    const int lane = threadIdx.x;
-    u64* st = lb + 1 + (i64)col * NTL;
-    // (relaxed read-modify-writes at device scope: the status word carries all it tells,
-    // and release / acquire ordering would write back and invalidate the XCD's L2 each time)
-    if (t > 0 && lane == 0) (void)atomicExch((unsigned long long*)&st[t], (unsigned long long)(CSL_AGG | tot));
-    u32 prefix = 0;
-    for (i64 q = t - 1; q >= 0;) {  // tiles q, q - 1, ... in lanes 0, 1, ... (before the column: INC 0)
-      const i64 i = q - lane;
-      const u64 x = i >= 0 ? (u64)atomicOr((unsigned long long*)&st[i], 0ull) : CSL_INC;
-      const u64 inc = __ballot((x & CSL_INC) != 0), none = __ballot((x & (CSL_INC | CSL_AGG)) == 0);
-      const int f = inc ? __ffsll((unsigned long long)inc) - 1 : WAVE - 1;  // the nearest INC (or the window's end)
-      const u64 upto = f == WAVE - 1 ? ~0ull : (2ull << f) - 1;
-      if (none & upto) continue;  // a tile up to there has not published yet: read again
-      const u32 sum = (u32)__builtin_amdgcn_readlane((int)wave_incl_sum_u32(lane <= f ? (u32)(x & CSL_VAL) : 0u),
-                                                      WAVE - 1);
-      prefix += sum;
-      if (inc) break;
-      q -= WAVE;
-    }
-    if (lane == 0) {
-      (void)atomicExch((unsigned long long*)&st[t], (unsigned long long)(CSL_INC | (u64)(prefix + tot)));
-      sh[1] = prefix;
-      if (t == ntc - 1) cscan_finish_col(colp, C, side, k, (u64)prefix + tot, meta, nwin);
-    }
-  }
-  __syncthreads();
-  run += sh[1];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (b + j < C) colp[b + j] = run;
-    run += v[j];
-  }
-}
-__global__ void __launch_bounds__(BLOCK) k_fpart_cslb(const u64* __restrict__ ts, const u64* __restrict__ tsB,
-                                                      const u64* __restrict__ sA, const u64* __restrict__ sB, i64 na,
-                                                      i64 nb, i64 W, i64 tgt, i64 D, i64* __restrict__ bnd,
-                                                      ComposeMeta* meta, u32* long_host, u32* __restrict__ cnt,
-                                                      i64 CM, i64 NTL, u64* __restrict__ lb, i64 nfp) {
-  __shared__ u32 s[NWAVES + 1];
-  __shared__ u32 sh[2];
-  if ((i64)blockIdx.x < nfp) fpart_body(ts, tsB, sA, sB, na, nb, W, tgt, D, bnd, meta, long_host, blockIdx.x, nfp);
-  else cscan_lb_body(cnt, na, nb, CM, NTL, lb, meta, (u64)W, s, sh);
-}
-
-// k_zero over two ranges in one launch (the meta and the look-back scan's status words)
-__global__ void k_zero2(u32* __restrict__ p, u64 nw, u32* __restrict__ q, u64 nq) {
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nw + nq; i += (u64)gridDim.x * blockDim.x) {
-    if (i < nw) p[i] = 0u;
-    else q[i - nw] = 0u;
-  }
 }
 
 // Per-window counts: each kind and renames per branch (+ moves with a None value
@@ -1484,7 +1372,7 @@ static Layout layout(i64 na, i64 nb, i64 n_sym) {
   sz[B_TBHIST] = (size_t)(TB_MAXBK + 1) * SMX_CEIL_DIV(nn, (i64)TB_TILE) * 4;  // k_tb_scatter's lst
   sz[B_CCNT] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)256) + 2) * 4;
   sz[B_SMP] = (size_t)(SMX_CEIL_DIV(nn, (i64)CH) + 4) * 8;
-  sz[B_TSUM] = (size_t)(2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)CH * CS_TILE) + 2) + 1) * 8;  // (u32 tile sums, or the look-back scan's u64 status words)
+  sz[B_TSUM] = (size_t)2 * SMX_N_KINDS * (SMX_CEIL_DIV(nn, (i64)CH * CS_TILE) + 2) * 4;
   Layout L{};
   size_t acc = 0;
   for (int i = 0; i < B_N; ++i) {
@@ -2032,17 +1920,10 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
   tgt -= tgt % CH;  // chunk-aligned diagonals (k_fpart's sampled first level)
   const i64 W = SMX_CEIL_DIV(C.n, tgt);
   const i64 CM = SMX_CEIL_DIV(C.na > C.nb ? C.na : C.nb, (i64)CH) + 1;
-  // the column scan: one block per column (small merges, with k_fpart), a single-pass
-  // look-back scan with k_fpart (SMX_CSCAN_LB), or k_cscan_up / mid / down
+  // (a single-pass look-back column scan fused with k_fpart measured slower on config 3:
+  // plan 0.133 -> 0.157 ms -- the blocks' tickets and status round trips, profiles/r06)
   const bool cs_small = CM <= CS_SMALL_CM;
-  const bool cs_lb = SMX_CSCAN_LB && !cs_small;
-  const i64 NTL = SMX_CEIL_DIV(CM, (i64)CS_TILE);
-  u64* lb = C.ws<u64>(B_TSUM);  // (the look-back scan's ticket and status words)
-  if (cs_lb) {
-    hipLaunchKernelGGL(k_zero2, dim3(8), dim3(BLOCK), 0, st, (u32*)meta, (u64)(sizeof(ComposeMeta) / 4), (u32*)lb,
-                       (u64)(1 + 2 * SMX_N_KINDS * NTL) * 2);
-    HIP_TRY(hipGetLastError());
-  } else {
+  {
     const int rc = zero_async(meta, sizeof(ComposeMeta), st);
     if (rc) return rc;
   }
@@ -2070,11 +1951,7 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
   }
   const i64 nfp = SMX_CEIL_DIV(W + 1, (i64)BLOCK);
   const bool fused = SMX_FPART_CS && cs_small && !early;
-  if (cs_lb)
-    hipLaunchKernelGGL(k_fpart_cslb, dim3(nfp + 2 * SMX_N_KINDS * NTL), dim3(BLOCK), 0, st, C.ops->ts,
-                       C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na, C.nb, W, tgt, cap / CH, bnd, meta,
-                       early ? early->flag_dev : nullptr, ccnt, CM, NTL, lb, nfp);
-  else if (fused)
+  if (fused)
     hipLaunchKernelGGL(k_fpart_cscan, dim3(nfp + 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, C.ops->ts,
                        C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na, C.nb, W, tgt, cap / CH, bnd, meta,
                        (u32*)nullptr, ccnt, CM, nfp);
@@ -2082,8 +1959,8 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
     hipLaunchKernelGGL(k_fpart, dim3(nfp), dim3(BLOCK), 0, st, C.ops->ts, C.ops->ts + C.na + C.ops->b_gap, sA, sB,
                        C.na, C.nb, W, tgt, cap / CH, bnd, meta, early ? early->flag_dev : nullptr);
   if (early) HIP_TRY(hipEventRecord(early->ev, st));
-  if (fused || cs_lb) {
-    // (k_fpart_cscan / k_fpart_cslb scanned the columns)
+  if (fused) {
+    // (k_fpart_cscan scanned the columns)
   } else if (cs_small) {
     hipLaunchKernelGGL(k_cscan_small, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, meta, (u64)W);
   } else {
