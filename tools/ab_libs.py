@@ -37,6 +37,15 @@ def main():
     for item in a.libs:
         name, path = item.split("=", 1)
         libs.append((name, _abi.declare(C.CDLL(os.path.abspath(path)))))
+    # one workspace large enough for every build (their layouts may differ)
+    need = 0
+    for _, L in libs:
+        ws = C.c_size_t(0)
+        assert L.smx_compose_workspace_bytes(soa.n_a, soa.n_b, soa.n_sym, C.byref(ws)) == 0
+        need = max(need, ws.value)
+    if need > dc.ws_bytes:
+        dc.ws = torch.empty(need, dtype=torch.uint8, device=dc.device)
+        dc.ws_bytes = need
     ref = None
     if a.verify:
         from oracle import oracle
