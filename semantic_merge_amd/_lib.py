@@ -136,6 +136,7 @@ class ComposeSession:
     `last` holds the host / device split of the last merge in seconds."""
 
     _IN = (("kind", 1), ("ts", 8), ("oid_hi", 8), ("oid_lo", 8), ("sym", 4), ("v0", 4), ("v1", 4))
+    ASYNC_MAX = 1 << 22  # smx_compose_async + one sync below this many ops (SMX_EARLY_MIN)
 
     def __init__(self, device: str = "cuda") -> None:
         self.torch = _torch()
@@ -191,13 +192,27 @@ class ComposeSession:
                           ptrs["oid_lo"], ptrs["sym"], ptrs["v0"], ptrs["v1"])
         cnt_off = 4 * q + _al(8 * ccap)
         out = _abi.SmxComposeOut(o0, o0 + q, o0 + 2 * q, o0 + 3 * q, o0 + 4 * q, ccap, o0 + cnt_off)
-        check(lib().smx_compose(C.byref(ops), C.byref(out), self.ws.data_ptr(), ws.value, stream.cuda_stream))
-        with torch.cuda.stream(stream):
-            self.h_out[:cnt_off + 16].copy_(self.d_out[:cnt_off + 16], non_blocking=True)
-        stream.synchronize()
-        t2 = time.perf_counter()
+        args = (C.byref(ops), C.byref(out), self.ws.data_ptr(), ws.value, stream.cuda_stream)
         hout = self.h_out.numpy()
-        k, nc = (int(x) for x in hout[cnt_off: cnt_off + 16].view(np.int64))
+
+        def copy_back():
+            with torch.cuda.stream(stream):
+                self.h_out[:cnt_off + 16].copy_(self.d_out[:cnt_off + 16], non_blocking=True)
+            stream.synchronize()
+            return (int(x) for x in hout[cnt_off: cnt_off + 16].view(np.int64))
+        if n < self.ASYNC_MAX:
+            # merges below the early-verdict size: the asynchronous part, the copy back and
+            # ONE stream sync; smx_compose_finish only when the counts ask for it (a plan
+            # that failed, None-valued moves: counts[0] < -1)
+            check(lib().smx_compose_async(*args))
+            k, nc = copy_back()
+            if k < -1:
+                check(lib().smx_compose_finish(*args))
+                k, nc = copy_back()
+        else:  # (larger: the synchronous call, which waits for the plan's early verdict)
+            check(lib().smx_compose(*args))
+            k, nc = copy_back()
+        t2 = time.perf_counter()
         if k < 0:
             raise SmxError(-1, "invalid input: sym >= n_sym or kind >= 18")
         if nc > ccap:

@@ -95,7 +95,7 @@ static hipEvent_t ev_acquire() {
   hipEvent_t e = nullptr;
   // timing only (read after the caller's sync): no system-scope fence, whose cache
   // write-back and invalidate at every record cost the timed merges ~40 us on config 3
-  // (2.380 ms with the stage timers on against 2.342 ms off, profiles/r05_final2)
+  // (2.380 ms with the stage timers on against 2.342 ms off, measured in round 5)
   (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   return e;
 }
@@ -382,7 +382,7 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 #endif
 #define CH_PER_BLOCK (KH_NT / 16)   // 16 lanes x 16 kind bytes per 256-op chunk
 #ifndef KH_BF
-#define KH_BF 0                    // branch-free byte counting: plan 0.134 -> 0.137 ms (profiles/r04_k); off
+#define KH_BF 0                    // branch-free byte counting: plan 0.134 -> 0.137 ms (round 4); off
 #endif
 #ifndef KH_R
 #define KH_R 1                     // chunk rounds per block (4 measured slower: profiles/r02_k/khist_rounds_ab.txt)
@@ -1020,7 +1020,7 @@ struct EmitArgs {
 // final-state table from L2.  The output stores are plain: an output range starts
 // anywhere (after the skipped renames), so its first and last lines are shared with
 // the neighbouring waves, and non-temporal partial-line stores measured 1.4-1.8x
-// slower than plain ones (tools/_build variants, profiles/r02_*).
+// slower than plain ones (tools/_build variants, round 2).
 #if SMX_EMIT_NT
 #define NTLD(p) __builtin_nontemporal_load(p)
 #else
@@ -1538,7 +1538,7 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
                        (const i64*)sh->in_state_dev, meta, C.out->conflicts, (u64)C.out->conflict_cap, skiplist,
                        skipbits);
   // (one k_scan1 block over the window counts measured slower on config 3: walk 0.165 ->
-  // 0.185 ms, profiles/r03_w; small merges are launch-bound: one block)
+  // 0.185 ms, round 3; small merges are launch-bound: one block)
   if (lb_cc) {
     // (k_boundary_cc's last block did the scan and the compaction)
   } else if (Wmax <= WALK_CC_FUSED_MAXW) {
@@ -1741,7 +1741,7 @@ static int side_stream(hipStream_t caller, SideStream** out) {
   // (device-scope events: both streams are on this device.  A default event's record
   // also fences at system scope -- an L2 write-back the next kernel on the recording
   // stream waits behind: ~11 us before k_boundary and ~6 us before the reduce on config 3,
-  // profiles/r06_c/c3_timeline.txt)
+  // profiles/r06/c3_timeline_start.txt)
 #ifndef SMX_SIDE_SYSFENCE
 #define SMX_SIDE_SYSFENCE 0
 #endif

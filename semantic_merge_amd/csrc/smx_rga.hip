@@ -318,7 +318,7 @@ __global__ void __launch_bounds__(RR_NT) k_rrec_scatter(smx_rga_ops o, const u32
 #define RGA_OUT_PRE 2
 #endif
 #ifndef RGA_OUT_LPW
-#define RGA_OUT_LPW 1  // lists per wave in k_rga_out_fused (4: 28.8 us either way, profiles/r04_aj)
+#define RGA_OUT_LPW 1  // lists per wave in k_rga_out_fused (4: 28.8 us either way, round 4)
 #endif
 // err word bits: RGA_E_INPUT a list id >= n_lists or an op > 2 (the call fails);
 // RGA_E_UNGROUPED a call that said its events come grouped by list (SMX_RGA_GROUPED) has a
@@ -1726,7 +1726,7 @@ static int rga_impl(const smx_rga_ops* ops, const smx_rga_out* out, void* ws, si
                        scnt, tomb, (const i32*)err);
   // lists of more than RW_CAP events (a few, if any).  (On a second stream beside
   // k_rga_wave they measured no faster: their workgroups trail k_rga_wave's, and the
-  // join costs ~14 us, profiles/r04_s.)
+  // join costs ~14 us, round 4.)
   hipLaunchKernelGGL(k_rga_wave2, dim3(64), dim3(WAVE * RW_WAVES), 0, st, o, rec, lstart, n, nl, def2, ndef + 1,
                      tmp_v, tmp_s, scnt, tomb, (const i32*)err, (int)direct);
   hipLaunchKernelGGL(k_rga_big, dim3(RGA_BIG_GRID), dim3(1024), 0, st, o, rec, lstart, n, nl, def2, ndef + 1, bst, gp, tmp_v,

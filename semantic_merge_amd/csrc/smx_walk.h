@@ -134,7 +134,7 @@ __device__ u32 walk_rank_next(const WalkArgs& W, int o, u64 x) {
 // sources are read per step, all in flight together (the scan usually ends within a
 // step: the branches' renames interleave), instead of one dependent load per position.
 #ifndef WALK_NEXT_VEC
-#define WALK_NEXT_VEC 1  // 8: config 3 walk 0.145 -> 0.163 ms, config 2 0.046 -> 0.052 ms (profiles/r04_j); off
+#define WALK_NEXT_VEC 1  // 8: config 3 walk 0.145 -> 0.163 ms, config 2 0.046 -> 0.052 ms (round 4); off
 #endif
 __device__ __forceinline__ u32 walk_next(const WalkArgs& W, int o, u64 from) {
   u64 m = from;

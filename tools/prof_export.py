@@ -1,6 +1,6 @@
 """Export the per-kernel summary of a rocprofv3 --kernel-trace --stats database to CSV.
 
-    python tools/prof_export.py gpurun_out/prof4 profiles/r01_v5/kernel_stats.csv
+    python tools/prof_export.py gpurun_out/prof4 profiles/r06_final/kernel_stats.csv
 """
 import csv
 import glob
