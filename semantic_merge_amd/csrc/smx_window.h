@@ -331,7 +331,7 @@ __device__ __forceinline__ void win_rename_flags(const WinArgs& P, i64 w, u64 Mb
 #define WF_BOUNDS __launch_bounds__(WF_NT, WF_MINB)
 #endif
 template <int CAP, int NT, bool DBG, bool MAP, bool RUNS = false>
-__global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : WF_MINB) k_window_f(WinArgs P) {
+__global__ void __launch_bounds__(NT, CAP > WF_CAP ? 4 : WF_MINB) k_window_f(WinArgs P) {
   // CAP ops per window on NT threads: (2048, 512) four windows per CU; (8192, 1024) one
   // window per CU for logs whose equal-timestamp groups need it (config 5)
   constexpr int ITEMS = CAP / NT, NCH = CAP / WAVE, WAVES = NT / WAVE, KP = (2 * CH + NT - 1) / NT;
