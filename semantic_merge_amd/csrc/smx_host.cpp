@@ -164,7 +164,19 @@ int hexval(unsigned char ch) {
   return -1;
 }
 
-// Canonical lowercase UUID (exact str) -> 128-bit value.
+// lowercase hex digit value, or 0x80 (any other byte)
+struct HexTable {
+  uint8_t v[256];
+  constexpr HexTable() : v() {
+    for (int i = 0; i < 256; ++i) v[i] = 0x80;
+    for (int i = 0; i < 10; ++i) v['0' + i] = (uint8_t)i;
+    for (int i = 0; i < 6; ++i) v['a' + i] = (uint8_t)(10 + i);
+  }
+};
+constexpr HexTable kHex{};
+
+// Canonical lowercase UUID (exact str) -> 128-bit value.  Table-driven and branch-free
+// over the 32 digits (a per-character branch chain measured ~0.3 us per id).
 bool uuid_key(PyObject* s, uint64_t* hi, uint64_t* lo) {
   if (!PyUnicode_CheckExact(s)) return false;
   if (PyUnicode_READY(s) < 0) {
@@ -173,19 +185,23 @@ bool uuid_key(PyObject* s, uint64_t* hi, uint64_t* lo) {
   }
   if (PyUnicode_KIND(s) != PyUnicode_1BYTE_KIND || PyUnicode_GET_LENGTH(s) != 36) return false;
   const unsigned char* c = PyUnicode_1BYTE_DATA(s);
+  if ((c[8] != '-') | (c[13] != '-') | (c[18] != '-') | (c[23] != '-')) return false;
+  // digit positions: 0-7, 9-12, 14-17 (hi); 19-22, 24-35 (lo)
+  static constexpr uint8_t pos[32] = {0,  1,  2,  3,  4,  5,  6,  7,  9,  10, 11, 12, 14, 15, 16, 17,
+                                      19, 20, 21, 22, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35};
   uint64_t h = 0, l = 0;
-  int nd = 0;
-  for (int i = 0; i < 36; ++i) {
-    if (i == 8 || i == 13 || i == 18 || i == 23) {
-      if (c[i] != '-') return false;
-      continue;
-    }
-    const int v = hexval(c[i]);
-    if (v < 0) return false;
-    if (nd < 16) h = (h << 4) | (uint64_t)v;
-    else l = (l << 4) | (uint64_t)v;
-    ++nd;
+  uint8_t bad = 0;
+  for (int i = 0; i < 16; ++i) {
+    const uint8_t v = kHex.v[c[pos[i]]];
+    bad |= v;
+    h = (h << 4) | (v & 15u);
   }
+  for (int i = 16; i < 32; ++i) {
+    const uint8_t v = kHex.v[c[pos[i]]];
+    bad |= v;
+    l = (l << 4) | (v & 15u);
+  }
+  if (bad & 0x80) return false;
   *hi = h;
   *lo = l;
   return true;
