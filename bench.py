@@ -184,7 +184,7 @@ def cpu_baseline(soa, args) -> dict:
 def end_to_end(n_ops: int) -> dict:
     """The drop-in compose_oplogs on Op objects (config-2 shape), split into its legs."""
     from semantic_merge_amd import synth
-    from semantic_merge_amd._lib import compose_soa
+    from semantic_merge_amd._lib import compose_soa, session
     from semantic_merge_amd.marshal import marshal_native
     from semantic_merge_amd.materialize import materialize_conflicts, materialize_ops_native
     from semantic_merge_amd.oplog import ops_from_dicts
@@ -196,7 +196,7 @@ def end_to_end(n_ops: int) -> dict:
     t = [time.perf_counter()]
     soa = marshal_native(oa, ob)
     t.append(time.perf_counter())
-    order, addr, file, ctx, pairs = compose_soa(soa)
+    order, addr, file, ctx, pairs = session().compose(soa, copy=False)  # (as compose_oplogs)
     t.append(time.perf_counter())
     ops = oa + ob
     out = materialize_ops_native(ops, soa.kind, soa.strings, order, addr, file, ctx)
@@ -215,7 +215,7 @@ def small_merge(n_ops: int = 1000, reps: int = 50) -> dict:
     objects (marshal, device with its copies, materialise); medians."""
     import torch
     from semantic_merge_amd import synth
-    from semantic_merge_amd._lib import DeviceCompose, compose_soa
+    from semantic_merge_amd._lib import DeviceCompose, session
     from semantic_merge_amd.marshal import marshal_native
     from semantic_merge_amd.materialize import materialize_conflicts, materialize_ops_native
     from semantic_merge_amd.oplog import ops_from_dicts
@@ -236,18 +236,29 @@ def small_merge(n_ops: int = 1000, reps: int = 50) -> dict:
     A, B = synth.lift_op_dicts(logs)
     oa, ob = ops_from_dicts(A), ops_from_dicts(B)
     ops = oa + ob
-    te = []
+    te, legs = [], []
+    sess = session()
     for _ in range(max(reps // 2, 1)):
         t0 = time.perf_counter()
-        sa = marshal_native(oa, ob)
-        order, addr, file, ctx, pairs = compose_soa(sa)
+        sa = marshal_native(oa, ob, sess.staging(len(oa) + len(ob)))  # (as compose_oplogs)
+        t1 = time.perf_counter()
+        order, addr, file, ctx, pairs = sess.compose(sa, copy=False)
+        t2 = time.perf_counter()
         materialize_ops_native(ops, sa.kind, sa.strings, order, addr, file, ctx)
+        t3 = time.perf_counter()
         materialize_conflicts(ops, pairs)
-        te.append(time.perf_counter() - t0)
+        t4 = time.perf_counter()
+        te.append(t4 - t0)
+        legs.append((t1 - t0, t2 - t1, t3 - t2, t4 - t3))
+    lm = np.median(np.array(legs), axis=0) * 1e3
     return {"n_ops": n_ops, "plan": plan, "device_ms": round(float(np.median(td)) * 1e3, 4),
             "dropin_ms": round(float(np.median(te)) * 1e3, 4),
+            "dropin_legs_ms": {"marshal": round(float(lm[0]), 4), "compose_soa": round(float(lm[1]), 4),
+                               "materialize": round(float(lm[2]), 4), "conflicts": round(float(lm[3]), 4),
+                               "conflicts_n": int(len(pairs))},
             "note": "device_ms: smx_compose on resident buffers + one sync; dropin_ms: compose_oplogs "
-                    "on Op objects (marshal, copies, device, materialise)"}
+                    "on Op objects (marshal, copies, device, materialise); dropin_legs_ms: medians of "
+                    "each leg"}
 
 
 def main() -> None:

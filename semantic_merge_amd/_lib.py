@@ -52,6 +52,31 @@ def _ptr(t) -> int:
     return t.data_ptr() if t is not None and t.numel() > 0 else 0
 
 
+_hip: Optional[C.CDLL] = None
+
+
+def _hiprt() -> C.CDLL:
+    """The HIP runtime the process already runs (torch's, which libsmx shares: the same
+    soname), for the session's two copies and its one stream sync -- a ctypes call each,
+    against ~10 us of torch dispatch per copy_ / stream context on a 1k-op merge."""
+    global _hip
+    if _hip is None:
+        _torch()
+        lib()
+        h = C.CDLL("libamdhip64.so.7")  # (already loaded: dlopen returns that copy)
+        h.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        h.hipMemcpyAsync.restype = C.c_int
+        h.hipStreamSynchronize.argtypes = [C.c_void_p]
+        h.hipStreamSynchronize.restype = C.c_int
+        _hip = h
+    return _hip
+
+
+def _hip_check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise SmxError(rc, f"{what} failed (hipError_t {rc})")
+
+
 class DeviceCompose:
     """Device-resident inputs, outputs and workspace for repeated smx_compose calls."""
 
@@ -146,8 +171,23 @@ class ComposeSession:
         # its own stream: repeated merges of one size replay the library's HIP graph
         self.stream = self.torch.cuda.Stream(self.device)
 
+    _DT = {"kind": np.uint8, "ts": np.uint64, "oid_hi": np.uint64, "oid_lo": np.uint64, "sym": np.uint32,
+           "v0": np.int32, "v1": np.int32}
+
+    def staging(self, n: int) -> dict:
+        """The input columns of an n-op merge as views of the pinned staging area, laid out
+        as compose() copies it: a SoA marshalled into them is not packed again."""
+        self._ensure(n, 0)
+        hin = self.h_in.numpy()
+        cols, off = {}, 0
+        for name, w in self._IN:
+            cols[name] = hin[off: off + n * w].view(self._DT[name])
+            off += _al(n * w)
+        return cols
+
     def _ensure(self, n: int, ws_bytes: int) -> None:
         torch = self.torch
+        grown = n > self.cap_n or ws_bytes > self.cap_ws
         if n > self.cap_n:
             cap = max(n + n // 4, 1024)
             in_b = sum(_al(cap * w) for _, w in self._IN)
@@ -160,9 +200,13 @@ class ComposeSession:
         if ws_bytes > self.cap_ws:
             self.ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=self.device)
             self.cap_ws = ws_bytes
+        if grown:  # new buffers come from the current stream's pool: ready before the session's stream uses them
+            torch.cuda.synchronize(self.device)
 
-    def compose(self, soa: SoA):
-        """(order, addr, file, ctx, conflict_pairs) of one merge, computed on the GPU."""
+    def compose(self, soa: SoA, copy: bool = True):
+        """(order, addr, file, ctx, conflict_pairs) of one merge, computed on the GPU.
+        copy=False: views of the session's pinned staging area, valid until its next merge
+        (the drop-in materialises them at once)."""
         import time
         t0 = time.perf_counter()
         n = soa.n
@@ -175,16 +219,17 @@ class ComposeSession:
         hin = self.h_in.numpy()
         off, ptrs = 0, {}
         d0 = self.d_in.data_ptr()
+        h0 = hin.ctypes.data
         for name, w in self._IN:   # pack the columns into the pinned staging area (laid out for n)
-            hin[off: off + n * w] = np.ascontiguousarray(getattr(soa, name)).view(np.uint8).reshape(-1)
-            ptrs[name] = d0 + off
+            col = getattr(soa, name)
+            if not (isinstance(col, np.ndarray) and col.ctypes.data == h0 + off and col.nbytes == n * w):
+                hin[off: off + n * w] = np.ascontiguousarray(col).view(np.uint8).reshape(-1)
+            ptrs[name] = d0 + off  # (a column marshalled into staging() is in place already)
             off += _al(n * w)
         t1 = time.perf_counter()
-        torch = self.torch
-        stream = self.stream
-        stream.wait_stream(torch.cuda.current_stream(self.device))  # buffers (re)allocated on it
-        with torch.cuda.stream(stream):
-            self.d_in[:off].copy_(self.h_in[:off], non_blocking=True)
+        hip = _hiprt()
+        st = self.stream.cuda_stream
+        _hip_check(hip.hipMemcpyAsync(d0, self.h_in.data_ptr(), off, 1, st), "hipMemcpyAsync (inputs)")
         ccap = max(min(soa.n_a, soa.n_b), 1)
         o0 = self.d_out.data_ptr()
         q = _al(n * 4)             # outputs laid out for n: one contiguous copy back
@@ -192,13 +237,12 @@ class ComposeSession:
                           ptrs["oid_lo"], ptrs["sym"], ptrs["v0"], ptrs["v1"])
         cnt_off = 4 * q + _al(8 * ccap)
         out = _abi.SmxComposeOut(o0, o0 + q, o0 + 2 * q, o0 + 3 * q, o0 + 4 * q, ccap, o0 + cnt_off)
-        args = (C.byref(ops), C.byref(out), self.ws.data_ptr(), ws.value, stream.cuda_stream)
+        args = (C.byref(ops), C.byref(out), self.ws.data_ptr(), ws.value, st)
         hout = self.h_out.numpy()
 
         def copy_back():
-            with torch.cuda.stream(stream):
-                self.h_out[:cnt_off + 16].copy_(self.d_out[:cnt_off + 16], non_blocking=True)
-            stream.synchronize()
+            _hip_check(hip.hipMemcpyAsync(self.h_out.data_ptr(), o0, cnt_off + 16, 2, st), "hipMemcpyAsync (outputs)")
+            _hip_check(hip.hipStreamSynchronize(st), "hipStreamSynchronize")
             return (int(x) for x in hout[cnt_off: cnt_off + 16].view(np.int64))
         if n < self.ASYNC_MAX:
             # merges below the early-verdict size: the asynchronous part, the copy back and
@@ -217,8 +261,10 @@ class ComposeSession:
             raise SmxError(-1, "invalid input: sym >= n_sym or kind >= 18")
         if nc > ccap:
             raise SmxError(-2, f"{nc} conflicts exceed capacity {ccap}")
-        res = tuple(hout[i * q: i * q + 4 * k].view(np.int32).copy() for i in range(4))
-        pairs = hout[4 * q: 4 * q + 8 * nc].view(np.int32).reshape(nc, 2).copy()
+        res = tuple(hout[i * q: i * q + 4 * k].view(np.int32) for i in range(4))
+        pairs = hout[4 * q: 4 * q + 8 * nc].view(np.int32).reshape(nc, 2)
+        if copy:
+            res, pairs = tuple(x.copy() for x in res), pairs.copy()
         self.last = {"pack_s": t1 - t0, "device_s": t2 - t1, "unpack_s": time.perf_counter() - t2}
         return res + (pairs,)
 

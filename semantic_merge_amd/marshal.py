@@ -30,7 +30,7 @@ from collections import OrderedDict
 
 import re
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Sequence
+from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -238,20 +238,20 @@ def marshal(delta_a: Sequence[Any], delta_b: Sequence[Any]) -> SoA:
                list(strings), ts_mode, id_mode)
 
 
-def marshal_native(delta_a: Sequence[Any], delta_b: Sequence[Any]) -> SoA:
+def marshal_native(delta_a: Sequence[Any], delta_b: Sequence[Any], cols: Optional[dict] = None) -> SoA:
     """``marshal`` done by the native host module (csrc/smx_host.cpp): same SoA, same
     exceptions.  Only non-ISO timestamps and ids that are neither canonical UUIDs nor
-    short strings go back to the Python encoders above (dense ranks need a sort)."""
+    short strings go back to the Python encoders above (dense ranks need a sort).
+    cols: preallocated output columns (kind, ts, oid_hi, oid_lo, sym, v0, v1 of n ops,
+    e.g. ComposeSession.staging's pinned views)."""
     from ._host import host
     ops = list(delta_a) + list(delta_b)
     n = len(ops)
-    kind = np.empty(n, np.uint8)
-    ts = np.empty(n, np.uint64)
-    hi = np.empty(n, np.uint64)
-    lo = np.empty(n, np.uint64)
-    sym = np.empty(n, np.uint32)
-    v0 = np.empty(n, np.int32)
-    v1 = np.empty(n, np.int32)
+    if cols is None:
+        kind, ts, hi, lo = np.empty(n, np.uint8), np.empty(n, np.uint64), np.empty(n, np.uint64), np.empty(n, np.uint64)
+        sym, v0, v1 = np.empty(n, np.uint32), np.empty(n, np.int32), np.empty(n, np.int32)
+    else:
+        kind, ts, hi, lo, sym, v0, v1 = (cols[k] for k in ("kind", "ts", "oid_hi", "oid_lo", "sym", "v0", "v1"))
     n_sym, strings, ts_ok, id_mode, ts_str, ids = host().marshal_ops(
         ops, KIND_RANK, KIND_UNKNOWN, KIND_MOVE, KIND_RENAME, DEFAULT_TIMESTAMP, eq_key,
         kind, ts, hi, lo, sym, v0, v1)

@@ -157,10 +157,10 @@ def decode_pair(text_a: Any, text_b: Any, op_cls: type = Op, target_cls: type = 
 def compose_json(text_a: Any, text_b: Any, op_cls: type = Op, target_cls: type = Target):
     """compose_oplogs(OpLog.from_json(text_a).ops, OpLog.from_json(text_b).ops) with the
     decode and the marshal fused (decode_pair)."""
-    from ._lib import compose_soa
+    from ._lib import session
     from .materialize import materialize_conflicts, materialize_ops_native
     ops_a, ops_b, soa = decode_pair(text_a, text_b, op_cls, target_cls)
-    order, addr, file, ctx, pairs = compose_soa(soa)
+    order, addr, file, ctx, pairs = session().compose(soa, copy=False)  # (materialised at once)
     ops = ops_a + ops_b
     return materialize_ops_native(ops, soa.kind, soa.strings, order, addr, file, ctx), \
         materialize_conflicts(ops, pairs)
