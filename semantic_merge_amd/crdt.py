@@ -138,9 +138,9 @@ class RGA:
     a prefix of the stream (each live element as its insert; each tombstoned one as an
     insert of a private value that is then deleted, so no later event can touch it) and
     keeps the existing ``Elem`` objects: a later ``delete`` sets ``tombstone`` on them in
-    place, as crdt.py:40-43 does.  The device replay relies on the list being in key
-    order (what ``insert`` and ``move`` maintain, crdt.py:48-57); a state the caller put
-    out of key order raises ``ValueError`` instead of being replayed differently."""
+    place, as crdt.py:40-43 does.  A state the caller put out of key order replays with
+    each element keyed by the running maximum of the keys before it (``_effective_keys``):
+    the same insert slots as crdt.py:48-57's scan of the list as it stands."""
 
     def __init__(self) -> None:
         self._events: List[Event] = []
@@ -166,39 +166,21 @@ class RGA:
         base = self._list or []
         if not base:
             return replay_lists([self._events])[0]
-        prev = None
-        stream: List[Event] = []
-        origin: List[int] = []  # stream index -> base index (-1: a later event)
-        for i, e in enumerate(base):
-            k = (e.key.anchor, e.key.t, e.key.author, e.key.opid)
-            if prev is not None and k < prev:
-                raise ValueError("RGA.list is not in key order (element %d): the GPU replay needs the "
-                                 "order insert() and move() keep" % i)
-            prev = k
-            if e.tombstone:
-                tag = object()  # equal to nothing else: no later move/delete reaches it
-                stream.append((INSERT, e.key, tag))
-                stream.append((DELETE, None, tag))
-                origin += [i, -1]
-            else:
-                stream.append((INSERT, e.key, e.value))
-                origin.append(i)
-        nb = len(stream)
-        stream += self._events
-        origin += [-1] * len(self._events)
-        src, tomb = _replay_list_src(stream)
-        out: List[Elem] = []
-        for s, tb in zip(src, tomb):
-            if s < nb:
-                e = base[origin[s]]
-                if tb:
-                    e.tombstone = True
-            else:
-                _, key, value = stream[s]
-                e = Elem(key, value, bool(tb))
-            out.append(e)
-        return out
-
+        events = self._events
+        while True:
+            eff, ordered = _effective_keys(base)
+            j = -1 if ordered else next((i for i, ev in enumerate(events) if ev[0] == MOVE), -1)
+            if j < 0:
+                return _replay_onto(base, eff, events)
+            # A list out of key order whose events hold a move: the move's pop can lower
+            # the effective keys after it, so the events are replayed up to it, then its pop
+            # alone (its insert dropped), and its insert opens the next round on the new list.
+            if j:
+                base = _replay_onto(base, eff, events[:j])
+                eff, _ = _effective_keys(base)
+            _, key, value = events[j]
+            base = _replay_onto(base, eff, [events[j]], drop_new=True)
+            events = [(INSERT, key, value)] + list(events[j + 1:])
     def insert(self, key: Key, value: str) -> None:
         self._events.append((INSERT, key, value))
 
@@ -212,6 +194,66 @@ class RGA:
         if self._list is None:
             return replay([self._events])[0]
         return [e.value for e in self.list if not e.tombstone]
+
+
+def _effective_keys(base: Sequence[Elem]) -> Tuple[List[Key], bool]:
+    """Each element's insert key for the replay of a list state, and whether the list is
+    in key order.  An insert goes before the first element, in list order, whose key is
+    strictly greater (crdt.py:48-57): the first element whose running maximum of keys
+    is greater.  So the state replays as inserts keyed by that running maximum -- the
+    list's own keys when it is in key order (what insert() and move() keep); the
+    running maximum makes a caller-reordered list a key-ordered one with the same
+    insert slots, and a new element's maximum is its own key.  Inserts and deletes leave
+    the other elements' maxima unchanged; a move's pop may lower them (RGA._fold)."""
+    eff: List[Key] = []
+    ordered = True
+    top = None
+    for e in base:
+        k = (e.key.anchor, e.key.t, e.key.author, e.key.opid)
+        if top is None or k >= top:
+            top = k
+            eff.append(e.key)
+        else:  # (below the running maximum: inserts see the maximum here)
+            ordered = False
+            eff.append(eff[-1])
+    return eff, ordered
+
+
+def _replay_onto(base: Sequence[Elem], eff: Sequence[Key], events: Sequence[Event],
+                 drop_new: bool = False) -> List[Elem]:
+    """The list state `base` (insert keys `eff`) followed by `events`, replayed on the
+    GPU.  Each live element replays as its insert, each tombstoned one as an insert of
+    a private value that is then deleted (no later event can touch it); the existing
+    Elem objects are kept (a delete tombstones them in place, crdt.py:40-43), every
+    event-created element is a new Elem.  drop_new: leave the event-created elements
+    out (a move's pop replayed alone)."""
+    stream: List[Event] = []
+    origin: List[int] = []  # stream index -> base index (-1: a later event)
+    for i, e in enumerate(base):
+        if e.tombstone:
+            tag = object()  # equal to nothing else: no later move/delete reaches it
+            stream.append((INSERT, eff[i], tag))
+            stream.append((DELETE, None, tag))
+            origin += [i, -1]
+        else:
+            stream.append((INSERT, eff[i], e.value))
+            origin.append(i)
+    nb = len(stream)
+    stream += list(events)
+    src, tomb = _replay_list_src(stream)
+    out: List[Elem] = []
+    for s, tb in zip(src, tomb):
+        if s < nb:
+            e = base[origin[s]]
+            if tb:
+                e.tombstone = True
+        elif drop_new:
+            continue
+        else:
+            _, key, value = stream[s]
+            e = Elem(key, value, bool(tb))
+        out.append(e)
+    return out
 
 
 def _replay_list_src(stream: Sequence[Event]) -> Tuple[List[int], List[int]]:

@@ -125,12 +125,74 @@ def test_rga_list_object_held_across_events():
     assert L[0] is x and x.tombstone  # tombstoned in place (crdt.py:40-43)
 
 
-def test_rga_list_out_of_key_order_fails_loudly():
-    r = RGA()
-    r.list = [Elem(Key("b", 0, "u", "o"), "x"), Elem(Key("a", 0, "u", "o"), "y")]
-    r.insert(Key("c", 0, "u", "o"), "z")
-    with pytest.raises(ValueError, match="key order"):
-        r.list
+def _out_of_order_script(rng, n_steps):
+    """A random script over a caller-reordered list: assignments of shuffled lists,
+    out-of-order appends, reversals, and inserts / moves / deletes with duplicate keys
+    and values."""
+    keys = [(a, t, u, o) for a in "abc" for t in range(2) for u in ("u1", "u2") for o in ("o1",)]
+    vals = ["v%d" % i for i in range(5)]
+    steps = []
+    for _ in range(n_steps):
+        r = rng.random()
+        k = list(keys[rng.integers(len(keys))])
+        v = vals[rng.integers(len(vals))]
+        if r < 0.08:
+            m = int(rng.integers(0, 7))
+            steps.append(("assign", [(list(keys[rng.integers(len(keys))]), vals[rng.integers(len(vals))],
+                                      bool(rng.random() < 0.2)) for _ in range(m)]))
+        elif r < 0.16:
+            steps.append(("append", k, v, bool(rng.random() < 0.2)))
+        elif r < 0.2:
+            steps.append(("reverse",))
+        elif r < 0.5:
+            steps.append(("insert", v, k))
+        elif r < 0.7:
+            steps.append(("move", v, k))
+        elif r < 0.8:
+            steps.append(("delete", v))
+        else:
+            steps.append(("read",))
+    steps.append(("read",))
+    return steps
+
+
+def test_rga_list_out_of_key_order_matches_reference_semantics():
+    """A list the caller put out of key order (assigned, appended to, reversed): later
+    inserts go before the first greater key in the list as it stands, moves pop the first
+    live element with the value (crdt.py:29-57).  Checked against the list-state
+    restatement oracle/rga_list_ref.py on 60 random scripts."""
+    from oracle.rga_list_ref import ListRga
+    rng = np.random.default_rng(29)
+    n_unordered = 0
+    for case in range(60):
+        r, ref = RGA(), ListRga()
+        for st in _out_of_order_script(rng, 30):
+            op = st[0]
+            if op == "assign":
+                r.list = [Elem(Key(*k), v, tb) for k, v, tb in st[1]]
+                ref = ListRga([(tuple(k), v, tb) for k, v, tb in st[1]])
+            elif op == "append":
+                r.list.append(Elem(Key(*st[1]), st[2], st[3]))
+                ref.rows.append([tuple(st[1]), st[2], st[3]])
+            elif op == "reverse":
+                r.list.reverse()
+                ref.rows.reverse()
+            elif op == "insert":
+                r.insert(Key(*st[2]), st[1])
+                ref.insert(tuple(st[2]), st[1])
+            elif op == "move":
+                r.move(st[1], Key(*st[2]))
+                ref.move(st[1], tuple(st[2]))
+            elif op == "delete":
+                r.delete(st[1])
+                ref.delete(st[1])
+            else:
+                got = [((e.key.anchor, e.key.t, e.key.author, e.key.opid), e.value, e.tombstone) for e in r.list]
+                assert got == ref.state(), f"script {case}"
+                ks = [g[0] for g in got]
+                n_unordered += any(b < a for a, b in zip(ks, ks[1:]))
+                assert r.materialize() == [v for _, v, tb in got if not tb]
+    assert n_unordered > 20  # the scripts do reach states out of key order
 
 
 @pytest.mark.parametrize("n_ops,n_lists,seed", [(1_000_000, 5_000, 14), (300_000, 30, 15)])
