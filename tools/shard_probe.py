@@ -85,6 +85,17 @@ def main():
         print(f"N={n}: {soa.n:,} ops per rank: plain smx_compose {plain:.3f} ms, one-rank sharded step "
               f"{sh:.3f} ms (+{sh - plain:.3f})", flush=True)
         print(f"   phases (synced): {breakdown(sc)}", flush=True)
+        if os.environ.get("SHARD_PROBE_PROFILE"):  # host-side hot spots of the step (cProfile)
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+            for _ in range(20):
+                sc.run()
+            torch.cuda.synchronize()
+            pr.disable()
+            pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+            pstats.Stats(pr).sort_stats("cumtime").print_stats(40)
         del sc, a, b, soa
         torch.cuda.empty_cache()
     dist.destroy_process_group()
