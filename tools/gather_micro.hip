@@ -51,6 +51,34 @@ __device__ __forceinline__ u32 look(const uint8_t* __restrict__ tab, u32 s) {
   return p[0] ^ (p[1] & ((o & 2) ? 0xffffffffu : 0xffffu));
 }
 
+// Shapes 6..8: some of a lane's four 6-byte lookups through the SCALAR memory path
+// (each lane's symbol broadcast with readlane, one uniform-address load per lane, the
+// result put back into its lane): the scalar cache and its L2 requests instead of the
+// texture path (TA / TD), which bounds the vector gathers.  6: one of four scalar,
+// 7: two of four, 8: all four.
+__device__ __forceinline__ u32 look_scalar(const uint8_t* __restrict__ tab, u32 s) {
+  const int lane = threadIdx.x & 63;
+  u32 res = 0;
+#pragma unroll 16
+  for (int l = 0; l < 64; ++l) {
+    const u32 sl = __builtin_amdgcn_readlane(s, l);
+    const u64 o = off48(sl);
+    const u64 w = *reinterpret_cast<const u64_a4*>(tab + (o & ~3ull));
+    const u64 x = (w >> ((o & 2) * 8)) & 0xffffffffffffull;
+    const u32 r = (u32)x ^ (u32)(x >> 32);
+    res = lane == l ? r : res;
+  }
+  return res;
+}
+
+template <int V>
+__device__ __forceinline__ u32 look_u(const uint8_t* __restrict__ tab, u32 s, int u) {
+  if (V == 6) return u == 3 ? look_scalar(tab, s) : look<3>(tab, s);
+  if (V == 7) return u >= 2 ? look_scalar(tab, s) : look<3>(tab, s);
+  if (V == 8) return look_scalar(tab, s);
+  return look<V>(tab, s);
+}
+
 template <int V>
 __global__ void __launch_bounds__(NT) k_gather(const v4u* __restrict__ idx, const uint8_t* __restrict__ tab,
                                                u32 smask, i64 nq, v4u* __restrict__ out) {
@@ -65,8 +93,8 @@ __global__ void __launch_bounds__(NT) k_gather(const v4u* __restrict__ idx, cons
 #pragma unroll
   for (int j = 0; j < B; ++j) {
     const i64 q = q0 + (i64)j * NT;
-    const v4u r = v4u{look<V>(tab, s[j].x & smask), look<V>(tab, s[j].y & smask),
-                      look<V>(tab, s[j].z & smask), look<V>(tab, s[j].w & smask)};
+    const v4u r = v4u{look_u<V>(tab, s[j].x & smask, 0), look_u<V>(tab, s[j].y & smask, 1),
+                      look_u<V>(tab, s[j].z & smask, 2), look_u<V>(tab, s[j].w & smask, 3)};
     if (q < nq) __builtin_nontemporal_store(r, &out[q]);
   }
 }
@@ -84,6 +112,9 @@ extern "C" int gather_run(int v, const void* idx, const void* tab, u32 smask, i6
     case 3: hipLaunchKernelGGL(k_gather<3>, dim3(blocks), dim3(NT), 0, st, I, T, smask, nq, O); break;
     case 4: hipLaunchKernelGGL(k_gather<4>, dim3(blocks), dim3(NT), 0, st, I, T, smask, nq, O); break;
     case 5: hipLaunchKernelGGL(k_gather<5>, dim3(blocks), dim3(NT), 0, st, I, T, smask, nq, O); break;
+    case 6: hipLaunchKernelGGL(k_gather<6>, dim3(blocks), dim3(NT), 0, st, I, T, smask, nq, O); break;
+    case 7: hipLaunchKernelGGL(k_gather<7>, dim3(blocks), dim3(NT), 0, st, I, T, smask, nq, O); break;
+    case 8: hipLaunchKernelGGL(k_gather<8>, dim3(blocks), dim3(NT), 0, st, I, T, smask, nq, O); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;

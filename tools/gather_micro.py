@@ -14,8 +14,9 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SHAPES = {0: "streams only", 1: "4 B aligned", 2: "8 B aligned", 3: "6 B packed, 8 B load at 4-aligned",
-          4: "16 B aligned", 5: "6 B packed, two dword loads"}
-BYTES = {0: 0, 1: 4, 2: 8, 3: 6.1, 4: 16, 5: 6.1}
+          4: "16 B aligned", 5: "6 B packed, two dword loads", 6: "6 B packed, 1 of 4 via scalar loads",
+          7: "6 B packed, 2 of 4 via scalar loads", 8: "6 B packed, all via scalar loads"}
+BYTES = {0: 0, 1: 4, 2: 8, 3: 6.1, 4: 16, 5: 6.1, 6: 6.1, 7: 6.1, 8: 6.1}
 
 
 def main():
