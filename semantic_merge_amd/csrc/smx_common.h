@@ -27,6 +27,7 @@ typedef uint8_t u8;
 // Counters written by kernels; read by later kernels and (once) by the host.
 #define SEG_FAIL_BIT 8ull
 #define F_LONG 22ull  // f_fail from k_fpart's long-group check (bits 1, 2 and 4), before any window ran
+#define F_WLONG 32ull // f_fail bit 5: after an early F_LONG (k_khist), a group no wide window holds either
 #define SEG_DECREASE 2ull  // meta->seg_over: a timestamp decreases (the segmented sort)
 struct ComposeMeta {
   u64 kcnt[SMX_N_KINDS];     // ops per precedence rank (stats kernel)

@@ -251,12 +251,30 @@ __global__ void k_meta_init(ComposeMeta* meta) {
 // B[CH*j + CH-1]; 1/256 of the keys, cache-resident): the first level of the
 // search runs on them, the second inside one chunk.  The snap gallops back over
 // the (short) run of equal timestamps.
+// LongW (the synchronous merge's early verdict): k_khist made the long-group test; on its
+// F_LONG these are the wide plan's boundaries (tgt_w, W_w windows of D_w chunks, its own
+// long test flagging F_WLONG) and k_cscan_mid then clears F_LONG, so no normal window, no
+// re-arm and no second k_fpart run (config 5's doomed attempt).
+struct LongW {
+  i64 tgt_w = 0, W_w = 0, D_w = 0;  // tgt_w 0: off
+};
 __device__ __forceinline__ void fpart_body(const u64* __restrict__ ts, const u64* __restrict__ tsB,
                                            const u64* __restrict__ sA, const u64* __restrict__ sB, i64 na, i64 nb,
                                            i64 W, i64 tgt, i64 D, i64* __restrict__ bnd, ComposeMeta* meta,
-                                           u32* long_host, i64 blk, i64 nblk) {
+                                           u32* long_host, i64 blk, i64 nblk, LongW lw = LongW{}) {
   const i64 k = blk * BLOCK + threadIdx.x;
-  if (SMX_KHIST_LONG) {
+  bool chk = SMX_KHIST_LONG;
+  u64 fl = F_LONG;
+  if (lw.tgt_w) {
+    if ((__hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & F_LONG) == F_LONG) {
+      W = lw.W_w, tgt = lw.tgt_w, D = lw.D_w;  // the wide plan, tested at its own capacity
+      fl = F_WLONG;
+      long_host = nullptr;
+    } else {
+      chk = false;  // (k_khist tested the normal capacity)
+    }
+  }
+  if (chk) {
     // A chunk sample equal to the sample D chunks (one window capacity) later (A: first
     // ops of chunks c and c + D; B: last ops of full chunks): that timestamp group alone
     // overflows a window, so the presorted plan cannot hold.  Flagged before the windows
@@ -268,8 +286,8 @@ __device__ __forceinline__ void fpart_body(const u64* __restrict__ ts, const u64
     for (i64 c = k; c + D < cb; c += nt) lg |= sB[c] == sB[c + D];
     const u64 lgw = __ballot(lg);
     if (lgw && (threadIdx.x & (WAVE - 1)) == 0 &&
-        __hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != F_LONG) {
-      atomicOr((unsigned long long*)&meta->f_fail, F_LONG);
+        (__hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & fl) != fl) {
+      atomicOr((unsigned long long*)&meta->f_fail, fl);
       // ... and, on the synchronous path, to the host (pinned, coherent), which then
       // launches no tail behind this failed plan
       if (long_host) __hip_atomic_store(long_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -347,8 +365,8 @@ __device__ __forceinline__ void fpart_body(const u64* __restrict__ ts, const u64
 }
 __global__ void k_fpart(const u64* __restrict__ ts, const u64* __restrict__ tsB, const u64* __restrict__ sA,
                         const u64* __restrict__ sB, i64 na, i64 nb, i64 W, i64 tgt, i64 D, i64* __restrict__ bnd,
-                        ComposeMeta* meta, u32* long_host) {
-  fpart_body(ts, tsB, sA, sB, na, nb, W, tgt, D, bnd, meta, long_host, blockIdx.x, gridDim.x);
+                        ComposeMeta* meta, u32* long_host, LongW lw) {
+  fpart_body(ts, tsB, sA, sB, na, nb, W, tgt, D, bnd, meta, long_host, blockIdx.x, gridDim.x, lw);
 }
 
 // Generic windows over branch logs sorted by (ts, oid): fixed diagonals of WIN_CAP.
@@ -393,24 +411,31 @@ __global__ void k_gpart(const u64* __restrict__ sts, const u64* __restrict__ shi
 // aligned), so a chunk is one 16-lane DPP row.  No atomics: each lane counts its 16
 // kinds in packed 5-bit fields (6 kinds per word), widens them to 10-bit fields and
 // the row adds them up with DPP shifts; the row's last lane holds the chunk's counts.
+// Dl > 0 (the synchronous merge's early verdict): k_fpart's long-group test is made here,
+// on the input itself (the timestamp Dl chunks later, one more load per chunk), so that
+// the host learns it right behind this kernel and launches the windows that hold the
+// groups (smx_compose.hip enqueue_async); f_fail = F_LONG and long_host[0] = 1.
 __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, const u64* __restrict__ ts,
                                                  i64 na, i64 nb, i64 bgap, i64 CM, u32* __restrict__ cnt,
                                                  u64* __restrict__ sA, u64* __restrict__ sB, ComposeMeta* meta,
-                                                 u32* long_host) {
+                                                 u32* long_host, i64 Dl) {
   __shared__ u32 c[CH_PER_BLOCK * KH_R][SMX_N_KINDS];
   __shared__ u32 km[2];
+  __shared__ u32 lgb;  // the block saw a group longer than a window (Dl)
   const i64 CA = SMX_CEIL_DIV(na, (i64)CH), CB = SMX_CEIL_DIV(nb, (i64)CH);
   const int j = threadIdx.x / 16, q = threadIdx.x % 16;
   if (threadIdx.x < 2) km[threadIdx.x] = 0;
+  if (threadIdx.x == 0) lgb = 0;
   // KH_R rounds of CH_PER_BLOCK chunks per block; every round's loads are issued first
   u32 w[KH_R][4];
   int nvr[KH_R];
   // timestamp samples for k_fpart: first op of each A chunk, last op of each full B chunk
   // (stored after the counting: their loads then wait beside the kind bytes', not ahead of
   // them; separate registers for A and B, or the second load waits on the first)
-  u64 smpA[KH_R], smpB[KH_R];
+  u64 smpA[KH_R], smpB[KH_R], farA[KH_R], farB[KH_R];  // (far: the sample Dl chunks later)
   u64* atA[KH_R];
   u64* atB[KH_R];
+  bool chkA[KH_R], chkB[KH_R];
 #pragma unroll
   for (int rd = 0; rd < KH_R; ++rd) {
     const i64 g = ((i64)blockIdx.x * KH_R + rd) * CH_PER_BLOCK + j;
@@ -431,15 +456,24 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
         if (y < nv) w[rd][y >> 2] |= (u32)src[y] << (8 * (y & 3));
     }
     atA[rd] = atB[rd] = nullptr;
-    smpA[rd] = smpB[rd] = 0;
+    smpA[rd] = smpB[rd] = farA[rd] = farB[rd] = 0;
+    chkA[rd] = chkB[rd] = false;
     if (g < CA + CB) {
       if (!side && q == 0) {
         atA[rd] = sA + cc;
         smpA[rd] = ts[cc * CH];
+        if (Dl > 0 && cc + Dl < CA) {
+          chkA[rd] = true;
+          farA[rd] = ts[(cc + Dl) * CH];
+        }
       }
       if (side && q == 15 && nv == 16) {
         atB[rd] = sB + cc;
         smpB[rd] = ts[na + bgap + cc * CH + CH - 1];
+        if (Dl > 0 && cc + Dl < nb / CH) {  // (B samples: last ops of full chunks)
+          chkB[rd] = true;
+          farB[rd] = ts[na + bgap + (cc + Dl) * CH + CH - 1];
+        }
       }
     }
   }
@@ -482,16 +516,29 @@ __global__ void __launch_bounds__(KH_NT) k_khist(const u8* __restrict__ kind, co
       for (int k = 0; k < SMX_N_KINDS; ++k) c[rd * CH_PER_BLOCK + j][k] = (f[k / 3] >> (10 * (k % 3))) & 1023u;
     }
   }
+  bool lg = false;
 #pragma unroll
   for (int rd = 0; rd < KH_R; ++rd) {
     if (atA[rd]) *atA[rd] = smpA[rd];
     if (atB[rd]) *atB[rd] = smpB[rd];
+    lg |= (chkA[rd] && farA[rd] == smpA[rd]) || (chkB[rd] && farB[rd] == smpB[rd]);
   }
+  // a sample equal to the one Dl chunks (one window capacity) later: that timestamp group
+  // alone overflows a window (k_fpart's test, SMX_KHIST_LONG); published below, once per
+  // block, and to the host by the one block whose atomic set it (thousands of waves
+  // storing to the pinned flag over the bus slowed this kernel and its completion)
+  if (__ballot(lg) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(&lgb, 1u);
   if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) {
     meta->bad_sym = 1;
     if (long_host) __hip_atomic_store(long_host + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
+  if (threadIdx.x == 0 && lgb &&
+      (__hip_atomic_load(&meta->f_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & F_LONG) != F_LONG) {
+    const u64 was = atomicOr((unsigned long long*)&meta->f_fail, F_LONG);
+    if ((was & F_LONG) != F_LONG && long_host)
+      __hip_atomic_store(long_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   // column-major output: consecutive threads write consecutive chunks of one column;
   // the kinds present per branch (the scans skip the all-zero columns)
   u32 m0 = 0, m1 = 0;
@@ -660,8 +707,20 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_up(const u32* __restrict__ cnt,
   if (threadIdx.x == 0) tsum[(i64)col * NT + blockIdx.x] = tot;
 }
 
+// The window count the plan's windows read (meta->n_win): nwin, or after an early
+// F_LONG (k_khist) with the wide boundaries in place (nwin_long > 0, k_fpart's LongW) the
+// wide plan's -- and F_LONG is cleared so the wide windows and the tail run.
+__device__ __forceinline__ void set_n_win(ComposeMeta* meta, u64 nwin, u64 nwin_long) {
+  if (nwin_long && meta->f_fail == F_LONG) {
+    meta->f_fail = 0;
+    nwin = nwin_long;
+  }
+  meta->n_win = nwin;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_cscan_mid(u32* __restrict__ tsum, i64 na, i64 nb, i64 CM, i64 NT,
-                                                     u32* __restrict__ cnt, ComposeMeta* meta, u64 nwin) {
+                                                     u32* __restrict__ cnt, ComposeMeta* meta, u64 nwin,
+                                                     u64 nwin_long) {
   __shared__ u32 s[NWAVES + 1];
   const int col = blockIdx.x;
   if (SMX_CSCAN_FAILCHK && meta->f_fail) return;  // (k_khist saw a group no window holds)
@@ -685,7 +744,7 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_mid(u32* __restrict__ tsum, i64
     __threadfence();
     if (atomicAdd((unsigned long long*)&meta->cs_done, 1ull) == (unsigned long long)gridDim.x - 1) {
       __threadfence();
-      meta->n_win = nwin;
+      set_n_win(meta, nwin, nwin_long);
       u64 acc = 0;
       for (int kk = 0; kk < SMX_N_KINDS; ++kk) {
         meta->base[kk] = acc;
@@ -729,7 +788,7 @@ __global__ void __launch_bounds__(BLOCK) k_cscan_down(u32* __restrict__ cnt, i64
 #define CS_SMALL_CM 16384
 #endif
 __device__ __forceinline__ void cscan_small_body(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM, ComposeMeta* meta,
-                                                 u64 nwin, int col, u32* s) {
+                                                 u64 nwin, int col, u32* s, u64 nwin_long = 0) {
   const int side = col / SMX_N_KINDS, k = col % SMX_N_KINDS;
   const i64 C = SMX_CEIL_DIV(side ? nb : na, (i64)CH);
   u32* colp = cnt + (i64)col * CM;
@@ -761,7 +820,7 @@ __device__ __forceinline__ void cscan_small_body(u32* __restrict__ cnt, i64 na, 
     __threadfence();
     if (atomicAdd((unsigned long long*)&meta->cs_done, 1ull) == (unsigned long long)(2 * SMX_N_KINDS - 1)) {
       __threadfence();
-      meta->n_win = nwin;
+      set_n_win(meta, nwin, nwin_long);
       u64 acc = 0;
       for (int kk = 0; kk < SMX_N_KINDS; ++kk) {
         meta->base[kk] = acc;
@@ -775,9 +834,9 @@ __device__ __forceinline__ void cscan_small_body(u32* __restrict__ cnt, i64 na, 
 #define SMX_FPART_CS 1  // small merges: k_fpart and k_cscan_small in one launch
 #endif
 __global__ void __launch_bounds__(BLOCK) k_cscan_small(u32* __restrict__ cnt, i64 na, i64 nb, i64 CM,
-                                                       ComposeMeta* meta, u64 nwin) {
+                                                       ComposeMeta* meta, u64 nwin, u64 nwin_long) {
   __shared__ u32 s[NWAVES + 1];
-  cscan_small_body(cnt, na, nb, CM, meta, nwin, blockIdx.x, s);
+  cscan_small_body(cnt, na, nb, CM, meta, nwin, blockIdx.x, s, nwin_long);
 }
 // Small merges (launch-bound): k_fpart and k_cscan_small are independent (both read
 // only k_khist's outputs), so one launch runs both: the first nfp blocks are k_fpart's,
@@ -1841,9 +1900,11 @@ static int launch_tail(const Ctx& C) {
 // emits).  Speculative: k_window_f verifies the layout and flags f_fail.
 
 // early (optional, not inside a graph capture): k_khist raises early->flag[0] when a
-// timestamp group is longer than a window (the plan then fails for sure) and flag[1] on
-// an invalid kind; early->ev is recorded right behind k_khist, so the host knows before
-// the windows are done.
+// timestamp group is longer than a window (the normal windows cannot hold the log) and
+// flag[1] on an invalid kind; early->ev is recorded right behind k_khist, so the host
+// knows while k_fpart and the column scans run, and launches the windows that hold the
+// groups (run_presorted's Deferred).  (Off the normal level, k_fpart raises flag[0] and
+// the event follows it.)
 struct EarlyFail {
   u32* flag_host = nullptr;
   u32* flag_dev = nullptr;
@@ -1908,7 +1969,17 @@ static int launch_presorted_windows(const Ctx& C, i64 W, i64 CM, int level) {
 
 // wide: WF_WIDE_CAP-op windows on WF_WIDE_NT threads (one per CU) for logs whose
 // equal-timestamp groups no WF_CAP window holds (config 5: 8192-op groups).
-static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr, int level = WL_NORMAL) {
+// With `early` at the normal level (the synchronous merge): k_khist makes the long-group
+// test and early->ev is recorded behind it; k_fpart and the column scans are enqueued
+// for either outcome (normal boundaries, or the wide plan's after F_LONG: LongW), and the
+// windows are left to the caller (*defer), which launches the normal or the wide ones
+// once the host has read the verdict.
+struct Deferred {
+  bool on = false;
+  i64 W = 0, W_w = 0, CM = 0;
+};
+static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr, int level = WL_NORMAL,
+                         Deferred* defer = nullptr) {
   hipStream_t st = C.st;
   ComposeMeta* meta = C.ws<ComposeMeta>(B_META);
   i64* bnd = C.ws<i64>(B_BND);
@@ -1931,6 +2002,13 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
   u32* ccnt = C.ws<u32>(B_CCNT);
   u64* sA = C.ws<u64>(B_SMP);
   u64* sB = sA + SMX_CEIL_DIV(C.na, (i64)CH) + 1;
+  const bool lmode = early && defer && level == WL_NORMAL && !KH_PERSIST;
+  LongW lw{};
+  if (lmode) {
+    lw.tgt_w = level_cap(WL_WIDE) - level_cap(WL_WIDE) % CH;  // (the first wide attempt of order_fallbacks)
+    lw.W_w = SMX_CEIL_DIV(C.n, lw.tgt_w);
+    lw.D_w = level_cap(WL_WIDE) / CH;
+  }
   if (KH_PERSIST) {
     static int ncu_of[64] = {};  // CUs per device (a benign race: every writer stores the same)
     int dev = 0;
@@ -1947,9 +2025,10 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
   } else {
     hipLaunchKernelGGL(k_khist, dim3(SMX_CEIL_DIV(nchunk, (i64)CH_PER_BLOCK * KH_R)), dim3(KH_NT), 0, st,
                        C.ops->kind, C.ops->ts, C.na, C.nb, C.ops->b_gap, CM, ccnt, sA, sB, meta,
-                       early ? early->flag_dev : nullptr);
+                       early ? early->flag_dev : nullptr, lmode ? cap / CH : (i64)0);
   }
-  const i64 nfp = SMX_CEIL_DIV(W + 1, (i64)BLOCK);
+  if (lmode) HIP_TRY(hipEventRecord(early->ev, st));  // (k_khist's verdict)
+  const i64 nfp = SMX_CEIL_DIV(W + 1, (i64)BLOCK);   // (>= the wide plan's W_w + 1 boundaries)
   const bool fused = SMX_FPART_CS && cs_small && !early;
   if (fused)
     hipLaunchKernelGGL(k_fpart_cscan, dim3(nfp + 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, C.ops->ts,
@@ -1957,24 +2036,30 @@ static int run_presorted(const Ctx& C, i64 tgt, const EarlyFail* early = nullptr
                        (u32*)nullptr, ccnt, CM, nfp);
   else
     hipLaunchKernelGGL(k_fpart, dim3(nfp), dim3(BLOCK), 0, st, C.ops->ts, C.ops->ts + C.na + C.ops->b_gap, sA, sB,
-                       C.na, C.nb, W, tgt, cap / CH, bnd, meta, early ? early->flag_dev : nullptr);
-  if (early) HIP_TRY(hipEventRecord(early->ev, st));
+                       C.na, C.nb, W, tgt, cap / CH, bnd, meta, (early && !lmode) ? early->flag_dev : nullptr, lw);
+  if (early && !lmode) HIP_TRY(hipEventRecord(early->ev, st));
+  const u64 nwin_long = lmode ? (u64)lw.W_w : 0ull;
   if (fused) {
     // (k_fpart_cscan scanned the columns)
   } else if (cs_small) {
-    hipLaunchKernelGGL(k_cscan_small, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, meta, (u64)W);
+    hipLaunchKernelGGL(k_cscan_small, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, meta, (u64)W,
+                       nwin_long);
   } else {
     const i64 NT = SMX_CEIL_DIV(CM, (i64)CS_TILE);
     u32* tsum = C.ws<u32>(B_TSUM);
     hipLaunchKernelGGL(k_cscan_up, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT, tsum,
                        meta);
     hipLaunchKernelGGL(k_cscan_mid, dim3(2 * SMX_N_KINDS), dim3(BLOCK), 0, st, tsum, C.na, C.nb, CM, NT, ccnt,
-                       meta, (u64)W);
+                       meta, (u64)W, nwin_long);
     hipLaunchKernelGGL(k_cscan_down, dim3(NT, 2 * SMX_N_KINDS), dim3(BLOCK), 0, st, ccnt, C.na, C.nb, CM, NT,
                        tsum, meta);
   }
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_PLAN);
+  if (lmode) {
+    *defer = Deferred{true, W, lw.W_w, CM};
+    return SMX_OK;
+  }
   return launch_presorted_windows(C, W, CM, level);
 }
 
@@ -2002,7 +2087,7 @@ static int run_presorted_rewide(const Ctx& C, i64 tgt, int level = WL_WIDE) {
   hipLaunchKernelGGL(k_plan_rearm, dim3(1), dim3(1), 0, st, meta, (u64)W);
   hipLaunchKernelGGL(k_fpart, dim3(SMX_CEIL_DIV(W + 1, (i64)BLOCK)), dim3(BLOCK), 0, st, C.ops->ts,
                      C.ops->ts + C.na + C.ops->b_gap, sA, sB, C.na, C.nb, W, tgt, level_cap(level) / CH,
-                     C.ws<i64>(B_BND), meta, (u32*)nullptr);
+                     C.ws<i64>(B_BND), meta, (u32*)nullptr, LongW{});
   HIP_TRY(hipGetLastError());
   C.tm->end(ST_PLAN);
   return launch_presorted_windows(C, W, CM, level);
@@ -2716,8 +2801,8 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
     return SMX_OK;
   }
   // A large synchronous merge (not captured): the host waits for k_khist's verdict while
-  // the windows run, and launches no tail (~20 launches that would only see the failure)
-  // behind a plan that fails for sure -- smx_compose_finish then runs the fallback plan.
+  // k_fpart and the column scans run, then launches the normal or the wide windows and
+  // the tail; on an invalid kind no window and no tail (smx_compose_finish reports it).
   EarlyFail early;
   bool use_early = false;
   if (early_ok && n >= SMX_EARLY_MIN) {
@@ -2728,10 +2813,20 @@ static int enqueue_async(const smx_ops* ops, const smx_compose_out* out, void* w
     use_early = cs == hipStreamCaptureStatusNone && early_fail_of(dev, &early) == SMX_OK;
     if (use_early) early.flag_host[0] = early.flag_host[1] = 0u;  // (the previous merge on this thread has synced)
   }
-  if ((rc = run_presorted(C, first_tgt(C), use_early ? &early : nullptr, first_level(C)))) return rc;
+  Deferred dw;
+  if ((rc = run_presorted(C, first_tgt(C), use_early ? &early : nullptr, first_level(C), &dw))) return rc;
   if (use_early) {
     HIP_TRY(hipEventSynchronize(early.ev));
-    if (((volatile u32*)early.flag_host)[0]) {
+    const bool lng = ((volatile u32*)early.flag_host)[0] != 0;
+    if (dw.on && !((volatile u32*)early.flag_host)[1]) {
+      // k_khist's verdict: the windows that hold the log's timestamp groups.  After
+      // F_LONG k_fpart has placed the wide plan's boundaries and the scans its window
+      // count (config 5: no doomed normal launch, no re-arm, no second k_fpart)
+      if (lng) g_plan = SMX_PLAN_PRESORTED_WIDE;
+      if ((rc = lng ? launch_presorted_windows(C, dw.W_w, dw.CM, WL_WIDE)
+                    : launch_presorted_windows(C, dw.W, dw.CM, first_level(C))))
+        return rc;
+    } else if (lng || ((volatile u32*)early.flag_host)[1]) {
       const bool bad = ((volatile u32*)early.flag_host)[1] != 0;
       if (verdict) {
         verdict->failed = true;
