@@ -336,28 +336,27 @@ class ShardedCompose:
     @staticmethod
     def _host_cuts(g: np.ndarray, tau: np.ndarray):
         """allc [W, 2, W] from the gathered range info alone, or None when a splitter
-        falls between a slice's RH head and RH tail keys (then the device searches)."""
+        falls between a slice's RH head and RH tail keys (then the device searches).
+        Every (rank, branch, splitter) at once (a loop over the W x 2 slices cost ~0.5 ms
+        of numpy calls per exchange at W = 8): a cut is the count of head keys below the
+        splitter, or the slice length less RH plus the count of tail keys below it when
+        the splitter lies past the head (keys sorted, so counts are searchsorted 'left')."""
         W = g.shape[0]
-        allc = np.zeros((W, 2, W), np.int64)
-        for q in range(W):
-            for br in range(2):
-                n = int(g[q, br])
-                if n == 0:
-                    continue
-                h = min(RH, n)
-                o = 9 + 2 * RH * br
-                head, tail = g[q, o: o + h], g[q, o + 2 * RH - h: o + 2 * RH]
-                if n <= RH:                    # the head is the whole slice
-                    cuts = np.searchsorted(head, tau, side="left")
-                else:
-                    in_head = tau <= head[-1]  # every key below tau lies in the head
-                    in_tail = tau > tail[0]    # every key before the tail lies below tau
-                    if not np.all(in_head | in_tail):
-                        return None
-                    cuts = np.where(in_head, np.searchsorted(head, tau, side="left"),
-                                    n - h + np.searchsorted(tail, tau, side="left"))
-                allc[q, br] = np.diff(np.concatenate([[0], np.clip(cuts, 0, n), [n]]).astype(np.int64))
-        return allc
+        n = g[:, 0:2]                                          # [W, 2] slice lengths
+        keys = g[:, 9: 9 + 4 * RH].reshape(W, 2, 2, RH)       # [rank, branch, head / tail, RH]
+        head, tail = keys[:, :, 0, :], keys[:, :, 1, :]
+        t = tau[None, None, None, :]
+        valid = np.arange(RH)[None, None, :] < np.minimum(n, RH)[:, :, None]  # (short slices: padding)
+        ch = ((head[..., None] < t) & valid[..., None]).sum(axis=2)           # [W, 2, W-1]
+        ct = (tail[..., None] < t).sum(axis=2)
+        big = (n > RH)[:, :, None]
+        in_head = tau[None, None, :] <= head[:, :, RH - 1:RH]  # every key below tau is in the head
+        in_tail = tau[None, None, :] > tail[:, :, 0:1]         # every key before the tail is below tau
+        if np.any(big & ~(in_head | in_tail)):
+            return None
+        nn = n[:, :, None]
+        cuts = np.clip(np.where(big & ~in_head, nn - RH + ct, ch), 0, nn)
+        return np.diff(np.concatenate([np.zeros_like(nn), cuts, nn], axis=2), axis=2)
 
     @staticmethod
     def _range_plan(g: np.ndarray):
