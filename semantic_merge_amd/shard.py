@@ -461,19 +461,26 @@ class ShardedCompose:
             got = self.comm.all_to_all(pack_records(cols), in_splits, out_splits)
             f_in, _ = unpack_records(got, self.dtypes)
             roff = np.concatenate([[0], np.cumsum(out_splits)])
+            # every arriving op's (received row, buffer position): the lower ranks' ops of a
+            # branch go below its slice, the higher ranks' above; one index copy to the
+            # device and one gather / scatter per field (not one per branch and side)
+            src, dst = [], []
             for br in range(2):
-                for part, qs, dst0 in (("lo", range(r), self.rng[br][0]),
-                                       ("hi", range(r + 1, W), base[br] + n0[br] - int(hi_s[br]))):
+                for qs, dst0 in ((range(r), self.rng[br][0]),
+                                 (range(r + 1, W), base[br] + n0[br] - int(hi_s[br]))):
                     ii = [np.arange(roff[q] + (recv[q, 0] if br else 0),
                                     roff[q] + (recv[q, 0] if br else 0) + recv[q, br]) for q in qs]
                     ii = np.concatenate(ii) if ii else np.zeros(0, np.int64)
-                    if len(ii) == 0:
-                        continue
-                    ix = torch.from_numpy(ii.astype(np.int64)).to(self.dev)
-                    for f in FIELDS:
-                        if self.restore:  # originals under the arriving ops, put back after the step
-                            self._saved.append((f, dst0, self.buf[f][dst0: dst0 + len(ii)].clone()))
-                        self.buf[f][dst0: dst0 + len(ii)] = f_in[f][ix]
+                    src.append(ii)
+                    dst.append(np.arange(dst0, dst0 + len(ii)))
+            sd = np.stack([np.concatenate(src), np.concatenate(dst)]).astype(np.int64)
+            if sd.shape[1]:
+                sd = torch.from_numpy(sd).to(self.dev)
+                ix, at = sd[0], sd[1]
+                for f in FIELDS:
+                    if self.restore:  # originals under the arriving ops, put back after the step
+                        self._saved.append((f, at, self.buf[f][at]))
+                    self.buf[f][at] = f_in[f][ix]
         self.n_a = self.rng[0][1] - self.rng[0][0]
         self.n_b = self.rng[1][1] - self.rng[1][0]
         self._fields = self.buf
@@ -580,8 +587,8 @@ class ShardedCompose:
         self._bind()
 
     def _restore(self) -> None:
-        for f, at, t in reversed(self._saved):
-            self.buf[f][at: at + t.numel()] = t
+        for f, at, t in reversed(self._saved):  # (at: buffer positions, t: their originals)
+            self.buf[f][at] = t
         self._saved = []
 
     # -- device structs -----------------------------------------------------------------
