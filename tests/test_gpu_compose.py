@@ -180,6 +180,27 @@ def test_gpu_segmented_plan_when_wide_windows_overflow():
     assert dc.last_plan() == "segmented"
 
 
+@pytest.mark.parametrize("shape,plan", [("c5", "presorted-wide"), ("alt8100", "segmented"), ("long20000", "radix")])
+def test_gpu_early_verdict_plans(shape, plan):
+    """Merges from 4M ops take the synchronous early verdict: k_khist tests the groups,
+    k_fpart places the wide plan's boundaries on F_LONG and the host launches the wide
+    windows; when even those overflow (groups of 8100 + 200 in turn), or k_fpart's wide
+    test fails (20000-op groups: F_WLONG), the fallbacks take over from the meta."""
+    spec = synth.LiftSpec(4_500_000, 20_000, 79, mix=synth.ADVERSARIAL_MIX)
+    if shape == "c5":
+        soa = synth.lift_soa(synth.lift_logs(synth.LiftSpec(4_500_000, 20_000, 79, ops_per_ms=4096,
+                                                             mix=synth.ADVERSARIAL_MIX)))
+    elif shape == "alt8100":
+        soa = _alternating_groups(spec, 4050, 100)
+    else:
+        soa = _alternating_groups(spec, 10000, 10000)
+    assert soa.n >= (1 << 22)
+    dc = DeviceCompose(soa)
+    dc.run()
+    _eq_soa(dc.results(), oracle.compose(soa), f"early verdict, {shape}")
+    assert dc.last_plan() == plan
+
+
 def test_gpu_segmented_plan_duplicate_ids():
     """Config-5-shaped log (ordered, 4096-op timestamp groups per branch: the wide
     windows) with duplicate ids and ids equal in their top bits inside groups: equal
