@@ -17,6 +17,7 @@
 // is 4 bytes, relative to its tile:
 //   bits  0..13  index inside the tile          bits 14..25 symbol offset in its bucket
 //   bit  26      the move has a newAddress      bit  27     the move has a newFile
+// (one bit more for the index, and the fields above it shifted, with 32768-record tiles)
 #pragma once
 
 #include "smx_scan.h"
@@ -34,9 +35,13 @@
 #define TB_NBK_TGT 256      // target bucket count (width = n_sym / this, <= TB_WIDTH)
 #endif
 #define TB_TILE (TB_NT * TB_ITEMS)
-static_assert(TB_TILE <= (1 << 14), "tile-relative record index is 14 bits");
-#define REC_HAS_A (1u << 26)
-#define REC_HAS_F (1u << 27)
+// record bits: the index inside the tile (REC_IB bits), the symbol offset in its bucket
+// (12 bits, TB_WIDTH), the two move flags
+#define REC_IB (TB_TILE <= (1 << 14) ? 14 : 15)
+static_assert(TB_TILE <= (1 << 15), "tile-relative record index is at most 15 bits");
+#define REC_IMASK ((1u << REC_IB) - 1u)
+#define REC_HAS_A (1u << (REC_IB + 12))
+#define REC_HAS_F (1u << (REC_IB + 13))
 
 struct TbArgs {
   const u32* msym;    // moves: T-ordered symbol | has-address << 30 | has-file << 31
@@ -148,7 +153,7 @@ __global__ void __launch_bounds__(TB_NT) k_tb_scatter(TbArgs A0, u32* __restrict
       if (ok[it]) {
         const u32 b = s[it] / A.width;
         bk[it] = b;
-        q[it] = loc | ((s[it] - b * A.width) << 14) | fl[it];
+        q[it] = loc | ((s[it] - b * A.width) << REC_IB) | fl[it];
         atomicAdd(&lstart[b], 1u);
       }
     }
@@ -217,7 +222,7 @@ __global__ void k_tb_unskip(TbArgs A0, const u32* __restrict__ lst, u32* __restr
     const u32 e = lt[b + 1];
     for (u32 j = lt[b] + lane; j < e; j += WAVE) {
       const u32 q = rec[rb + j];
-      if (q != REC_DEAD && (q & 0x3fffu) == loc) rec[rb + j] = REC_DEAD;
+      if (q != REC_DEAD && (q & REC_IMASK) == loc) rec[rb + j] = REC_DEAD;
     }
   }
 }
@@ -230,6 +235,9 @@ __global__ void k_tb_unskip(TbArgs A0, const u32* __restrict__ lst, u32* __restr
 #define TBR_TK 16
 #endif
 // TBR_TK: tiles per wave step in k_tb_reduce
+#ifndef TBR_U
+#define TBR_U 2         // records per lane and tile in a k_tb_reduce step (longer runs: the tail loop)
+#endif
 #ifndef TBR_PREFETCH
 #define TBR_PREFETCH 1  // k_tb_reduce loads the next step's run bounds before this step's records are used
 #endif
@@ -276,8 +284,8 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
   for (u32 i = threadIdx.x; i < A.width; i += TBR_NT) tA[i] = tF[i] = tC[i] = 0;
   __syncthreads();
   auto put = [&](u32 q, u64 rb) {
-    const u32 r1 = (u32)(rb + (q & 0x3fffu)) + 1u;
-    const u32 ls = (q >> 14) & 0xfffu;
+    const u32 r1 = (u32)(rb + (q & REC_IMASK)) + 1u;
+    const u32 ls = (q >> REC_IB) & 0xfffu;
     if ((u64)(r1 - 1) < A.nMv) {
       if (q & REC_HAS_A) atomicMax(&tA[ls], r1);
       if (q & REC_HAS_F) atomicMax(&tF[ls], r1);
@@ -307,13 +315,13 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
   for (int t0 = wv * TBR_TK; t0 < nt; t0 += NW * TBR_TK) {
     u32 lo = lo_n, hi = hi_n;
     if (!TBR_PREFETCH) bounds(t0, &lo, &hi);
-    u32 q[TBR_TK][2];
+    u32 q[TBR_TK][TBR_U];
 #pragma unroll
     for (int k = 0; k < TBR_TK; ++k) {
       const u32 lk = __builtin_amdgcn_readlane(lo, k), hk = __builtin_amdgcn_readlane(hi, k);
       const u64 rb = (u64)(t0 + k) * TB_TILE;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < TBR_U; ++u) {
         const u32 i = lk + (u32)lane + (u32)(u * WAVE);
         q[k][u] = i < hk ? __builtin_nontemporal_load(&rec[rb + i]) : ~0u;
       }
@@ -322,13 +330,13 @@ __global__ void __launch_bounds__(TBR_NT) k_tb_reduce(TbArgs A0, const u32* __re
 #pragma unroll
     for (int k = 0; k < TBR_TK; ++k)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < TBR_U; ++u)
         if (q[k][u] != ~0u) put(q[k][u], (u64)(t0 + k) * TB_TILE);
 #pragma unroll
     for (int k = 0; k < TBR_TK; ++k) {
       const u32 lk = __builtin_amdgcn_readlane(lo, k), hk = __builtin_amdgcn_readlane(hi, k);
       const u64 rb = (u64)(t0 + k) * TB_TILE;
-      for (u32 i = lk + 2 * WAVE + (u32)lane; i < hk; i += WAVE) {
+      for (u32 i = lk + TBR_U * WAVE + (u32)lane; i < hk; i += WAVE) {
         const u32 x = rec[rb + i];
         if (x != REC_DEAD) put(x, rb);
       }
