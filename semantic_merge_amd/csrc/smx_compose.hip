@@ -1581,7 +1581,10 @@ static int launch_walk(const Ctx& C, const smx_shard* sh) {
   u32* ncand32 = (u32*)&meta->n_cand;
   const u64* ncand_dev = &meta->n_cand;
   const i64 Wmax = max_windows(n);
-  const int gsmall = 256;  // grid for loops over the (few) candidates
+#ifndef WALK_GSMALL
+#define WALK_GSMALL 256  // (64 and 1024 measured the same on configs 2 and 3: profiles/r06/ab_c3_walk_grid.txt)
+#endif
+  const int gsmall = WALK_GSMALL;  // grid for loops over the (few) candidates
   // small single merges: the one-block steps run in the last block of the grid before
   // them (k_boundary_cc, k_replay_q_cl), two launches fewer
   const bool lb_cc = SMX_WALK_LB && !sh && Wmax <= WALK_CC_FUSED_MAXW;
