@@ -438,7 +438,8 @@ PyObject* marshal_ops(PyObject*, PyObject* args) {
   Marshaler M;
   if (!parse_marshal_args(args, &ops, M, cols) || !M.init()) return nullptr;
   const Py_ssize_t n = PyList_GET_SIZE(ops);
-  M.kind.reserve(n);
+  M.kind.reserve(n), M.ts.reserve(n), M.hi.reserve(n), M.lo.reserve(n), M.sym.reserve(n), M.v0.reserve(n),
+      M.v1.reserve(n);
   for (Py_ssize_t k = 0; k < n; ++k)
     if (!M.add(PyList_GET_ITEM(ops, k))) return nullptr;
   Ref sum(M.summary());  // (packs the short ids into hi / lo)
