@@ -1075,11 +1075,12 @@ struct EmitArgs {
 #ifndef SMX_EMIT_NTST
 #define SMX_EMIT_NTST 1
 #endif
-// Streams read once: non-temporal, so that they do not evict the gathered
-// final-state table from L2.  The output stores are plain: an output range starts
-// anywhere (after the skipped renames), so its first and last lines are shared with
-// the neighbouring waves, and non-temporal partial-line stores measured 1.4-1.8x
-// slower than plain ones (tools/_build variants, round 2).
+// Streams read once and outputs written once: non-temporal, so that they do not evict
+// the gathered final-state table from L2 (k_emit4's aligned 16-byte stores; plain ones
+// measured emit 0.753 -> 0.821 ms on config 3, profiles/r06/ab_c3_emit_stores.txt).  A
+// wave's outputs are an aligned range, so no line is shared between waves; the partial
+// stores at the range's ends are plain (round 2 measured non-temporal partial-line
+// stores 1.4-1.8x slower than plain ones, when ranges were not aligned).
 #if SMX_EMIT_NT
 #define NTLD(p) __builtin_nontemporal_load(p)
 #else
@@ -1094,7 +1095,7 @@ struct EmitArgs {
 #define SMX_EMIT_NOGATHER 0
 #endif
 #ifndef EMIT_WT
-#define EMIT_WT 1024  // positions per wave
+#define EMIT_WT 1024  // positions per wave (2048: emit 0.753 -> 0.749 ms, within noise, profiles/r06/ab_c3_emit_stores.txt)
 #endif
 #ifndef EMIT_B
 #define EMIT_B 8      // wave steps whose loads are issued together
