@@ -41,6 +41,18 @@ def test_edge_cases_gpu():
         assert_case(compose_soa, case, f"case {i}")
 
 
+def test_edge_cases_dropin_gpu():
+    """All 600 reference cases through the drop-in itself: native marshal straight into the
+    session's pinned staging columns (and the Python encoders' replacement columns when
+    timestamps or ids are not ISO / canonical), the device merge, native materialise from
+    the staging area's views, the conflicts -- on Op objects, as the CLI calls it."""
+    for i, case in enumerate(load("compose_cases.json")):
+        A, B = to_ops(case["A"]), to_ops(case["B"])
+        out, conf = compose_oplogs(A, B)
+        assert jline([o.to_dict() for o in out]) == jline(case["out"]), f"case {i}: composed ops differ"
+        assert jline([c.to_dict() for c in conf]) == jline(case["conflicts"]), f"case {i}: conflicts differ"
+
+
 def test_dropin_compose_oplogs_matches_reference():
     case = load("compose_scenarios.json")["e2e_rename_move_decl"]
     A, B = to_ops(case["A"]), to_ops(case["B"])
