@@ -237,7 +237,7 @@ def small_merge(n_ops: int = 1000, reps: int = 50) -> dict:
     oa, ob = ops_from_dicts(A), ops_from_dicts(B)
     ops = oa + ob
     te, legs = [], []
-    sess = session()
+    sess = session()  # (the drop-in's: _lib.dropin_session holds it the same way)
     for _ in range(max(reps // 2, 1)):
         t0 = time.perf_counter()
         sa = marshal_native(oa, ob, sess.staging(len(oa) + len(ob)))  # (as compose_oplogs)

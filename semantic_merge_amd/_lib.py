@@ -168,6 +168,7 @@ class ComposeSession:
         self.device = self.torch.device(device)
         self.cap_n = self.cap_ws = -1
         self.last = {}
+        self.busy = False  # results handed out as views are being read (dropin_session)
         # its own stream: repeated merges of one size replay the library's HIP graph
         self.stream = self.torch.cuda.Stream(self.device)
 
@@ -282,10 +283,31 @@ def session(device: str = "cuda") -> ComposeSession:
     return s
 
 
+class dropin_session:
+    """The thread's session for one drop-in merge whose results are read as views of its
+    staging area (marshal into it, compose, materialise): marked busy meanwhile, so that a
+    merge started from inside that materialise -- a caller's Op class or deepcopy hook
+    composing again -- gets buffers of its own instead of overwriting the views."""
+
+    def __init__(self, device: str = "cuda") -> None:
+        self.device = device
+
+    def __enter__(self) -> ComposeSession:
+        s = session(self.device)
+        self.s = s if not s.busy else ComposeSession(self.device)
+        self.s.busy = True
+        return self.s
+
+    def __exit__(self, *exc) -> None:
+        self.s.busy = False
+
+
 def compose_soa(soa: SoA, device: str = "cuda"):
     """(order, addr, file, ctx, conflict_pairs) of one merge, computed on the GPU
-    (through the thread's reusable ComposeSession)."""
-    return session(device).compose(soa)
+    (through the thread's reusable ComposeSession, or buffers of its own while a drop-in
+    merge of this thread holds that session)."""
+    s = session(device)
+    return (s if not s.busy else ComposeSession(device)).compose(soa)
 
 
 def set_small_limit(n: int) -> int:

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 from typing import Any, List, Sequence, Tuple
 
-from ._lib import session
+from ._lib import dropin_session
 from .marshal import marshal_native
 from .materialize import materialize_conflicts, materialize_ops_native
 
@@ -24,12 +24,12 @@ def compose_oplogs(delta_a: Sequence[Any], delta_b: Sequence[Any]) -> Tuple[List
     """Compose two op logs into one deterministic sequence plus DivergentRename conflicts."""
     ops_a = list(delta_a)
     ops_b = list(delta_b)
-    sess = session()
-    # marshalled straight into the session's pinned staging columns; the results are views
-    # of its staging area too, materialised before the thread's next merge
-    soa = marshal_native(ops_a, ops_b, sess.staging(len(ops_a) + len(ops_b)))
-    order, addr, file, ctx, pairs = sess.compose(soa, copy=False)
-    ops = ops_a + ops_b
-    out = materialize_ops_native(ops, soa.kind, soa.strings, order, addr, file, ctx)
-    conflicts = materialize_conflicts(ops, pairs)
+    with dropin_session() as sess:
+        # marshalled straight into the session's pinned staging columns; the results are
+        # views of its staging area too, materialised while the session is held
+        soa = marshal_native(ops_a, ops_b, sess.staging(len(ops_a) + len(ops_b)))
+        order, addr, file, ctx, pairs = sess.compose(soa, copy=False)
+        ops = ops_a + ops_b
+        out = materialize_ops_native(ops, soa.kind, soa.strings, order, addr, file, ctx)
+        conflicts = materialize_conflicts(ops, pairs)
     return out, conflicts

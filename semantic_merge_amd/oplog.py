@@ -157,13 +157,14 @@ def decode_pair(text_a: Any, text_b: Any, op_cls: type = Op, target_cls: type = 
 def compose_json(text_a: Any, text_b: Any, op_cls: type = Op, target_cls: type = Target):
     """compose_oplogs(OpLog.from_json(text_a).ops, OpLog.from_json(text_b).ops) with the
     decode and the marshal fused (decode_pair)."""
-    from ._lib import session
+    from ._lib import dropin_session
     from .materialize import materialize_conflicts, materialize_ops_native
     ops_a, ops_b, soa = decode_pair(text_a, text_b, op_cls, target_cls)
-    order, addr, file, ctx, pairs = session().compose(soa, copy=False)  # (materialised at once)
-    ops = ops_a + ops_b
-    return materialize_ops_native(ops, soa.kind, soa.strings, order, addr, file, ctx), \
-        materialize_conflicts(ops, pairs)
+    with dropin_session() as sess:  # (views of its staging area, materialised while held)
+        order, addr, file, ctx, pairs = sess.compose(soa, copy=False)
+        ops = ops_a + ops_b
+        return materialize_ops_native(ops, soa.kind, soa.strings, order, addr, file, ctx), \
+            materialize_conflicts(ops, pairs)
 
 
 def ops_from_worker_result(result: Dict[str, Any], op_cls: type = Op,

@@ -385,3 +385,42 @@ def test_gpu_presorted_id_prefix_ties(frac, dup):
     got = dc.results()
     assert DeviceCompose.last_plan() == "presorted"
     _eq_soa(got, oracle.compose(soa), f"id prefix ties frac={frac} dup={dup}")
+
+
+def test_dropin_reentrant_merge_from_materialise():
+    """A merge started while the drop-in materialises (here from a value's __deepcopy__,
+    which the native copier hands to copy.deepcopy) gets buffers of its own: the outer
+    merge's results, read as views of the thread's staging area, stay intact."""
+    import copy
+    case = load("compose_scenarios.json")["e2e_rename_move_decl"]
+    inner = [to_ops(c["A"]) for c in load("compose_cases.json")[:2]]
+
+    class Hook:
+        calls = 0
+
+        def __init__(self, tag, nested):
+            self.tag, self.nested = tag, nested
+
+        def __deepcopy__(self, memo):
+            if self.nested:
+                compose_oplogs(inner[0], inner[1])
+                Hook.calls += 1
+            return Hook(self.tag, self.nested)
+
+        def __eq__(self, other):
+            return isinstance(other, Hook) and other.tag == self.tag
+
+    def run(nested):
+        A, B = to_ops(case["A"]), to_ops(case["B"])
+        for i, o in enumerate(A + B):
+            o.guards = {**o.guards, "hook": Hook(i, nested)}
+        out, conf = compose_oplogs(A, B)
+        return [(o.id, o.type, o.target.addressId, dict(o.params), o.guards["hook"].tag) for o in out], conf
+
+    Hook.calls = 0
+    want = run(False)
+    got = run(True)
+    assert Hook.calls > 0
+    assert got == want
+    assert [(i, t, a, p) for i, t, a, p, _ in want[0]] == [
+        (d["id"], d["type"], d["target"]["addressId"], d["params"]) for d in case["out"]]
