@@ -63,7 +63,18 @@ def _hiprt() -> C.CDLL:
     if _hip is None:
         _torch()
         lib()
-        h = C.CDLL("libamdhip64.so.7")  # (already loaded: dlopen returns that copy)
+        # the copy this process already mapped (torch's; libsmx resolved to it), by its
+        # path: dlopen returns that same copy, never a second runtime
+        path = None
+        with open("/proc/self/maps") as fh:
+            for line in fh:
+                f = line.split()[-1] if line.strip() else ""
+                if os.path.basename(f).startswith("libamdhip64.so"):
+                    path = f
+                    break
+        if path is None:
+            raise RuntimeError("the HIP runtime (libamdhip64) is not loaded in this process")
+        h = C.CDLL(path)
         h.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
         h.hipMemcpyAsync.restype = C.c_int
         h.hipStreamSynchronize.argtypes = [C.c_void_p]
